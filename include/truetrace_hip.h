@@ -1,0 +1,297 @@
+/*
+ * truetrace_hip.h — C ABI of the MI355X-native CWBVH8 closest-hit engine.
+ *
+ * This library replaces ONE dispatch of the TrueTrace path tracer:
+ *
+ *     cmd.DispatchCompute(IntersectionShader, TraceKernel, CurBounceInfoBuffer, 0)
+ *         TrueTrace/Resources/RayTracingMaster.cs:964-970
+ *     -> kernel_trace / IntersectBVH
+ *         TrueTrace/Resources/MainCompute/IntersectionKernels.compute:60-260
+ *
+ * It consumes the exact buffers TrueTrace's AssetManager binds for that kernel
+ * (AssetManager.SetMeshTraceBuffers, TrueTrace/Resources/AssetManager.cs:75-88):
+ *
+ *     cwbvh_nodes      80 B  BVHNode8Data            CommonData.cginc:174-181, CommonVars.cs:413-434
+ *     AggTris          88 B  CudaTriangle            CommonData.cginc:63-77,   CommonVars.cs:436-456
+ *     TLASBVH8Indices   4 B  int                     CommonData.cginc:160
+ *     _MeshData        88 B  MyMeshDataCompacted     CommonData.cginc:162-172, CommonVars.cs:245-255
+ *     _Materials      252 B  MaterialData            CommonData.cginc:215-258
+ *
+ * and the per-frame buffers RayTracingMaster binds (RayTracingMaster.cs:645-650):
+ *
+ *     GlobalRays           48 B RayData (hits written in place)   CommonData.cginc:100-107
+ *     _PrimaryTriangleInfo 16 B uint4 per pixel                   IntersectionKernels.compute:11,229-238
+ *     GlobalColors         64 B ColData (only Data.w is read)     CommonData.cginc:129-138
+ *
+ * Conventions: extern "C", cdecl, no exceptions cross the boundary, every call
+ * returns tt_status. One host thread drives a context at a time (Unity issues
+ * trace dispatches from its single render thread); one context per GPU.
+ *
+ * Numerics (pinned; the reference leaves them to DXC + the D3D driver):
+ *   rcp(x) = IEEE 1.0f/x (correctly rounded); mad(a,b,c) = fmaf(a,b,c);
+ *   dot(a,b) = fmaf(a.z,b.z, fmaf(a.y,b.y, a.x*b.x));
+ *   cross(a,b).x = fmaf(a.y,b.z, -(a.z*b.y)) (cyclic);
+ *   mul(M,v3).r = fmaf(m[r][2],v.z, fmaf(m[r][1],v.y, m[r][0]*v.x));
+ *   mul(M,(o,1)).r = fmaf(m[r][2],o.z, fmaf(m[r][1],o.y, m[r][0]*o.x)) + m[r][3];
+ *   min/max = IEEE minNum/maxNum (NaN-ignoring); no other contraction;
+ *   fp32 denormals are preserved (no flush) on both the GPU and the oracle.
+ */
+#ifndef TRUETRACE_HIP_H
+#define TRUETRACE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#define TT_STATIC_ASSERT(c, m) static_assert(c, m)
+#else
+#define TT_STATIC_ASSERT(c, m) _Static_assert(c, m)
+#endif
+
+#define TT_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+typedef int32_t tt_status;
+enum {
+    TT_OK = 0,
+    TT_ERR_INVALID_ARG = 1,
+    TT_ERR_OOM = 2,
+    TT_ERR_HIP = 3,
+    TT_ERR_UNSUPPORTED = 4,     /* e.g. a Cutout material reachable by the trace kernel */
+    TT_ERR_STACK_OVERFLOW = 5,  /* a ray needed more than TT_STACK_SIZE stack entries   */
+    TT_ERR_NO_DEVICE = 6,
+    TT_ERR_NO_SCENE = 7
+};
+
+/* Traversal stack depth of the reference: uint2 stack[16]
+ * (IntersectionKernels.compute:65). */
+#define TT_STACK_SIZE 16
+/* Hard loop bound of the reference: while (Reps < 1000)
+ * (IntersectionKernels.compute:155). On exhaustion no hit is written. */
+#define TT_MAX_REPS 1000
+
+/* ------------------------------------------------------ buffer layouts */
+/* BVHNode8Data, 80 B (CommonData.cginc:174-181). */
+typedef struct tt_cwbvh_node {
+    float p[3];          /* node_0xyz: quantization origin                        */
+    uint32_t e_imask;    /* node_0w: e_x | e_y<<8 | e_z<<16 | imask<<24             */
+    uint32_t base_child; /* node_1.x                                             */
+    uint32_t base_tri;   /* node_1.y                                             */
+    uint32_t meta[2];    /* node_1.zw: 8 meta bytes                              */
+    uint32_t qlo_x[2], qhi_x[2]; /* node_2 */
+    uint32_t qlo_y[2], qhi_y[2]; /* node_3 */
+    uint32_t qlo_z[2], qhi_z[2]; /* node_4 */
+} tt_cwbvh_node;
+TT_STATIC_ASSERT(sizeof(tt_cwbvh_node) == 80, "BVHNode8Data is 80 bytes");
+
+/* CudaTriangle, 88 B (CommonData.cginc:63-77, CommonVars.cs:436-456). */
+typedef struct tt_cuda_triangle {
+    float pos0[3];
+    float posedge1[3];
+    float posedge2[3];
+    uint32_t norms[3];   /* octahedral 16:16 (CommonVars.cs:816-833)       */
+    uint32_t tans[3];
+    float tex0[2];
+    float texedge1[2];   /* raw vertex UV, not an edge (ParentObject.cs:1039-1041) */
+    float texedge2[2];
+    uint32_t MatDat;
+} tt_cuda_triangle;
+TT_STATIC_ASSERT(sizeof(tt_cuda_triangle) == 88, "CudaTriangle is 88 bytes");
+
+/* MyMeshDataCompacted, 88 B (CommonData.cginc:162-172, CommonVars.cs:245-255).
+ * W2L is Unity's worldToLocalMatrix, column-major: element (row r, col c) at W2L[c*4+r]. */
+typedef struct tt_mesh_data {
+    float W2L[16];
+    int32_t TriOffset;            /* C#: AggIndexCount */
+    int32_t NodeOffset;           /* C#: AggNodeCount  */
+    int32_t MaterialOffset;
+    int32_t mesh_data_bvh_offsets;/* BLAS root (& 0x7fffffff) */
+    int32_t LightTriCount;
+    int32_t LightNodeOffset;
+} tt_mesh_data;
+TT_STATIC_ASSERT(sizeof(tt_mesh_data) == 88, "MyMeshDataCompacted is 88 bytes");
+
+/* MaterialData, 252 B (CommonData.cginc:215-258). Only the fields the trace kernel
+ * reads are named; the rest is opaque to this library. */
+typedef struct tt_material {
+    int32_t AlbedoTex[2];
+    int32_t NormalTex[2];
+    int32_t EmissiveTex[2];
+    int32_t MetallicTex[2];
+    int32_t RoughnessTex[2];
+    int32_t AlphaTex[2];         /* @40  */
+    int32_t MatCapMask[2];
+    int32_t MatCapTex[2];
+    float surfaceColor[3];       /* @64  */
+    float emmissive;
+    float EmissionColor[3];
+    uint32_t Tag;                /* @92: flag bits, Invisible = bit 7 (GlobalDefines.cginc:46) */
+    float roughness;
+    int32_t MatType;             /* @100: CutoutIndex = 2 (GlobalDefines.cginc:24) */
+    float transmittanceColor[3];
+    float ior;
+    float metallic, sheen, sheenTint, specularTint, clearcoat, clearcoatGloss;
+    float anisotropic, flatness, diffTrans;
+    float specTrans;             /* @156 */
+    float Specular, scatterDistance;
+    float AlbedoTexScale[4];     /* @168 */
+    float MetallicRemap[2];
+    float RoughnessRemap[2];
+    float AlphaCutoff;           /* @200 */
+    float NormalStrength, Hue, Saturation, Contrast, Brightness;
+    float BlendColor[3];
+    float BlendFactor;
+    float SecondaryTexScale[2];
+    float Rotation;              /* @248 */
+} tt_material;
+TT_STATIC_ASSERT(sizeof(tt_material) == 252, "MaterialData is 252 bytes");
+
+#define TT_MAT_CUTOUT_INDEX 2   /* GlobalDefines.cginc:24 */
+#define TT_FLAG_INVISIBLE   7   /* GlobalDefines.cginc:46 */
+
+/* RayData, 48 B (CommonData.cginc:100-107). hits = (mesh_id, triangle_id, asuint(t),
+ * (uint)(u*65535) | (uint)(v*65535)<<16) — set(), CommonData.cginc:430-434. */
+typedef struct tt_ray_data {
+    float origin[3];
+    uint32_t PixelIndex;
+    float direction[3];
+    float last_pdf;
+    uint32_t hits[4];
+} tt_ray_data;
+TT_STATIC_ASSERT(sizeof(tt_ray_data) == 48, "RayData is 48 bytes");
+
+/* ColData, 64 B (CommonData.cginc:129-138); the trace kernel reads Data.w only. */
+typedef struct tt_col_data {
+    float throughput[3];
+    float Direct[3];
+    float Indirect[3];
+    uint32_t PrimaryNEERay, Flags, MetRoughIsSpec;
+    float Data[4];
+} tt_col_data;
+TT_STATIC_ASSERT(sizeof(tt_col_data) == 64, "ColData is 64 bytes");
+
+/* --------------------------------------------------------- context */
+typedef struct tt_ctx tt_ctx;
+
+typedef struct tt_config {
+    int32_t device;        /* HIP device ordinal                                 */
+    uint32_t flags;        /* reserved, 0                                        */
+    uint64_t max_rays;     /* capacity of the staging ray buffer for host-pointer
+                              traces (2*W*H for a wavefront ray buffer); 0 = none */
+    void* stream;          /* hipStream_t to issue on; NULL = library-owned stream */
+} tt_config;
+
+/* Create / destroy a per-GPU context. */
+tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out);
+tt_status tt_ctx_destroy(tt_ctx* ctx);
+/* Last error message of this context (never NULL). */
+const char* tt_last_error(const tt_ctx* ctx);
+int32_t tt_abi_version(void);
+/* Number of visible HIP devices (0 on a machine without a GPU). */
+int32_t tt_device_count(void);
+
+/* ---------------------------------------------------------- scene */
+/* Replaces AssetManager.SetMeshTraceBuffers (AssetManager.cs:75-88): copies the
+ * aggregated buffers into HBM (the host keeps ownership of its arrays). Any previous
+ * scene of the context is released. n_mat may be 0 (no material checks). */
+tt_status tt_scene_upload(tt_ctx* ctx,
+                          const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                          const tt_cuda_triangle* tris, uint32_t n_tris,
+                          const int32_t* tlas_indices, uint32_t n_tlas_indices,
+                          const tt_mesh_data* meshdata, uint32_t n_mesh,
+                          const tt_material* materials, uint32_t n_mat);
+/* Per-frame TLAS refit region rewrite (BVH8AggregatedBuffer.SetData at
+ * AssetManager.cs:1760 / GPU refit AssetManager.cs:1821-1822). */
+tt_status tt_scene_update_nodes(tt_ctx* ctx, uint32_t first, uint32_t count,
+                                const tt_cwbvh_node* nodes);
+/* Per-frame transform update (MeshDataBuffer.SetData, AssetManager.cs:1825). */
+tt_status tt_scene_update_meshdata(tt_ctx* ctx, uint32_t first, uint32_t count,
+                                   const tt_mesh_data* meshdata);
+/* Bytes of HBM the scene occupies (device copies + derived traversal layouts). */
+tt_status tt_scene_bytes(const tt_ctx* ctx, uint64_t* bytes);
+
+/* ---------------------------------------------------------- trace */
+enum {
+    TT_TRACE_DEVICE_PTRS = 1u << 0,  /* ray/info/colors pointers are HIP device memory */
+    TT_TRACE_USE_RESTIRGI = 1u << 1, /* uniform UseReSTIRGI (RayTracingMaster.cs:558)   */
+    TT_TRACE_USE_ASVGF = 1u << 2,    /* uniform UseASVGF    (RayTracingMaster.cs:562)   */
+    TT_TRACE_STATS = 1u << 3,        /* count node visits / tri tests into tt_stats     */
+    TT_TRACE_ASYNC = 1u << 4         /* device pointers only: return without syncing    */
+};
+
+typedef struct tt_trace_params {
+    uint32_t n_rays;         /* BufferSizes[CurBounce].tracerays                     */
+    int32_t bounce;          /* CurBounce; odd bounces read GlobalRays[W*H + i]      */
+    float far_plane;         /* FarPlane (miss t)                                    */
+    uint32_t screen_width;   /* screen_width  (ping-pong offset, pixel decode)       */
+    uint32_t screen_height;  /* screen_height                                        */
+    uint32_t flags;          /* TT_TRACE_*                                            */
+} tt_trace_params;
+
+typedef struct tt_stats {
+    uint64_t rays;           /* rays traced                                           */
+    uint64_t node_visits;    /* internal node tests (Reps increments)                  */
+    uint64_t tri_tests;      /* IntersectTriangle calls                                */
+    uint64_t blas_entries;   /* TLAS -> BLAS switches                                  */
+    uint64_t hits;           /* rays whose final t < FarPlane                          */
+    uint64_t reps_exhausted; /* rays that hit the Reps >= 1000 bound (no write)        */
+    uint64_t stack_overflows;/* rays that would have pushed a 17th stack entry        */
+    float kernel_ms;         /* trace kernel time (HIP events), sync traces only       */
+    uint32_t pad;
+} tt_stats;
+
+/* kernel_trace replacement (IntersectionKernels.compute:60-260).
+ *   global_rays    : RayData[2*W*H] (or at least bounce-half + n_rays); hits written
+ *                    in place into GlobalRays[i].hits.
+ *   primary_info   : nullable uint4[W*H] (_PrimaryTriangleInfo).
+ *   global_colors  : ColData[W*H]; required when primary_info != NULL and bounce > 0.
+ *   stats          : nullable; counters require TT_TRACE_STATS. */
+tt_status tt_trace_closest(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
+                           uint32_t* primary_info, const tt_col_data* global_colors,
+                           tt_stats* stats);
+/* Wait for all work issued on the context's stream. */
+tt_status tt_sync(tt_ctx* ctx);
+/* The hipStream_t the context issues on. */
+void* tt_ctx_stream(tt_ctx* ctx);
+
+/* ------------------------------------------------- attribute resolve */
+/* Parity aid for "normals within 1e-5": per hit, the interpolated shading normal
+ * (GetTriangleNormal, CommonData.cginc:904-911) with Inverse = transpose of W2L's
+ * 3x3 (RayTracingShader.compute:99-118) and the geometric normal. Out: float[6] per
+ * ray (shading xyz, geometric xyz); misses write zeros. */
+tt_status tt_resolve_normals(tt_ctx* ctx, const tt_trace_params* p,
+                             const tt_ray_data* global_rays, float* normals6);
+
+/* ------------------------------------------- ray producers */
+/* Camera for Generate (RayGenKernels.compute:40-57) + CreateCameraRay (CommonData.cginc:511-567),
+ * UseDoF off. Matrices are Unity's cameraToWorldMatrix and projectionMatrix.inverse,
+ * column-major (m[c*4+r]). */
+typedef struct tt_camera {
+    float cam_to_world[16];
+    float cam_inv_proj[16];
+    float near_plane;
+    float far_plane;
+    uint32_t width;
+    uint32_t height;
+    int32_t jitter;             /* 1: random(0,pixel)-0.5 sub-pixel jitter (the !UseReCur path) */
+    int32_t frames_accumulated; /* random() seed inputs (non-ASVGF branch)                      */
+    int32_t max_bounce;
+    uint32_t flags;             /* TT_TRACE_DEVICE_PTRS                                          */
+} tt_camera;
+
+/* Writes W*H RayData (hits = (0,0,asuint(FarPlane),0)) into GlobalRays[pixel]. */
+tt_status tt_generate_primary(tt_ctx* ctx, const tt_camera* cam, tt_ray_data* global_rays);
+
+/* Diffuse-lobe next-bounce enqueue for the rays traced at p->bounce (the subset of kernel_shade
+ * in RayTracingShader.compute:52-84, 99-122, 293, 498-506 that produces the next ray): hits
+ * spawn a cosine-weighted ray about the shading normal, offset 1e-4 along the geometric normal;
+ * misses terminate. Survivors are compacted (wave ballot, one atomic per wave) into the other
+ * half of the ping-pong buffer; *n_next receives their count. */
+tt_status tt_enqueue_diffuse_bounce(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
+                                    int32_t frames_accumulated, int32_t max_bounce, uint32_t* n_next);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* TRUETRACE_HIP_H */

@@ -1,0 +1,522 @@
+/*
+ * tt_oracle.c — TEST INFRASTRUCTURE ONLY (see tt_oracle.h for the policy and the
+ * parity status). A deliberately literal, one-ray-at-a-time restatement of the reference
+ * HLSL; every block cites the reference lines it follows. Build with -ffp-contract=off:
+ * the only fused operations are the explicit fmaf() calls of the numerics contract.
+ */
+#include "tt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <string.h>
+#include <unistd.h>
+
+typedef struct { float x, y, z; } v3;
+typedef struct { v3 origin, direction, direction_inv; } Ray;        /* CommonData.cginc:80-84 */
+typedef struct { float t, u, v; int mesh_id, triangle_id; } RayHit;  /* CommonData.cginc:91-96 */
+typedef struct { uint32_t x, y; } uint2;
+
+typedef struct scene {
+    const tt_cwbvh_node* nodes; uint32_t n_nodes;
+    const tt_cuda_triangle* tris; uint32_t n_tris;
+    const int32_t* tlas; uint32_t n_tlas;
+    const tt_mesh_data* md; uint32_t n_mesh;
+    const tt_material* mats; uint32_t n_mat;
+} scene;
+
+/* ---------------------------------------------------------- pinned numerics */
+static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 vrcp(v3 a) { return mk(1.0f / a.x, 1.0f / a.y, 1.0f / a.z); }
+static inline float vdot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline v3 vcross(v3 a, v3 b) {
+    return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static inline v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+static inline uint32_t asuint(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float asfloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t firstbithigh(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+static inline uint32_t countbits(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+
+/* Unity column-major matrix: element (r,c) at m[c*4+r]. */
+static inline float M(const float* m, int r, int c) { return m[c * 4 + r]; }
+/* mul((float3x3)W2L, d) */
+static inline v3 mul33(const float* m, v3 d) {
+    return mk(fmaf(M(m, 0, 2), d.z, fmaf(M(m, 0, 1), d.y, M(m, 0, 0) * d.x)),
+              fmaf(M(m, 1, 2), d.z, fmaf(M(m, 1, 1), d.y, M(m, 1, 0) * d.x)),
+              fmaf(M(m, 2, 2), d.z, fmaf(M(m, 2, 1), d.y, M(m, 2, 0) * d.x)));
+}
+/* mul(W2L, float4(o, 1)).xyz */
+static inline v3 mul34(const float* m, v3 o) {
+    return mk(fmaf(M(m, 0, 2), o.z, fmaf(M(m, 0, 1), o.y, M(m, 0, 0) * o.x)) + M(m, 0, 3),
+              fmaf(M(m, 1, 2), o.z, fmaf(M(m, 1, 1), o.y, M(m, 1, 0) * o.x)) + M(m, 1, 3),
+              fmaf(M(m, 2, 2), o.z, fmaf(M(m, 2, 1), o.y, M(m, 2, 0) * o.x)) + M(m, 2, 3));
+}
+
+/* ray_get_octant_inv4 — CommonData.cginc:635-640 */
+static inline uint32_t ray_get_octant_inv4(v3 d) {
+    return (d.x < 0.0f ? 0u : 0x04040404u) | (d.y < 0.0f ? 0u : 0x02020202u) |
+           (d.z < 0.0f ? 0u : 0x01010101u);
+}
+
+/* cwbvh_node_intersect — CommonData.cginc:641-707 */
+static uint32_t cwbvh_node_intersect(const Ray* ray, uint32_t oct_inv4, float max_distance,
+                                     const tt_cwbvh_node* n) {
+    const uint32_t node_0w = n->e_imask;
+    const uint32_t e_x = node_0w & 0xff, e_y = (node_0w >> 8) & 0xff, e_z = (node_0w >> 16) & 0xff;
+    const v3 adjusted_ray_direction_inv = mk(asfloat(e_x << 23) * ray->direction_inv.x,
+                                             asfloat(e_y << 23) * ray->direction_inv.y,
+                                             asfloat(e_z << 23) * ray->direction_inv.z);
+    const v3 adjusted_ray_origin = vmul(ray->direction_inv, vsub(ld3(n->p), ray->origin));
+    uint32_t hit_mask = 0;
+    for (int i = 0; i < 2; i++) {
+        const uint32_t meta4 = n->meta[i];
+        const uint32_t is_inner4 = (meta4 & (meta4 << 1)) & 0x10101010u;
+        const uint32_t inner_mask4 = (((is_inner4 << 3) >> 7) & 0x01010101u) * 0xffu;
+        const uint32_t bit_index4 = (meta4 ^ (oct_inv4 & inner_mask4)) & 0x1f1f1f1fu;
+        const uint32_t child_bits4 = (meta4 >> 5) & 0x07070707u;
+        const uint32_t q_lo_x = n->qlo_x[i], q_hi_x = n->qhi_x[i];
+        const uint32_t q_lo_y = n->qlo_y[i], q_hi_y = n->qhi_y[i];
+        const uint32_t q_lo_z = n->qlo_z[i], q_hi_z = n->qhi_z[i];
+        const uint32_t x_min = ray->direction.x < 0.0f ? q_hi_x : q_lo_x;
+        const uint32_t x_max = ray->direction.x < 0.0f ? q_lo_x : q_hi_x;
+        const uint32_t y_min = ray->direction.y < 0.0f ? q_hi_y : q_lo_y;
+        const uint32_t y_max = ray->direction.y < 0.0f ? q_lo_y : q_hi_y;
+        const uint32_t z_min = ray->direction.z < 0.0f ? q_hi_z : q_lo_z;
+        const uint32_t z_max = ray->direction.z < 0.0f ? q_lo_z : q_hi_z;
+        for (int j = 0; j < 4; j++) {
+            v3 tmin3 = mk((float)((x_min >> (j * 8)) & 0xff), (float)((y_min >> (j * 8)) & 0xff),
+                          (float)((z_min >> (j * 8)) & 0xff));
+            v3 tmax3 = mk((float)((x_max >> (j * 8)) & 0xff), (float)((y_max >> (j * 8)) & 0xff),
+                          (float)((z_max >> (j * 8)) & 0xff));
+            tmin3 = mk(fmaf(tmin3.x, adjusted_ray_direction_inv.x, adjusted_ray_origin.x),
+                       fmaf(tmin3.y, adjusted_ray_direction_inv.y, adjusted_ray_origin.y),
+                       fmaf(tmin3.z, adjusted_ray_direction_inv.z, adjusted_ray_origin.z));
+            tmax3 = mk(fmaf(tmax3.x, adjusted_ray_direction_inv.x, adjusted_ray_origin.x),
+                       fmaf(tmax3.y, adjusted_ray_direction_inv.y, adjusted_ray_origin.y),
+                       fmaf(tmax3.z, adjusted_ray_direction_inv.z, adjusted_ray_origin.z));
+            const float tmin = fmaxf(fmaxf(tmin3.x, tmin3.y), fmaxf(tmin3.z, 1e-8f)); /* EPSILON :3 */
+            const float tmax = fminf(fminf(tmax3.x, tmax3.y), fminf(tmax3.z, max_distance));
+            if (tmin < tmax) {
+                const uint32_t child_bits = (child_bits4 >> (j * 8)) & 0xff;
+                const uint32_t bit_index = (bit_index4 >> (j * 8)) & 0xff;
+                hit_mask |= child_bits << bit_index;
+            }
+        }
+    }
+    return hit_mask;
+}
+
+/* IntersectTriangle — IntersectionKernels.compute:14-57 (AdvancedAlphaMapped on,
+ * IgnoreGlassMain off, IgnoreBackfacing off; GlobalDefines.cginc:1-11). Returns 0, or 3
+ * when a Cutout material would need the alpha atlas (unsupported). */
+static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray* ray,
+                              RayHit* ray_hit, int MatOffset, int CurBounce, uint32_t* accepts) {
+    const tt_cuda_triangle* T = &s->tris[tri_id];
+    const v3 pos0 = ld3(T->pos0), posedge1 = ld3(T->posedge1), posedge2 = ld3(T->posedge2);
+    const v3 h = vcross(ray->direction, posedge2);
+    const float a = vdot(posedge1, h);
+    const float f = 1.0f / a;
+    const v3 sv = vsub(ray->origin, pos0);
+    const float u = f * vdot(sv, h);
+    if (u >= 0.0f && u <= 1.0f) {
+        const v3 q = vcross(sv, posedge1);
+        const float v = f * vdot(ray->direction, q);
+        if (v >= 0.0f && u + v <= 1.0f) {
+            const float t = f * vdot(posedge2, q);
+            if (t > 0 && t < ray_hit->t) {
+                ++*accepts;
+                if (s->n_mat) {
+                    const int MaterialIndex = MatOffset + (int)T->MatDat;
+                    const tt_material* m = &s->mats[MaterialIndex];
+                    if (m->MatType == TT_MAT_CUTOUT_INDEX) return 3;
+                    if (CurBounce == 0 && ((((int)m->Tag) >> TT_FLAG_INVISIBLE) & 1) == 1) return 0;
+                }
+                ray_hit->t = t;
+                ray_hit->u = u;
+                ray_hit->v = v;
+                ray_hit->mesh_id = mesh_id;
+                ray_hit->triangle_id = tri_id;
+            }
+        }
+    }
+    return 0;
+}
+
+/* set() — CommonData.cginc:430-434 */
+static void set_hit(tt_ray_data* r, const RayHit* h) {
+    const uint32_t uv = (uint32_t)(h->u * 65535.0f) | ((uint32_t)(h->v * 65535.0f) << 16);
+    r->hits[0] = (uint32_t)h->mesh_id;
+    r->hits[1] = (uint32_t)h->triangle_id;
+    r->hits[2] = asuint(h->t);
+    r->hits[3] = uv;
+}
+
+typedef struct trace_job {
+    const scene* s;
+    const tt_trace_params* p;
+    tt_ray_data* rays;
+    uint32_t* info;
+    const tt_col_data* colors;
+    tt_oracle_ray_counts* counts;
+} trace_job;
+
+/* IntersectBVH — IntersectionKernels.compute:60-254 (HardwareRT off). */
+static int intersect_bvh(const trace_job* J, uint32_t i) {
+    const scene* s = J->s;
+    const tt_trace_params* P = J->p;
+    const int CurBounce = P->bounce;
+    const float FarPlane = P->far_plane;
+    tt_oracle_ray_counts cnt = {0, 0, 0, 0, 0, 0};
+
+    uint2 stack[TT_STACK_SIZE];
+    int stack_size = 0;
+    uint2 current_group, triangle_group;
+    uint32_t oct_inv4;
+    int tlas_stack_size;
+    Ray ray, ray2;
+    int NodeOffset, TriOffset, MatOffset;
+    int mesh_id = -1;
+    int Reps;
+
+    /* :79-83 ray pop; odd bounces read the second half of the ping-pong buffer */
+    uint32_t ray_index = i;
+    if (CurBounce % 2 == 1) ray_index += P->screen_width * P->screen_height;
+    tt_ray_data* GlobalRay = &J->rays[ray_index];
+    /* CreateRayHit — CommonData.cginc:364-372 */
+    RayHit bestHit = {FarPlane, 0.0f, 0.0f, 0, -1};
+
+    /* :139-153 */
+    TriOffset = 0;
+    MatOffset = 0;
+    Reps = 0;
+    ray.origin = ld3(GlobalRay->origin);
+    ray.direction = ld3(GlobalRay->direction);
+    ray.direction_inv = vrcp(ray.direction);
+    NodeOffset = 0;
+    tlas_stack_size = -1;
+    ray2 = ray;
+    oct_inv4 = ray_get_octant_inv4(ray.direction);
+    current_group.x = 0u;
+    current_group.y = 0x80000000u;
+    int status = 1; /* Reps exhausted unless the loop returns */
+
+    while (Reps < TT_MAX_REPS) {
+        if (current_group.y & 0xff000000u) { /* :157-187 internal node step */
+            const uint32_t child_index_offset = firstbithigh(current_group.y);
+            const uint32_t slot_index = (child_index_offset - 24) ^ (oct_inv4 & 0xff);
+            const uint32_t relative_index = countbits(current_group.y & ~(0xffffffffu << slot_index));
+            const uint32_t child_node_index = current_group.x + relative_index;
+            current_group.y &= ~(1u << child_index_offset);
+            if (current_group.y & 0xff000000u) {
+                if (stack_size == TT_STACK_SIZE) { status = 2; goto done; }
+                stack[stack_size++] = current_group;
+                if ((uint32_t)stack_size > cnt.max_stack) cnt.max_stack = (uint32_t)stack_size;
+            }
+            const tt_cwbvh_node* TempNode = &s->nodes[child_node_index];
+            const uint32_t hitmask = cwbvh_node_intersect(&ray, oct_inv4, bestHit.t, TempNode);
+            current_group.y = (hitmask & 0xff000000u) | ((TempNode->e_imask >> 24) & 0xff);
+            triangle_group.y = (hitmask & 0x00ffffffu);
+            current_group.x = TempNode->base_child + (uint32_t)NodeOffset;
+            triangle_group.x = TempNode->base_tri + (uint32_t)TriOffset;
+            Reps++;
+            cnt.node_visits++;
+        } else { /* :188-191 */
+            triangle_group = current_group;
+            current_group.x = 0u;
+            current_group.y = 0u;
+        }
+
+        if (triangle_group.y != 0) {
+            if (tlas_stack_size == -1) { /* :194-219 TLAS leaf -> enter BLAS */
+                const uint32_t mesh_offset = firstbithigh(triangle_group.y);
+                triangle_group.y &= ~(1u << mesh_offset);
+                mesh_id = s->tlas[triangle_group.x + mesh_offset];
+                const tt_mesh_data* MD = &s->md[mesh_id];
+                NodeOffset = MD->NodeOffset;
+                TriOffset = MD->TriOffset;
+                if (triangle_group.y != 0) {
+                    if (stack_size == TT_STACK_SIZE) { status = 2; goto done; }
+                    stack[stack_size++] = triangle_group;
+                }
+                if (current_group.y & 0xff000000u) {
+                    if (stack_size == TT_STACK_SIZE) { status = 2; goto done; }
+                    stack[stack_size++] = current_group;
+                }
+                if ((uint32_t)stack_size > cnt.max_stack) cnt.max_stack = (uint32_t)stack_size;
+                tlas_stack_size = stack_size;
+                const int root_index = (MD->mesh_data_bvh_offsets & 0x7fffffff);
+                MatOffset = MD->MaterialOffset;
+                ray.direction = mul33(MD->W2L, ray.direction);
+                ray.origin = mul34(MD->W2L, ray.origin);
+                ray.direction_inv = vrcp(ray.direction);
+                oct_inv4 = ray_get_octant_inv4(ray.direction);
+                current_group.x = (uint32_t)root_index;
+                current_group.y = 0x80000000u;
+                cnt.blas_entries++;
+            } else { /* :220-226 leaf triangles, highest bit first */
+                while (triangle_group.y != 0) {
+                    const uint32_t triangle_index = firstbithigh(triangle_group.y);
+                    triangle_group.y &= ~(1u << triangle_index);
+                    cnt.tri_tests++;
+                    if (intersect_triangle(s, mesh_id, (int)(triangle_group.x + triangle_index), &ray,
+                                           &bestHit, MatOffset, CurBounce, &cnt.accepts)) {
+                        status = 3;
+                        goto done;
+                    }
+                }
+            }
+        }
+
+        if ((current_group.y & 0xff000000u) == 0) {
+            if (stack_size == 0) { /* :229-241 finished: write _PrimaryTriangleInfo + hit */
+                const uint32_t PixIndex = GlobalRay->PixelIndex;
+                const uint32_t W = P->screen_width, H = P->screen_height;
+                const uint32_t tx = PixIndex % W, ty = PixIndex / W;
+                if (J->info && ty < H) {
+                    uint32_t* o = &J->info[(size_t)4 * ((size_t)ty * W + tx)];
+                    if (CurBounce == 0) {
+                        o[0] = (uint32_t)bestHit.mesh_id;
+                        o[1] = (uint32_t)(bestHit.triangle_id - s->md[bestHit.mesh_id].TriOffset);
+                        o[2] = asuint(bestHit.u);
+                        o[3] = asuint(bestHit.v);
+                    } else {
+                        const float w = J->colors[PixIndex].Data[3];
+                        if (w == -1.0f || (float)CurBounce == w) {
+                            const int restir = (P->flags & TT_TRACE_USE_RESTIRGI) != 0;
+                            const int asvgf = (P->flags & TT_TRACE_USE_ASVGF) != 0;
+                            if (restir && bestHit.t != FarPlane) {
+                                o[0] = (uint32_t)bestHit.mesh_id;
+                                o[1] = (uint32_t)(bestHit.triangle_id - s->md[bestHit.mesh_id].TriOffset);
+                                o[2] = (uint32_t)(bestHit.u * 65535.0f) | ((uint32_t)(bestHit.v * 65535.0f) << 16);
+                            } else if (asvgf || bestHit.t != FarPlane) {
+                                o[0] = asuint(ray2.direction.x);
+                                o[1] = asuint(ray2.direction.y);
+                                o[2] = asuint(ray2.direction.z);
+                            } else {
+                                o[0] = asuint(ray2.direction.x * bestHit.t + ray2.origin.x);
+                                o[1] = asuint(ray2.direction.y * bestHit.t + ray2.origin.y);
+                                o[2] = asuint(ray2.direction.z * bestHit.t + ray2.origin.z);
+                            }
+                            o[3] = bestHit.t == FarPlane ? 1u : 0u;
+                        }
+                    }
+                }
+                set_hit(GlobalRay, &bestHit);
+                status = 0;
+                goto done;
+            }
+            if (stack_size == tlas_stack_size) { /* :243-249 BLAS -> TLAS */
+                NodeOffset = 0;
+                TriOffset = 0;
+                tlas_stack_size = -1;
+                ray = ray2;
+                oct_inv4 = ray_get_octant_inv4(ray.direction);
+            }
+            current_group = stack[--stack_size];
+        }
+    }
+done:
+    cnt.status = (uint32_t)status;
+    if (J->counts) J->counts[i] = cnt;
+    return status;
+}
+
+typedef struct worker {
+    const trace_job* J;
+    uint32_t tid, nthreads;
+    int worst;
+} worker;
+
+#define TT_ORACLE_CHUNK 4096u
+
+static void* worker_main(void* arg) {
+    worker* w = (worker*)arg;
+    const uint32_t n = w->J->p->n_rays;
+    for (uint32_t base = w->tid * TT_ORACLE_CHUNK; base < n; base += w->nthreads * TT_ORACLE_CHUNK) {
+        const uint32_t end = base + TT_ORACLE_CHUNK < n ? base + TT_ORACLE_CHUNK : n;
+        for (uint32_t i = base; i < end; i++) {
+            const int st = intersect_bvh(w->J, i);
+            if (st > w->worst) w->worst = st;
+        }
+    }
+    return NULL;
+}
+
+static tt_status check_scene(const scene* s) {
+    for (uint32_t m = 0; m < s->n_mat; m++)
+        if (s->mats[m].MatType == TT_MAT_CUTOUT_INDEX) return TT_ERR_UNSUPPORTED;
+    return TT_OK;
+}
+
+tt_status tt_oracle_trace(const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                          const tt_cuda_triangle* tris, uint32_t n_tris,
+                          const int32_t* tlas_indices, uint32_t n_tlas,
+                          const tt_mesh_data* meshdata, uint32_t n_mesh,
+                          const tt_material* materials, uint32_t n_mat,
+                          const tt_trace_params* p, tt_ray_data* global_rays,
+                          uint32_t* primary_info, const tt_col_data* global_colors,
+                          tt_oracle_ray_counts* counts, int32_t nthreads) {
+    if (!nodes || !tris || !tlas_indices || !meshdata || !p || !global_rays) return TT_ERR_INVALID_ARG;
+    if (n_mat && !materials) return TT_ERR_INVALID_ARG;
+    if (primary_info && p->bounce > 0 && !global_colors) return TT_ERR_INVALID_ARG;
+    if (p->screen_width == 0 || p->screen_height == 0) return TT_ERR_INVALID_ARG;
+    scene s = {nodes, n_nodes, tris, n_tris, tlas_indices, n_tlas, meshdata, n_mesh, materials, n_mat};
+    tt_status st = check_scene(&s);
+    if (st != TT_OK) return st;
+    trace_job J = {&s, p, global_rays, primary_info, global_colors, counts};
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    worker ws[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) {
+        ws[t].J = &J;
+        ws[t].tid = (uint32_t)t;
+        ws[t].nthreads = (uint32_t)nthreads;
+        ws[t].worst = 0;
+    }
+    if (nthreads == 1) {
+        worker_main(&ws[0]);
+    } else {
+        for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, worker_main, &ws[t]);
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    }
+    int worst = 0;
+    for (int t = 0; t < nthreads; t++) if (ws[t].worst > worst) worst = ws[t].worst;
+    if (worst == 2) return TT_ERR_STACK_OVERFLOW;
+    if (worst == 3) return TT_ERR_UNSUPPORTED;
+    return TT_OK;
+}
+
+/* ------------------------------------------------------------ normal resolve */
+/* i_octahedral_32 — CommonData.cginc:849-857 (normalize pinned as v * (1/sqrt(dot))). */
+static v3 vnormalize(v3 v) {
+    const float inv = 1.0f / sqrtf(vdot(v, v));
+    return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+static v3 i_octahedral_32(uint32_t data) {
+    const uint32_t ix = data & 65535u, iy = (data >> 16) & 65535u;
+    const float vx = (float)ix / 32767.5f - 1.0f, vy = (float)iy / 32767.5f - 1.0f;
+    v3 nor = mk(vx, vy, 1.0f - fabsf(vx) - fabsf(vy));
+    const float t = fmaxf(-nor.z, 0.0f);
+    nor.x += (nor.x > 0.0f) ? -t : t;
+    nor.y += (nor.y > 0.0f) ? -t : t;
+    return vnormalize(nor);
+}
+
+/* GetTriangleNormal (CommonData.cginc:904-911) and the unsmoothed geometric normal
+ * (RayTracingShader.compute:111-118), Inverse = transpose((float3x3)W2L). */
+tt_status tt_oracle_resolve_normals(const tt_cuda_triangle* tris, uint32_t n_tris,
+                                    const tt_mesh_data* meshdata, uint32_t n_mesh,
+                                    const tt_trace_params* p, const tt_ray_data* global_rays,
+                                    float* normals6) {
+    if (!tris || !meshdata || !p || !global_rays || !normals6) return TT_ERR_INVALID_ARG;
+    const uint32_t off = (p->bounce % 2 == 1) ? p->screen_width * p->screen_height : 0;
+    for (uint32_t i = 0; i < p->n_rays; i++) {
+        const tt_ray_data* r = &global_rays[off + i];
+        float* o = &normals6[(size_t)6 * i];
+        const float t = asfloat(r->hits[2]);
+        const int mesh_id = (int)r->hits[0], tri = (int)r->hits[1];
+        if (!(t < p->far_plane) || tri < 0 || (uint32_t)tri >= n_tris || (uint32_t)mesh_id >= n_mesh) {
+            for (int k = 0; k < 6; k++) o[k] = 0.0f;
+            continue;
+        }
+        /* get() — CommonData.cginc:441-455 */
+        const float u = (float)(r->hits[3] & 0xffff) / 65535.0f;
+        const float v = (float)(r->hits[3] >> 16) / 65535.0f;
+        const float* W = meshdata[mesh_id].W2L;
+        /* Inverse[r][c] = W2L[c][r]; mul(Inverse, x).r = sum_c W2L[c][r] * x_c */
+        const tt_cuda_triangle* T = &tris[tri];
+        const v3 n0 = i_octahedral_32(T->norms[0]), n1 = i_octahedral_32(T->norms[1]),
+                 n2 = i_octahedral_32(T->norms[2]);
+        const float w0 = 1.0f - u - v;
+        const v3 ni = mk(n0.x * w0 + u * n1.x + v * n2.x, n0.y * w0 + u * n1.y + v * n2.y,
+                         n0.z * w0 + u * n1.z + v * n2.z);
+        v3 g = mk(fmaf(M(W, 2, 0), ni.z, fmaf(M(W, 1, 0), ni.y, M(W, 0, 0) * ni.x)),
+                  fmaf(M(W, 2, 1), ni.z, fmaf(M(W, 1, 1), ni.y, M(W, 0, 1) * ni.x)),
+                  fmaf(M(W, 2, 2), ni.z, fmaf(M(W, 1, 2), ni.y, M(W, 0, 2) * ni.x)));
+        const float gs = 1.0f / sqrtf(vdot(g, g));
+        g = mk(gs * g.x, gs * g.y, gs * g.z);
+        const v3 c = vcross(vnormalize(ld3(T->posedge1)), vnormalize(ld3(T->posedge2)));
+        v3 us = mk(fmaf(M(W, 2, 0), c.z, fmaf(M(W, 1, 0), c.y, M(W, 0, 0) * c.x)),
+                   fmaf(M(W, 2, 1), c.z, fmaf(M(W, 1, 1), c.y, M(W, 0, 1) * c.x)),
+                   fmaf(M(W, 2, 2), c.z, fmaf(M(W, 1, 2), c.y, M(W, 0, 2) * c.x)));
+        const float us_s = 1.0f / sqrtf(vdot(us, us));
+        us = mk(-(us_s * us.x), -(us_s * us.y), -(us_s * us.z));
+        if (vdot(us, g) < 0) us = mk(-us.x, -us.y, -us.z);
+        o[0] = g.x; o[1] = g.y; o[2] = g.z;
+        o[3] = us.x; o[4] = us.y; o[5] = us.z;
+    }
+    return TT_OK;
+}
+
+/* ------------------------------------------------------------ camera rays */
+/* pcg_hash / hash_with — CommonData.cginc:374-389; random() non-ASVGF branch :413-426 */
+static uint32_t pcg_hash(uint32_t seed) {
+    const uint32_t state = seed * 747796405u + 2891336453u;
+    const uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+static uint32_t hash_with(uint32_t seed, uint32_t hash) {
+    seed = (seed ^ 61u) ^ hash;
+    seed += seed << 3;
+    seed ^= seed >> 4;
+    seed *= 0x27d4eb2du;
+    return seed;
+}
+static void random2(uint32_t samdim, uint32_t pixel_index, int32_t frames, int32_t max_bounce,
+                    int32_t cur_bounce, float* x, float* y) {
+    const uint32_t hash = pcg_hash((pixel_index * 258u + samdim) * (uint32_t)(max_bounce + 1) + (uint32_t)cur_bounce);
+    const float k = asfloat(0x2f7fffffu);
+    *x = (float)hash_with((uint32_t)frames, hash) * k;
+    *y = (float)hash_with((uint32_t)frames + 0xdeadbeefu, hash) * k;
+}
+
+tt_status tt_oracle_generate(const float* c2w, const float* ip, uint32_t width, uint32_t height,
+                             float near_plane, float far_plane, int32_t jitter,
+                             int32_t frames_accumulated, int32_t max_bounce,
+                             tt_ray_data* global_rays) {
+    if (!c2w || !ip || !global_rays || !width || !height) return TT_ERR_INVALID_ARG;
+    for (uint32_t y = 0; y < height; y++) {
+        for (uint32_t x = 0; x < width; x++) {
+            const uint32_t pixel_index = y * width + x;
+            float jx = 0.0f, jy = 0.0f;
+            if (jitter) {
+                random2(0, pixel_index, frames_accumulated, max_bounce, 0, &jx, &jy);
+                jx -= 0.5f;
+                jy -= 0.5f;
+            }
+            const float uvx = ((float)x + jx) / (float)width * 2.0f - 1.0f;
+            const float uvy = ((float)y + jy) / (float)height * 2.0f - 1.0f;
+            /* origin = mul(CamToWorld, (0,0,0,1)).xyz */
+            const v3 origin = mk(M(c2w, 0, 3), M(c2w, 1, 3), M(c2w, 2, 3));
+            /* direction = mul(CamInvProj, (uv, 0, 1)).xyz */
+            v3 d = mk(fmaf(M(ip, 0, 1), uvy, M(ip, 0, 0) * uvx) + M(ip, 0, 3),
+                      fmaf(M(ip, 1, 1), uvy, M(ip, 1, 0) * uvx) + M(ip, 1, 3),
+                      fmaf(M(ip, 2, 1), uvy, M(ip, 2, 0) * uvx) + M(ip, 2, 3));
+            /* direction = mul(CamToWorld, (d, 0)).xyz; normalize */
+            d = mul33(c2w, d);
+            d = vnormalize(d);
+            tt_ray_data* r = &global_rays[pixel_index];
+            r->origin[0] = origin.x + near_plane * d.x;
+            r->origin[1] = origin.y + near_plane * d.y;
+            r->origin[2] = origin.z + near_plane * d.z;
+            r->PixelIndex = pixel_index;
+            r->direction[0] = d.x;
+            r->direction[1] = d.y;
+            r->direction[2] = d.z;
+            r->last_pdf = 0.0f;
+            r->hits[0] = 0;
+            r->hits[1] = 0;
+            r->hits[2] = asuint(far_plane);
+            r->hits[3] = 0;
+        }
+    }
+    return TT_OK;
+}
+
+int32_t tt_oracle_hardware_threads(void) {
+    const long n = sysconf(_SC_NPROCESSORS_ONLN);
+    return n > 0 ? (int32_t)n : 1;
+}

@@ -1,0 +1,69 @@
+/*
+ * tt_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * Scalar CPU restatement of TrueTrace's closest-hit CWBVH8 traversal
+ * (kernel_trace / IntersectBVH, TrueTrace/Resources/MainCompute/IntersectionKernels.compute:14-260)
+ * and of the few producers/consumers either side of it that the parity tests need
+ * (camera ray generation, diffuse bounce enqueue, normal resolve).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / CPU baseline. The product path (libtruetrace_hip.so)
+ * never links or calls it.
+ *
+ * Parity status: the reference (HLSL compiled by Unity's DXC for D3D12) cannot be compiled
+ * or run in this environment and ships no golden vectors, so parity against reference
+ * OUTPUTS is UNPINNED. The oracle is pinned by (1) analytic known-answer vectors whose
+ * results are exact under any legal rounding of the reference HLSL (tests/test_oracle_kat.py)
+ * and (2) the numerics contract in include/truetrace_hip.h, which the GPU kernel also follows.
+ */
+#ifndef TT_ORACLE_H
+#define TT_ORACLE_H
+#include "../include/truetrace_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tt_oracle_ray_counts {
+    uint32_t node_visits;  /* Reps: internal node tests            */
+    uint32_t tri_tests;    /* IntersectTriangle calls              */
+    uint32_t blas_entries; /* TLAS -> BLAS switches                */
+    uint32_t accepts;      /* candidate t passed (0 < t < best.t)  */
+    uint32_t max_stack;    /* deepest stack_size reached            */
+    uint32_t status;       /* 0 = wrote, 1 = Reps exhausted, 2 = stack overflow, 3 = unsupported */
+} tt_oracle_ray_counts;
+
+/* Trace rays [0, p->n_rays) (ray i lives at GlobalRays[i + (bounce odd ? W*H : 0)]).
+ * Writes hits in place, and primary_info if non-NULL. counts (nullable) is indexed by i.
+ * nthreads <= 1: single-threaded. Returns TT_OK or the first error (TT_ERR_STACK_OVERFLOW
+ * when any ray overflowed, TT_ERR_UNSUPPORTED for cutout materials). */
+tt_status tt_oracle_trace(const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                          const tt_cuda_triangle* tris, uint32_t n_tris,
+                          const int32_t* tlas_indices, uint32_t n_tlas,
+                          const tt_mesh_data* meshdata, uint32_t n_mesh,
+                          const tt_material* materials, uint32_t n_mat,
+                          const tt_trace_params* p, tt_ray_data* global_rays,
+                          uint32_t* primary_info, const tt_col_data* global_colors,
+                          tt_oracle_ray_counts* counts, int32_t nthreads);
+
+/* Shading / geometric normal for the hit stored in GlobalRays (see tt_resolve_normals). */
+tt_status tt_oracle_resolve_normals(const tt_cuda_triangle* tris, uint32_t n_tris,
+                                    const tt_mesh_data* meshdata, uint32_t n_mesh,
+                                    const tt_trace_params* p, const tt_ray_data* global_rays,
+                                    float* normals6);
+
+/* Generate (RayGenKernels.compute:40-57) + CreateCameraRay (CommonData.cginc:511-567),
+ * UseDoF off. cam_to_world / cam_inv_proj are Unity matrices, column-major (m[c*4+r]).
+ * jitter != 0 applies random(0, pixel) - 0.5 (the !UseReCur branch) with
+ * frames_accumulated/MaxBounce/CurBounce=0 as the non-ASVGF random() path. */
+tt_status tt_oracle_generate(const float* cam_to_world, const float* cam_inv_proj,
+                             uint32_t width, uint32_t height, float near_plane,
+                             float far_plane, int32_t jitter, int32_t frames_accumulated,
+                             int32_t max_bounce, tt_ray_data* global_rays);
+
+int32_t tt_oracle_hardware_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,651 @@
+// tt_api.hip — the C ABI of include/truetrace_hip.h: context lifecycle, scene upload with
+// structural validation, trace dispatch (the kernel_trace replacement) and the normal resolve.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tt_device.h"
+
+hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
+hipError_t tt_trace_occupancy(int* blocks_per_cu);
+uint32_t tt_trace_block_size();
+hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uint32_t h, float near_plane, float far_plane,
+                              int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays, hipStream_t st);
+hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
+                            int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
+                            const tt_mesh_data* md, uint32_t* counter, hipStream_t st);
+hipError_t tt_launch_resolve(const tt_ray_data* rays, uint32_t ray_offset, uint32_t n, float far_plane,
+                             const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* md, uint32_t n_mesh,
+                             float* out, hipStream_t st);
+
+namespace {
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t alloc(size_t count) {
+        release();
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        n = count;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct SceneHost {
+    std::vector<tt_cwbvh_node> nodes;
+    std::vector<int32_t> tlas;
+    std::vector<tt_mesh_data> mesh;
+    uint32_t n_tris = 0;
+    uint32_t n_mat = 0;
+    std::vector<uint32_t> matdat;  // only kept when a material sets the Invisible flag
+};
+
+}  // namespace
+
+struct tt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 0;
+    int blocks_per_cu = 0;
+    uint32_t grid = 0;
+    TraceControl* ctl = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    // scene
+    bool has_scene = false;
+    bool any_invisible = false;
+    SceneHost host;
+    DevBuf<tt_cwbvh_node> nodes;
+    DevBuf<tt_cuda_triangle> tris_raw;
+    DevBuf<TriPos> tris;
+    DevBuf<int32_t> tlas;
+    DevBuf<tt_mesh_data> mesh_raw;
+    DevBuf<MeshGpu> mesh;
+    DevBuf<uint32_t> mat_tag;
+    // host-pointer staging
+    uint64_t max_rays = 0;
+    DevBuf<tt_ray_data> st_rays;
+    DevBuf<uint32_t> st_info;
+    DevBuf<tt_col_data> st_colors;
+    DevBuf<float> st_normals;
+    DevBuf<float> cam;          // 32 floats: cam_to_world | cam_inv_proj
+    DevBuf<uint32_t> counter;   // bounce enqueue counter
+};
+
+namespace {
+
+tt_status fail(tt_ctx* c, tt_status s, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return s;
+}
+
+tt_status hip_fail(tt_ctx* c, hipError_t e, const char* what) {
+    return fail(c, e == hipErrorOutOfMemory ? TT_ERR_OOM : TT_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define TT_HIP(c, call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
+    } while (0)
+
+// Structural validation of everything the trace kernel can reach (IntersectBVH's index
+// arithmetic, IntersectionKernels.compute:157-213): every reachable node, triangle, TLAS slot
+// and mesh record must be in range, so the GPU kernel needs no per-access bounds checks.
+struct Validator {
+    const SceneHost& s;
+    std::vector<uint32_t> epoch_of;
+    uint32_t epoch = 0;
+    std::string why;
+    explicit Validator(const SceneHost& h) : s(h), epoch_of(h.nodes.size(), 0u) {}
+
+    uint32_t max_matdat = 0;
+    bool walk(uint32_t root, uint32_t node_offset, uint32_t tri_offset, bool tlas_level) {
+        epoch++;
+        max_matdat = 0;
+        std::vector<uint32_t> work{root};
+        while (!work.empty()) {
+            const uint32_t ni = work.back();
+            work.pop_back();
+            if (ni >= s.nodes.size()) {
+                why = "node index " + std::to_string(ni) + " out of range";
+                return false;
+            }
+            if (epoch_of[ni] == epoch) continue;
+            epoch_of[ni] = epoch;
+            const tt_cwbvh_node& n = s.nodes[ni];
+            const uint32_t imask = n.e_imask >> 24;
+            for (int k = 0; k < 8; k++) {
+                const uint32_t meta = (n.meta[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+                const uint32_t low5 = meta & 0x1fu, bits = (meta >> 5) & 7u;
+                const bool inner = (meta & 0x18u) == 0x18u;
+                if (inner) {
+                    if (bits != 1u) {
+                        why = "inner meta with child bits != 1";
+                        return false;
+                    }
+                    const uint32_t slot = low5 - 24u;
+                    const uint32_t child = n.base_child + node_offset + (uint32_t)__builtin_popcount(imask & ((1u << slot) - 1u));
+                    work.push_back(child);
+                } else if (bits) {
+                    const uint32_t top = low5 + (31u - (uint32_t)__builtin_clz(bits));
+                    if (top >= 24u) {
+                        why = "leaf meta spills into the internal-child bits";
+                        return false;
+                    }
+                    for (uint32_t b = 0; b < 3; b++) {
+                        if (!((bits >> b) & 1u)) continue;
+                        const uint64_t t = (uint64_t)n.base_tri + tri_offset + low5 + b;
+                        if (tlas_level) {
+                            if (t >= s.tlas.size()) {
+                                why = "TLAS leaf slot out of range";
+                                return false;
+                            }
+                            const int32_t m = s.tlas[t];
+                            if (m < 0 || (size_t)m >= s.mesh.size()) {
+                                why = "TLASBVH8Indices entry out of range";
+                                return false;
+                            }
+                        } else if (t >= s.n_tris) {
+                            why = "triangle index out of range";
+                            return false;
+                        } else if (!s.matdat.empty()) {
+                            max_matdat = std::max(max_matdat, s.matdat[(size_t)t]);
+                        }
+                    }
+                }
+            }
+        }
+        return true;
+    }
+
+    bool run() {
+        if (s.nodes.empty() || s.mesh.empty()) {
+            why = "empty scene";
+            return false;
+        }
+        if (!walk(0, 0, 0, true)) return false;
+        // every mesh record reachable through the TLAS (validate them all: cheap, and update
+        // paths may re-point TLAS leaves)
+        struct Seen {
+            uint64_t key;
+            uint32_t root, max_matdat;
+        };
+        std::vector<Seen> seen;
+        for (size_t m = 0; m < s.mesh.size(); m++) {
+            const tt_mesh_data& md = s.mesh[m];
+            const uint32_t root = (uint32_t)(md.mesh_data_bvh_offsets & 0x7fffffff);
+            if (md.NodeOffset < 0 || md.TriOffset < 0) {
+                why = "negative mesh offsets";
+                return false;
+            }
+            const uint64_t key = ((uint64_t)(uint32_t)md.NodeOffset << 32) | (uint32_t)md.TriOffset;
+            uint32_t mm = 0;
+            bool dup = false;
+            for (auto& p : seen)
+                if (p.key == key && p.root == root) {
+                    dup = true;
+                    mm = p.max_matdat;
+                }
+            if (!dup) {
+                if (!walk(root, (uint32_t)md.NodeOffset, (uint32_t)md.TriOffset, false)) return false;
+                mm = max_matdat;
+                seen.push_back(Seen{key, root, mm});
+            }
+            if (!s.matdat.empty() && (md.MaterialOffset < 0 || (uint64_t)md.MaterialOffset + mm >= s.n_mat)) {
+                why = "MaterialOffset + MatDat out of range for mesh " + std::to_string(m);
+                return false;
+            }
+        }
+        return true;
+    }
+};
+
+void derive_mesh(const tt_mesh_data& in, MeshGpu& o) {
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) o.m[r * 4 + c] = in.W2L[c * 4 + r];
+    o.TriOffset = in.TriOffset;
+    o.NodeOffset = in.NodeOffset;
+    o.MaterialOffset = in.MaterialOffset;
+    o.root = in.mesh_data_bvh_offsets & 0x7fffffff;
+}
+
+void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
+    o.p0x = t.pos0[0];
+    o.p0y = t.pos0[1];
+    o.p0z = t.pos0[2];
+    o.e1x = t.posedge1[0];
+    o.e1y = t.posedge1[1];
+    o.e1z = t.posedge1[2];
+    o.e2x = t.posedge2[0];
+    o.e2y = t.posedge2[1];
+    o.e2z = t.posedge2[2];
+    o.matdat = t.MatDat;
+    o.pad0 = o.pad1 = 0;
+}
+
+bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t tt_abi_version(void) { return TT_ABI_VERSION; }
+
+int32_t tt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+const char* tt_last_error(const tt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
+    if (!cfg || !out) return TT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        return TT_ERR_NO_DEVICE;
+    }
+    if (cfg->device < 0 || cfg->device >= ndev) return TT_ERR_INVALID_ARG;
+    tt_ctx* c = new tt_ctx();
+    c->device = cfg->device;
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) {
+        delete c;
+        return TT_ERR_HIP;
+    }
+    if (cfg->stream) {
+        c->stream = static_cast<hipStream_t>(cfg->stream);
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return TT_ERR_HIP;
+        }
+        c->own_stream = true;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
+        tt_ctx_destroy(c);
+        return TT_ERR_HIP;
+    }
+    c->num_cus = prop.multiProcessorCount;
+    int bpc = 0;
+    if (tt_trace_occupancy(&bpc) != hipSuccess || bpc <= 0) bpc = 2;
+    c->blocks_per_cu = std::min(bpc, 8);
+    c->grid = (uint32_t)(c->num_cus * c->blocks_per_cu);
+    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        tt_ctx_destroy(c);
+        return TT_ERR_OOM;
+    }
+    c->max_rays = cfg->max_rays;
+    if (c->max_rays) {
+        if (c->st_rays.alloc(c->max_rays) != hipSuccess) {
+            tt_ctx_destroy(c);
+            return TT_ERR_OOM;
+        }
+    }
+    *out = c;
+    return TT_OK;
+}
+
+tt_status tt_ctx_destroy(tt_ctx* c) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->nodes.release();
+    c->tris_raw.release();
+    c->tris.release();
+    c->tlas.release();
+    c->mesh_raw.release();
+    c->mesh.release();
+    c->mat_tag.release();
+    c->st_rays.release();
+    c->st_info.release();
+    c->st_colors.release();
+    c->st_normals.release();
+    c->cam.release();
+    c->counter.release();
+    if (c->ctl) (void)hipFree(c->ctl);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return TT_OK;
+}
+
+void* tt_ctx_stream(tt_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+tt_status tt_sync(tt_ctx* c) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris,
+                          uint32_t n_tris, const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md,
+                          uint32_t n_mesh, const tt_material* mats, uint32_t n_mat) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!nodes || !n_nodes || !tris || !n_tris || !tlas || !n_tlas || !md || !n_mesh || (n_mat && !mats))
+        return fail(c, TT_ERR_INVALID_ARG, "tt_scene_upload: null or empty buffer");
+    TT_HIP(c, hipSetDevice(c->device));
+    c->has_scene = false;
+    SceneHost h;
+    h.nodes.assign(nodes, nodes + n_nodes);
+    h.tlas.assign(tlas, tlas + n_tlas);
+    h.mesh.assign(md, md + n_mesh);
+    h.n_tris = n_tris;
+    h.n_mat = n_mat;
+    bool any_invisible = false;
+    std::vector<uint32_t> tags(std::max<uint32_t>(n_mat, 1u), 0u);
+    for (uint32_t m = 0; m < n_mat; m++) {
+        if (mats[m].MatType == TT_MAT_CUTOUT_INDEX)
+            return fail(c, TT_ERR_UNSUPPORTED,
+                        "material %u is Cutout (alpha-atlas test, IntersectionKernels.compute:35-40) — not supported", m);
+        tags[m] = mats[m].Tag;
+        any_invisible |= ((mats[m].Tag >> TT_FLAG_INVISIBLE) & 1u) != 0;
+    }
+    if (any_invisible) {
+        h.matdat.resize(n_tris);
+        for (uint32_t t = 0; t < n_tris; t++) h.matdat[t] = tris[t].MatDat;
+    }
+    Validator v(h);
+    if (!v.run()) return fail(c, TT_ERR_INVALID_ARG, "scene validation failed: %s", v.why.c_str());
+    std::vector<TriPos> tp(n_tris);
+    for (uint32_t t = 0; t < n_tris; t++) derive_tri(tris[t], tp[t]);
+    std::vector<MeshGpu> mg(n_mesh);
+    for (uint32_t m = 0; m < n_mesh; m++) derive_mesh(md[m], mg[m]);
+    c->nodes.release();
+    c->tris_raw.release();
+    c->tris.release();
+    c->tlas.release();
+    c->mesh_raw.release();
+    c->mesh.release();
+    c->mat_tag.release();
+    hipError_t e;
+    if ((e = c->nodes.alloc(n_nodes)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
+        (e = c->tris.alloc(n_tris)) != hipSuccess || (e = c->tlas.alloc(n_tlas)) != hipSuccess ||
+        (e = c->mesh_raw.alloc(n_mesh)) != hipSuccess || (e = c->mesh.alloc(n_mesh)) != hipSuccess ||
+        (e = c->mat_tag.alloc(tags.size())) != hipSuccess)
+        return hip_fail(c, e, "scene allocation");
+    TT_HIP(c, hipMemcpy(c->nodes.p, nodes, sizeof(tt_cwbvh_node) * n_nodes, hipMemcpyHostToDevice));
+    TT_HIP(c, hipMemcpy(c->tris_raw.p, tris, sizeof(tt_cuda_triangle) * n_tris, hipMemcpyHostToDevice));
+    TT_HIP(c, hipMemcpy(c->tris.p, tp.data(), sizeof(TriPos) * n_tris, hipMemcpyHostToDevice));
+    TT_HIP(c, hipMemcpy(c->tlas.p, tlas, sizeof(int32_t) * n_tlas, hipMemcpyHostToDevice));
+    TT_HIP(c, hipMemcpy(c->mesh_raw.p, md, sizeof(tt_mesh_data) * n_mesh, hipMemcpyHostToDevice));
+    TT_HIP(c, hipMemcpy(c->mesh.p, mg.data(), sizeof(MeshGpu) * n_mesh, hipMemcpyHostToDevice));
+    TT_HIP(c, hipMemcpy(c->mat_tag.p, tags.data(), sizeof(uint32_t) * tags.size(), hipMemcpyHostToDevice));
+    c->host = std::move(h);
+    c->any_invisible = any_invisible;
+    c->has_scene = true;
+    return TT_OK;
+}
+
+tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!nodes || (uint64_t)first + count > c->host.nodes.size())
+        return fail(c, TT_ERR_INVALID_ARG, "node update range out of bounds");
+    std::vector<tt_cwbvh_node> saved(c->host.nodes.begin() + first, c->host.nodes.begin() + first + count);
+    std::copy(nodes, nodes + count, c->host.nodes.begin() + first);
+    Validator v(c->host);
+    if (!v.run()) {
+        std::copy(saved.begin(), saved.end(), c->host.nodes.begin() + first);
+        return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after node update: %s", v.why.c_str());
+    }
+    TT_HIP(c, hipSetDevice(c->device));
+    TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, nodes, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, const tt_mesh_data* md) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!md || (uint64_t)first + count > c->host.mesh.size())
+        return fail(c, TT_ERR_INVALID_ARG, "meshdata update range out of bounds");
+    std::vector<tt_mesh_data> saved(c->host.mesh.begin() + first, c->host.mesh.begin() + first + count);
+    std::copy(md, md + count, c->host.mesh.begin() + first);
+    Validator v(c->host);
+    if (!v.run()) {
+        std::copy(saved.begin(), saved.end(), c->host.mesh.begin() + first);
+        return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: %s", v.why.c_str());
+    }
+    std::vector<MeshGpu> mg(count);
+    for (uint32_t i = 0; i < count; i++) derive_mesh(md[i], mg[i]);
+    TT_HIP(c, hipSetDevice(c->device));
+    TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, md, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
+    TT_HIP(c, hipMemcpyAsync(c->mesh.p + first, mg.data(), sizeof(MeshGpu) * count, hipMemcpyHostToDevice, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_scene_bytes(const tt_ctx* c, uint64_t* bytes) {
+    if (!c || !bytes) return TT_ERR_INVALID_ARG;
+    *bytes = c->nodes.n * sizeof(tt_cwbvh_node) + c->tris_raw.n * sizeof(tt_cuda_triangle) + c->tris.n * sizeof(TriPos) +
+             c->tlas.n * 4 + c->mesh_raw.n * sizeof(tt_mesh_data) + c->mesh.n * sizeof(MeshGpu) + c->mat_tag.n * 4;
+    return TT_OK;
+}
+
+tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
+                           const tt_col_data* colors, tt_stats* stats) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or rays");
+    if (p->screen_width == 0 || p->screen_height == 0) return fail(c, TT_ERR_INVALID_ARG, "zero screen size");
+    if (p->bounce < 0) return fail(c, TT_ERR_INVALID_ARG, "negative bounce");
+    if (info && p->bounce > 0 && !colors)
+        return fail(c, TT_ERR_INVALID_ARG, "GlobalColors required for _PrimaryTriangleInfo at bounce > 0");
+    const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
+    if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
+    const uint32_t off = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u;
+    if ((uint64_t)off + p->n_rays > 0xffffffffull) return fail(c, TT_ERR_INVALID_ARG, "ray range overflows");
+    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    const bool async = dev && (p->flags & TT_TRACE_ASYNC);
+    const bool want_stats = (p->flags & TT_TRACE_STATS) != 0;
+    const int info_mode = info ? (p->bounce == 0 ? 1 : 2) : 0;
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (p->n_rays == 0) return TT_OK;
+    if (reinterpret_cast<uintptr_t>(rays) % 16 || (info && reinterpret_cast<uintptr_t>(info) % 16))
+        return fail(c, TT_ERR_INVALID_ARG, "GlobalRays / _PrimaryTriangleInfo must be 16-byte aligned");
+    TT_HIP(c, hipSetDevice(c->device));
+
+    tt_ray_data* d_rays = rays;
+    uint32_t* d_info = info;
+    const tt_col_data* d_colors = colors;
+    const size_t ray_end = (size_t)off + p->n_rays;
+    if (dev) {
+        if (!is_device_ptr(rays)) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but rays is not device memory");
+    } else {
+        if (c->st_rays.n < ray_end) TT_HIP(c, c->st_rays.alloc(ray_end));
+        d_rays = c->st_rays.p;
+        TT_HIP(c, hipMemcpyAsync(d_rays + off, rays + off, sizeof(tt_ray_data) * p->n_rays, hipMemcpyHostToDevice, c->stream));
+        if (info) {
+            if (c->st_info.n < wh * 4) TT_HIP(c, c->st_info.alloc(wh * 4));
+            d_info = c->st_info.p;
+            TT_HIP(c, hipMemcpyAsync(d_info, info, sizeof(uint32_t) * 4 * wh, hipMemcpyHostToDevice, c->stream));
+        }
+        if (info && p->bounce > 0) {
+            if (c->st_colors.n < wh) TT_HIP(c, c->st_colors.alloc(wh));
+            TT_HIP(c, hipMemcpyAsync(c->st_colors.p, colors, sizeof(tt_col_data) * wh, hipMemcpyHostToDevice, c->stream));
+            d_colors = c->st_colors.p;
+        }
+    }
+    TraceArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
+    a.tris = c->tris.p;
+    a.tlas = c->tlas.p;
+    a.mesh = c->mesh.p;
+    a.mat_tag = c->mat_tag.p;
+    a.rays = d_rays;
+    a.info = d_info;
+    a.colors = d_colors;
+    a.ctl = c->ctl;
+    a.n_rays = p->n_rays;
+    a.ray_offset = off;
+    a.width = p->screen_width;
+    a.height = p->screen_height;
+    a.far_plane = p->far_plane;
+    a.bounce = p->bounce;
+    a.flags = p->flags;
+    a.tile_swizzle = (p->n_rays == wh && p->screen_width % 8 == 0 && p->screen_height % 8 == 0) ? 1u : 0u;
+    const bool matcheck = c->any_invisible && p->bounce == 0;
+    const uint32_t waves_needed = (p->n_rays + 255u) / 256u;  // one TT_CHUNK per wave at least
+    const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
+    const uint32_t grid = std::max(1u, std::min(c->grid, blocks_needed));
+    TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
+    TT_HIP(c, hipEventRecord(c->ev0, c->stream));
+    TT_HIP(c, tt_launch_trace(a, want_stats, matcheck, info_mode, grid, c->stream));
+    TT_HIP(c, hipEventRecord(c->ev1, c->stream));
+    if (async) return TT_OK;
+    TraceControl ctl;
+    TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
+    if (!dev) {
+        TT_HIP(c, hipMemcpyAsync(rays + off, d_rays + off, sizeof(tt_ray_data) * p->n_rays, hipMemcpyDeviceToHost, c->stream));
+        if (info) TT_HIP(c, hipMemcpyAsync(info, d_info, sizeof(uint32_t) * 4 * wh, hipMemcpyDeviceToHost, c->stream));
+    }
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    float ms = 0.0f;
+    TT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (stats) {
+        stats->kernel_ms = ms;
+        if (want_stats) {
+            stats->rays = ctl.stats[0];
+            stats->node_visits = ctl.stats[1];
+            stats->tri_tests = ctl.stats[2];
+            stats->blas_entries = ctl.stats[3];
+            stats->hits = ctl.stats[4];
+            stats->reps_exhausted = ctl.stats[5];
+            stats->stack_overflows = ctl.stats[6];
+        }
+        stats->stack_overflows = std::max<uint64_t>(stats->stack_overflows, ctl.err_overflow);
+    }
+    if (ctl.err_overflow)
+        return fail(c, TT_ERR_STACK_OVERFLOW, "%u rays needed more than %d traversal stack entries", ctl.err_overflow,
+                    TT_STACK_SIZE);
+    return TT_OK;
+}
+
+tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_data* rays, float* normals6) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!p || !rays || !normals6) return fail(c, TT_ERR_INVALID_ARG, "null argument");
+    const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
+    const uint32_t off = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u;
+    if (p->n_rays == 0) return TT_OK;
+    TT_HIP(c, hipSetDevice(c->device));
+    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    const tt_ray_data* d_rays = rays;
+    float* d_out = normals6;
+    if (!dev) {
+        const size_t ray_end = (size_t)off + p->n_rays;
+        if (c->st_rays.n < ray_end) TT_HIP(c, c->st_rays.alloc(ray_end));
+        TT_HIP(c, hipMemcpyAsync(c->st_rays.p + off, rays + off, sizeof(tt_ray_data) * p->n_rays, hipMemcpyHostToDevice, c->stream));
+        d_rays = c->st_rays.p;
+        if (c->st_normals.n < (size_t)6 * p->n_rays) TT_HIP(c, c->st_normals.alloc((size_t)6 * p->n_rays));
+        d_out = c->st_normals.p;
+    }
+    TT_HIP(c, tt_launch_resolve(d_rays, off, p->n_rays, p->far_plane, c->tris_raw.p, (uint32_t)c->tris_raw.n,
+                                c->mesh_raw.p, (uint32_t)c->mesh_raw.n, d_out, c->stream));
+    if (!dev) TT_HIP(c, hipMemcpyAsync(normals6, d_out, sizeof(float) * 6 * p->n_rays, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!cam || !rays || !cam->width || !cam->height) return fail(c, TT_ERR_INVALID_ARG, "bad camera or rays");
+    const uint64_t wh = (uint64_t)cam->width * cam->height;
+    if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
+    TT_HIP(c, hipSetDevice(c->device));
+    if (c->cam.n < 32) TT_HIP(c, c->cam.alloc(32));
+    float m[32];
+    std::memcpy(m, cam->cam_to_world, 64);
+    std::memcpy(m + 16, cam->cam_inv_proj, 64);
+    TT_HIP(c, hipMemcpyAsync(c->cam.p, m, sizeof(m), hipMemcpyHostToDevice, c->stream));
+    const bool dev = (cam->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    tt_ray_data* d = rays;
+    if (!dev) {
+        if (c->st_rays.n < wh) TT_HIP(c, c->st_rays.alloc(wh));
+        d = c->st_rays.p;
+    } else if (!is_device_ptr(rays)) {
+        return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but rays is not device memory");
+    }
+    TT_HIP(c, tt_launch_generate(c->cam.p, c->cam.p + 16, cam->width, cam->height, cam->near_plane, cam->far_plane,
+                                 cam->jitter, cam->frames_accumulated, cam->max_bounce, d, c->stream));
+    if (!dev) TT_HIP(c, hipMemcpyAsync(rays, d, sizeof(tt_ray_data) * wh, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, int32_t frames,
+                                    int32_t max_bounce, uint32_t* n_next) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!p || !rays || !n_next) return fail(c, TT_ERR_INVALID_ARG, "null argument");
+    const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
+    if (!wh || wh > 0x7fffffffull || p->n_rays > wh) return fail(c, TT_ERR_INVALID_ARG, "bad ray count / screen");
+    const uint32_t src = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u, dst = (p->bounce % 2 == 1) ? 0u : (uint32_t)wh;
+    TT_HIP(c, hipSetDevice(c->device));
+    if (c->counter.n < 4) TT_HIP(c, c->counter.alloc(4));
+    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    tt_ray_data* d = rays;
+    if (!dev) {
+        if (c->st_rays.n < 2 * wh) {
+            // keep nothing: the host copy is the source of truth for host-pointer calls
+            TT_HIP(c, c->st_rays.alloc(2 * wh));
+        }
+        d = c->st_rays.p;
+        TT_HIP(c, hipMemcpyAsync(d + src, rays + src, sizeof(tt_ray_data) * p->n_rays, hipMemcpyHostToDevice, c->stream));
+    }
+    TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 16, c->stream));
+    TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
+                               c->mesh_raw.p, c->counter.p, c->stream));
+    uint32_t cnt = 0;
+    TT_HIP(c, hipMemcpyAsync(&cnt, c->counter.p, 4, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    if (!dev && cnt) {
+        TT_HIP(c, hipMemcpy(rays + dst, d + dst, sizeof(tt_ray_data) * cnt, hipMemcpyDeviceToHost));
+    }
+    *n_next = cnt;
+    return TT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// tt_device.h — device-side layouts derived at tt_scene_upload from the reference buffers,
+// and the launch-argument blocks shared by tt_trace.hip and tt_api.cpp.
+#ifndef TT_DEVICE_H
+#define TT_DEVICE_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/truetrace_hip.h"
+
+// Traversal-layout triangle, 48 B: the 36 B of positions the Moller-Trumbore test reads
+// (CudaTriangle pos0/posedge1/posedge2, CommonData.cginc:63-66) + MatDat, padded so one
+// triangle is three 16-B loads. Built from AggTris at upload; AggTris itself also stays in
+// HBM for the attribute resolve.
+struct TriPos {
+    float p0x, p0y, p0z, e1x;
+    float e1y, e1z, e2x, e2y;
+    float e2z;
+    uint32_t matdat;
+    uint32_t pad0, pad1;
+};
+static_assert(sizeof(TriPos) == 48, "TriPos is 48 bytes");
+
+// Traversal-layout mesh record, 64 B: W2L rows 0-2 (row-major, 12 floats) + the four offsets
+// IntersectBVH reads on a TLAS->BLAS switch (IntersectionKernels.compute:197-213).
+struct MeshGpu {
+    float m[12];      // m[r*4+c] = W2L(r, c)
+    int32_t TriOffset;
+    int32_t NodeOffset;
+    int32_t MaterialOffset;
+    int32_t root;     // mesh_data_bvh_offsets & 0x7fffffff
+};
+static_assert(sizeof(MeshGpu) == 64, "MeshGpu is 64 bytes");
+
+// Control block, zeroed by hipMemsetAsync before every trace launch.
+struct TraceControl {
+    uint32_t next_ray;        // work counter (chunks of rays)
+    uint32_t err_overflow;    // rays that overflowed the 16-entry stack
+    uint32_t err_unsupported; // cutout material reached (never with a validated scene)
+    uint32_t pad;
+    unsigned long long stats[8];  // rays, nodes, tris, blas, hits, reps_exhausted, overflow, accepts
+};
+
+struct TraceArgs {
+    const uint4* nodes;          // 80 B nodes as 5 x uint4
+    const TriPos* tris;          // traversal-layout triangles
+    const int32_t* tlas;         // TLASBVH8Indices
+    const MeshGpu* mesh;         // traversal-layout mesh records
+    const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
+    tt_ray_data* rays;           // GlobalRays
+    uint32_t* info;              // _PrimaryTriangleInfo (uint4 per pixel), nullable
+    const tt_col_data* colors;   // GlobalColors (bounce > 0 with info)
+    TraceControl* ctl;
+    uint32_t n_rays;
+    uint32_t ray_offset;         // W*H on odd bounces
+    uint32_t width, height;
+    float far_plane;
+    int32_t bounce;
+    uint32_t flags;              // TT_TRACE_*
+    uint32_t tile_swizzle;       // 1: work index -> 8x8 screen tiles (n_rays == W*H, W,H % 8 == 0)
+};
+
+#endif

@@ -1,0 +1,440 @@
+// tt_trace.hip — gfx950 closest-hit CWBVH8 traversal (replaces kernel_trace,
+// TrueTrace/Resources/MainCompute/IntersectionKernels.compute:60-260).
+//
+// Design (MI355X-first, not a translation of the HLSL dispatch):
+//  * persistent waves: grid = CUs x resident blocks; every wave owns a private pool of rays
+//    fetched CHUNK at a time with ONE atomic (the reference pops one ray per thread from a
+//    single globally-coherent counter, IntersectionKernels.compute:79-81);
+//  * lanes that finish are refilled in place (ballot + mbcnt prefix over idle lanes) so the
+//    64-wide wave keeps working instead of idling behind its slowest ray;
+//  * the 16-entry uint2 traversal stack lives in LDS, [entry][thread] so a wave's 64 stack
+//    accesses hit 64 distinct banks (ds_read_b64/ds_write_b64, conflict-free);
+//  * 80-B nodes are five 16-B loads; triangles use a 48-B traversal layout (three 16-B loads)
+//    derived from AggTris at upload;
+//  * the per-ray visit order, the culling distance and the strict t < best.t acceptance are
+//    exactly the reference's, so t / primID / instID are bit-identical to the oracle.
+// Numerics follow include/truetrace_hip.h (compiled with -ffp-contract=off).
+#include "tt_device.h"
+
+#define TT_WAVE 64
+#define TT_BLOCK 256
+#define TT_CHUNK 256
+#ifndef TT_REFILL_MIN
+#define TT_REFILL_MIN 16
+#endif
+
+namespace {
+
+struct LaneRay {
+    float ox, oy, oz, dx, dy, dz, ix, iy, iz;
+};
+
+__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ uint32_t firstbithigh(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+
+// ray_get_octant_inv4 — CommonData.cginc:635-640
+__device__ __forceinline__ uint32_t octant_inv4(const LaneRay& r) {
+    return (r.dx < 0.0f ? 0u : 0x04040404u) | (r.dy < 0.0f ? 0u : 0x02020202u) |
+           (r.dz < 0.0f ? 0u : 0x01010101u);
+}
+
+// cwbvh_node_intersect — CommonData.cginc:641-707
+__device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n1, const uint4 n2,
+                                                   const uint4 n3, const uint4 n4, const LaneRay& r,
+                                                   uint32_t oct_inv4, float max_distance) {
+    const uint32_t w = n0.w;
+    const float adjx = __uint_as_float((w & 0xffu) << 23) * r.ix;
+    const float adjy = __uint_as_float(((w >> 8) & 0xffu) << 23) * r.iy;
+    const float adjz = __uint_as_float(((w >> 16) & 0xffu) << 23) * r.iz;
+    const float orgx = r.ix * (__uint_as_float(n0.x) - r.ox);
+    const float orgy = r.iy * (__uint_as_float(n0.y) - r.oy);
+    const float orgz = r.iz * (__uint_as_float(n0.z) - r.oz);
+    const bool nx = r.dx < 0.0f, ny = r.dy < 0.0f, nz = r.dz < 0.0f;
+    uint32_t hit_mask = 0;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const uint32_t meta4 = i == 0 ? n1.z : n1.w;
+        const uint32_t is_inner4 = (meta4 & (meta4 << 1)) & 0x10101010u;
+        const uint32_t inner_mask4 = (((is_inner4 << 3) >> 7) & 0x01010101u) * 0xffu;
+        const uint32_t bit_index4 = (meta4 ^ (oct_inv4 & inner_mask4)) & 0x1f1f1f1fu;
+        const uint32_t child_bits4 = (meta4 >> 5) & 0x07070707u;
+        const uint32_t qlx = i == 0 ? n2.x : n2.y, qhx = i == 0 ? n2.z : n2.w;
+        const uint32_t qly = i == 0 ? n3.x : n3.y, qhy = i == 0 ? n3.z : n3.w;
+        const uint32_t qlz = i == 0 ? n4.x : n4.y, qhz = i == 0 ? n4.z : n4.w;
+        const uint32_t x_min = nx ? qhx : qlx, x_max = nx ? qlx : qhx;
+        const uint32_t y_min = ny ? qhy : qly, y_max = ny ? qly : qhy;
+        const uint32_t z_min = nz ? qhz : qlz, z_max = nz ? qlz : qhz;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const float tminx = fma_((float)((x_min >> (j * 8)) & 0xffu), adjx, orgx);
+            const float tminy = fma_((float)((y_min >> (j * 8)) & 0xffu), adjy, orgy);
+            const float tminz = fma_((float)((z_min >> (j * 8)) & 0xffu), adjz, orgz);
+            const float tmaxx = fma_((float)((x_max >> (j * 8)) & 0xffu), adjx, orgx);
+            const float tmaxy = fma_((float)((y_max >> (j * 8)) & 0xffu), adjy, orgy);
+            const float tmaxz = fma_((float)((z_max >> (j * 8)) & 0xffu), adjz, orgz);
+            const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
+            const float tmax = fminf(fminf(tmaxx, tmaxy), fminf(tmaxz, max_distance));
+            const uint32_t bits = ((child_bits4 >> (j * 8)) & 0xffu) << ((bit_index4 >> (j * 8)) & 0xffu);
+            hit_mask |= (tmin < tmax) ? bits : 0u;
+        }
+    }
+    return hit_mask;
+}
+
+struct Best {
+    float t, u, v;
+    int32_t mesh_id, tri_id;
+};
+
+// IntersectTriangle — IntersectionKernels.compute:14-57 (Moller-Trumbore on pos0/edges).
+// Evaluated branch-free; the accept predicate is exactly the reference's nested conditions.
+template <bool MATCHECK>
+__device__ __forceinline__ bool intersect_triangle(const TriPos* __restrict__ tris, const uint32_t* __restrict__ mat_tag,
+                                                   int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
+                                                   const LaneRay& r, Best& best) {
+    const uint4* tp = reinterpret_cast<const uint4*>(tris + tri_id);
+    const uint4 a = tp[0], b = tp[1], c = tp[2];
+    const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
+    const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
+    const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);
+    // h = cross(d, e2); a = dot(e1, h)
+    const float hx = fma_(r.dy, e2z, -(r.dz * e2y));
+    const float hy = fma_(r.dz, e2x, -(r.dx * e2z));
+    const float hz = fma_(r.dx, e2y, -(r.dy * e2x));
+    const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
+    const float f = 1.0f / aa;
+    const float sx = r.ox - p0x, sy = r.oy - p0y, sz = r.oz - p0z;
+    const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
+    // q = cross(s, e1)
+    const float qx = fma_(sy, e1z, -(sz * e1y));
+    const float qy = fma_(sz, e1x, -(sx * e1z));
+    const float qz = fma_(sx, e1y, -(sy * e1x));
+    const float v = f * fma_(r.dz, qz, fma_(r.dy, qy, r.dx * qx));
+    const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
+    bool accept = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best.t);
+    if (MATCHECK && accept) {
+        // GetFlag(_Materials[MatOffset + MatDat].Tag, Invisible) at CurBounce == 0 (:48)
+        const uint32_t tag = mat_tag[mat_offset + (int32_t)c.y];
+        if ((tag >> TT_FLAG_INVISIBLE) & 1u) accept = false;
+    }
+    if (accept) {
+        best.t = t;
+        best.u = u;
+        best.v = v;
+        best.mesh_id = mesh_id;
+        best.tri_id = tri_id;
+    }
+    return accept;
+}
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, TT_WAVE);
+    return v;
+}
+
+}  // namespace
+
+// INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
+template <bool STATS, bool MATCHECK, int INFO>
+__global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
+    __shared__ uint2 s_stack[TT_STACK_SIZE][TT_BLOCK];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & (TT_WAVE - 1);
+
+    // wave-uniform ray pool
+    uint32_t pool_next = 0, pool_end = 0;
+    bool exhausted = false;
+
+    // lane traversal state (IntersectionKernels.compute:62-77)
+    bool active = false;
+    uint32_t ray_index = 0;
+    LaneRay ray{}, wray{};
+    Best best{};
+    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
+    uint32_t oct = 0;
+    int32_t stack_size = 0, tlas_ss = -1;
+    int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
+    uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
+
+    while (true) {
+        // ---------------------------------------------------------------- refill
+        const uint64_t idle = __ballot(!active);
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        const bool pool_dry = exhausted && pool_next >= pool_end;
+        if (n_idle == TT_WAVE && pool_dry) break;
+        if (n_idle >= TT_REFILL_MIN && !pool_dry) {
+            const uint32_t avail = pool_end - pool_next;
+            uint32_t new_base = 0, new_count = 0;
+            if (avail < n_idle && !exhausted) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(&A.ctl->next_ray, (uint32_t)TT_CHUNK);
+                new_base = __builtin_amdgcn_readfirstlane(b);
+                if (new_base < A.n_rays) new_count = min((uint32_t)TT_CHUNK, A.n_rays - new_base);
+                if (new_base + (uint32_t)TT_CHUNK >= A.n_rays) exhausted = true;
+            }
+            const uint32_t take_old = min(avail, n_idle);
+            const uint32_t take_new = min(n_idle - take_old, new_count);
+            const uint32_t rank = lane_prefix(idle);
+            uint32_t widx = 0xffffffffu;
+            if (rank < take_old) widx = pool_next + rank;
+            else if (rank - take_old < take_new) widx = new_base + (rank - take_old);
+            if (new_count > 0) {  // the old pool was fully consumed (avail < n_idle)
+                pool_next = new_base + take_new;
+                pool_end = new_base + new_count;
+            } else {
+                pool_next += take_old;
+            }
+            if (!active && widx != 0xffffffffu) {
+                // work index -> ray index (8x8 screen tiles for full-frame primary batches)
+                uint32_t local = widx;
+                if (A.tile_swizzle) {
+                    const uint32_t tw = A.width >> 3;
+                    const uint32_t t = widx >> 6, l = widx & 63u;
+                    const uint32_t ty = t / tw, tx = t - ty * tw;
+                    local = (ty * 8u + (l >> 3)) * A.width + tx * 8u + (l & 7u);
+                }
+                ray_index = A.ray_offset + local;
+                const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
+                const uint4 r0 = rp[0], r1 = rp[1];
+                ray.ox = __uint_as_float(r0.x);
+                ray.oy = __uint_as_float(r0.y);
+                ray.oz = __uint_as_float(r0.z);
+                ray.dx = __uint_as_float(r1.x);
+                ray.dy = __uint_as_float(r1.y);
+                ray.dz = __uint_as_float(r1.z);
+                ray.ix = 1.0f / ray.dx;
+                ray.iy = 1.0f / ray.dy;
+                ray.iz = 1.0f / ray.dz;
+                wray = ray;
+                oct = octant_inv4(ray);
+                best.t = A.far_plane;
+                best.u = 0.0f;
+                best.v = 0.0f;
+                best.mesh_id = 0;
+                best.tri_id = -1;
+                cg = make_uint2(0u, 0x80000000u);
+                tg = make_uint2(0u, 0u);
+                stack_size = 0;
+                tlas_ss = -1;
+                NodeOffset = 0;
+                TriOffset = 0;
+                MatOffset = 0;
+                mesh_id = -1;
+                Reps = 0;
+                active = true;
+                if (STATS) c_rays++;
+            }
+        }
+
+        // ------------------------------------------------------------- node phase
+        bool finish = false;
+        if (active && tg.y == 0u) {
+            if (Reps >= TT_MAX_REPS) {
+                active = false;  // loop bound hit: the reference writes nothing
+                if (STATS) c_reps++;
+            } else {
+                if (cg.y & 0xff000000u) {  // IntersectionKernels.compute:157-187
+                    const uint32_t cio = firstbithigh(cg.y);
+                    const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
+                    const uint32_t rel = __builtin_popcount(cg.y & ~(0xffffffffu << slot));
+                    const uint32_t child = cg.x + rel;
+                    cg.y &= ~(1u << cio);
+                    bool ok = true;
+                    if (cg.y & 0xff000000u) {
+                        if (stack_size == TT_STACK_SIZE) ok = false;
+                        else s_stack[stack_size++][tid] = cg;
+                    }
+                    if (ok) {
+                        const uint4* np = A.nodes + (size_t)child * 5u;
+                        const uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
+                        const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
+                        cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
+                        tg.y = hitmask & 0x00ffffffu;
+                        cg.x = n1.x + (uint32_t)NodeOffset;
+                        tg.x = n1.y + (uint32_t)TriOffset;
+                        Reps++;
+                        if (STATS) c_nodes++;
+                    } else {
+                        active = false;
+                        tg.y = 0u;
+                        if (STATS) c_ovf++;
+                        atomicAdd(&A.ctl->err_overflow, 1u);
+                    }
+                } else {  // :188-191
+                    tg = cg;
+                    cg = make_uint2(0u, 0u);
+                }
+                if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
+                    const uint32_t mo = firstbithigh(tg.y);
+                    tg.y &= ~(1u << mo);
+                    mesh_id = A.tlas[tg.x + mo];
+                    const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                    const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
+                    const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                    NodeOffset = mo4.y;
+                    TriOffset = mo4.x;
+                    bool ok = true;
+                    if (tg.y != 0u) {
+                        if (stack_size == TT_STACK_SIZE) ok = false;
+                        else s_stack[stack_size++][tid] = tg;
+                    }
+                    if (ok && (cg.y & 0xff000000u)) {
+                        if (stack_size == TT_STACK_SIZE) ok = false;
+                        else s_stack[stack_size++][tid] = cg;
+                    }
+                    if (ok) {
+                        tlas_ss = stack_size;
+                        MatOffset = mo4.z;
+                        LaneRay nr;
+                        nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
+                        nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
+                        nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
+                        nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
+                        nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
+                        nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
+                        nr.ix = 1.0f / nr.dx;
+                        nr.iy = 1.0f / nr.dy;
+                        nr.iz = 1.0f / nr.dz;
+                        ray = nr;
+                        oct = octant_inv4(ray);
+                        cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                        if (STATS) c_blas++;
+                    } else {
+                        active = false;
+                        if (STATS) c_ovf++;
+                        atomicAdd(&A.ctl->err_overflow, 1u);
+                    }
+                    tg.y = 0u;
+                }
+                // :228-251 pop / finish when no leaf triangles are pending
+                if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+                    if (stack_size == 0) {
+                        finish = true;
+                    } else {
+                        if (stack_size == tlas_ss) {
+                            NodeOffset = 0;
+                            TriOffset = 0;
+                            tlas_ss = -1;
+                            ray = wray;
+                            oct = octant_inv4(ray);
+                        }
+                        cg = s_stack[--stack_size][tid];
+                    }
+                }
+            }
+        }
+
+        // --------------------------------------------------------- triangle phase
+        if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
+            const uint32_t ti = firstbithigh(tg.y);
+            tg.y &= ~(1u << ti);
+            const bool acc = intersect_triangle<MATCHECK>(A.tris, A.mat_tag, (int32_t)(tg.x + ti), mesh_id,
+                                                          MatOffset, ray, best);
+            if (STATS) {
+                c_tris++;
+                c_acc += acc ? 1u : 0u;
+            }
+            if (tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+                if (stack_size == 0) {
+                    finish = true;
+                } else {
+                    if (stack_size == tlas_ss) {
+                        NodeOffset = 0;
+                        TriOffset = 0;
+                        tlas_ss = -1;
+                        ray = wray;
+                        oct = octant_inv4(ray);
+                    }
+                    cg = s_stack[--stack_size][tid];
+                }
+            }
+        }
+
+        // ------------------------------------------------------------------ finish
+        if (finish) {  // :229-241 + set() CommonData.cginc:430-434
+            tt_ray_data* R = A.rays + ray_index;
+            if (INFO != 0) {
+                const uint32_t pix = R->PixelIndex;
+                const uint32_t tx = pix % A.width, ty = pix / A.width;
+                if (ty < A.height) {
+                    uint4 o;
+                    bool write = false;
+                    if (INFO == 1) {
+                        const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                        o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to), __float_as_uint(best.u),
+                                       __float_as_uint(best.v));
+                        write = true;
+                    } else {
+                        const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
+                        if (w == -1.0f || (float)A.bounce == w) {
+                            write = true;
+                            const bool miss = best.t == A.far_plane;
+                            if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
+                                const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                                o.x = (uint32_t)best.mesh_id;
+                                o.y = (uint32_t)(best.tri_id - to);
+                                o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                            } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
+                                o.x = __float_as_uint(wray.dx);
+                                o.y = __float_as_uint(wray.dy);
+                                o.z = __float_as_uint(wray.dz);
+                            } else {
+                                o.x = __float_as_uint(wray.dx * best.t + wray.ox);
+                                o.y = __float_as_uint(wray.dy * best.t + wray.oy);
+                                o.z = __float_as_uint(wray.dz * best.t + wray.oz);
+                            }
+                            o.w = miss ? 1u : 0u;
+                        }
+                    }
+                    if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+                }
+            }
+            const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+            reinterpret_cast<uint4*>(R)[2] =
+                make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+            if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
+            active = false;
+        }
+    }
+
+    if (STATS) {
+        const uint32_t v[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
+                               wave_sum(c_hits), wave_sum(c_reps), wave_sum(c_ovf), wave_sum(c_acc)};
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (v[k]) atomicAdd(&A.ctl->stats[k], (unsigned long long)v[k]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+template <bool S, bool M, int I>
+static hipError_t launch_one(const TraceArgs& a, uint32_t grid, hipStream_t st) {
+    hipLaunchKernelGGL((tt_trace_kernel<S, M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+    return hipGetLastError();
+}
+
+template <bool S, bool M>
+static hipError_t launch_info(const TraceArgs& a, int info, uint32_t grid, hipStream_t st) {
+    if (info == 0) return launch_one<S, M, 0>(a, grid, st);
+    if (info == 1) return launch_one<S, M, 1>(a, grid, st);
+    return launch_one<S, M, 2>(a, grid, st);
+}
+
+hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid,
+                           hipStream_t st) {
+    if (stats) return matcheck ? launch_info<true, true>(a, info, grid, st) : launch_info<true, false>(a, info, grid, st);
+    return matcheck ? launch_info<false, true>(a, info, grid, st) : launch_info<false, false>(a, info, grid, st);
+}
+
+hipError_t tt_trace_occupancy(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, tt_trace_kernel<false, false, 1>, TT_BLOCK, 0);
+}
+
+uint32_t tt_trace_block_size() { return TT_BLOCK; }

@@ -1,0 +1,566 @@
+"""tthip — Python (ctypes) view of the C ABI in include/truetrace_hip.h and
+include/truetrace_scene.h.
+
+The product is the C-ABI library ``lib/libtruetrace_hip.so`` (gfx950 kernels); this module is
+thin plumbing so tests and bench.py can drive it. It never falls back to a CPU path: if the
+HIP library is missing or no GPU is visible, the trace entry points raise.
+
+Names mirror the reference dispatch surface:
+  * ``AssetManager`` — owns the aggregated buffers (AssetManager.cs:75-88 SetMeshTraceBuffers,
+    :986-1227 AccumulateData, :1610-1766 UpdateTLAS) and uploads them (tt_scene_upload);
+  * ``Engine.trace`` — one ``kernel_trace`` dispatch (RayTracingMaster.cs:964-970).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+
+# ---------------------------------------------------------------- status codes
+TT_OK = 0
+TT_ERR_INVALID_ARG = 1
+TT_ERR_OOM = 2
+TT_ERR_HIP = 3
+TT_ERR_UNSUPPORTED = 4
+TT_ERR_STACK_OVERFLOW = 5
+TT_ERR_NO_DEVICE = 6
+TT_ERR_NO_SCENE = 7
+STATUS_NAMES = {0: "TT_OK", 1: "TT_ERR_INVALID_ARG", 2: "TT_ERR_OOM", 3: "TT_ERR_HIP", 4: "TT_ERR_UNSUPPORTED",
+                5: "TT_ERR_STACK_OVERFLOW", 6: "TT_ERR_NO_DEVICE", 7: "TT_ERR_NO_SCENE"}
+
+TT_TRACE_DEVICE_PTRS = 1 << 0
+TT_TRACE_USE_RESTIRGI = 1 << 1
+TT_TRACE_USE_ASVGF = 1 << 2
+TT_TRACE_STATS = 1 << 3
+TT_TRACE_ASYNC = 1 << 4
+TT_STACK_SIZE = 16
+TT_MAX_REPS = 1000
+
+# ---------------------------------------------------------------- numpy layouts
+NODE_DTYPE = np.dtype([("p", "<f4", 3), ("e_imask", "<u4"), ("base_child", "<u4"), ("base_tri", "<u4"),
+                       ("meta", "<u4", 2), ("qlo_x", "<u4", 2), ("qhi_x", "<u4", 2), ("qlo_y", "<u4", 2),
+                       ("qhi_y", "<u4", 2), ("qlo_z", "<u4", 2), ("qhi_z", "<u4", 2)])
+TRI_DTYPE = np.dtype([("pos0", "<f4", 3), ("posedge1", "<f4", 3), ("posedge2", "<f4", 3), ("norms", "<u4", 3),
+                      ("tans", "<u4", 3), ("tex0", "<f4", 2), ("texedge1", "<f4", 2), ("texedge2", "<f4", 2),
+                      ("MatDat", "<u4")])
+MESH_DTYPE = np.dtype([("W2L", "<f4", 16), ("TriOffset", "<i4"), ("NodeOffset", "<i4"), ("MaterialOffset", "<i4"),
+                       ("mesh_data_bvh_offsets", "<i4"), ("LightTriCount", "<i4"), ("LightNodeOffset", "<i4")])
+MAT_DTYPE = np.dtype([("AlbedoTex", "<i4", 2), ("NormalTex", "<i4", 2), ("EmissiveTex", "<i4", 2),
+                      ("MetallicTex", "<i4", 2), ("RoughnessTex", "<i4", 2), ("AlphaTex", "<i4", 2),
+                      ("MatCapMask", "<i4", 2), ("MatCapTex", "<i4", 2), ("surfaceColor", "<f4", 3),
+                      ("emmissive", "<f4"), ("EmissionColor", "<f4", 3), ("Tag", "<u4"), ("roughness", "<f4"),
+                      ("MatType", "<i4"), ("transmittanceColor", "<f4", 3), ("ior", "<f4"), ("rest", "<f4", 12),
+                      ("AlbedoTexScale", "<f4", 4), ("MetallicRemap", "<f4", 2), ("RoughnessRemap", "<f4", 2),
+                      ("AlphaCutoff", "<f4"), ("tail", "<f4", 12)])
+RAY_DTYPE = np.dtype([("origin", "<f4", 3), ("PixelIndex", "<u4"), ("direction", "<f4", 3), ("last_pdf", "<f4"),
+                      ("hits", "<u4", 4)])
+COL_DTYPE = np.dtype([("throughput", "<f4", 3), ("Direct", "<f4", 3), ("Indirect", "<f4", 3),
+                      ("PrimaryNEERay", "<u4"), ("Flags", "<u4"), ("MetRoughIsSpec", "<u4"), ("Data", "<f4", 4)])
+for _dt, _sz in ((NODE_DTYPE, 80), (TRI_DTYPE, 88), (MESH_DTYPE, 88), (MAT_DTYPE, 252), (RAY_DTYPE, 48),
+                 (COL_DTYPE, 64)):
+    assert _dt.itemsize == _sz, (_dt, _sz)
+assert MAT_DTYPE.fields["Tag"][1] == 92 and MAT_DTYPE.fields["MatType"][1] == 100
+assert MAT_DTYPE.fields["AlbedoTexScale"][1] == 168 and MAT_DTYPE.fields["AlphaCutoff"][1] == 200
+
+MAT_CUTOUT_INDEX = 2
+FLAG_INVISIBLE = 7
+
+
+# ---------------------------------------------------------------- ctypes structs
+class TraceParams(C.Structure):
+    _fields_ = [("n_rays", C.c_uint32), ("bounce", C.c_int32), ("far_plane", C.c_float),
+                ("screen_width", C.c_uint32), ("screen_height", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("blas_entries", C.c_uint64), ("hits", C.c_uint64), ("reps_exhausted", C.c_uint64),
+                ("stack_overflows", C.c_uint64), ("kernel_ms", C.c_float), ("pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("max_rays", C.c_uint64), ("stream", C.c_void_p)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("cam_to_world", C.c_float * 16), ("cam_inv_proj", C.c_float * 16), ("near_plane", C.c_float),
+                ("far_plane", C.c_float), ("width", C.c_uint32), ("height", C.c_uint32), ("jitter", C.c_int32),
+                ("frames_accumulated", C.c_int32), ("max_bounce", C.c_int32), ("flags", C.c_uint32)]
+
+
+class MeshInput(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("n_vertices", C.c_uint32), ("normals", C.c_void_p),
+                ("tangents", C.c_void_p), ("uvs", C.c_void_p), ("indices", C.c_void_p), ("n_indices", C.c_uint32),
+                ("matdat", C.c_void_p), ("lossy_scale", C.c_float * 3)]
+
+
+class BlasInfo(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("n_tris", C.c_uint32), ("bvh2_depth", C.c_uint32),
+                ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("build_seconds", C.c_double)]
+
+
+class ParentDesc(C.Structure):
+    _fields_ = [("blas", C.c_void_p), ("local_to_world", C.c_float * 16), ("world_to_local", C.c_float * 16),
+                ("material_count", C.c_uint32)]
+
+
+class InstanceDesc(C.Structure):
+    _fields_ = [("instance_parent", C.c_uint32), ("local_to_world", C.c_float * 16),
+                ("world_to_local", C.c_float * 16)]
+
+
+class SceneBuildInfo(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("n_tris", C.c_uint32), ("n_tlas_indices", C.c_uint32),
+                ("n_mesh", C.c_uint32), ("tlas_nodes", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class TTError(RuntimeError):
+    def __init__(self, status: int, msg: str = ""):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"], "arrays passed to the C ABI must be contiguous"
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):  # torch tensor
+        return a.data_ptr()
+    return int(a)
+
+
+# ---------------------------------------------------------------- library loading
+_SCENE = None
+_HIP = None
+
+HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_destroy", "tt_last_error",
+               "tt_scene_upload", "tt_scene_update_nodes", "tt_scene_update_meshdata", "tt_scene_bytes",
+               "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
+               "tt_enqueue_diffuse_bounce"]
+SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
+                 "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
+                 "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
+                 "tt_synth_prop", "tt_synth_mesh_view", "tt_synth_mesh_free", "tt_synth_mesh_from_arrays"]
+
+
+def scene_lib():
+    global _SCENE
+    if _SCENE is None:
+        path = os.path.join(LIB_DIR, "libtruetrace_scene.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C truetrace-unity-pathtracer_amd` or __graft_entry__.build()")
+        L = C.CDLL(path)
+        vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int32
+        L.tt_blas_build.argtypes = [C.POINTER(MeshInput), C.POINTER(vp)]
+        L.tt_blas_get_info.argtypes = [vp, C.POINTER(BlasInfo)]
+        L.tt_blas_copy.argtypes = [vp, vp, vp]
+        L.tt_blas_free.argtypes = [vp]
+        L.tt_blas_free.restype = None
+        L.tt_scene_assemble.argtypes = [vp, u32, vp, u32, vp, u32, C.POINTER(vp)]
+        L.tt_scene_build_get_info.argtypes = [vp, C.POINTER(SceneBuildInfo)]
+        L.tt_scene_build_copy.argtypes = [vp, vp, vp, vp, vp]
+        L.tt_scene_build_free.argtypes = [vp]
+        L.tt_scene_build_free.restype = None
+        L.tt_pack_octahedral.argtypes = [C.c_float, C.c_float, C.c_float]
+        L.tt_pack_octahedral.restype = u32
+        L.tt_bvh2_build.argtypes = [vp, u32, vp, vp, vp, vp]
+        L.tt_dotnet_sort_by_key.argtypes = [vp, u32, vp]
+        L.tt_dotnet_sort_by_key.restype = None
+        L.tt_synth_cornell.argtypes = [C.POINTER(vp)]
+        L.tt_synth_soup.argtypes = [C.c_uint64, u32, C.c_float, C.c_float, C.POINTER(vp)]
+        L.tt_synth_sponza.argtypes = [C.c_uint64, u32, C.POINTER(vp)]
+        L.tt_synth_prop.argtypes = [C.c_uint64, u32, C.POINTER(vp)]
+        L.tt_synth_mesh_view.argtypes = [vp, C.POINTER(MeshInput)]
+        L.tt_synth_mesh_free.argtypes = [vp]
+        L.tt_synth_mesh_free.restype = None
+        L.tt_synth_mesh_from_arrays.argtypes = [vp, u32, vp, u32, vp]
+        L.tt_synth_mesh_from_arrays.restype = vp
+        for s in ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_scene_assemble", "tt_scene_build_get_info",
+                  "tt_scene_build_copy", "tt_bvh2_build", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
+                  "tt_synth_prop", "tt_synth_mesh_view"]:
+            getattr(L, s).restype = i32
+        _SCENE = L
+    return _SCENE
+
+
+def hip_lib():
+    """The gfx950 engine. Raises if the library was not built — there is no CPU fallback."""
+    global _HIP
+    if _HIP is None:
+        path = os.path.join(LIB_DIR, "libtruetrace_hip.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: the HIP engine was not built (no fallback exists)")
+        L = C.CDLL(path)
+        vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int32
+        L.tt_abi_version.restype = i32
+        L.tt_device_count.restype = i32
+        L.tt_ctx_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+        L.tt_ctx_destroy.argtypes = [vp]
+        L.tt_last_error.argtypes = [vp]
+        L.tt_last_error.restype = C.c_char_p
+        L.tt_scene_upload.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp, u32, vp, u32]
+        L.tt_scene_update_nodes.argtypes = [vp, u32, u32, vp]
+        L.tt_scene_update_meshdata.argtypes = [vp, u32, u32, vp]
+        L.tt_scene_bytes.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
+        L.tt_sync.argtypes = [vp]
+        L.tt_ctx_stream.argtypes = [vp]
+        L.tt_ctx_stream.restype = vp
+        L.tt_resolve_normals.argtypes = [vp, C.POINTER(TraceParams), vp, vp]
+        L.tt_generate_primary.argtypes = [vp, C.POINTER(Camera), vp]
+        L.tt_enqueue_diffuse_bounce.argtypes = [vp, C.POINTER(TraceParams), vp, i32, i32, C.POINTER(u32)]
+        for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
+                  "tt_scene_update_meshdata", "tt_scene_bytes", "tt_trace_closest", "tt_sync", "tt_resolve_normals",
+                  "tt_generate_primary", "tt_enqueue_diffuse_bounce"]:
+            getattr(L, s).restype = i32
+        _HIP = L
+    return _HIP
+
+
+# ---------------------------------------------------------------- matrices
+def trs_matrix(translation=(0, 0, 0), rotation_y_deg=0.0, scale=1.0) -> np.ndarray:
+    """4x4 localToWorld (row-major numpy, math convention) of a rigid + uniform scale transform."""
+    a = np.deg2rad(rotation_y_deg)
+    c, s = np.cos(a), np.sin(a)
+    m = np.eye(4)
+    m[:3, :3] = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]]) * scale
+    m[:3, 3] = translation
+    return m
+
+
+def unity_colmajor(m: np.ndarray) -> np.ndarray:
+    """Unity stores Matrix4x4 column-major: element (r, c) at [c*4 + r]."""
+    return np.asarray(m, dtype=np.float64).T.reshape(16).astype(np.float32)
+
+
+def unity_camera(position, forward, up, vfov_deg, width, height, near=0.3, far=1000.0):
+    """(cameraToWorldMatrix, projectionMatrix.inverse) as Unity computes them (OpenGL conventions:
+    camera looks down -z in camera space)."""
+    f = np.asarray(forward, np.float64)
+    f = f / np.linalg.norm(f)
+    r = np.cross(np.asarray(up, np.float64), f)  # Unity is left-handed: right = up x forward
+    r = r / np.linalg.norm(r)
+    u = np.cross(f, r)
+    l2w = np.eye(4)
+    l2w[:3, 0], l2w[:3, 1], l2w[:3, 2], l2w[:3, 3] = r, u, f, position
+    c2w = l2w @ np.diag([1.0, 1.0, -1.0, 1.0])
+    aspect = width / height
+    ft = 1.0 / np.tan(np.deg2rad(vfov_deg) / 2.0)
+    P = np.zeros((4, 4))
+    P[0, 0], P[1, 1] = ft / aspect, ft
+    P[2, 2], P[2, 3] = (far + near) / (near - far), 2 * far * near / (near - far)
+    P[3, 2] = -1.0
+    return c2w, np.linalg.inv(P)
+
+
+# ---------------------------------------------------------------- scene building
+class Mesh:
+    """A ParentObject's merged object-space mesh (owned by the scene library)."""
+
+    def __init__(self, handle: int):
+        self.h = handle
+
+    @staticmethod
+    def _check(st, what):
+        if st != TT_OK:
+            raise TTError(st, what)
+
+    @classmethod
+    def cornell(cls) -> "Mesh":
+        h = C.c_void_p()
+        cls._check(scene_lib().tt_synth_cornell(C.byref(h)), "tt_synth_cornell")
+        return cls(h.value)
+
+    @classmethod
+    def soup(cls, seed: int, n_tris: int, extent: float = 1.0, tri_size: float = 0.1) -> "Mesh":
+        h = C.c_void_p()
+        cls._check(scene_lib().tt_synth_soup(seed, n_tris, extent, tri_size, C.byref(h)), "tt_synth_soup")
+        return cls(h.value)
+
+    @classmethod
+    def sponza(cls, seed: int = 0x53504F4E, n_tris: int = 262267) -> "Mesh":
+        h = C.c_void_p()
+        cls._check(scene_lib().tt_synth_sponza(seed, n_tris, C.byref(h)), "tt_synth_sponza")
+        return cls(h.value)
+
+    @classmethod
+    def prop(cls, seed: int, n_tris: int) -> "Mesh":
+        h = C.c_void_p()
+        cls._check(scene_lib().tt_synth_prop(seed, n_tris, C.byref(h)), "tt_synth_prop")
+        return cls(h.value)
+
+    @classmethod
+    def from_arrays(cls, positions: np.ndarray, indices: np.ndarray, matdat: Optional[np.ndarray] = None) -> "Mesh":
+        pos = np.ascontiguousarray(positions, np.float32).reshape(-1)
+        idx = np.ascontiguousarray(indices, np.int32).reshape(-1)
+        md = None if matdat is None else np.ascontiguousarray(matdat, np.int32)
+        h = scene_lib().tt_synth_mesh_from_arrays(pos.ctypes.data, pos.size // 3, idx.ctypes.data, idx.size,
+                                                  None if md is None else md.ctypes.data)
+        if not h:
+            raise TTError(TT_ERR_OOM, "tt_synth_mesh_from_arrays")
+        return cls(h)
+
+    def view(self) -> MeshInput:
+        v = MeshInput()
+        self._check(scene_lib().tt_synth_mesh_view(self.h, C.byref(v)), "tt_synth_mesh_view")
+        return v
+
+    def __del__(self):
+        if getattr(self, "h", None) and _SCENE is not None:
+            _SCENE.tt_synth_mesh_free(self.h)
+            self.h = None
+
+
+class Blas:
+    """A built ParentObject: CWBVH8 nodes + leaf-ordered CudaTriangles (ParentObject.BuildTotal)."""
+
+    def __init__(self, mesh: Mesh, lossy_scale=(1.0, 1.0, 1.0)):
+        v = mesh.view()
+        v.lossy_scale[:] = lossy_scale
+        h = C.c_void_p()
+        st = scene_lib().tt_blas_build(C.byref(v), C.byref(h))
+        if st != TT_OK:
+            raise TTError(st, "tt_blas_build")
+        self.h = h.value
+        info = BlasInfo()
+        scene_lib().tt_blas_get_info(self.h, C.byref(info))
+        self.info = info
+
+    @property
+    def n_nodes(self):
+        return self.info.n_nodes
+
+    @property
+    def n_tris(self):
+        return self.info.n_tris
+
+    def arrays(self):
+        nodes = np.zeros(self.info.n_nodes, NODE_DTYPE)
+        tris = np.zeros(self.info.n_tris, TRI_DTYPE)
+        scene_lib().tt_blas_copy(self.h, nodes.ctypes.data, tris.ctypes.data)
+        return nodes, tris
+
+    def __del__(self):
+        if getattr(self, "h", None) and _SCENE is not None:
+            _SCENE.tt_blas_free(self.h)
+            self.h = None
+
+
+@dataclass
+class Scene:
+    """Aggregated trace buffers exactly as AssetManager.SetMeshTraceBuffers binds them."""
+    nodes: np.ndarray
+    tris: np.ndarray
+    tlas: np.ndarray
+    meshdata: np.ndarray
+    materials: np.ndarray
+    tlas_nodes: int = 0
+    meta: dict = field(default_factory=dict)
+
+    def save(self, path: str):
+        np.savez_compressed(path, nodes=self.nodes.view(np.uint8), tris=self.tris.view(np.uint8),
+                            tlas=self.tlas, meshdata=self.meshdata.view(np.uint8),
+                            materials=self.materials.view(np.uint8), tlas_nodes=np.int64(self.tlas_nodes))
+
+    @classmethod
+    def load(cls, path: str) -> "Scene":
+        z = np.load(path, allow_pickle=False)
+        return cls(nodes=z["nodes"].view(NODE_DTYPE).copy(), tris=z["tris"].view(TRI_DTYPE).copy(),
+                   tlas=z["tlas"].astype(np.int32), meshdata=z["meshdata"].view(MESH_DTYPE).copy(),
+                   materials=z["materials"].view(MAT_DTYPE).copy(), tlas_nodes=int(z["tlas_nodes"]))
+
+
+class AssetManager:
+    """Host mirror of the reference AssetManager's aggregation (AccumulateData + UpdateTLAS +
+    ConstructNewTLAS): RenderQue parents, InstanceData parents and InstancedObjects."""
+
+    def __init__(self):
+        self.parents: List = []          # (Blas, l2w 4x4, material_count)
+        self.instance_parents: List = []  # (Blas, material_count)
+        self.instances: List = []        # (instance_parent index, l2w 4x4)
+        self.materials: List[np.ndarray] = []
+
+    def add_parent(self, blas: Blas, local_to_world=None, materials: Optional[np.ndarray] = None):
+        mats = materials if materials is not None else np.zeros(1, MAT_DTYPE)
+        self.parents.append((blas, np.eye(4) if local_to_world is None else np.asarray(local_to_world), len(mats)))
+        self.materials.append(mats)
+
+    def add_instance_parent(self, blas: Blas, materials: Optional[np.ndarray] = None) -> int:
+        mats = materials if materials is not None else np.zeros(1, MAT_DTYPE)
+        self.instance_parents.append((blas, len(mats)))
+        self._ip_mats = getattr(self, "_ip_mats", [])
+        self._ip_mats.append(mats)
+        return len(self.instance_parents) - 1
+
+    def add_instance(self, parent_index: int, local_to_world):
+        self.instances.append((parent_index, np.asarray(local_to_world)))
+
+    def build(self) -> Scene:
+        P = (ParentDesc * max(1, len(self.parents)))()
+        for i, (b, l2w, nm) in enumerate(self.parents):
+            P[i].blas = b.h
+            P[i].local_to_world[:] = unity_colmajor(l2w)
+            P[i].world_to_local[:] = unity_colmajor(np.linalg.inv(l2w))
+            P[i].material_count = nm
+        IP = (ParentDesc * max(1, len(self.instance_parents)))()
+        for i, (b, nm) in enumerate(self.instance_parents):
+            IP[i].blas = b.h
+            IP[i].local_to_world[:] = unity_colmajor(np.eye(4))
+            IP[i].world_to_local[:] = unity_colmajor(np.eye(4))
+            IP[i].material_count = nm
+        I = (InstanceDesc * max(1, len(self.instances)))()
+        for i, (pi, l2w) in enumerate(self.instances):
+            I[i].instance_parent = pi
+            I[i].local_to_world[:] = unity_colmajor(l2w)
+            I[i].world_to_local[:] = unity_colmajor(np.linalg.inv(l2w))
+        h = C.c_void_p()
+        L = scene_lib()
+        st = L.tt_scene_assemble(C.addressof(P), len(self.parents), C.addressof(IP), len(self.instance_parents),
+                                 C.addressof(I), len(self.instances), C.byref(h))
+        if st != TT_OK:
+            raise TTError(st, "tt_scene_assemble")
+        try:
+            info = SceneBuildInfo()
+            L.tt_scene_build_get_info(h, C.byref(info))
+            nodes = np.zeros(info.n_nodes, NODE_DTYPE)
+            tris = np.zeros(info.n_tris, TRI_DTYPE)
+            tlas = np.zeros(info.n_tlas_indices, np.int32)
+            md = np.zeros(info.n_mesh, MESH_DTYPE)
+            L.tt_scene_build_copy(h, nodes.ctypes.data, tris.ctypes.data, tlas.ctypes.data, md.ctypes.data)
+        finally:
+            L.tt_scene_build_free(h)
+        mats = self.materials + getattr(self, "_ip_mats", [])
+        materials = np.concatenate(mats) if mats else np.zeros(1, MAT_DTYPE)
+        return Scene(nodes, tris, tlas, md, materials, tlas_nodes=info.tlas_nodes)
+
+
+def single_object_scene(mesh: Mesh, local_to_world=None, n_materials: int = 8) -> Scene:
+    am = AssetManager()
+    am.add_parent(Blas(mesh), local_to_world, np.zeros(n_materials, MAT_DTYPE))
+    return am.build()
+
+
+# ---------------------------------------------------------------- ray buffers
+def camera_rays_host(cam_to_world: np.ndarray, cam_inv_proj: np.ndarray, width: int, height: int,
+                     near: float, far: float) -> np.ndarray:
+    """Vectorised float32 restatement of Generate for tests without a GPU (pinned like the
+    kernel up to normalize's rounding; parity tests use rays from one source on both sides)."""
+    c2w = unity_colmajor(cam_to_world).reshape(4, 4).T.astype(np.float32)
+    ip = unity_colmajor(cam_inv_proj).reshape(4, 4).T.astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(height, dtype=np.float32), np.arange(width, dtype=np.float32), indexing="ij")
+    uvx = xs / np.float32(width) * np.float32(2) - np.float32(1)
+    uvy = ys / np.float32(height) * np.float32(2) - np.float32(1)
+    d = np.stack([ip[r, 0] * uvx + ip[r, 1] * uvy + ip[r, 3] for r in range(3)], -1).astype(np.float32)
+    d = np.stack([c2w[r, 0] * d[..., 0] + c2w[r, 1] * d[..., 1] + c2w[r, 2] * d[..., 2] for r in range(3)], -1)
+    d = (d / np.sqrt((d * d).sum(-1, keepdims=True))).astype(np.float32)
+    o = c2w[:3, 3].astype(np.float32)
+    rays = np.zeros(2 * width * height, RAY_DTYPE)
+    prim = rays[: width * height]
+    prim["origin"] = (o + np.float32(near) * d).reshape(-1, 3)
+    prim["direction"] = d.reshape(-1, 3)
+    prim["PixelIndex"] = np.arange(width * height, dtype=np.uint32)
+    prim["hits"][:, 2] = np.array([far], np.float32).view(np.uint32)[0]
+    return rays
+
+
+# ---------------------------------------------------------------- engine
+class Engine:
+    """One context per GPU (tt_ctx_create). ``trace`` is the kernel_trace dispatch."""
+
+    def __init__(self, device: int = 0, max_rays: int = 0, stream: Optional[int] = None):
+        L = hip_lib()
+        cfg = Config(device=device, flags=0, max_rays=max_rays, stream=stream)
+        h = C.c_void_p()
+        st = L.tt_ctx_create(C.byref(cfg), C.byref(h))
+        if st != TT_OK:
+            raise TTError(st, "tt_ctx_create (no GPU visible?)")
+        self.L, self.h = L, h.value
+
+    def _check(self, st, what):
+        if st != TT_OK:
+            raise TTError(st, f"{what}: {self.L.tt_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tt_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    @property
+    def stream(self) -> int:
+        return self.L.tt_ctx_stream(self.h)
+
+    def upload(self, s: Scene):
+        """AssetManager.SetMeshTraceBuffers — copies the aggregated buffers into HBM."""
+        st = self.L.tt_scene_upload(self.h, _ptr(s.nodes), len(s.nodes), _ptr(s.tris), len(s.tris), _ptr(s.tlas),
+                                    len(s.tlas), _ptr(s.meshdata), len(s.meshdata), _ptr(s.materials),
+                                    len(s.materials))
+        self._check(st, "tt_scene_upload")
+
+    def update_nodes(self, first: int, nodes: np.ndarray):
+        self._check(self.L.tt_scene_update_nodes(self.h, first, len(nodes), _ptr(nodes)), "tt_scene_update_nodes")
+
+    def update_meshdata(self, first: int, md: np.ndarray):
+        self._check(self.L.tt_scene_update_meshdata(self.h, first, len(md), _ptr(md)), "tt_scene_update_meshdata")
+
+    def scene_bytes(self) -> int:
+        b = C.c_uint64()
+        self._check(self.L.tt_scene_bytes(self.h, C.byref(b)), "tt_scene_bytes")
+        return b.value
+
+    def trace(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int, info=None,
+              colors=None, flags: int = 0, device: bool = False, stats: bool = False, check: bool = True):
+        p = TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
+                        flags=flags | (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0))
+        s = Stats()
+        st = self.L.tt_trace_closest(self.h, C.byref(p), _ptr(rays), _ptr(info), _ptr(colors), C.byref(s))
+        if check:
+            self._check(st, "tt_trace_closest")
+        return (s, st) if not check else s
+
+    def resolve_normals(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int,
+                        out=None, device: bool = False):
+        p = TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
+                        flags=TT_TRACE_DEVICE_PTRS if device else 0)
+        if out is None:
+            out = np.zeros((n_rays, 6), np.float32)
+        self._check(self.L.tt_resolve_normals(self.h, C.byref(p), _ptr(rays), _ptr(out)), "tt_resolve_normals")
+        return out
+
+    def generate(self, rays, cam_to_world, cam_inv_proj, width, height, near, far, jitter=0, frames=0,
+                 max_bounce=3, device=False):
+        cam = Camera()
+        cam.cam_to_world[:] = unity_colmajor(cam_to_world)
+        cam.cam_inv_proj[:] = unity_colmajor(cam_inv_proj)
+        cam.near_plane, cam.far_plane, cam.width, cam.height = near, far, width, height
+        cam.jitter, cam.frames_accumulated, cam.max_bounce = jitter, frames, max_bounce
+        cam.flags = TT_TRACE_DEVICE_PTRS if device else 0
+        self._check(self.L.tt_generate_primary(self.h, C.byref(cam), _ptr(rays)), "tt_generate_primary")
+
+    def enqueue_bounce(self, rays, n_rays, bounce, far_plane, width, height, frames=0, max_bounce=3,
+                       device=False) -> int:
+        p = TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
+                        flags=TT_TRACE_DEVICE_PTRS if device else 0)
+        n = C.c_uint32()
+        self._check(self.L.tt_enqueue_diffuse_bounce(self.h, C.byref(p), _ptr(rays), frames, max_bounce,
+                                                     C.byref(n)), "tt_enqueue_diffuse_bounce")
+        return n.value
+
+
+def device_count() -> int:
+    try:
+        return hip_lib().tt_device_count()
+    except (FileNotFoundError, OSError):
+        return 0
