@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric: Mrays/s for primary + 1-bounce closest-hit CWBVH8 traversal
+on a Sponza-shaped scene at 1920x1080, with the trace kernel's roofline fraction and a CPU
+baseline (the scalar oracle on the host cores) on the same workload.
+
+One "step" = one pass of the hot path over one batch: the kernel_trace replacement run on the
+2,073,600 primary rays (bounce 0, with _PrimaryTriangleInfo) and then on the compacted bounce-1
+rays (bounce 1, _PrimaryTriangleInfo written where GlobalColors.Data.w == 1), both already
+resident in HBM in the reference's 2*W*H ping-pong RayData buffer. Ray generation and the
+bounce enqueue run once during setup (they are the caller's kernels, not the trace).
+
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): one process per GPU, scene
+replicated per GPU, each rank traces its own independent sample (frames_accumulated = rank,
+sub-pixel jitter) of the 1080p view — weak scaling with no data-path collective. An optional
+RCCL gather of the hit records to rank 0 runs after the timed region (--gather).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"))
+
+METRIC = "Mrays/sec (primary+1-bounce) on Sponza CWBVH at 1080p; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def alg_bytes(stats, bounce: int, info_written: int) -> float:
+    """Algorithmic bytes of one trace launch:
+    B_ray = 48 (RayData) + 16 (hit) + 16*[info written] + 80*N_node + 36*N_tri + 8*N_accept + 68*N_blas."""
+    return (48.0 * stats.rays + 16.0 * stats.rays + 16.0 * info_written + 80.0 * stats.node_visits
+            + 36.0 * stats.tri_tests + 8.0 * stats.accepts + 68.0 * stats.blas_entries)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--tris", type=int, default=262267)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x53504F4E)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true", help="RCCL-gather hit records to rank 0 after timing")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # first: tthip must bind to torch's HIP runtime (see tthip.hip_lib)
+    import torch.distributed as dist
+    import tthip
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (the HIP engine has no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=dev)
+    W, H = args.width, args.height
+    WH = W * H
+    far = 1000.0
+
+    # ------------------------------------------------------------------ scene (replicated)
+    t0 = time.time()
+    blas = tthip.Blas(tthip.Mesh.sponza(args.seed, args.tris))
+    am = tthip.AssetManager()
+    mats = np.zeros(7, tthip.MAT_DTYPE)
+    am.add_parent(blas, None, mats)
+    scene = am.build()
+    log(f"rank {rank}: scene {len(scene.tris)} tris, {len(scene.nodes)} nodes, build {time.time() - t0:.2f}s")
+    eng = tthip.Engine(local_rank, stream=torch.cuda.current_stream(dev).cuda_stream)
+    eng.upload(scene)
+
+    # ------------------------------------------------------------------ resident rays
+    rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+    info = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+    colors = np.zeros(WH, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = 1.0  # shade set Data.w = CurBounce + 1 = 1 at bounce 0
+    colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+    c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H, 0.3, far)
+    eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
+    s_prim = eng.trace(rays, WH, 0, far, W, H, info=info, device=True, stats=True)
+    nb = eng.enqueue_bounce(rays, WH, 0, far, W, H, frames=rank, max_bounce=1, device=True)
+    s_bnc = eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
+    torch.cuda.synchronize(dev)
+    rays_per_step = WH + nb
+    B_prim = alg_bytes(s_prim, 0, WH)
+    B_bnc = alg_bytes(s_bnc, 1, nb)
+    log(f"rank {rank}: primary {WH} rays nodes/ray {s_prim.node_visits / WH:.2f} tris/ray {s_prim.tri_tests / WH:.2f} "
+        f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(nb, 1):.2f} "
+        f"tris/ray {s_bnc.tri_tests / max(nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}")
+
+    def step():
+        eng.trace(rays, WH, 0, far, W, H, info=info, device=True, asynchronous=True)
+        eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.timing_reset()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    launch_ms = eng.timing_read()
+    total_rays = float(rays_per_step * args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([total_rays], dtype=torch.float64, device=dev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        total_rays = float(r.item())
+
+    prim_ms = launch_ms[0::2]
+    bnc_ms = launch_ms[1::2]
+    avg_ms = float(np.mean(launch_ms))
+    achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9  # GB/s per launch, averaged over both launches
+
+    gather_ms = None
+    if args.gather and world > 1:
+        hits = rays[: WH * 48].view(WH, 48)[:, 32:48].contiguous()
+        out = [torch.empty_like(hits) for _ in range(world)] if rank == 0 else None
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        dist.gather(hits, out, dst=0)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ctypes as O  # the oracle is only the CPU baseline here, never the measured path
+
+        host_rays = rays.cpu().numpy().view(tthip.RAY_DTYPE).copy()
+        host_info = np.zeros((WH, 4), np.uint32)
+        nthreads = max(1, args.cpu_threads)
+        done, reps, tc0 = 0, 0, time.perf_counter()
+        while True:
+            O.trace(scene, host_rays, WH, 0, far, W, H, info=host_info, nthreads=nthreads)
+            O.trace(scene, host_rays, nb, 1, far, W, H, info=host_info, colors=colors, nthreads=nthreads)
+            done += rays_per_step
+            reps += 1
+            if time.perf_counter() - tc0 >= args.cpu_seconds:
+                break
+        tcpu = time.perf_counter() - tc0
+        cpu = {"value": round(done / tcpu / 1e6, 3), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+               "sample": f"full step workload ({WH} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
+                         f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {nthreads} threads; "
+                         f"C# scalar baseline not run: no .NET runtime on the box"}
+        log(f"cpu baseline {cpu['value']} Mrays/s ({reps} reps, {tcpu:.1f}s)")
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    result = {
+        "metric": METRIC,
+        "value": round(total_rays / elapsed / 1e6, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza)",
+        "config": {"workload": "sponza_primary_plus_1_bounce_1080p", "scene": "Sponza-shaped CWBVH8 (C2)",
+                   "tris": int(len(scene.tris)), "cwbvh_nodes": int(len(scene.nodes)), "width": W, "height": H,
+                   "primary_rays": WH, "bounce_rays": int(nb), "rays_per_step_per_gpu": int(rays_per_step),
+                   "seed": hex(args.seed), "parallelism": f"sample-sharded x{world} (frames_accumulated=rank)",
+                   "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
+                   "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
+                   "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
+                   "gather_ms": None if gather_ms is None else round(gather_ms, 3)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "note": "achieved = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean HIP-event "
+                             "launch time; bytes are served mostly from L2/MALL, see DESIGN.md"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

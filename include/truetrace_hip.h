@@ -237,6 +237,7 @@ typedef struct tt_stats {
     uint64_t hits;           /* rays whose final t < FarPlane                          */
     uint64_t reps_exhausted; /* rays that hit the Reps >= 1000 bound (no write)        */
     uint64_t stack_overflows;/* rays that would have pushed a 17th stack entry        */
+    uint64_t accepts;        /* candidates that passed 0 < t < best.t                  */
     float kernel_ms;         /* trace kernel time (HIP events), sync traces only       */
     uint32_t pad;
 } tt_stats;
@@ -250,6 +251,11 @@ typedef struct tt_stats {
 tt_status tt_trace_closest(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
                            uint32_t* primary_info, const tt_col_data* global_colors,
                            tt_stats* stats);
+/* Per-launch trace kernel durations (HIP events on the context stream), recorded for every
+ * tt_trace_closest since the last tt_timing_reset (ring of 256 launches). Synchronizes. */
+tt_status tt_timing_reset(tt_ctx* ctx);
+tt_status tt_timing_read(tt_ctx* ctx, float* ms, uint32_t max, uint32_t* n);
+
 /* Wait for all work issued on the context's stream. */
 tt_status tt_sync(tt_ctx* ctx);
 /* The hipStream_t the context issues on. */

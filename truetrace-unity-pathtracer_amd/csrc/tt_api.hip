@@ -11,6 +11,8 @@
 
 #include "tt_device.h"
 
+#define TT_RING 256u
+
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
 hipError_t tt_trace_occupancy(int* blocks_per_cu);
 uint32_t tt_trace_block_size();
@@ -66,7 +68,9 @@ struct tt_ctx {
     int blocks_per_cu = 0;
     uint32_t grid = 0;
     TraceControl* ctl = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
+    hipEvent_t ring0[256] = {}, ring1[256] = {};
+    uint32_t ring_n = 0, ring_base = 0;
     std::string err;
     // scene
     bool has_scene = false;
@@ -309,10 +313,15 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     if (tt_trace_occupancy(&bpc) != hipSuccess || bpc <= 0) bpc = 2;
     c->blocks_per_cu = std::min(bpc, 8);
     c->grid = (uint32_t)(c->num_cus * c->blocks_per_cu);
-    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess) {
         tt_ctx_destroy(c);
         return TT_ERR_OOM;
+    }
+    for (uint32_t i = 0; i < TT_RING; i++) {
+        if (hipEventCreate(&c->ring0[i]) != hipSuccess || hipEventCreate(&c->ring1[i]) != hipSuccess) {
+            tt_ctx_destroy(c);
+            return TT_ERR_HIP;
+        }
     }
     c->max_rays = cfg->max_rays;
     if (c->max_rays) {
@@ -343,10 +352,33 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->cam.release();
     c->counter.release();
     if (c->ctl) (void)hipFree(c->ctl);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (uint32_t i = 0; i < TT_RING; i++) {
+        if (c->ring0[i]) (void)hipEventDestroy(c->ring0[i]);
+        if (c->ring1[i]) (void)hipEventDestroy(c->ring1[i]);
+    }
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+    return TT_OK;
+}
+
+tt_status tt_timing_reset(tt_ctx* c) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    c->ring_base = c->ring_n;
+    return TT_OK;
+}
+
+tt_status tt_timing_read(tt_ctx* c, float* ms, uint32_t max, uint32_t* n) {
+    if (!c || !n || (max && !ms)) return TT_ERR_INVALID_ARG;
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    const uint32_t total = c->ring_n - c->ring_base;
+    const uint32_t avail = std::min(total, TT_RING);
+    const uint32_t k = std::min(avail, max);
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t slot = (c->ring_n - avail + i) % TT_RING;
+        TT_HIP(c, hipEventElapsedTime(&ms[i], c->ring0[slot], c->ring1[slot]));
+    }
+    *n = k;
     return TT_OK;
 }
 
@@ -531,9 +563,13 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
     const uint32_t grid = std::max(1u, std::min(c->grid, blocks_needed));
     TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
-    TT_HIP(c, hipEventRecord(c->ev0, c->stream));
+    const uint32_t slot = c->ring_n % TT_RING;
+    TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     TT_HIP(c, tt_launch_trace(a, want_stats, matcheck, info_mode, grid, c->stream));
-    TT_HIP(c, hipEventRecord(c->ev1, c->stream));
+    TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
+    c->ring_n++;
+    c->ev0 = c->ring0[slot];
+    c->ev1 = c->ring1[slot];
     if (async) return TT_OK;
     TraceControl ctl;
     TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
@@ -554,6 +590,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
             stats->hits = ctl.stats[4];
             stats->reps_exhausted = ctl.stats[5];
             stats->stack_overflows = ctl.stats[6];
+            stats->accepts = ctl.stats[7];
         }
         stats->stack_overflows = std::max<uint64_t>(stats->stack_overflows, ctl.err_overflow);
     }

@@ -81,7 +81,8 @@ class TraceParams(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("blas_entries", C.c_uint64), ("hits", C.c_uint64), ("reps_exhausted", C.c_uint64),
-                ("stack_overflows", C.c_uint64), ("kernel_ms", C.c_float), ("pad", C.c_uint32)]
+                ("stack_overflows", C.c_uint64), ("accepts", C.c_uint64), ("kernel_ms", C.c_float),
+                ("pad", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
@@ -147,7 +148,7 @@ _HIP = None
 HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_destroy", "tt_last_error",
                "tt_scene_upload", "tt_scene_update_nodes", "tt_scene_update_meshdata", "tt_scene_bytes",
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
-               "tt_enqueue_diffuse_bounce"]
+               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
@@ -198,6 +199,13 @@ def hip_lib():
     """The gfx950 engine. Raises if the library was not built — there is no CPU fallback."""
     global _HIP
     if _HIP is None:
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so, SONAME libamdhip64.so.7). Load it
+        # first so our NEEDED libamdhip64.so.7 binds to that same runtime: two HIP/HSA runtimes in one
+        # process break torch.cuda / RCCL. Without torch the system ROCm runtime is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         path = os.path.join(LIB_DIR, "libtruetrace_hip.so")
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: the HIP engine was not built (no fallback exists)")
@@ -220,9 +228,11 @@ def hip_lib():
         L.tt_resolve_normals.argtypes = [vp, C.POINTER(TraceParams), vp, vp]
         L.tt_generate_primary.argtypes = [vp, C.POINTER(Camera), vp]
         L.tt_enqueue_diffuse_bounce.argtypes = [vp, C.POINTER(TraceParams), vp, i32, i32, C.POINTER(u32)]
+        L.tt_timing_reset.argtypes = [vp]
+        L.tt_timing_read.argtypes = [vp, vp, u32, C.POINTER(u32)]
         for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
                   "tt_scene_update_meshdata", "tt_scene_bytes", "tt_trace_closest", "tt_sync", "tt_resolve_normals",
-                  "tt_generate_primary", "tt_enqueue_diffuse_bounce"]:
+                  "tt_generate_primary", "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read"]:
             getattr(L, s).restype = i32
         _HIP = L
     return _HIP
@@ -515,15 +525,29 @@ class Engine:
     def update_meshdata(self, first: int, md: np.ndarray):
         self._check(self.L.tt_scene_update_meshdata(self.h, first, len(md), _ptr(md)), "tt_scene_update_meshdata")
 
+    def sync(self):
+        self._check(self.L.tt_sync(self.h), "tt_sync")
+
+    def timing_reset(self):
+        self._check(self.L.tt_timing_reset(self.h), "tt_timing_reset")
+
+    def timing_read(self) -> np.ndarray:
+        ms = np.zeros(256, np.float32)
+        n = C.c_uint32()
+        self._check(self.L.tt_timing_read(self.h, ms.ctypes.data, 256, C.byref(n)), "tt_timing_read")
+        return ms[: n.value].copy()
+
     def scene_bytes(self) -> int:
         b = C.c_uint64()
         self._check(self.L.tt_scene_bytes(self.h, C.byref(b)), "tt_scene_bytes")
         return b.value
 
     def trace(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int, info=None,
-              colors=None, flags: int = 0, device: bool = False, stats: bool = False, check: bool = True):
+              colors=None, flags: int = 0, device: bool = False, stats: bool = False, check: bool = True,
+              asynchronous: bool = False):
         p = TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
-                        flags=flags | (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0))
+                        flags=flags | (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0)
+                        | (TT_TRACE_ASYNC if asynchronous else 0))
         s = Stats()
         st = self.L.tt_trace_closest(self.h, C.byref(p), _ptr(rays), _ptr(info), _ptr(colors), C.byref(s))
         if check:
