@@ -201,6 +201,16 @@ tt_status tt_scene_upload(tt_ctx* ctx,
                           const int32_t* tlas_indices, uint32_t n_tlas_indices,
                           const tt_mesh_data* meshdata, uint32_t n_mesh,
                           const tt_material* materials, uint32_t n_mat);
+/* The structural check tt_scene_upload runs (no GPU needed): every node, triangle, TLAS slot,
+ * mesh record and (when any material is Invisible) material index reachable by IntersectBVH's
+ * index arithmetic (IntersectionKernels.compute:157-213) is in range. why (nullable) receives
+ * the first violation. Returns TT_OK, TT_ERR_INVALID_ARG or TT_ERR_UNSUPPORTED (Cutout). */
+tt_status tt_scene_validate(const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                            const tt_cuda_triangle* tris, uint32_t n_tris,
+                            const int32_t* tlas_indices, uint32_t n_tlas_indices,
+                            const tt_mesh_data* meshdata, uint32_t n_mesh,
+                            const tt_material* materials, uint32_t n_mat,
+                            char* why, uint32_t why_len);
 /* Per-frame TLAS refit region rewrite (BVH8AggregatedBuffer.SetData at
  * AssetManager.cs:1760 / GPU refit AssetManager.cs:1821-1822). */
 tt_status tt_scene_update_nodes(tt_ctx* ctx, uint32_t first, uint32_t count,

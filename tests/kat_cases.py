@@ -1,0 +1,154 @@
+"""Known-answer cases for the closest-hit traversal (test infrastructure).
+
+Every case is a hand-built scene (tests/handbuilt.py) whose expected hit record follows from
+the reference's semantics with exact dyadic arithmetic, so it holds under any legal rounding of
+the reference HLSL (IntersectionKernels.compute:14-260, CommonData.cginc:635-707). The same
+cases run against the oracle (tests/test_oracle_kat.py) and the GPU (tests/test_gpu_parity.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import handbuilt as hb
+import tthip
+
+E6 = 121  # scale 2^-6
+
+
+def _leaf_root(tris_count=1, z_lo=63, z_hi=65):
+    # BLAS root: p = (-1,-1,-1), scale 1/64: box x,y in [0, 1], z in [-1/64, 1/64]
+    return hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0,
+                        [(0, "leaf", (64, 64, z_lo), (128, 128, z_hi), (0, tris_count))])
+
+
+UNIT_TRI = hb.tri((0.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0))
+
+
+def case_single_triangle():
+    sc = hb.scene([_leaf_root()], [UNIT_TRI])
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0), (0.0, 0.0, 1.0), (2.0, 2.0, 1.0), (0.25, 0.25, -1.0)],
+                          [(0.0, 0.0, -1.0), (0.5, 0.25, -1.0), (0.0, 0.0, -1.0), (0.0, 0.0, -1.0)])
+    far = np.uint32(np.float32(1000.0).view(np.uint32))
+    expected = [hb.expected_hit(0, 0, 1.0, 0.25, 0.25),   # axis-parallel: NaN slabs ignored (maxNum)
+                hb.expected_hit(0, 0, 1.0, 0.5, 0.25),    # oblique, exact
+                [0, 0xFFFFFFFF, int(far), 0],             # outside the node box: miss
+                [0, 0xFFFFFFFF, int(far), 0]]             # behind the origin: t < 0 rejected
+    return "single_triangle", sc, rays, 4, expected
+
+
+def case_tie_first_found_wins():
+    # two coincident triangles in one leaf: bit 1 is visited first (IntersectionKernels.compute:222)
+    # and the strict t < best.t (:33) keeps it.
+    sc = hb.scene([_leaf_root(2)], [UNIT_TRI, UNIT_TRI])
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)])
+    return "tie_first_found_wins", sc, rays, 1, [hb.expected_hit(0, 1, 1.0, 0.25, 0.25)]
+
+
+def _two_child_scene():
+    # root with two internal children: k=0 far (z = -0.5), k=1 near (z = 0)
+    root = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 1, 0,
+                        [(0, "inner", (64, 64, 31), (128, 128, 33), 0),
+                         (1, "inner", (64, 64, 63), (128, 128, 65), 1)])
+    far_child = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0,
+                             [(0, "leaf", (64, 64, 31), (128, 128, 33), (0, 1))])
+    near_child = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 1,
+                              [(0, "leaf", (64, 64, 63), (128, 128, 65), (0, 1))])
+    tris = [hb.tri((0.0, 0.0, -0.5), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0)), UNIT_TRI]
+    return hb.scene([root, far_child, near_child], tris)
+
+
+def case_octant_order_and_culling():
+    # dir.z < 0, x,y >= 0: oct byte 6, child k=1 sits at bit 24 + (1^6) = 31 and is visited first;
+    # the near hit (t = 1) then culls the far child's leaf (tri tests = 1).
+    sc = _two_child_scene()
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0), (0.25, 0.25, -2.0)], [(0.0, 0.0, -1.0), (0.0, 0.0, 1.0)])
+    # second ray travels +z from below: hits far tri (z=-0.5) at t=1.5 first in distance
+    expected = [hb.expected_hit(0, 1, 1.0, 0.25, 0.25), hb.expected_hit(0, 0, 1.5, 0.25, 0.25)]
+    return "octant_order_and_culling", sc, rays, 2, expected
+
+
+def case_reps_exhausted():
+    # a chain of 1001 internal nodes: the ray reaches Reps == 1000 and writes nothing (:155)
+    n = 1001
+    nodes = []
+    for i in range(n):
+        if i < n - 1:
+            nodes.append(hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), i + 1, 0,
+                                      [(0, "inner", (0, 0, 0), (255, 255, 255), 0)]))
+        else:
+            nodes.append(_leaf_root())
+    sc = hb.scene(nodes, [UNIT_TRI])
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)])
+    rays["hits"][0] = [7, 8, 9, 10]  # sentinel: must survive
+    return "reps_exhausted", sc, rays, 1, [[7, 8, 9, 10]]
+
+
+def case_chain_within_bound():
+    # 998 internal nodes + the leaf node: 999 node visits below the TLAS node => 1000 total, the
+    # ray finishes in the same iteration it reaches Reps == 1000 and writes its hit.
+    n = 999
+    nodes = []
+    for i in range(n):
+        if i < n - 1:
+            nodes.append(hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), i + 1, 0,
+                                      [(0, "inner", (0, 0, 0), (255, 255, 255), 0)]))
+        else:
+            nodes.append(_leaf_root())
+    sc = hb.scene(nodes, [UNIT_TRI])
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)])
+    return "chain_within_bound", sc, rays, 1, [hb.expected_hit(0, 0, 1.0, 0.25, 0.25)]
+
+
+def stack_overflow_scene(depth=18):
+    """Every level has two internal children that the ray hits; descending one pushes the
+    other, so the stack grows by one per level and overflows past 16 (:65, :166-168)."""
+    nodes = []
+    for i in range(depth):
+        # children: k=0 -> next level (index 2*i+1), k=1 -> an empty dead-end node (2*i+2)
+        nodes.append(hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 2 * i + 1, 0,
+                                  [(0, "inner", (0, 0, 0), (255, 255, 255), 0),
+                                   (1, "inner", (0, 0, 0), (255, 255, 255), 1)]))
+        nodes.append(hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0, []))
+    nodes.append(_leaf_root())
+    sc = hb.scene(nodes, [UNIT_TRI])
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)])
+    return sc, rays
+
+
+def case_two_instances():
+    """Two instances of one BLAS (AssetManager.cs:1714-1750): translations (+4,0,0) and (0,0,0).
+    TLAS node 0 holds both in one leaf; slot bit 1 (tlas[1]) is entered first."""
+    blas = [_leaf_root()]
+    nodes = np.zeros(4 + 1, tthip.NODE_DTYPE)  # TLAS region 2*2 = 4 slots, BLAS at 4
+    nodes[0] = hb.make_node((-8.0, -8.0, -8.0), (E6 + 3, E6 + 3, E6 + 3), 0, 0,
+                            [(0, "leaf", (64, 64, 56), (128, 128, 72), (0, 2))])
+    nodes[4] = blas[0]
+    t_a = np.eye(4)
+    t_a[0, 3] = 4.0
+    md = np.zeros(2, tthip.MESH_DTYPE)
+    md[0] = hb.mesh_record(4, 0, 4, tthip.unity_colmajor(np.linalg.inv(t_a)))
+    md[1] = hb.mesh_record(4, 0, 4, tthip.unity_colmajor(np.eye(4)))
+    sc = tthip.Scene(nodes, np.array([UNIT_TRI], tthip.TRI_DTYPE), np.array([0, 1], np.int32), md,
+                     np.zeros(1, tthip.MAT_DTYPE), tlas_nodes=1)
+    rays = hb.rays_buffer([(4.25, 0.25, 1.0), (0.25, 0.25, 1.0), (2.25, 0.25, 1.0)],
+                          [(0.0, 0.0, -1.0), (0.0, 0.0, -1.0), (0.0, 0.0, -1.0)])
+    far = int(np.float32(1000.0).view(np.uint32))
+    expected = [hb.expected_hit(0, 0, 1.0, 0.25, 0.25), hb.expected_hit(1, 0, 1.0, 0.25, 0.25), [0, 0xFFFFFFFF, far, 0]]
+    return "two_instances", sc, rays, 3, expected
+
+
+def case_invisible_bounce0():
+    """Material Invisible flag (bit 7 of Tag) hides a triangle at CurBounce == 0 only (:48)."""
+    tris = [hb.tri((0.0, 0.0, -0.5), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=0),
+            hb.tri((0.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=1)]
+    root = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0,
+                        [(0, "leaf", (64, 64, 31), (128, 128, 65), (0, 2))])
+    mats = np.zeros(2, tthip.MAT_DTYPE)
+    mats[1]["Tag"] = 1 << tthip.FLAG_INVISIBLE
+    sc = hb.scene([root], tris, materials=mats)
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)])
+    return sc, rays, hb.expected_hit(0, 0, 1.5, 0.25, 0.25), hb.expected_hit(0, 1, 1.0, 0.25, 0.25)
+
+
+ALL_CASES = [case_single_triangle, case_tie_first_found_wins, case_octant_order_and_culling, case_reps_exhausted,
+             case_chain_within_bound, case_two_instances]

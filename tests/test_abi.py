@@ -1,0 +1,62 @@
+"""C-ABI surface: every function the public headers declare is exported by the built libraries,
+struct layouts agree between C and Python, and the engine refuses to run without a GPU."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import tthip
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    src = open(os.path.join(REPO, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b(tt_[a-z0-9_]+)\s*\(", src, flags=re.M)))
+
+
+def test_hip_library_exports_every_declared_symbol():
+    names = declared("truetrace_hip.h")
+    assert "tt_trace_closest" in names and "tt_scene_upload" in names
+    lib = C.CDLL(os.path.join(tthip.LIB_DIR, "libtruetrace_hip.so"))
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(tthip.HIP_SYMBOLS) <= set(names)
+
+
+def test_scene_library_exports_every_declared_symbol():
+    names = declared("truetrace_scene.h")
+    lib = C.CDLL(os.path.join(tthip.LIB_DIR, "libtruetrace_scene.so"))
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_abi_version_and_layouts():
+    L = tthip.hip_lib()
+    assert L.tt_abi_version() == 1
+    assert C.sizeof(tthip.TraceParams) == 24
+    assert C.sizeof(tthip.Stats) == 8 * 8 + 8
+    assert tthip.RAY_DTYPE.fields["hits"][1] == 32  # RayData.hits at byte 32 (CommonData.cginc:106)
+    assert tthip.MESH_DTYPE.fields["TriOffset"][1] == 64
+    assert tthip.MESH_DTYPE.fields["mesh_data_bvh_offsets"][1] == 76
+    assert tthip.COL_DTYPE.fields["Data"][1] == 48
+
+
+@pytest.mark.skipif(tthip.device_count() > 0, reason="checks the no-GPU behaviour")
+def test_no_device_is_loud():
+    L = tthip.hip_lib()
+    assert L.tt_device_count() == 0
+    with pytest.raises(tthip.TTError) as e:
+        tthip.Engine(0)
+    assert e.value.status == tthip.TT_ERR_NO_DEVICE
+
+
+def test_null_context_is_rejected():
+    L = tthip.hip_lib()
+    p = tthip.TraceParams(n_rays=1, bounce=0, far_plane=1.0, screen_width=1, screen_height=1, flags=0)
+    assert L.tt_trace_closest(None, C.byref(p), None, None, None, None) == tthip.TT_ERR_INVALID_ARG
+    assert L.tt_scene_upload(None, None, 0, None, 0, None, 0, None, 0, None, 0) == tthip.TT_ERR_INVALID_ARG
+    assert L.tt_last_error(None) == b"null context"

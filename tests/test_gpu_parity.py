@@ -1,0 +1,318 @@
+"""GPU parity: the gfx950 engine, called through the C ABI, against the CPU oracle.
+
+The bar is bit-exact hit records (mesh_id, triangle_id, asuint(t), packed u/v) and
+_PrimaryTriangleInfo for every ray; normals within 1e-5. Sizes run from single hand-built rays
+(known answers) to the full BASELINE.json C2 configuration (Sponza-shaped, 1920x1080 primary
+plus bounce 1), where the oracle is multithreaded.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io
+import handbuilt as hb
+import kat_cases as K
+import oracle_ctypes as O
+import tthip
+
+pytestmark = pytest.mark.gpu
+FAR = 1000.0
+CPU_THREADS = 16
+
+
+def trace_both(engine, sc, rays, n, bounce, W, H, info=True, colors=None, flags=0, upload=True):
+    if upload:
+        engine.upload(sc)
+    rg, rc = rays.copy(), rays.copy()
+    ig = np.zeros((W * H, 4), np.uint32) if info else None
+    ic = np.zeros((W * H, 4), np.uint32) if info else None
+    s = engine.trace(rg, n, bounce, FAR, W, H, info=ig, colors=colors, flags=flags, stats=True)
+    st, cnt = O.trace(sc, rc, n, bounce, FAR, W, H, info=ic, colors=colors, flags=flags, counts=True,
+                      nthreads=CPU_THREADS)
+    assert st == 0
+    return rg, rc, ig, ic, s, cnt
+
+
+def assert_same(rg, rc, ig, ic, off, n):
+    hg, hc = rg["hits"][off:off + n], rc["hits"][off:off + n]
+    bad = np.nonzero((hg != hc).any(1))[0]
+    assert len(bad) == 0, f"{len(bad)} of {n} hit records differ, first {bad[:5]}: {hg[bad[:3]]} vs {hc[bad[:3]]}"
+    assert np.array_equal(rg, rc), "bytes outside the hit records must be untouched"
+    if ig is not None:
+        badi = np.nonzero((ig != ic).any(1))[0]
+        assert len(badi) == 0, f"{len(badi)} _PrimaryTriangleInfo texels differ"
+
+
+# ------------------------------------------------------------------ known answers
+@pytest.mark.parametrize("case", K.ALL_CASES, ids=lambda c: c.__name__)
+def test_kat_on_gpu(engine, case):
+    name, sc, rays, n, expected = case()
+    engine.upload(sc)
+    r = rays.copy()
+    engine.trace(r, n, 0, FAR, n, 1)
+    assert r["hits"][:n].tolist() == [list(map(int, e)) for e in expected], name
+
+
+def test_kat_stack_overflow_on_gpu(engine):
+    sc, rays = K.stack_overflow_scene(17)
+    engine.upload(sc)
+    s, st = engine.trace(rays.copy(), 1, 0, FAR, 1, 1, check=False)
+    assert st == tthip.TT_ERR_STACK_OVERFLOW and s.stack_overflows == 1
+    sc, rays = K.stack_overflow_scene(16)
+    engine.upload(sc)
+    r = rays.copy()
+    engine.trace(r, 1, 0, FAR, 1, 1)
+    assert r["hits"][0, 1] == 0
+
+
+def test_kat_invisible_on_gpu(engine):
+    sc, rays, exp0, exp1 = K.case_invisible_bounce0()
+    engine.upload(sc)
+    r0 = rays.copy()
+    engine.trace(r0, 1, 0, FAR, 1, 1)
+    assert r0["hits"][0].tolist() == exp0
+    r1 = rays.copy()
+    r1[1] = r1[0]
+    engine.trace(r1, 1, 1, FAR, 1, 1)
+    assert r1["hits"][1].tolist() == exp1
+
+
+def test_cutout_material_is_refused(engine):
+    sc, _, _, _ = K.case_invisible_bounce0()
+    sc.materials[0]["MatType"] = tthip.MAT_CUTOUT_INDEX
+    with pytest.raises(tthip.TTError) as e:
+        engine.upload(sc)
+    assert e.value.status == tthip.TT_ERR_UNSUPPORTED
+
+
+def test_malformed_scene_is_refused(engine):
+    sc = tthip.single_object_scene(tthip.Mesh.soup(3, 200, 1.0, 0.1))
+    sc.nodes[2]["base_child"] = 10 ** 6
+    with pytest.raises(tthip.TTError) as e:
+        engine.upload(sc)
+    assert e.value.status == tthip.TT_ERR_INVALID_ARG
+
+
+# ------------------------------------------------------------------ golden fixtures
+@pytest.mark.parametrize("name", golden_io.NAMES)
+def test_golden_on_gpu(engine, name):
+    g = golden_io.load(name)
+    sc, W, H = g["scene"], g["W"], g["H"]
+    engine.upload(sc)
+    r0 = g["rays0"].copy()
+    info0 = np.zeros((W * H, 4), np.uint32)
+    s = engine.trace(r0, W * H, 0, g["far"], W, H, info=info0, stats=True)
+    assert np.array_equal(r0["hits"][: W * H], g["hits0"])
+    assert np.array_equal(info0, g["info0"])
+    c0 = g["counts0"].view(O.COUNTS_DTYPE)
+    assert s.node_visits == int(c0["node_visits"].sum()) and s.tri_tests == int(c0["tri_tests"].sum())
+    assert s.blas_entries == int(c0["blas_entries"].sum()) and s.accepts == int(c0["accepts"].sum())
+    r1 = g["rays1"].copy()
+    info1 = np.zeros((W * H, 4), np.uint32)
+    engine.trace(r1, g["n1"], 1, g["far"], W, H, info=info1, colors=g["colors"])
+    assert np.array_equal(r1["hits"][W * H:W * H + g["n1"]], g["hits1"])
+    assert np.array_equal(info1, g["info1"])
+
+
+def test_golden_device_pointers(engine):
+    import torch
+
+    g = golden_io.load("instanced")
+    sc, W, H = g["scene"], g["W"], g["H"]
+    engine.upload(sc)
+    dev = torch.device("cuda:0")
+    rt = torch.from_numpy(g["rays0"].view(np.uint8).copy()).to(dev)
+    it = torch.zeros(W * H * 16, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    engine.trace(rt, W * H, 0, g["far"], W, H, info=it, device=True)
+    r = rt.cpu().numpy().view(tthip.RAY_DTYPE)
+    assert np.array_equal(r["hits"][: W * H], g["hits0"])
+    assert np.array_equal(it.cpu().numpy().view(np.uint32).reshape(-1, 4), g["info0"])
+
+
+# ------------------------------------------------------------------ random scenes
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_random_soup_random_camera(engine, seed):
+    rng = np.random.default_rng(seed)
+    sc = tthip.single_object_scene(tthip.Mesh.soup(seed, int(rng.integers(500, 40000)), 1.0,
+                                                   float(rng.uniform(0.02, 0.2))))
+    W, H = int(rng.integers(17, 200)), int(rng.integers(9, 120))  # ragged, not multiples of 64
+    pos = rng.uniform(-2.5, 2.5, 3)
+    c2w, ip = tthip.unity_camera(pos, -pos + rng.normal(0, 0.3, 3), (0, 1, 0), float(rng.uniform(30, 100)), W, H,
+                                 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    assert s.node_visits == int(cnt["node_visits"].sum())
+
+
+def instanced_scene(seed, n_props=12, n_inst=200):
+    rng = np.random.default_rng(seed)
+    am = tthip.AssetManager()
+    am.add_parent(tthip.Blas(tthip.Mesh.soup(seed, 3000, 20.0, 0.5)), tthip.trs_matrix((0, 0, 0)),
+                  np.zeros(2, tthip.MAT_DTYPE))
+    props = [am.add_instance_parent(tthip.Blas(tthip.Mesh.prop(seed * 100 + k, int(rng.integers(50, 4000)))),
+                                    np.zeros(2, tthip.MAT_DTYPE)) for k in range(n_props)]
+    for i in range(n_inst):
+        am.add_instance(props[i % n_props], tthip.trs_matrix(rng.uniform(-40, 40, 3) * [1, 0.1, 1],
+                                                             float(rng.uniform(0, 360)), float(rng.uniform(0.3, 2))))
+    return am.build()
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_instanced_two_level(engine, seed):
+    sc = instanced_scene(seed)
+    W, H = 160, 90
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    assert s.blas_entries == int(cnt["blas_entries"].sum()) > W * H
+
+
+def test_update_meshdata_and_nodes(engine):
+    """Per-frame transform update (AssetManager.cs:1825) and TLAS node rewrite (:1760)."""
+    sc = instanced_scene(9, n_props=3, n_inst=20)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    engine.upload(sc)
+    md = sc.meshdata.copy()
+    md["W2L"][1:] = tthip.unity_colmajor(np.linalg.inv(tthip.trs_matrix((1.0, 0, 0), 5.0, 1.1)))
+    engine.update_meshdata(0, md)
+    sc2 = tthip.Scene(sc.nodes, sc.tris, sc.tlas, md, sc.materials)
+    rg, rc, ig, ic, _, _ = trace_both(engine, sc2, rays, W * H, 0, W, H, upload=False)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    nodes = sc.nodes.copy()
+    nodes[0]["p"] = nodes[0]["p"] - 1.0  # a (conservatively wrong) refit of the TLAS root
+    engine.update_nodes(0, nodes[:1])
+    sc3 = tthip.Scene(nodes, sc.tris, sc.tlas, md, sc.materials)
+    rg, rc, ig, ic, _, _ = trace_both(engine, sc3, rays, W * H, 0, W, H, upload=False)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    bad = nodes[:1].copy()
+    bad[0]["base_child"] = 10 ** 7
+    with pytest.raises(tthip.TTError):
+        engine.update_nodes(0, bad)
+
+
+def test_info_forms_at_later_bounce(engine):
+    g = golden_io.load("soup")
+    sc, W, H = g["scene"], g["W"], g["H"]
+    for flags in (0, tthip.TT_TRACE_USE_RESTIRGI, tthip.TT_TRACE_USE_ASVGF,
+                  tthip.TT_TRACE_USE_RESTIRGI | tthip.TT_TRACE_USE_ASVGF):
+        for bounce in (1, 2, 3):
+            rays = g["rays1"].copy()
+            if bounce % 2 == 0:  # even bounces read the first half of the ping-pong buffer
+                rays[: W * H] = rays[W * H:]
+            off = W * H if bounce % 2 else 0
+            colors = g["colors"].copy()
+            colors["Data"][:, 3] = np.where(np.arange(W * H) % 2 == 0, float(bounce), -1.0)
+            rg, rc, ig, ic, _, _ = trace_both(engine, sc, rays, g["n1"], bounce, W, H, colors=colors, flags=flags)
+            assert_same(rg, rc, ig, ic, off, g["n1"])
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 65, 257, 4097])
+def test_ragged_ray_counts(engine, n):
+    g = golden_io.load("soup")
+    sc, W, H = g["scene"], g["W"], g["H"]
+    rng = np.random.default_rng(n)
+    rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+    m = min(n, W * H)
+    src = g["rays0"][rng.permutation(W * H)[:m]]
+    rays[:m] = src
+    rg, rc, ig, ic, s, _ = trace_both(engine, sc, rays, m, 0, W, H)
+    assert_same(rg, rc, ig, ic, 0, m)
+    assert s.rays == m
+
+
+def test_normals_within_1e5(engine):
+    sc = instanced_scene(11, n_props=4, n_inst=30)
+    W, H = 128, 72
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    engine.upload(sc)
+    engine.trace(rays, W * H, 0, FAR, W, H)
+    ng = engine.resolve_normals(rays, W * H, 0, FAR, W, H)
+    nc = O.resolve_normals(sc, rays, W * H, 0, FAR, W, H)
+    hit = rays["hits"][: W * H, 1] != 0xFFFFFFFF
+    assert hit.sum() > 100
+    assert np.abs(ng - nc).max() <= 1e-5
+    assert np.allclose(np.linalg.norm(ng[hit, :3], axis=1), 1.0, atol=1e-5)
+
+
+def test_raygen_matches_restatement(engine):
+    sc = tthip.single_object_scene(tthip.Mesh.cornell())
+    engine.upload(sc)
+    W, H = 320, 200
+    c2w, ip = tthip.unity_camera((0.1, 0.2, 3.4), (0, 0, -1), (0, 1, 0), 40, W, H, 0.3, FAR)
+    for jitter in (0, 1):
+        rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+        engine.generate(rays, c2w, ip, W, H, 0.3, FAR, jitter=jitter, frames=3, max_bounce=5)
+        ref = O.generate(c2w, ip, W, H, 0.3, FAR, jitter=jitter, frames=3, max_bounce=5)
+        assert np.array_equal(rays[: W * H].view(np.uint32), ref[: W * H].view(np.uint32))
+
+
+def test_bounce_enqueue_compaction(engine):
+    g = golden_io.load("soup")
+    sc, W, H = g["scene"], g["W"], g["H"]
+    engine.upload(sc)
+    r = g["rays0"].copy()
+    engine.trace(r, W * H, 0, FAR, W, H)
+    nb = engine.enqueue_bounce(r, W * H, 0, FAR, W, H)
+    hit = r["hits"][: W * H, 1] != 0xFFFFFFFF
+    assert nb == hit.sum()
+    out = r[W * H:W * H + nb]
+    assert sorted(out["PixelIndex"].tolist()) == sorted(r["PixelIndex"][: W * H][hit].tolist())
+    assert np.allclose(np.linalg.norm(out["direction"], axis=1), 1.0, atol=1e-5)
+    # the compacted bounce rays trace identically on both sides
+    rg, rc, ig, ic, _, _ = trace_both(engine, sc, r, nb, 1, W, H, info=False)
+    assert_same(rg, rc, ig, ic, W * H, nb)
+
+
+# ------------------------------------------------------------------ BASELINE.json C2 at full size
+@pytest.fixture(scope="module")
+def sponza():
+    blas = tthip.Blas(tthip.Mesh.sponza())
+    am = tthip.AssetManager()
+    am.add_parent(blas, None, np.zeros(7, tthip.MAT_DTYPE))
+    return am.build()
+
+
+def test_sponza_1080p_primary_and_bounce_full_parity(engine, sponza):
+    W, H = 1920, 1080
+    c2w, ip = tthip.unity_camera((-10, 2, 0), (1, 0, 0), (0, 1, 0), 60, W, H, 0.3, FAR)
+    engine.upload(sponza)
+    rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+    engine.generate(rays, c2w, ip, W, H, 0.3, FAR, jitter=0)  # no jitter: the centre ray is axis-parallel
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sponza, rays, W * H, 0, W, H, upload=False)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    assert s.reps_exhausted == int((cnt["status"] == 1).sum())
+    nb = engine.enqueue_bounce(rg, W * H, 0, FAR, W, H)
+    assert nb > 0.9 * W * H
+    colors = np.zeros(W * H, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = 1.0
+    rg2, rc2, ig2, ic2, s2, cnt2 = trace_both(engine, sponza, rg, nb, 1, W, H, colors=colors, upload=False)
+    assert_same(rg2, rc2, ig2, ic2, W * H, nb)
+    assert s2.node_visits == int(cnt2["node_visits"].sum())
+
+
+def test_sponza_4k_properties(engine, sponza):
+    """At C5's ray count (3840x2160): determinism (two launches give identical bytes) and a
+    strided 1/64 sample against the oracle."""
+    W, H = 3840, 2160
+    c2w, ip = tthip.unity_camera((-12, 6, 3), (1, -0.2, -0.1), (0, 1, 0), 75, W, H, 0.3, FAR)
+    engine.upload(sponza)
+    rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+    engine.generate(rays, c2w, ip, W, H, 0.3, FAR, jitter=1, frames=7)
+    a = rays.copy()
+    engine.trace(a, W * H, 0, FAR, W, H)
+    b = rays.copy()
+    engine.trace(b, W * H, 0, FAR, W, H)
+    assert np.array_equal(a, b)
+    idx = np.arange(0, W * H, 64)
+    sample = np.zeros(2 * len(idx), tthip.RAY_DTYPE)
+    sample[: len(idx)] = rays[idx]
+    st, _ = O.trace(sponza, sample, len(idx), 0, FAR, len(idx), 1, nthreads=CPU_THREADS)
+    assert st == 0
+    assert np.array_equal(sample["hits"][: len(idx)], a["hits"][idx])

@@ -1,0 +1,107 @@
+"""Oracle vs analytic known answers (parity pin for the CPU restatement; no GPU)."""
+import numpy as np
+import pytest
+
+import handbuilt as hb
+import kat_cases as K
+import oracle_ctypes as O
+import tthip
+
+
+@pytest.mark.parametrize("case", K.ALL_CASES, ids=lambda c: c.__name__)
+def test_kat_hits(case):
+    name, sc, rays, n, expected = case()
+    st, cnt = O.trace(sc, rays, n, 0, 1000.0, n, 1, counts=True)
+    assert st == tthip.TT_OK
+    got = rays["hits"][:n].tolist()
+    assert got == [list(map(int, e)) for e in expected], name
+
+
+def test_kat_culling_counts():
+    _, sc, rays, n, _ = K.case_octant_order_and_culling()
+    st, cnt = O.trace(sc, rays, n, 0, 1000.0, n, 1, counts=True)
+    assert st == 0
+    # TLAS node + root + first child visited + second child visited (its leaf is culled)
+    assert cnt["node_visits"].tolist() == [4, 4]
+    assert cnt["tri_tests"].tolist() == [1, 1]
+    assert cnt["blas_entries"].tolist() == [1, 1]
+
+
+def test_kat_reps_counts():
+    _, sc, rays, n, _ = K.case_reps_exhausted()
+    st, cnt = O.trace(sc, rays, n, 0, 1000.0, n, 1, counts=True)
+    assert st == 0 and cnt["status"][0] == 1 and cnt["node_visits"][0] == 1000
+    _, sc, rays, n, _ = K.case_chain_within_bound()
+    st, cnt = O.trace(sc, rays, n, 0, 1000.0, n, 1, counts=True)
+    assert st == 0 and cnt["status"][0] == 0 and cnt["node_visits"][0] == 1000
+
+
+def test_kat_stack_overflow():
+    # one push per level: 16 levels fill uint2 stack[16] exactly, the 17th push overflows
+    sc, rays = K.stack_overflow_scene(17)
+    st, cnt = O.trace(sc, rays, 1, 0, 1000.0, 1, 1, counts=True)
+    assert st == tthip.TT_ERR_STACK_OVERFLOW and cnt["status"][0] == 2
+    sc, rays = K.stack_overflow_scene(16)
+    st, cnt = O.trace(sc, rays, 1, 0, 1000.0, 1, 1, counts=True)
+    assert st == 0 and cnt["max_stack"][0] == 16 and cnt["status"][0] == 0
+
+
+def test_kat_invisible_only_at_bounce0():
+    sc, rays, exp0, exp1 = K.case_invisible_bounce0()
+    r0 = rays.copy()
+    assert O.trace(sc, r0, 1, 0, 1000.0, 1, 1)[0] == 0
+    assert r0["hits"][0].tolist() == exp0
+    r1 = rays.copy()
+    r1[1] = r1[0]  # odd bounces read GlobalRays[W*H + i] (IntersectionKernels.compute:82)
+    assert O.trace(sc, r1, 1, 1, 1000.0, 1, 1)[0] == 0
+    assert r1["hits"][1].tolist() == exp1
+
+
+def test_cutout_unsupported():
+    sc, rays, _, _ = K.case_invisible_bounce0()
+    sc.materials[0]["MatType"] = tthip.MAT_CUTOUT_INDEX
+    assert O.trace(sc, rays, 1, 0, 1000.0, 1, 1)[0] == tthip.TT_ERR_UNSUPPORTED
+
+
+def test_primary_info_bounce0_and_miss():
+    _, sc, rays, n, expected = K.case_single_triangle()
+    info = np.zeros((n, 4), np.uint32)
+    assert O.trace(sc, rays, n, 0, 1000.0, n, 1, info=info)[0] == 0
+    # hit: (mesh_id, tri - TriOffset, asuint(u), asuint(v)) at full precision (:233)
+    assert info[0].tolist() == [0, 0, int(np.float32(0.25).view(np.uint32)), int(np.float32(0.25).view(np.uint32))]
+    # miss: mesh 0, -1 - MeshData[0].TriOffset, u = v = 0
+    assert info[2].tolist() == [0, 0xFFFFFFFF, 0, 0]
+
+
+def test_primary_info_later_bounce_forms():
+    _, sc, rays, n, _ = K.case_single_triangle()
+    r = rays.copy()
+    r[n:2 * n] = rays[:n]
+    colors = np.zeros(n, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = [1.0, -1.0, 1.0, 2.0]  # ray 3: Data.w = 2 != CurBounce -> no write
+    for flags in (0, tthip.TT_TRACE_USE_RESTIRGI, tthip.TT_TRACE_USE_ASVGF):
+        info = np.full((n, 4), 0xABCDEF, np.uint32)
+        rr = r.copy()
+        assert O.trace(sc, rr, n, 1, 1000.0, n, 1, info=info, colors=colors, flags=flags)[0] == 0
+        d = rays["direction"][:n].view(np.uint32)
+        if flags == tthip.TT_TRACE_USE_RESTIRGI:
+            assert info[0, :3].tolist() == [0, 0, (16383 | (16383 << 16))]
+        else:
+            assert info[0, :3].tolist() == d[0].tolist()
+        assert info[0, 3] == 0
+        # miss (ray 2): ASVGF -> direction; otherwise direction * FarPlane + origin
+        if flags == tthip.TT_TRACE_USE_ASVGF:
+            assert info[2, :3].tolist() == d[2].tolist()
+        else:
+            pos = (rays["direction"][2] * np.float32(1000.0) + rays["origin"][2]).astype(np.float32)
+            assert info[2, :3].tolist() == pos.view(np.uint32).tolist()
+        assert info[2, 3] == 1
+        assert info[3].tolist() == [0xABCDEF] * 4
+
+
+def test_zero_rays_and_bad_args():
+    _, sc, rays, n, _ = K.case_single_triangle()
+    before = rays.copy()
+    assert O.trace(sc, rays, 0, 0, 1000.0, n, 1)[0] == 0
+    assert np.array_equal(before, rays)
+    assert O.trace(sc, rays, 1, 0, 1000.0, 0, 1)[0] == tthip.TT_ERR_INVALID_ARG

@@ -229,6 +229,42 @@ struct Validator {
     }
 };
 
+tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris, uint32_t n_tris,
+                      const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md, uint32_t n_mesh,
+                      const tt_material* mats, uint32_t n_mat, SceneHost& h, std::vector<uint32_t>& tags,
+                      bool& any_invisible, std::string& why) {
+    if (!nodes || !n_nodes || !tris || !n_tris || !tlas || !n_tlas || !md || !n_mesh || (n_mat && !mats)) {
+        why = "null or empty buffer";
+        return TT_ERR_INVALID_ARG;
+    }
+    h.nodes.assign(nodes, nodes + n_nodes);
+    h.tlas.assign(tlas, tlas + n_tlas);
+    h.mesh.assign(md, md + n_mesh);
+    h.n_tris = n_tris;
+    h.n_mat = n_mat;
+    any_invisible = false;
+    tags.assign(std::max<uint32_t>(n_mat, 1u), 0u);
+    for (uint32_t m = 0; m < n_mat; m++) {
+        if (mats[m].MatType == TT_MAT_CUTOUT_INDEX) {
+            why = "material " + std::to_string(m) +
+                  " is Cutout (alpha-atlas test, IntersectionKernels.compute:35-40): not supported";
+            return TT_ERR_UNSUPPORTED;
+        }
+        tags[m] = mats[m].Tag;
+        any_invisible |= ((mats[m].Tag >> TT_FLAG_INVISIBLE) & 1u) != 0;
+    }
+    if (any_invisible) {
+        h.matdat.resize(n_tris);
+        for (uint32_t t = 0; t < n_tris; t++) h.matdat[t] = tris[t].MatDat;
+    }
+    Validator v(h);
+    if (!v.run()) {
+        why = v.why;
+        return TT_ERR_INVALID_ARG;
+    }
+    return TT_OK;
+}
+
 void derive_mesh(const tt_mesh_data& in, MeshGpu& o) {
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 4; c++) o.m[r * 4 + c] = in.W2L[c * 4 + r];
@@ -399,26 +435,12 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     TT_HIP(c, hipSetDevice(c->device));
     c->has_scene = false;
     SceneHost h;
-    h.nodes.assign(nodes, nodes + n_nodes);
-    h.tlas.assign(tlas, tlas + n_tlas);
-    h.mesh.assign(md, md + n_mesh);
-    h.n_tris = n_tris;
-    h.n_mat = n_mat;
+    std::vector<uint32_t> tags;
     bool any_invisible = false;
-    std::vector<uint32_t> tags(std::max<uint32_t>(n_mat, 1u), 0u);
-    for (uint32_t m = 0; m < n_mat; m++) {
-        if (mats[m].MatType == TT_MAT_CUTOUT_INDEX)
-            return fail(c, TT_ERR_UNSUPPORTED,
-                        "material %u is Cutout (alpha-atlas test, IntersectionKernels.compute:35-40) — not supported", m);
-        tags[m] = mats[m].Tag;
-        any_invisible |= ((mats[m].Tag >> TT_FLAG_INVISIBLE) & 1u) != 0;
-    }
-    if (any_invisible) {
-        h.matdat.resize(n_tris);
-        for (uint32_t t = 0; t < n_tris; t++) h.matdat[t] = tris[t].MatDat;
-    }
-    Validator v(h);
-    if (!v.run()) return fail(c, TT_ERR_INVALID_ARG, "scene validation failed: %s", v.why.c_str());
+    std::string why;
+    const tt_status vs = check_scene(nodes, n_nodes, tris, n_tris, tlas, n_tlas, md, n_mesh, mats, n_mat, h, tags,
+                                     any_invisible, why);
+    if (vs != TT_OK) return fail(c, vs, "scene validation failed: %s", why.c_str());
     std::vector<TriPos> tp(n_tris);
     for (uint32_t t = 0; t < n_tris; t++) derive_tri(tris[t], tp[t]);
     std::vector<MeshGpu> mg(n_mesh);
@@ -447,6 +469,22 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->any_invisible = any_invisible;
     c->has_scene = true;
     return TT_OK;
+}
+
+tt_status tt_scene_validate(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris, uint32_t n_tris,
+                            const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md, uint32_t n_mesh,
+                            const tt_material* mats, uint32_t n_mat, char* why, uint32_t why_len) {
+    SceneHost h;
+    std::vector<uint32_t> tags;
+    bool any_invisible = false;
+    std::string w;
+    const tt_status st = check_scene(nodes, n_nodes, tris, n_tris, tlas, n_tlas, md, n_mesh, mats, n_mat, h, tags,
+                                     any_invisible, w);
+    if (why && why_len) {
+        std::strncpy(why, w.c_str(), why_len - 1);
+        why[why_len - 1] = 0;
+    }
+    return st;
 }
 
 tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {

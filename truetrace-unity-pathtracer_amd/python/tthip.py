@@ -148,7 +148,7 @@ _HIP = None
 HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_destroy", "tt_last_error",
                "tt_scene_upload", "tt_scene_update_nodes", "tt_scene_update_meshdata", "tt_scene_bytes",
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
-               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read"]
+               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read", "tt_scene_validate"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
@@ -228,6 +228,8 @@ def hip_lib():
         L.tt_resolve_normals.argtypes = [vp, C.POINTER(TraceParams), vp, vp]
         L.tt_generate_primary.argtypes = [vp, C.POINTER(Camera), vp]
         L.tt_enqueue_diffuse_bounce.argtypes = [vp, C.POINTER(TraceParams), vp, i32, i32, C.POINTER(u32)]
+        L.tt_scene_validate.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, C.c_char_p, u32]
+        L.tt_scene_validate.restype = i32
         L.tt_timing_reset.argtypes = [vp]
         L.tt_timing_read.argtypes = [vp, vp, u32, C.POINTER(u32)]
         for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
@@ -581,6 +583,15 @@ class Engine:
         self._check(self.L.tt_enqueue_diffuse_bounce(self.h, C.byref(p), _ptr(rays), frames, max_bounce,
                                                      C.byref(n)), "tt_enqueue_diffuse_bounce")
         return n.value
+
+
+def validate(s: Scene):
+    """tt_scene_validate: (status, message) of the structural check tt_scene_upload runs."""
+    buf = C.create_string_buffer(512)
+    st = hip_lib().tt_scene_validate(_ptr(s.nodes), len(s.nodes), _ptr(s.tris), len(s.tris), _ptr(s.tlas),
+                                     len(s.tlas), _ptr(s.meshdata), len(s.meshdata), _ptr(s.materials),
+                                     len(s.materials), buf, 512)
+    return st, buf.value.decode()
 
 
 def device_count() -> int:
