@@ -127,8 +127,10 @@ static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray
             const float t = f * vdot(posedge2, q);
             if (t > 0 && t < ray_hit->t) {
                 ++*accepts;
-                if (s->n_mat) {
-                    const int MaterialIndex = MatOffset + (int)T->MatDat;
+                /* _Materials[MatOffset + MatDat]; an out-of-range StructuredBuffer read returns zeros
+                 * in D3D, i.e. a material with no flags (MatType 0, Tag 0) */
+                const int MaterialIndex = MatOffset + (int)T->MatDat;
+                if (MaterialIndex >= 0 && (uint32_t)MaterialIndex < s->n_mat) {
                     const tt_material* m = &s->mats[MaterialIndex];
                     if (m->MatType == TT_MAT_CUTOUT_INDEX) return 3;
                     if (CurBounce == 0 && ((((int)m->Tag) >> TT_FLAG_INVISIBLE) & 1) == 1) return 0;

@@ -198,9 +198,3 @@ def test_validator_rejects_malformed():
     meta = int(nodes[2]["meta"][0]) & ~0xFF
     nodes[2]["meta"][0] = meta | (0b111 << 5) | 23
     assert tthip.validate(tthip.Scene(nodes, sc.tris, sc.tlas, sc.meshdata, sc.materials))[0] == tthip.TT_ERR_INVALID_ARG
-    # Invisible materials: MaterialOffset + MatDat must stay inside _Materials
-    mats = np.zeros(1, tthip.MAT_DTYPE)
-    mats[0]["Tag"] = 1 << tthip.FLAG_INVISIBLE
-    tris = sc.tris.copy()
-    tris["MatDat"] = 1
-    assert tthip.validate(tthip.Scene(sc.nodes, tris, sc.tlas, sc.meshdata, mats))[0] == tthip.TT_ERR_INVALID_ARG

@@ -105,3 +105,13 @@ def test_zero_rays_and_bad_args():
     assert O.trace(sc, rays, 0, 0, 1000.0, n, 1)[0] == 0
     assert np.array_equal(before, rays)
     assert O.trace(sc, rays, 1, 0, 1000.0, 0, 1)[0] == tthip.TT_ERR_INVALID_ARG
+
+
+def test_out_of_range_material_reads_as_zero():
+    """D3D returns zeros for an out-of-range StructuredBuffer read: a triangle whose
+    MaterialOffset + MatDat is past _Materials behaves as an unflagged material."""
+    sc, rays, exp0, exp1 = K.case_invisible_bounce0()
+    sc.tris["MatDat"][1] = 5  # past the 2-entry material buffer: not invisible any more
+    r = rays.copy()
+    assert O.trace(sc, r, 1, 0, 1000.0, 1, 1)[0] == 0
+    assert r["hits"][0].tolist() == exp1

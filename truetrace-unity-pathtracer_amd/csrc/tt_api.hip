@@ -220,10 +220,7 @@ struct Validator {
                 mm = max_matdat;
                 seen.push_back(Seen{key, root, mm});
             }
-            if (!s.matdat.empty() && (md.MaterialOffset < 0 || (uint64_t)md.MaterialOffset + mm >= s.n_mat)) {
-                why = "MaterialOffset + MatDat out of range for mesh " + std::to_string(m);
-                return false;
-            }
+
         }
         return true;
     }
@@ -584,6 +581,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.tlas = c->tlas.p;
     a.mesh = c->mesh.p;
     a.mat_tag = c->mat_tag.p;
+    a.n_mat = c->host.n_mat;
     a.rays = d_rays;
     a.info = d_info;
     a.colors = d_colors;

@@ -46,6 +46,7 @@ struct TraceArgs {
     const int32_t* tlas;         // TLASBVH8Indices
     const MeshGpu* mesh;         // traversal-layout mesh records
     const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
+    uint32_t n_mat;
     tt_ray_data* rays;           // GlobalRays
     uint32_t* info;              // _PrimaryTriangleInfo (uint4 per pixel), nullable
     const tt_col_data* colors;   // GlobalColors (bounce > 0 with info)

@@ -90,7 +90,7 @@ struct Best {
 // Evaluated branch-free; the accept predicate is exactly the reference's nested conditions.
 template <bool MATCHECK>
 __device__ __forceinline__ bool intersect_triangle(const TriPos* __restrict__ tris, const uint32_t* __restrict__ mat_tag,
-                                                   int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
+                                                   uint32_t n_mat, int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
                                                    const LaneRay& r, Best& best) {
     const uint4* tp = reinterpret_cast<const uint4*>(tris + tri_id);
     const uint4 a = tp[0], b = tp[1], c = tp[2];
@@ -111,10 +111,13 @@ __device__ __forceinline__ bool intersect_triangle(const TriPos* __restrict__ tr
     const float qz = fma_(sx, e1y, -(sy * e1x));
     const float v = f * fma_(r.dz, qz, fma_(r.dy, qy, r.dx * qx));
     const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
-    bool accept = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best.t);
+    const bool cand = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best.t);
+    bool accept = cand;
     if (MATCHECK && accept) {
-        // GetFlag(_Materials[MatOffset + MatDat].Tag, Invisible) at CurBounce == 0 (:48)
-        const uint32_t tag = mat_tag[mat_offset + (int32_t)c.y];
+        // GetFlag(_Materials[MatOffset + MatDat].Tag, Invisible) at CurBounce == 0 (:48); an
+        // out-of-range StructuredBuffer read returns zeros in D3D (no flags)
+        const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
+        const uint32_t tag = mi < n_mat ? mat_tag[mi] : 0u;
         if ((tag >> TT_FLAG_INVISIBLE) & 1u) accept = false;
     }
     if (accept) {
@@ -124,7 +127,7 @@ __device__ __forceinline__ bool intersect_triangle(const TriPos* __restrict__ tr
         best.mesh_id = mesh_id;
         best.tri_id = tri_id;
     }
-    return accept;
+    return cand;  // counted as an "accept" (candidate passed the t test) before the material check
 }
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
-            const bool acc = intersect_triangle<MATCHECK>(A.tris, A.mat_tag, (int32_t)(tg.x + ti), mesh_id,
+            const bool acc = intersect_triangle<MATCHECK>(A.tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), mesh_id,
                                                           MatOffset, ray, best);
             if (STATS) {
                 c_tris++;
