@@ -266,6 +266,11 @@ tt_status tt_trace_closest(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* g
 tt_status tt_timing_reset(tt_ctx* ctx);
 tt_status tt_timing_read(tt_ctx* ctx, float* ms, uint32_t max, uint32_t* n);
 
+/* SIMD-efficiency diagnostics of the last synchronous TT_TRACE_STATS launch: wave loop
+ * iterations, iterations with node-phase work, node-phase lanes, iterations with triangle-phase
+ * work, triangle-phase lanes, active lanes (sums over waves); out8[6..7] reserved. */
+tt_status tt_trace_diagnostics(const tt_ctx* ctx, uint64_t* out8);
+
 /* Wait for all work issued on the context's stream. */
 tt_status tt_sync(tt_ctx* ctx);
 /* The hipStream_t the context issues on. */

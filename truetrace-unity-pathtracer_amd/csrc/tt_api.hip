@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -16,6 +17,8 @@
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
 hipError_t tt_trace_occupancy(int* blocks_per_cu);
 uint32_t tt_trace_block_size();
+uint32_t tt_trace_spill_entries();
+uint32_t tt_trace_lds_bytes();
 hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uint32_t h, float near_plane, float far_plane,
                               int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays, hipStream_t st);
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
@@ -91,6 +94,8 @@ struct tt_ctx {
     DevBuf<float> st_normals;
     DevBuf<float> cam;          // 32 floats: cam_to_world | cam_inv_proj
     DevBuf<uint32_t> counter;   // bounce enqueue counter
+    DevBuf<uint2> spill;        // deep traversal-stack entries (tt_trace_spill_entries() per thread)
+    unsigned long long last_diag[8] = {};
 };
 
 namespace {
@@ -344,7 +349,16 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     c->num_cus = prop.multiProcessorCount;
     int bpc = 0;
     if (tt_trace_occupancy(&bpc) != hipSuccess || bpc <= 0) bpc = 2;
+    // Residency check beyond the occupancy API: measured on MI355X, five 32-KiB-LDS blocks were
+    // not co-resident (the fifth started only when another exited), consistent with the LDS being
+    // allocated per half-CU (2 x 80 KiB). Size the persistent grid so every block is resident.
+    const uint32_t lds_block = tt_trace_lds_bytes();
+    if (lds_block) bpc = std::min<int>(bpc, 2 * (int)((80u * 1024u) / lds_block));
     c->blocks_per_cu = std::min(bpc, 8);
+    if (const char* e = std::getenv("TT_BLOCKS_PER_CU")) {  // tuning/diagnostic knob
+        const int v = std::atoi(e);
+        if (v > 0 && v <= c->blocks_per_cu) c->blocks_per_cu = v;
+    }
     c->grid = (uint32_t)(c->num_cus * c->blocks_per_cu);
     if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess) {
         tt_ctx_destroy(c);
@@ -354,6 +368,12 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
         if (hipEventCreate(&c->ring0[i]) != hipSuccess || hipEventCreate(&c->ring1[i]) != hipSuccess) {
             tt_ctx_destroy(c);
             return TT_ERR_HIP;
+        }
+    }
+    if (const uint32_t se = tt_trace_spill_entries()) {
+        if (c->spill.alloc((size_t)se * c->grid * tt_trace_block_size()) != hipSuccess) {
+            tt_ctx_destroy(c);
+            return TT_ERR_OOM;
         }
     }
     c->max_rays = cfg->max_rays;
@@ -384,6 +404,7 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->st_normals.release();
     c->cam.release();
     c->counter.release();
+    c->spill.release();
     if (c->ctl) (void)hipFree(c->ctl);
     for (uint32_t i = 0; i < TT_RING; i++) {
         if (c->ring0[i]) (void)hipEventDestroy(c->ring0[i]);
@@ -412,6 +433,12 @@ tt_status tt_timing_read(tt_ctx* c, float* ms, uint32_t max, uint32_t* n) {
         TT_HIP(c, hipEventElapsedTime(&ms[i], c->ring0[slot], c->ring1[slot]));
     }
     *n = k;
+    return TT_OK;
+}
+
+tt_status tt_trace_diagnostics(const tt_ctx* c, uint64_t* out8) {
+    if (!c || !out8) return TT_ERR_INVALID_ARG;
+    for (int k = 0; k < 8; k++) out8[k] = c->last_diag[k];
     return TT_OK;
 }
 
@@ -586,6 +613,8 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.info = d_info;
     a.colors = d_colors;
     a.ctl = c->ctl;
+    a.spill = c->spill.p;
+    if (const char* e = std::getenv("TT_DIAG_TIMES_PTR")) a.diag_times = reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0));
     a.n_rays = p->n_rays;
     a.ray_offset = off;
     a.width = p->screen_width;
@@ -627,6 +656,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
             stats->reps_exhausted = ctl.stats[5];
             stats->stack_overflows = ctl.stats[6];
             stats->accepts = ctl.stats[7];
+            for (int k = 0; k < 8; k++) c->last_diag[k] = ctl.diag[k];
         }
         stats->stack_overflows = std::max<uint64_t>(stats->stack_overflows, ctl.err_overflow);
     }

@@ -33,11 +33,13 @@ static_assert(sizeof(MeshGpu) == 64, "MeshGpu is 64 bytes");
 
 // Control block, zeroed by hipMemsetAsync before every trace launch.
 struct TraceControl {
-    uint32_t next_ray;        // work counter (chunks of rays)
+    uint32_t seg_ticket[8 * 32];  // per-segment dequeue tickets, one 128-B line each
     uint32_t err_overflow;    // rays that overflowed the 16-entry stack
     uint32_t err_unsupported; // cutout material reached (never with a validated scene)
-    uint32_t pad;
+    uint32_t pad[2];
     unsigned long long stats[8];  // rays, nodes, tris, blas, hits, reps_exhausted, overflow, accepts
+    unsigned long long diag[8];   // STATS-build SIMD diagnostics: wave iterations, node-phase iterations,
+                                  // node-phase lanes, tri-phase iterations, tri-phase lanes, active lanes
 };
 
 struct TraceArgs {
@@ -51,6 +53,8 @@ struct TraceArgs {
     uint32_t* info;              // _PrimaryTriangleInfo (uint4 per pixel), nullable
     const tt_col_data* colors;   // GlobalColors (bounce > 0 with info)
     TraceControl* ctl;
+    uint2* spill;                // traversal-stack entries beyond TT_LDS_STACK, [entry][thread]
+    unsigned long long* diag_times;  // TT_DIAG_TIMES builds: per wave (start, end, rays)
     uint32_t n_rays;
     uint32_t ray_offset;         // W*H on odd bounces
     uint32_t width, height;

@@ -18,9 +18,37 @@
 
 #define TT_WAVE 64
 #define TT_BLOCK 256
-#define TT_CHUNK 256
+#ifndef TT_SEGS
+#define TT_SEGS 8         // ray-range segments, one per XCD group (blockIdx % 8), with stealing
+#endif
+#ifndef TT_CHUNK_BIG
+#define TT_CHUNK_BIG 64   // rays per dequeue over the first 3/4 of a segment
+#endif
+#ifndef TT_CHUNK_SMALL
+#define TT_CHUNK_SMALL 64 // rays per dequeue over the last quarter (shortens the tail)
+#endif
 #ifndef TT_REFILL_MIN
-#define TT_REFILL_MIN 16
+#define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
+#endif
+#ifndef TT_LDS_STACK
+#define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
+#endif
+#ifndef TT_WAVES_PER_EU
+#define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
+#endif
+#ifndef TT_TRI_LOOP
+#define TT_TRI_LOOP 0     // 0: one triangle per lane per pass; 1: drain the lane's triangles
+#endif
+#ifndef TT_PREFETCH
+#define TT_PREFETCH 0     // 1: issue the next node's loads as soon as its index is known
+#endif
+#ifndef TT_WRAY_RELOAD
+#define TT_WRAY_RELOAD 0  // 1: re-read the world-space ray from GlobalRays on BLAS exit
+#endif
+#if TT_WAVES_PER_EU > 0
+#define TT_BOUNDS __launch_bounds__(TT_BLOCK, TT_WAVES_PER_EU)
+#else
+#define TT_BOUNDS __launch_bounds__(TT_BLOCK)
 #endif
 
 namespace {
@@ -144,14 +172,43 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
 template <bool STATS, bool MATCHECK, int INFO>
-__global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
-    __shared__ uint2 s_stack[TT_STACK_SIZE][TT_BLOCK];
+__global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
+    __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
+    const uint32_t gtid = blockIdx.x * TT_BLOCK + tid;
+    const uint32_t spill_stride = gridDim.x * TT_BLOCK;
+    uint2* __restrict__ spill = A.spill;
+    (void)gtid;
+    (void)spill_stride;
+    (void)spill;
+#define TT_PUSH(val, ok)                                                            \
+    do {                                                                            \
+        if (stack_size == TT_STACK_SIZE) {                                          \
+            ok = false;                                                             \
+        } else {                                                                    \
+            if (TT_LDS_STACK >= TT_STACK_SIZE || stack_size < TT_LDS_STACK)         \
+                s_stack[stack_size][tid] = (val);                                   \
+            else                                                                    \
+                spill[(size_t)(stack_size - TT_LDS_STACK) * spill_stride + gtid] = (val); \
+            stack_size++;                                                           \
+        }                                                                           \
+    } while (0)
+#define TT_POP(dst)                                                                 \
+    do {                                                                            \
+        --stack_size;                                                               \
+        if (TT_LDS_STACK >= TT_STACK_SIZE || stack_size < TT_LDS_STACK)             \
+            dst = s_stack[stack_size][tid];                                         \
+        else                                                                        \
+            dst = spill[(size_t)(stack_size - TT_LDS_STACK) * spill_stride + gtid]; \
+    } while (0)
     const uint32_t lane = tid & (TT_WAVE - 1);
 
-    // wave-uniform ray pool
+    // wave-uniform scheduler state: a private pool [pool_next, pool_end) of work indices, refilled
+    // from segment `seg` (segments = contiguous 1/TT_SEGS slices of the work range, dealt to XCD
+    // groups by blockIdx % TT_SEGS for L2 locality; exhausted segments are stolen from in turn)
     uint32_t pool_next = 0, pool_end = 0;
-    bool exhausted = false;
+    uint32_t seg = blockIdx.x % TT_SEGS, segs_left = TT_SEGS;
+    const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
 
     // lane traversal state (IntersectionKernels.compute:62-77)
     bool active = false;
@@ -163,22 +220,79 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
     int32_t stack_size = 0, tlas_ss = -1;
     int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
+    uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
+#if TT_PREFETCH
+    // next node of this lane, loaded as soon as its index is known (the group on top decides it:
+    // IntersectionKernels.compute:158-161), so its latency overlaps the leaf triangle tests
+    uint32_t pf_idx = 0xffffffffu;
+    uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0, pf2 = pf0, pf3 = pf0, pf4 = pf0;
+#define TT_PREFETCH_NEXT()                                                             \
+    do {                                                                               \
+        if (active && (cg.y & 0xff000000u)) {                                          \
+            const uint32_t pcio = firstbithigh(cg.y);                                  \
+            const uint32_t pslot = (pcio - 24u) ^ (oct & 0xffu);                       \
+            const uint32_t pchild = cg.x + __builtin_popcount(cg.y & ~(0xffffffffu << pslot)); \
+            if (pchild != pf_idx) {                                                    \
+                const uint4* pp = A.nodes + (size_t)pchild * 5u;                       \
+                pf0 = pp[0]; pf1 = pp[1]; pf2 = pp[2]; pf3 = pp[3]; pf4 = pp[4];       \
+                pf_idx = pchild;                                                       \
+            }                                                                          \
+        }                                                                              \
+    } while (0)
+#else
+#define TT_PREFETCH_NEXT() do {} while (0)
+#endif
+    // world-space ray (ray2, IntersectionKernels.compute:151): kept in registers, or re-read from
+    // GlobalRays with the same correctly rounded reciprocals (bit-identical either way)
+    auto world_ray = [&]() -> LaneRay {
+#if TT_WRAY_RELOAD
+        const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
+        const uint4 r0 = rp[0], r1 = rp[1];
+        LaneRay w;
+        w.ox = __uint_as_float(r0.x);
+        w.oy = __uint_as_float(r0.y);
+        w.oz = __uint_as_float(r0.z);
+        w.dx = __uint_as_float(r1.x);
+        w.dy = __uint_as_float(r1.y);
+        w.dz = __uint_as_float(r1.z);
+        w.ix = 1.0f / w.dx;
+        w.iy = 1.0f / w.dy;
+        w.iz = 1.0f / w.dz;
+        return w;
+#else
+        return wray;
+#endif
+    };
 
+#ifdef TT_DIAG_TIMES
+    const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
+#endif
     while (true) {
         // ---------------------------------------------------------------- refill
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
-        const bool pool_dry = exhausted && pool_next >= pool_end;
+        const bool pool_dry = segs_left == 0 && pool_next >= pool_end;
         if (n_idle == TT_WAVE && pool_dry) break;
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
-            if (avail < n_idle && !exhausted) {
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(&A.ctl->next_ray, (uint32_t)TT_CHUNK);
-                new_base = __builtin_amdgcn_readfirstlane(b);
-                if (new_base < A.n_rays) new_count = min((uint32_t)TT_CHUNK, A.n_rays - new_base);
-                if (new_base + (uint32_t)TT_CHUNK >= A.n_rays) exhausted = true;
+            while (avail < n_idle && segs_left > 0) {  // wave-uniform dequeue, one atomic per chunk
+                uint32_t t = 0;
+                if (lane == 0) t = atomicAdd(&A.ctl->seg_ticket[seg * 32u], 1u);
+                t = __builtin_amdgcn_readfirstlane(t);
+                const uint32_t lo = (uint32_t)(((uint64_t)n_tiles * seg / TT_SEGS) << 6);
+                const uint32_t hi = min((uint32_t)(((uint64_t)n_tiles * (seg + 1) / TT_SEGS) << 6), A.n_rays);
+                const uint32_t len = hi > lo ? hi - lo : 0u;
+                const uint32_t k1 = (len - len / 4u) / TT_CHUNK_BIG;
+                const uint32_t start = t < k1 ? t * TT_CHUNK_BIG : k1 * TT_CHUNK_BIG + (t - k1) * TT_CHUNK_SMALL;
+                const uint32_t size = t < k1 ? TT_CHUNK_BIG : TT_CHUNK_SMALL;
+                if (start < len) {
+                    new_base = lo + start;
+                    new_count = min(size, len - start);
+                    break;
+                }
+                seg = seg + 1u == TT_SEGS ? 0u : seg + 1u;
+                segs_left--;
             }
             const uint32_t take_old = min(avail, n_idle);
             const uint32_t take_new = min(n_idle - take_old, new_count);
@@ -213,7 +327,9 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                 ray.ix = 1.0f / ray.dx;
                 ray.iy = 1.0f / ray.dy;
                 ray.iz = 1.0f / ray.dz;
+#if !TT_WRAY_RELOAD
                 wray = ray;
+#endif
                 oct = octant_inv4(ray);
                 best.t = A.far_plane;
                 best.u = 0.0f;
@@ -230,12 +346,25 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                 mesh_id = -1;
                 Reps = 0;
                 active = true;
+#ifdef TT_DIAG_TIMES
+                c_rays++;
+#else
                 if (STATS) c_rays++;
+#endif
             }
         }
 
         // ------------------------------------------------------------- node phase
         bool finish = false;
+        if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)
+            const uint64_t nm = __ballot(active && tg.y == 0u && Reps < TT_MAX_REPS && (cg.y & 0xff000000u));
+            if (lane == 0) {
+                d_iter++;
+                d_node_lanes += (uint32_t)__popcll(nm);
+                d_node_iters += nm ? 1u : 0u;
+                d_active_lanes += (uint32_t)__popcll(__ballot(active));
+            }
+        }
         if (active && tg.y == 0u) {
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
@@ -248,13 +377,20 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                     const uint32_t child = cg.x + rel;
                     cg.y &= ~(1u << cio);
                     bool ok = true;
-                    if (cg.y & 0xff000000u) {
-                        if (stack_size == TT_STACK_SIZE) ok = false;
-                        else s_stack[stack_size++][tid] = cg;
-                    }
+                    if (cg.y & 0xff000000u) TT_PUSH(cg, ok);
                     if (ok) {
+#if TT_PREFETCH
+                        uint4 n0, n1, n2, n3, n4;
+                        if (pf_idx == child) {
+                            n0 = pf0; n1 = pf1; n2 = pf2; n3 = pf3; n4 = pf4;
+                        } else {
+                            const uint4* np = A.nodes + (size_t)child * 5u;
+                            n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3]; n4 = np[4];
+                        }
+#else
                         const uint4* np = A.nodes + (size_t)child * 5u;
                         const uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
+#endif
                         const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
                         cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
                         tg.y = hitmask & 0x00ffffffu;
@@ -282,14 +418,8 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                     NodeOffset = mo4.y;
                     TriOffset = mo4.x;
                     bool ok = true;
-                    if (tg.y != 0u) {
-                        if (stack_size == TT_STACK_SIZE) ok = false;
-                        else s_stack[stack_size++][tid] = tg;
-                    }
-                    if (ok && (cg.y & 0xff000000u)) {
-                        if (stack_size == TT_STACK_SIZE) ok = false;
-                        else s_stack[stack_size++][tid] = cg;
-                    }
+                    if (tg.y != 0u) TT_PUSH(tg, ok);
+                    if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
                     if (ok) {
                         tlas_ss = stack_size;
                         MatOffset = mo4.z;
@@ -323,21 +453,39 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                             NodeOffset = 0;
                             TriOffset = 0;
                             tlas_ss = -1;
-                            ray = wray;
+                            ray = world_ray();
                             oct = octant_inv4(ray);
                         }
-                        cg = s_stack[--stack_size][tid];
+                        TT_POP(cg);
                     }
                 }
             }
         }
 
+        TT_PREFETCH_NEXT();
+
+        if (STATS) {
+            const uint64_t tm = __ballot(active && tg.y != 0u);
+            if (lane == 0) {
+                d_tri_lanes += (uint32_t)__popcll(tm);
+                d_tri_iters += tm ? 1u : 0u;
+            }
+        }
         // --------------------------------------------------------- triangle phase
+#if TT_TRI_LOOP
+        while (active && tg.y != 0u) {  // :220-226, highest bit first, drain the lane's leaf bits
+#else
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
+#endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
+#ifdef TT_EXP_NO_TRI
+            const bool acc = false;
+            if (best.t == -1.0f) best.tri_id = (int32_t)(tg.x + ti);
+#else
             const bool acc = intersect_triangle<MATCHECK>(A.tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), mesh_id,
                                                           MatOffset, ray, best);
+#endif
             if (STATS) {
                 c_tris++;
                 c_acc += acc ? 1u : 0u;
@@ -350,11 +498,12 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                         NodeOffset = 0;
                         TriOffset = 0;
                         tlas_ss = -1;
-                        ray = wray;
+                        ray = world_ray();
                         oct = octant_inv4(ray);
                     }
-                    cg = s_stack[--stack_size][tid];
+                    TT_POP(cg);
                 }
+                TT_PREFETCH_NEXT();
             }
         }
 
@@ -375,6 +524,7 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                     } else {
                         const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
                         if (w == -1.0f || (float)A.bounce == w) {
+                            const LaneRay wr = world_ray();
                             write = true;
                             const bool miss = best.t == A.far_plane;
                             if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
@@ -383,13 +533,13 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                                 o.y = (uint32_t)(best.tri_id - to);
                                 o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
                             } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
-                                o.x = __float_as_uint(wray.dx);
-                                o.y = __float_as_uint(wray.dy);
-                                o.z = __float_as_uint(wray.dz);
+                                o.x = __float_as_uint(wr.dx);
+                                o.y = __float_as_uint(wr.dy);
+                                o.z = __float_as_uint(wr.dz);
                             } else {
-                                o.x = __float_as_uint(wray.dx * best.t + wray.ox);
-                                o.y = __float_as_uint(wray.dy * best.t + wray.oy);
-                                o.z = __float_as_uint(wray.dz * best.t + wray.oz);
+                                o.x = __float_as_uint(wr.dx * best.t + wr.ox);
+                                o.y = __float_as_uint(wr.dy * best.t + wr.oy);
+                                o.z = __float_as_uint(wr.dz * best.t + wr.oz);
                             }
                             o.w = miss ? 1u : 0u;
                         }
@@ -398,13 +548,29 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
                 }
             }
             const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+#ifndef TT_EXP_NO_STORE
             reinterpret_cast<uint4*>(R)[2] =
                 make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+#else
+            if (best.t == -12345.0f) reinterpret_cast<uint4*>(R)[2] = make_uint4(0, 0, 0, uv);
+#endif
             if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
             active = false;
         }
     }
 
+#ifdef TT_DIAG_TIMES
+    {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t rays_done = wave_sum(c_rays);
+        if (lane == 0 && A.diag_times) {
+            const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
+            A.diag_times[3 * w + 0] = t_begin;
+            A.diag_times[3 * w + 1] = t_end;
+            A.diag_times[3 * w + 2] = rays_done;
+        }
+    }
+#endif
     if (STATS) {
         const uint32_t v[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
                                wave_sum(c_hits), wave_sum(c_reps), wave_sum(c_ovf), wave_sum(c_acc)};
@@ -412,6 +578,9 @@ __global__ __launch_bounds__(TT_BLOCK) void tt_trace_kernel(TraceArgs A) {
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 if (v[k]) atomicAdd(&A.ctl->stats[k], (unsigned long long)v[k]);
+            const uint32_t d[6] = {d_iter, d_node_iters, d_node_lanes, d_tri_iters, d_tri_lanes, d_active_lanes};
+#pragma unroll
+            for (int k = 0; k < 6; k++) atomicAdd(&A.ctl->diag[k], (unsigned long long)d[k]);
         }
     }
 }
@@ -441,3 +610,5 @@ hipError_t tt_trace_occupancy(int* blocks_per_cu) {
 }
 
 uint32_t tt_trace_block_size() { return TT_BLOCK; }
+uint32_t tt_trace_lds_bytes() { return (uint32_t)(TT_LDS_STACK * TT_BLOCK * sizeof(uint2)); }
+uint32_t tt_trace_spill_entries() { return TT_LDS_STACK >= TT_STACK_SIZE ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK); }

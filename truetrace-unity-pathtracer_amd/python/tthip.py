@@ -148,7 +148,7 @@ _HIP = None
 HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_destroy", "tt_last_error",
                "tt_scene_upload", "tt_scene_update_nodes", "tt_scene_update_meshdata", "tt_scene_bytes",
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
-               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read", "tt_scene_validate"]
+               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
@@ -206,7 +206,7 @@ def hip_lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        path = os.path.join(LIB_DIR, "libtruetrace_hip.so")
+        path = os.environ.get("TT_HIP_LIB") or os.path.join(LIB_DIR, "libtruetrace_hip.so")
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: the HIP engine was not built (no fallback exists)")
         L = C.CDLL(path)
@@ -230,6 +230,8 @@ def hip_lib():
         L.tt_enqueue_diffuse_bounce.argtypes = [vp, C.POINTER(TraceParams), vp, i32, i32, C.POINTER(u32)]
         L.tt_scene_validate.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, C.c_char_p, u32]
         L.tt_scene_validate.restype = i32
+        L.tt_trace_diagnostics.argtypes = [vp, vp]
+        L.tt_trace_diagnostics.restype = i32
         L.tt_timing_reset.argtypes = [vp]
         L.tt_timing_read.argtypes = [vp, vp, u32, C.POINTER(u32)]
         for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
@@ -538,6 +540,12 @@ class Engine:
         n = C.c_uint32()
         self._check(self.L.tt_timing_read(self.h, ms.ctypes.data, 256, C.byref(n)), "tt_timing_read")
         return ms[: n.value].copy()
+
+    def diagnostics(self) -> dict:
+        d = np.zeros(8, np.uint64)
+        self._check(self.L.tt_trace_diagnostics(self.h, d.ctypes.data), "tt_trace_diagnostics")
+        keys = ["iterations", "node_iters", "node_lanes", "tri_iters", "tri_lanes", "active_lanes"]
+        return {k: int(v) for k, v in zip(keys, d[:6])}
 
     def scene_bytes(self) -> int:
         b = C.c_uint64()
