@@ -1,0 +1,127 @@
+// TrueTraceHip.cs — P/Invoke binding a TrueTrace maintainer adds to call the MI355X engine
+// (libtruetrace_hip.so, include/truetrace_hip.h) in place of the kernel_trace dispatch.
+//
+// Style follows the reference's only native-plugin boundary,
+// TrueTrace/Resources/Utility/UnityDenoiserPlugin/UnityDenoiserPlugin.cs:14-85: blittable
+// [StructLayout(Sequential)] structs, an IntPtr handle owned by an IDisposable wrapper.
+// Not compiled in this repository (no .NET toolchain in the build image); the struct layouts are
+// checked against the C header by tests/test_abi.py through the Python mirror of the same ABI.
+using System;
+using System.Runtime.InteropServices;
+
+namespace TrueTrace.Hip
+{
+    public enum TTStatus : int
+    {
+        Ok = 0, InvalidArg = 1, OutOfMemory = 2, Hip = 3, Unsupported = 4, StackOverflow = 5, NoDevice = 6, NoScene = 7
+    }
+
+    [Flags]
+    public enum TTTraceFlags : uint
+    {
+        None = 0, DevicePtrs = 1u << 0, UseReSTIRGI = 1u << 1, UseASVGF = 1u << 2, Stats = 1u << 3, Async = 1u << 4
+    }
+
+    [StructLayout(LayoutKind.Sequential)]
+    public struct TTConfig
+    {
+        public int device;
+        public uint flags;
+        public ulong maxRays;
+        public IntPtr stream;
+    }
+
+    [StructLayout(LayoutKind.Sequential)]
+    public struct TTTraceParams
+    {
+        public uint nRays;        // BufferSizes[CurBounce].tracerays
+        public int bounce;        // CurBounce
+        public float farPlane;    // FarPlane
+        public uint screenWidth;
+        public uint screenHeight;
+        public TTTraceFlags flags;
+    }
+
+    [StructLayout(LayoutKind.Sequential)]
+    public struct TTStats
+    {
+        public ulong rays, nodeVisits, triTests, blasEntries, hits, repsExhausted, stackOverflows, accepts;
+        public float kernelMs;
+        public uint pad;
+    }
+
+    public static class Native
+    {
+        const string Lib = "truetrace_hip";
+        [DllImport(Lib)] public static extern TTStatus tt_ctx_create(ref TTConfig cfg, out IntPtr ctx);
+        [DllImport(Lib)] public static extern TTStatus tt_ctx_destroy(IntPtr ctx);
+        [DllImport(Lib)] public static extern IntPtr tt_last_error(IntPtr ctx);
+        [DllImport(Lib)] public static extern int tt_device_count();
+        // Element types are the reference's own host structs: BVHNode8DataCompressed (80 B),
+        // CudaTriangle (88 B), int, MyMeshDataCompacted (88 B), MaterialData (252 B).
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload(IntPtr ctx,
+            void* nodes, uint nNodes, void* tris, uint nTris, int* tlasIndices, uint nTlas,
+            void* meshData, uint nMesh, void* materials, uint nMat);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_update_nodes(IntPtr ctx, uint first, uint count, void* nodes);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_update_meshdata(IntPtr ctx, uint first, uint count, void* meshData);
+        // GlobalRays (RayData, 48 B, hits written in place), _PrimaryTriangleInfo (uint4 per pixel),
+        // GlobalColors (ColData, 64 B).
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_closest(IntPtr ctx, ref TTTraceParams p,
+            void* globalRays, uint* primaryInfo, void* globalColors, out TTStats stats);
+        [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
+    }
+
+    /// Replaces `cmd.DispatchCompute(IntersectionShader, TraceKernel, CurBounceInfoBuffer, 0)`
+    /// (RayTracingMaster.cs:964-970) and the buffer binding of AssetManager.SetMeshTraceBuffers
+    /// (AssetManager.cs:75-88) with calls into the HIP engine.
+    public sealed class TrueTraceHipTracer : IDisposable
+    {
+        IntPtr m_ctx;
+
+        public TrueTraceHipTracer(int device, ulong maxRays)
+        {
+            var cfg = new TTConfig { device = device, flags = 0, maxRays = maxRays, stream = IntPtr.Zero };
+            Check(Native.tt_ctx_create(ref cfg, out m_ctx));
+        }
+
+        /// AssetManager.SetMeshTraceBuffers: the same arrays the AssetManager uploads with
+        /// ComputeBuffer.SetData (AssetManager.cs:1760, :1762; ParentObject.cs:270-271).
+        public unsafe void SetMeshTraceBuffers<TNode, TTri, TMesh, TMat>(TNode[] nodes, TTri[] tris, int[] tlasIndices,
+                                                                        TMesh[] meshData, TMat[] materials)
+            where TNode : unmanaged where TTri : unmanaged where TMesh : unmanaged where TMat : unmanaged
+        {
+            fixed (TNode* n = nodes) fixed (TTri* t = tris) fixed (int* i = tlasIndices)
+            fixed (TMesh* m = meshData) fixed (TMat* mt = materials)
+                Check(Native.tt_scene_upload(m_ctx, n, (uint)nodes.Length, t, (uint)tris.Length, i, (uint)tlasIndices.Length,
+                                             m, (uint)meshData.Length, mt, (uint)materials.Length));
+        }
+
+        /// One kernel_trace dispatch for bounce `curBounce`.
+        public unsafe TTStats Trace<TRay, TCol>(TRay[] globalRays, uint nRays, int curBounce, float farPlane,
+                                                int width, int height, uint[] primaryInfo = null, TCol[] globalColors = null,
+                                                bool useReSTIRGI = false, bool useASVGF = false)
+            where TRay : unmanaged where TCol : unmanaged
+        {
+            var p = new TTTraceParams
+            {
+                nRays = nRays, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width, screenHeight = (uint)height,
+                flags = (useReSTIRGI ? TTTraceFlags.UseReSTIRGI : 0) | (useASVGF ? TTTraceFlags.UseASVGF : 0)
+            };
+            TTStats s;
+            fixed (TRay* r = globalRays) fixed (uint* info = primaryInfo) fixed (TCol* col = globalColors)
+                Check(Native.tt_trace_closest(m_ctx, ref p, r, info, col, out s));
+            return s;
+        }
+
+        void Check(TTStatus st)
+        {
+            if (st != TTStatus.Ok)
+                throw new InvalidOperationException($"truetrace_hip: {st}: {Marshal.PtrToStringAnsi(Native.tt_last_error(m_ctx))}");
+        }
+
+        public void Dispose()
+        {
+            if (m_ctx != IntPtr.Zero) { Native.tt_ctx_destroy(m_ctx); m_ctx = IntPtr.Zero; }
+        }
+    }
+}

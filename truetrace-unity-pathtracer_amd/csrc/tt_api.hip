@@ -15,7 +15,7 @@
 #define TT_RING 256u
 
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
-hipError_t tt_trace_occupancy(int* blocks_per_cu);
+hipError_t tt_trace_occupancy_table(int* out12);
 uint32_t tt_trace_block_size();
 uint32_t tt_trace_spill_entries();
 uint32_t tt_trace_lds_bytes();
@@ -70,6 +70,7 @@ struct tt_ctx {
     int num_cus = 0;
     int blocks_per_cu = 0;
     uint32_t grid = 0;
+    uint32_t grid_of[12] = {};  // resident persistent grid per kernel instantiation
     TraceControl* ctl = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
     hipEvent_t ring0[256] = {}, ring1[256] = {};
@@ -347,19 +348,22 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
         return TT_ERR_HIP;
     }
     c->num_cus = prop.multiProcessorCount;
-    int bpc = 0;
-    if (tt_trace_occupancy(&bpc) != hipSuccess || bpc <= 0) bpc = 2;
+    int occ[12];
+    (void)tt_trace_occupancy_table(occ);
     // Residency check beyond the occupancy API: measured on MI355X, five 32-KiB-LDS blocks were
     // not co-resident (the fifth started only when another exited), consistent with the LDS being
-    // allocated per half-CU (2 x 80 KiB). Size the persistent grid so every block is resident.
+    // allocated per half-CU (2 x 80 KiB). Size every persistent grid so all its blocks are resident.
     const uint32_t lds_block = tt_trace_lds_bytes();
-    if (lds_block) bpc = std::min<int>(bpc, 2 * (int)((80u * 1024u) / lds_block));
-    c->blocks_per_cu = std::min(bpc, 8);
-    if (const char* e = std::getenv("TT_BLOCKS_PER_CU")) {  // tuning/diagnostic knob
-        const int v = std::atoi(e);
-        if (v > 0 && v <= c->blocks_per_cu) c->blocks_per_cu = v;
+    const int lds_cap = lds_block ? 2 * (int)((80u * 1024u) / lds_block) : 8;
+    int knob = 0;
+    if (const char* e = std::getenv("TT_BLOCKS_PER_CU")) knob = std::atoi(e);  // tuning/diagnostic knob
+    for (int k = 0; k < 12; k++) {
+        int b = std::max(1, std::min(std::min(occ[k], lds_cap), 8));
+        if (knob > 0 && knob < b) b = knob;
+        c->grid_of[k] = (uint32_t)(c->num_cus * b);
     }
-    c->grid = (uint32_t)(c->num_cus * c->blocks_per_cu);
+    c->blocks_per_cu = (int)(c->grid_of[1] / c->num_cus);
+    c->grid = c->grid_of[1];
     if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess) {
         tt_ctx_destroy(c);
         return TT_ERR_OOM;
@@ -626,7 +630,8 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const bool matcheck = c->any_invisible && p->bounce == 0;
     const uint32_t waves_needed = (p->n_rays + 255u) / 256u;  // one TT_CHUNK per wave at least
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
-    const uint32_t grid = std::max(1u, std::min(c->grid, blocks_needed));
+    const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],
+                                                 blocks_needed));
     TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));

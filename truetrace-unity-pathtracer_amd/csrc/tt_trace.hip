@@ -605,8 +605,28 @@ hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int in
     return matcheck ? launch_info<false, true>(a, info, grid, st) : launch_info<false, false>(a, info, grid, st);
 }
 
-hipError_t tt_trace_occupancy(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, tt_trace_kernel<false, false, 1>, TT_BLOCK, 0);
+// Occupancy (resident blocks per CU) of every instantiation: they differ in registers, so each
+// launch sizes its persistent grid from its own entry. index = stats*6 + matcheck*3 + info.
+template <bool S, bool M, int I>
+static int occ_one() {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_trace_kernel<S, M, I>, TT_BLOCK, 0) != hipSuccess) b = 1;
+    return b;
+}
+hipError_t tt_trace_occupancy_table(int* out12) {
+    out12[0] = occ_one<false, false, 0>();
+    out12[1] = occ_one<false, false, 1>();
+    out12[2] = occ_one<false, false, 2>();
+    out12[3] = occ_one<false, true, 0>();
+    out12[4] = occ_one<false, true, 1>();
+    out12[5] = occ_one<false, true, 2>();
+    out12[6] = occ_one<true, false, 0>();
+    out12[7] = occ_one<true, false, 1>();
+    out12[8] = occ_one<true, false, 2>();
+    out12[9] = occ_one<true, true, 0>();
+    out12[10] = occ_one<true, true, 1>();
+    out12[11] = occ_one<true, true, 2>();
+    return hipGetLastError();
 }
 
 uint32_t tt_trace_block_size() { return TT_BLOCK; }

@@ -1,0 +1,66 @@
+"""ttdist — multi-GPU sharding of the trace path (one process per GPU).
+
+The reference is single-GPU. On an 8×MI355X node the scene is replicated per GPU (it is at most
+~1.5 GB) and the rays are sharded; rays never interact, so the only collective is an optional
+gather of the 16-byte hit records to rank 0 (RCCL via torch.distributed "nccl", or "gloo" on
+CPU in the tests).
+
+Two shardings:
+  * ``sample`` (weak scaling, bench.py default): every rank traces its own full-frame sample of
+    the same view (``frames_accumulated = rank`` selects the sub-pixel jitter).
+  * ``tiles`` (strong scaling): the screen is cut into ``tile``×``tile`` pixel
+    tiles dealt round-robin to ranks (balances sky-heavy and geometry-heavy regions); each rank
+    builds a compact ray list of its pixels and the hit records are gathered and scattered back
+    into screen order on rank 0.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+
+
+def tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64) -> np.ndarray:
+    """Pixel indices owned by ``rank`` under round-robin tile sharding, in tile order."""
+    tx, ty = (width + tile - 1) // tile, (height + tile - 1) // tile
+    out = []
+    for t in range(rank, tx * ty, world):
+        x0, y0 = (t % tx) * tile, (t // tx) * tile
+        ys, xs = np.meshgrid(np.arange(y0, min(y0 + tile, height)), np.arange(x0, min(x0 + tile, width)),
+                             indexing="ij")
+        out.append((ys * width + xs).reshape(-1))
+    return np.concatenate(out).astype(np.int64) if out else np.zeros(0, np.int64)
+
+
+def shard_sizes(width: int, height: int, world: int, tile: int = 64) -> List[int]:
+    return [len(tile_pixels(width, height, world, r, tile)) for r in range(world)]
+
+
+def gather_hits(hits, world: int, rank: int, dst: int = 0):
+    """Gathers each rank's (n_r, 4) uint32/int32 hit-record tensor to ``dst``. Shards may differ
+    in length, so they are padded to the largest shard (one collective, equal message sizes).
+    Returns the list of per-rank tensors on ``dst`` (trimmed), None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    n = torch.tensor([hits.shape[0]], dtype=torch.int64, device=hits.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    m = int(max(int(s.item()) for s in sizes))
+    pad = torch.zeros((m, hits.shape[1]), dtype=hits.dtype, device=hits.device)
+    pad[: hits.shape[0]] = hits
+    out = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, out, dst=dst)
+    if rank != dst:
+        return None
+    return [o[: int(s.item())] for o, s in zip(out, sizes)]
+
+
+def assemble_tiles(parts, width: int, height: int, world: int, tile: int = 64) -> np.ndarray:
+    """Scatters gathered per-rank hit records back into screen order (W*H, 4)."""
+    full = np.zeros((width * height, 4), np.uint32)
+    for r, part in enumerate(parts):
+        pix = tile_pixels(width, height, world, r, tile)
+        arr = part.cpu().numpy() if hasattr(part, "cpu") else np.asarray(part)
+        full[pix] = arr.view(np.uint32).reshape(-1, 4)
+    return full
