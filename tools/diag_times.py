@@ -6,7 +6,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"))
 import torch
 dev = torch.device("cuda:0")
-buf = torch.zeros(3 * 8192, dtype=torch.int64, device=dev)
+buf = torch.zeros(4 * 8192, dtype=torch.int64, device=dev)
 os.environ["TT_DIAG_TIMES_PTR"] = str(buf.data_ptr())
 import tthip
 W, H, far = 1920, 1080, 1000.0
@@ -20,15 +20,16 @@ for b in (0, 1):
         nb = eng.enqueue_bounce(rays, W * H, 0, far, W, H, device=True)
     for _ in range(3):
         s = eng.trace(rays, W * H if b == 0 else nb, b, far, W, H, device=True)
-    t = buf.cpu().numpy().reshape(-1, 3)
+    t = buf.cpu().numpy().reshape(-1, 4)
     used = t[:, 1] > 0
     t = t[used]
-    st, en, n = t[:, 0], t[:, 1], t[:, 2]
+    st, en, n, cyc = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
     t0 = st.min()
     span = (en.max() - t0) / 100.0  # memrealtime 100 MHz -> us
     life = (en - st) / 100.0
     print(f"bounce {b}: waves {used.sum()} kernel {s.kernel_ms*1e3:.0f}us span {span:.0f}us start spread {(st.max()-t0)/100:.1f}us "
           f"wave life mean {life.mean():.0f} min {life.min():.0f} p10 {np.percentile(life,10):.0f} p50 {np.percentile(life,50):.0f} p90 {np.percentile(life,90):.0f} max {life.max():.0f}us; "
           f"rays/wave mean {n.mean():.0f} min {n.min()} max {n.max()}")
+    print(f"   shader clock {np.median(cyc / ((en - st) * 10.0)):.3f} GHz (memtime ticks / memrealtime)")
     end_rel = (en - t0) / 100.0
     print("   end-time percentiles", [round(float(np.percentile(end_rel, q))) for q in (1, 10, 25, 50, 75, 90, 99, 100)])

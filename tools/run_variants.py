@@ -42,12 +42,14 @@ p, b = float(np.median(ms[0::2])), float(np.median(ms[1::2]))
 print(json.dumps({"ok": ok, "primary_ms": round(p, 4), "bounce_ms": round(b, 4), "grays": round((W * H + nb) / (p + b) / 1e6, 3)}))
 '''
 libs = sorted(glob.glob(os.path.join(REPO, "truetrace-unity-pathtracer_amd", "lib", "variants", "*.so")))
-sel = sys.argv[1:]
-for lib in libs:
-    name = os.path.basename(lib)[len("libtruetrace_hip_"):-3]
-    if sel and name not in sel:
-        continue
+names = [os.path.basename(l)[len("libtruetrace_hip_"):-3] for l in libs]
+order = sys.argv[1:] or names  # a name may repeat (re-measure for noise)
+for spec in order:  # "name" or "name@B": B = TT_BLOCKS_PER_CU cap (256-thread blocks per CU)
+    name, _, bpc = spec.partition("@")
+    lib = libs[names.index(name)]
     env = dict(os.environ, TT_HIP_LIB=lib, REPO=REPO)
+    if bpc:
+        env["TT_BLOCKS_PER_CU"] = bpc
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-500:]
-    print(f"{name:10s} {line}", flush=True)
+    print(f"{spec:10s} {line}", flush=True)

@@ -608,6 +608,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     TraceArgs a;
     std::memset(&a, 0, sizeof(a));
     a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
+    a.n_nodes = (uint32_t)c->host.nodes.size();
     a.tris = c->tris.p;
     a.tlas = c->tlas.p;
     a.mesh = c->mesh.p;

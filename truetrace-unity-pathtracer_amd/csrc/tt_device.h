@@ -44,6 +44,7 @@ struct TraceControl {
 
 struct TraceArgs {
     const uint4* nodes;          // 80 B nodes as 5 x uint4
+    uint32_t n_nodes;
     const TriPos* tris;          // traversal-layout triangles
     const int32_t* tlas;         // TLASBVH8Indices
     const MeshGpu* mesh;         // traversal-layout mesh records

@@ -2,9 +2,9 @@
 // TrueTrace/Resources/MainCompute/IntersectionKernels.compute:60-260).
 //
 // Design (MI355X-first, not a translation of the HLSL dispatch):
-//  * persistent waves: grid = CUs x resident blocks; every wave owns a private pool of rays
-//    fetched CHUNK at a time with ONE atomic (the reference pops one ray per thread from a
-//    single globally-coherent counter, IntersectionKernels.compute:79-81);
+//  * persistent waves: grid = CUs x resident blocks; rays are dequeued per wave from per-XCD
+//    segment counters, TT_CHUNK_BIG at a time with ONE atomic (the reference pops one ray per
+//    thread from a single globally-coherent counter, IntersectionKernels.compute:79-81);
 //  * lanes that finish are refilled in place (ballot + mbcnt prefix over idle lanes) so the
 //    64-wide wave keeps working instead of idling behind its slowest ray;
 //  * the 16-entry uint2 traversal stack lives in LDS, [entry][thread] so a wave's 64 stack
@@ -21,11 +21,17 @@
 #ifndef TT_SEGS
 #define TT_SEGS 8         // ray-range segments, one per XCD group (blockIdx % 8), with stealing
 #endif
-#ifndef TT_CHUNK_BIG
-#define TT_CHUNK_BIG 64   // rays per dequeue over the first 3/4 of a segment
+#ifndef TT_SDWA_BITS
+#define TT_SDWA_BITS 1    // 1: per-child hit bits with one byte-selecting SDWA shift
 #endif
-#ifndef TT_CHUNK_SMALL
-#define TT_CHUNK_SMALL 64 // rays per dequeue over the last quarter (shortens the tail)
+#ifndef TT_NODE_PK
+#define TT_NODE_PK 0      // 1: node slab fmas as v_pk_fma_f32 pairs (measured ~2% slower on C2)
+#endif
+#ifndef TT_EXACT_TAIL
+#define TT_EXACT_TAIL 0   // 1: exact-size dequeues over the last quarter of each segment (measured: no gain on C2)
+#endif
+#ifndef TT_CHUNK_BIG
+#define TT_CHUNK_BIG 64   // rays per dequeue over the first 3/4 of a segment (then exact)
 #endif
 #ifndef TT_REFILL_MIN
 #define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
@@ -66,6 +72,9 @@ __device__ __forceinline__ uint32_t octant_inv4(const LaneRay& r) {
            (r.dz < 0.0f ? 0u : 0x01010101u);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // cwbvh_node_intersect — CommonData.cginc:641-707
 __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n1, const uint4 n2,
                                                    const uint4 n3, const uint4 n4, const LaneRay& r,
@@ -83,7 +92,9 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
     for (int i = 0; i < 2; i++) {
         const uint32_t meta4 = i == 0 ? n1.z : n1.w;
         const uint32_t is_inner4 = (meta4 & (meta4 << 1)) & 0x10101010u;
-        const uint32_t inner_mask4 = (((is_inner4 << 3) >> 7) & 0x01010101u) * 0xffu;
+        // 0x07 in each inner child's byte (oct_inv4 bytes are <= 7, so 3 bits of the reference's
+        // 0xff byte mask suffice); 8 - 1 per byte, no borrow: avoids the quarter-rate v_mul_lo_u32
+        const uint32_t inner_mask4 = (is_inner4 >> 1) - (is_inner4 >> 4);
         const uint32_t bit_index4 = (meta4 ^ (oct_inv4 & inner_mask4)) & 0x1f1f1f1fu;
         const uint32_t child_bits4 = (meta4 >> 5) & 0x07070707u;
         const uint32_t qlx = i == 0 ? n2.x : n2.y, qhx = i == 0 ? n2.z : n2.w;
@@ -94,6 +105,17 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
         const uint32_t z_min = nz ? qhz : qlz, z_max = nz ? qlz : qhz;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
+#if TT_NODE_PK
+            // (tmin, tmax) per axis as one v_pk_fma_f32: two IEEE fmas, bitwise the same as fmaf.
+            const f32x2 tx = pk_fma(f32x2{(float)((x_min >> (j * 8)) & 0xffu), (float)((x_max >> (j * 8)) & 0xffu)},
+                                    f32x2{adjx, adjx}, f32x2{orgx, orgx});
+            const f32x2 ty = pk_fma(f32x2{(float)((y_min >> (j * 8)) & 0xffu), (float)((y_max >> (j * 8)) & 0xffu)},
+                                    f32x2{adjy, adjy}, f32x2{orgy, orgy});
+            const f32x2 tz = pk_fma(f32x2{(float)((z_min >> (j * 8)) & 0xffu), (float)((z_max >> (j * 8)) & 0xffu)},
+                                    f32x2{adjz, adjz}, f32x2{orgz, orgz});
+            const float tmin = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 1e-8f));
+            const float tmax = fminf(fminf(tx.y, ty.y), fminf(tz.y, max_distance));
+#else
             const float tminx = fma_((float)((x_min >> (j * 8)) & 0xffu), adjx, orgx);
             const float tminy = fma_((float)((y_min >> (j * 8)) & 0xffu), adjy, orgy);
             const float tminz = fma_((float)((z_min >> (j * 8)) & 0xffu), adjz, orgz);
@@ -102,7 +124,25 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
             const float tmaxz = fma_((float)((z_max >> (j * 8)) & 0xffu), adjz, orgz);
             const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
             const float tmax = fminf(fminf(tmaxx, tmaxy), fminf(tmaxz, max_distance));
+#endif
+#if TT_SDWA_BITS
+            // child_bits byte j << bit_index byte j in ONE v_lshlrev_b32_sdwa (both operands byte-selected)
+            uint32_t bits;
+            if (j == 0)
+                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0"
+                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
+            else if (j == 1)
+                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1"
+                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
+            else if (j == 2)
+                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2"
+                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
+            else
+                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3"
+                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
+#else
             const uint32_t bits = ((child_bits4 >> (j * 8)) & 0xffu) << ((bit_index4 >> (j * 8)) & 0xffu);
+#endif
             hit_mask |= (tmin < tmax) ? bits : 0u;
         }
     }
@@ -158,6 +198,55 @@ __device__ __forceinline__ bool intersect_triangle(const TriPos* __restrict__ tr
     return cand;  // counted as an "accept" (candidate passed the t test) before the material check
 }
 
+// ------------------------------------------------------------------ ray scheduler
+// The work range is cut into TT_SEGS segments of whole 64-ray tiles; blocks start on segment
+// blockIdx % TT_SEGS (one per XCD under round-robin placement, for L2 locality). A dequeue is ONE
+// returning atomicAdd on the segment's counter (counted in rays). Over the first 3/4 of a
+// segment a wave reserves TT_CHUNK_BIG rays (fewer atomics; the surplus waits in the wave's pool);
+// over the last quarter exactly the lanes it can fill, so no ray waits in a busy wave's pool when
+// the launch drains. A wave whose segment is exhausted probes the others starting at an offset
+// derived from its wave id, so thieves spread over all counters instead of converging on one
+// (measured, tools/diag_tl.py: convergent stealing serialised thousands of atomics on one word).
+__device__ __forceinline__ uint32_t seg_lo(uint32_t n_tiles, uint32_t seg) {
+    return (uint32_t)(((uint64_t)n_tiles * seg / TT_SEGS) << 6);
+}
+struct SegState {
+    uint32_t seg;   // segment this wave dequeues from
+    uint32_t dead;  // bit k: segment k seen exhausted by this wave
+    uint32_t est;   // this wave's last known counter value of `seg`
+};
+// Reserves up to max(need, chunk) rays; returns the count (0 once every segment is exhausted).
+__device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_rays, uint32_t n_tiles, uint32_t lane,
+                                                  uint32_t need, uint32_t wave_id, SegState& S, uint32_t& base) {
+    while (S.dead != (1u << TT_SEGS) - 1u) {
+        const uint32_t lo = seg_lo(n_tiles, S.seg);
+        const uint32_t hi = min(seg_lo(n_tiles, S.seg + 1), n_rays);
+        const uint32_t len = hi > lo ? hi - lo : 0u;
+        const uint32_t want = (!TT_EXACT_TAIL || S.est < len - len / 4u) ? max(need, (uint32_t)TT_CHUNK_BIG) : need;
+        uint32_t off = 0;
+        if (lane == 0) off = atomicAdd(&ctl->seg_ticket[S.seg * 32u], want);
+        off = __builtin_amdgcn_readfirstlane(off);
+        if (off < len) {
+            S.est = off + want;
+            base = lo + off;
+            return min(want, len - off);
+        }
+        S.dead |= 1u << S.seg;
+        // next live segment, scanning from a per-wave offset
+        const uint32_t start = (S.seg + 1u + wave_id % (TT_SEGS - 1u)) % TT_SEGS;
+#pragma unroll
+        for (uint32_t k = 0; k < TT_SEGS; k++) {
+            const uint32_t c = (start + k) % TT_SEGS;
+            if (!((S.dead >> c) & 1u)) {
+                S.seg = c;
+                break;
+            }
+        }
+        S.est = 0;
+    }
+    return 0u;
+}
+
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
@@ -206,8 +295,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     // wave-uniform scheduler state: a private pool [pool_next, pool_end) of work indices, refilled
     // from segment `seg` (segments = contiguous 1/TT_SEGS slices of the work range, dealt to XCD
     // groups by blockIdx % TT_SEGS for L2 locality; exhausted segments are stolen from in turn)
-    uint32_t pool_next = 0, pool_end = 0;
-    uint32_t seg = blockIdx.x % TT_SEGS, segs_left = TT_SEGS;
+    uint32_t pool_next = 0, pool_end = 0, more = 1;
+    const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
+    SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
     const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
 
     // lane traversal state (IntersectionKernels.compute:62-77)
@@ -221,6 +311,12 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
     uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
+#ifdef TT_DIAG_TL
+    uint32_t d_tl = 0;
+#endif
+#ifdef TT_DIAG_RAYS  // per-ray (start, end, iterations, node visits): diag_times -> uint4[n_rays]
+    uint32_t r_t0 = 0, r_iter = 0, r_nodes = 0;
+#endif
 #if TT_PREFETCH
     // next node of this lane, loaded as soon as its index is known (the group on top decides it:
     // IntersectionKernels.compute:158-161), so its latency overlaps the leaf triangle tests
@@ -266,33 +362,21 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 
 #ifdef TT_DIAG_TIMES
     const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c_begin = __builtin_amdgcn_s_memtime();
 #endif
     while (true) {
         // ---------------------------------------------------------------- refill
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
-        const bool pool_dry = segs_left == 0 && pool_next >= pool_end;
+        const bool pool_dry = !more && pool_next >= pool_end;
         if (n_idle == TT_WAVE && pool_dry) break;
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
+            // wave-uniform: take from the wave's pool first, then one dequeue for the rest
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
-            while (avail < n_idle && segs_left > 0) {  // wave-uniform dequeue, one atomic per chunk
-                uint32_t t = 0;
-                if (lane == 0) t = atomicAdd(&A.ctl->seg_ticket[seg * 32u], 1u);
-                t = __builtin_amdgcn_readfirstlane(t);
-                const uint32_t lo = (uint32_t)(((uint64_t)n_tiles * seg / TT_SEGS) << 6);
-                const uint32_t hi = min((uint32_t)(((uint64_t)n_tiles * (seg + 1) / TT_SEGS) << 6), A.n_rays);
-                const uint32_t len = hi > lo ? hi - lo : 0u;
-                const uint32_t k1 = (len - len / 4u) / TT_CHUNK_BIG;
-                const uint32_t start = t < k1 ? t * TT_CHUNK_BIG : k1 * TT_CHUNK_BIG + (t - k1) * TT_CHUNK_SMALL;
-                const uint32_t size = t < k1 ? TT_CHUNK_BIG : TT_CHUNK_SMALL;
-                if (start < len) {
-                    new_base = lo + start;
-                    new_count = min(size, len - start);
-                    break;
-                }
-                seg = seg + 1u == TT_SEGS ? 0u : seg + 1u;
-                segs_left--;
+            if (avail < n_idle && more) {
+                new_count = sched_reserve(A.ctl, A.n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
+                more = new_count > 0 ? 1u : 0u;
             }
             const uint32_t take_old = min(avail, n_idle);
             const uint32_t take_new = min(n_idle - take_old, new_count);
@@ -346,6 +430,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 mesh_id = -1;
                 Reps = 0;
                 active = true;
+#ifdef TT_DIAG_RAYS
+                r_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                r_iter = 0;
+                r_nodes = 0;
+#endif
 #ifdef TT_DIAG_TIMES
                 c_rays++;
 #else
@@ -354,8 +443,33 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             }
         }
 
+#ifdef TT_DIAG_TL  // per-wave timeline: every 4th iteration (time, active lanes) -> diag_times
+        if (A.diag_times) {
+            const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
+            if ((d_tl & 3u) == 0u && (d_tl >> 2) < 64u && lane == 0) {
+                const uint32_t na = (uint32_t)__popcll(__ballot(active));
+                reinterpret_cast<uint2*>(A.diag_times)[(size_t)w * 64u + (d_tl >> 2)] =
+                    make_uint2((uint32_t)__builtin_amdgcn_s_memrealtime(), na | (more << 8) | ((uint32_t)__builtin_amdgcn_s_memtime() << 12));
+            }
+            d_tl++;
+        }
+#endif
+#ifdef TT_EXP_VALU_PAD  // diagnostic: N extra independent VALU ops per iteration (is the loop VALU-bound?)
+        {
+            float pad0 = __uint_as_float(lane), pad1 = pad0;
+#pragma unroll
+            for (int k = 0; k < TT_EXP_VALU_PAD / 2; k++) {
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pad0) : "v"(pad1));
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pad1) : "v"(pad0));
+            }
+            if (pad0 == 1234.5f) best.u = pad1;
+        }
+#endif
         // ------------------------------------------------------------- node phase
         bool finish = false;
+#ifdef TT_DIAG_RAYS
+        r_iter += active ? 1u : 0u;
+#endif
         if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)
             const uint64_t nm = __ballot(active && tg.y == 0u && Reps < TT_MAX_REPS && (cg.y & 0xff000000u));
             if (lane == 0) {
@@ -389,7 +503,14 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                         }
 #else
                         const uint4* np = A.nodes + (size_t)child * 5u;
+#ifdef TT_EXP_DOUBLE_FETCH  // diagnostic: a second, redundant fetch of the same node (same lines)
+                        uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
+                        const uint4* np2 = A.nodes + (size_t)((child ^ 1u) < A.n_nodes ? (child ^ 1u) : child) * 5u;
+                        const uint4 m0 = np2[0], m1 = np2[1], m2 = np2[2], m3 = np2[3], m4 = np2[4];
+                        if ((m0.x ^ m1.y ^ m2.z ^ m3.w ^ m4.x) == 0x9E3779B9u && m0.y == 0x7F7F7F7Fu) n0.w ^= 1u;
+#else
                         const uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
+#endif
 #endif
                         const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
                         cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
@@ -398,6 +519,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                         tg.x = n1.y + (uint32_t)TriOffset;
                         Reps++;
                         if (STATS) c_nodes++;
+#ifdef TT_DIAG_RAYS
+                        r_nodes++;
+#endif
                     } else {
                         active = false;
                         tg.y = 0u;
@@ -555,6 +679,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             if (best.t == -12345.0f) reinterpret_cast<uint4*>(R)[2] = make_uint4(0, 0, 0, uv);
 #endif
             if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
+#ifdef TT_DIAG_RAYS
+            if (A.diag_times)
+                reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
+                    make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
+#endif
             active = false;
         }
     }
@@ -565,9 +694,10 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         const uint32_t rays_done = wave_sum(c_rays);
         if (lane == 0 && A.diag_times) {
             const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
-            A.diag_times[3 * w + 0] = t_begin;
-            A.diag_times[3 * w + 1] = t_end;
-            A.diag_times[3 * w + 2] = rays_done;
+            A.diag_times[4 * w + 0] = t_begin;
+            A.diag_times[4 * w + 1] = t_end;
+            A.diag_times[4 * w + 2] = rays_done;
+            A.diag_times[4 * w + 3] = __builtin_amdgcn_s_memtime() - c_begin;  // shader clock ticks
         }
     }
 #endif
@@ -585,10 +715,374 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     }
 }
 
+// ------------------------------------------------------------- uniform-step kernel
+// Same traversal semantics as tt_trace_kernel, restructured so that a wave executes ONE
+// straight-line step per iteration: every lane runs the node test and the triangle test, and
+// what each lane commits is chosen with selects (v_cndmask) instead of divergent branches.
+// Hypothesis tested with it: the branchy form was stalled on control flow (~25 branches and
+// exec-mask updates per step). Measured on C2: branches 9.6 vs 25 per iteration and SALU -30%,
+// but VALU +10% and 4-5% slower overall (the loop is VALU-issue-bound at the margin: +100 VALU
+// per iteration cost +15%), so it stays an option (TT_KERNEL_UNIFORM=1), not the default.
+// Lanes that have nothing to do fetch node 0 / triangle 0 (one shared line) and discard the
+// result. Rare transitions (TLAS->BLAS entry, BLAS->TLAS return, ray completion, stack
+// overflow) stay as wave-uniform `if (__any(...))` blocks.
+#ifndef TT_UNIFORM_STACK
+#define TT_UNIFORM_STACK (TT_STACK_SIZE + 1)  // entry 16 is scratch for the unconditional push
+#endif
+template <bool STATS, bool MATCHECK, int INFO>
+__global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
+    __shared__ uint2 s_stack[TT_UNIFORM_STACK][TT_BLOCK];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & (TT_WAVE - 1);
+
+    uint32_t pool_next = 0, pool_end = 0, more = 1;
+    const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
+    SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
+    const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
+
+    bool active = false;
+    uint32_t ray_index = 0;
+    LaneRay ray{}, wray{};
+    Best best{};
+    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
+    uint32_t oct = 0;
+    int32_t stack_size = 0, tlas_ss = -1;
+    int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
+    uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
+    uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
+#ifdef TT_DIAG_TIMES
+    const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c_begin = __builtin_amdgcn_s_memtime();
+#endif
+
+    while (true) {
+        // ---------------------------------------------------------------- refill
+        const uint64_t idle = __ballot(!active);
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        const bool pool_dry = !more && pool_next >= pool_end;
+        if (n_idle == TT_WAVE && pool_dry) break;
+        if (n_idle >= TT_REFILL_MIN && !pool_dry) {
+            // wave-uniform: take from the wave's pool first, then one dequeue for the rest
+            const uint32_t avail = pool_end - pool_next;
+            uint32_t new_base = 0, new_count = 0;
+            if (avail < n_idle && more) {
+                new_count = sched_reserve(A.ctl, A.n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
+                more = new_count > 0 ? 1u : 0u;
+            }
+            const uint32_t take_old = min(avail, n_idle);
+            const uint32_t take_new = min(n_idle - take_old, new_count);
+            const uint32_t rank = lane_prefix(idle);
+            uint32_t widx = 0xffffffffu;
+            if (rank < take_old) widx = pool_next + rank;
+            else if (rank - take_old < take_new) widx = new_base + (rank - take_old);
+            if (new_count > 0) {  // the old pool was fully consumed (avail < n_idle)
+                pool_next = new_base + take_new;
+                pool_end = new_base + new_count;
+            } else {
+                pool_next += take_old;
+            }
+            if (!active && widx != 0xffffffffu) {
+                uint32_t local = widx;
+                if (A.tile_swizzle) {
+                    const uint32_t tw = A.width >> 3;
+                    const uint32_t t = widx >> 6, l = widx & 63u;
+                    const uint32_t ty = t / tw, tx = t - ty * tw;
+                    local = (ty * 8u + (l >> 3)) * A.width + tx * 8u + (l & 7u);
+                }
+                ray_index = A.ray_offset + local;
+                const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
+                const uint4 r0 = rp[0], r1 = rp[1];
+                ray.ox = __uint_as_float(r0.x);
+                ray.oy = __uint_as_float(r0.y);
+                ray.oz = __uint_as_float(r0.z);
+                ray.dx = __uint_as_float(r1.x);
+                ray.dy = __uint_as_float(r1.y);
+                ray.dz = __uint_as_float(r1.z);
+                ray.ix = 1.0f / ray.dx;
+                ray.iy = 1.0f / ray.dy;
+                ray.iz = 1.0f / ray.dz;
+                wray = ray;
+                oct = octant_inv4(ray);
+                best.t = A.far_plane;
+                best.u = 0.0f;
+                best.v = 0.0f;
+                best.mesh_id = 0;
+                best.tri_id = -1;
+                cg = make_uint2(0u, 0x80000000u);
+                tg = make_uint2(0u, 0u);
+                stack_size = 0;
+                tlas_ss = -1;
+                NodeOffset = 0;
+                TriOffset = 0;
+                MatOffset = 0;
+                mesh_id = -1;
+                Reps = 0;
+                active = true;
+                c_rays++;
+            }
+        }
+
+        // ------------------------------------------------------- node step (all lanes)
+        // IntersectionKernels.compute:155-191
+        const bool nodeable = active && tg.y == 0u;
+        const bool exhaust = nodeable && Reps >= TT_MAX_REPS;  // :155 loop bound: no write
+        const bool has_inner = (cg.y & 0xff000000u) != 0u;
+        const bool do_node = nodeable && !exhaust && has_inner;
+        const bool pop_tri = nodeable && !exhaust && !has_inner;  // :188-191
+        const uint32_t cio = firstbithigh(cg.y | 0x01000000u);
+        const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
+        const uint32_t rel = __builtin_popcount(cg.y & ~(0xffffffffu << slot));
+        const uint32_t rem = cg.y & ~(1u << cio);
+        const bool push = do_node && (rem & 0xff000000u) != 0u;
+        const bool overflow = push && stack_size == TT_STACK_SIZE;
+        s_stack[stack_size][tid] = make_uint2(cg.x, rem);  // above the top unless pushed
+        const uint32_t child = do_node ? cg.x + rel : 0u;
+        const uint4* np = A.nodes + (size_t)child * 5u;
+        const uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
+        const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
+        const bool commit = do_node && !overflow;
+        {
+            const uint2 ncg = make_uint2(n1.x + (uint32_t)NodeOffset, (hitmask & 0xff000000u) | (n0.w >> 24));
+            const uint2 ntg = make_uint2(n1.y + (uint32_t)TriOffset, hitmask & 0x00ffffffu);
+            const uint2 ocg = cg;
+            cg.x = commit ? ncg.x : (pop_tri ? 0u : ocg.x);
+            cg.y = commit ? ncg.y : (pop_tri ? 0u : ocg.y);
+            tg.x = commit ? ntg.x : (pop_tri ? ocg.x : tg.x);
+            tg.y = commit ? ntg.y : (pop_tri ? ocg.y : tg.y);
+        }
+        stack_size += (push && !overflow) ? 1 : 0;
+        Reps += commit ? 1 : 0;
+        if (STATS) {
+            c_nodes += commit ? 1u : 0u;
+            c_reps += exhaust ? 1u : 0u;
+            c_ovf += overflow ? 1u : 0u;
+            const uint64_t nm = __ballot(commit);
+            if (lane == 0) {
+                d_iter++;
+                d_node_lanes += (uint32_t)__popcll(nm);
+                d_node_iters += nm ? 1u : 0u;
+            }
+        }
+        if (__builtin_expect(__any(overflow), 0)) {
+            if (overflow) atomicAdd(&A.ctl->err_overflow, 1u);
+        }
+        if (exhaust || overflow) {
+            active = false;
+            stack_size = 0;
+            tg.y = 0u;
+            cg.y = 0u;
+        }
+
+        // ----------------------------------------------- TLAS leaf -> BLAS (:194-219)
+        const bool enter = active && tg.y != 0u && tlas_ss == -1;
+        if (__any(enter)) {
+            if (enter) {
+                const uint32_t mo = firstbithigh(tg.y);
+                tg.y &= ~(1u << mo);
+                mesh_id = A.tlas[tg.x + mo];
+                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
+                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                NodeOffset = mo4.y;
+                TriOffset = mo4.x;
+                bool ok = true;
+                if (tg.y != 0u) {
+                    if (stack_size == TT_STACK_SIZE) ok = false;
+                    else s_stack[stack_size++][tid] = tg;
+                }
+                if (ok && (cg.y & 0xff000000u)) {
+                    if (stack_size == TT_STACK_SIZE) ok = false;
+                    else s_stack[stack_size++][tid] = cg;
+                }
+                if (ok) {
+                    tlas_ss = stack_size;
+                    MatOffset = mo4.z;
+                    LaneRay nr;
+                    nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
+                    nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
+                    nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
+                    nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
+                    nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
+                    nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
+                    nr.ix = 1.0f / nr.dx;
+                    nr.iy = 1.0f / nr.dy;
+                    nr.iz = 1.0f / nr.dz;
+                    ray = nr;
+                    oct = octant_inv4(ray);
+                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                    if (STATS) c_blas++;
+                } else {
+                    active = false;
+                    stack_size = 0;
+                    cg.y = 0u;
+                    if (STATS) c_ovf++;
+                    atomicAdd(&A.ctl->err_overflow, 1u);
+                }
+                tg.y = 0u;
+            }
+        }
+
+        // --------------------------------------------- triangle test (all lanes, :220-226)
+        {
+            const bool do_tri = active && tg.y != 0u;
+            const uint32_t ti = firstbithigh(tg.y | 1u);
+            const int32_t tri_id = do_tri ? (int32_t)(tg.x + ti) : 0;
+            const uint4* tp = reinterpret_cast<const uint4*>(A.tris + tri_id);
+            const uint4 ta = tp[0], tb = tp[1], tc = tp[2];
+            const float p0x = __uint_as_float(ta.x), p0y = __uint_as_float(ta.y), p0z = __uint_as_float(ta.z);
+            const float e1x = __uint_as_float(ta.w), e1y = __uint_as_float(tb.x), e1z = __uint_as_float(tb.y);
+            const float e2x = __uint_as_float(tb.z), e2y = __uint_as_float(tb.w), e2z = __uint_as_float(tc.x);
+            const float hx = fma_(ray.dy, e2z, -(ray.dz * e2y));
+            const float hy = fma_(ray.dz, e2x, -(ray.dx * e2z));
+            const float hz = fma_(ray.dx, e2y, -(ray.dy * e2x));
+            const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
+            const float f = 1.0f / aa;
+            const float sx = ray.ox - p0x, sy = ray.oy - p0y, sz = ray.oz - p0z;
+            const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
+            const float qx = fma_(sy, e1z, -(sz * e1y));
+            const float qy = fma_(sz, e1x, -(sx * e1z));
+            const float qz = fma_(sx, e1y, -(sy * e1x));
+            const float v = f * fma_(ray.dz, qz, fma_(ray.dy, qy, ray.dx * qx));
+            const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
+            const bool cand = do_tri && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) &&
+                              (t > 0.0f && t < best.t);
+            bool accept = cand;
+            if (MATCHECK && __any(cand)) {
+                if (cand) {  // :48 Invisible at CurBounce == 0; out-of-range material reads as zeros
+                    const uint32_t mi = (uint32_t)(MatOffset + (int32_t)tc.y);
+                    const uint32_t tag = mi < A.n_mat ? A.mat_tag[mi] : 0u;
+                    if ((tag >> TT_FLAG_INVISIBLE) & 1u) accept = false;
+                }
+            }
+            best.t = accept ? t : best.t;
+            best.u = accept ? u : best.u;
+            best.v = accept ? v : best.v;
+            best.mesh_id = accept ? mesh_id : best.mesh_id;
+            best.tri_id = accept ? tri_id : best.tri_id;
+            tg.y = do_tri ? (tg.y & ~(1u << ti)) : tg.y;
+            if (STATS) {
+                c_tris += do_tri ? 1u : 0u;
+                c_acc += cand ? 1u : 0u;
+                const uint64_t tm = __ballot(do_tri);
+                if (lane == 0) {
+                    d_tri_lanes += (uint32_t)__popcll(tm);
+                    d_tri_iters += tm ? 1u : 0u;
+                }
+            }
+        }
+
+        // ------------------------------------------------------ pop / finish (:228-251)
+        const bool adv = active && tg.y == 0u && (cg.y & 0xff000000u) == 0u;
+        const bool fin = adv && stack_size == 0;
+        const bool pop = adv && stack_size > 0;
+        const bool restore = pop && stack_size == tlas_ss;
+        if (__any(restore)) {
+            if (restore) {  // :243-249 BLAS -> TLAS
+                NodeOffset = 0;
+                TriOffset = 0;
+                tlas_ss = -1;
+                ray = wray;
+                oct = octant_inv4(ray);
+            }
+        }
+        {
+            const uint2 top = s_stack[stack_size > 0 ? stack_size - 1 : 0][tid];
+            cg.x = pop ? top.x : cg.x;
+            cg.y = pop ? top.y : cg.y;
+            stack_size -= pop ? 1 : 0;
+        }
+        if (__any(fin)) {
+            if (fin) {  // :229-241 + set() CommonData.cginc:430-434
+                tt_ray_data* R = A.rays + ray_index;
+                if (INFO != 0) {
+                    const uint32_t pix = R->PixelIndex;
+                    const uint32_t tx = pix % A.width, ty = pix / A.width;
+                    if (ty < A.height) {
+                        uint4 o = make_uint4(0, 0, 0, 0);
+                        bool write = false;
+                        if (INFO == 1) {
+                            const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                            o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to), __float_as_uint(best.u),
+                                           __float_as_uint(best.v));
+                            write = true;
+                        } else {
+                            const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
+                            if (w == -1.0f || (float)A.bounce == w) {
+                                write = true;
+                                const bool miss = best.t == A.far_plane;
+                                if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
+                                    const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                                    o.x = (uint32_t)best.mesh_id;
+                                    o.y = (uint32_t)(best.tri_id - to);
+                                    o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                                } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
+                                    o.x = __float_as_uint(wray.dx);
+                                    o.y = __float_as_uint(wray.dy);
+                                    o.z = __float_as_uint(wray.dz);
+                                } else {
+                                    o.x = __float_as_uint(wray.dx * best.t + wray.ox);
+                                    o.y = __float_as_uint(wray.dy * best.t + wray.oy);
+                                    o.z = __float_as_uint(wray.dz * best.t + wray.oz);
+                                }
+                                o.w = miss ? 1u : 0u;
+                            }
+                        }
+                        if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+                    }
+                }
+                const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                reinterpret_cast<uint4*>(R)[2] =
+                    make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+                if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
+                active = false;
+                stack_size = 0;
+            }
+        }
+    }
+
+#ifdef TT_DIAG_TIMES
+    {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t rays_done = wave_sum(c_rays);
+        if (lane == 0 && A.diag_times) {
+            const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
+            A.diag_times[4 * w + 0] = t_begin;
+            A.diag_times[4 * w + 1] = t_end;
+            A.diag_times[4 * w + 2] = rays_done;
+            A.diag_times[4 * w + 3] = __builtin_amdgcn_s_memtime() - c_begin;  // shader clock ticks
+        }
+    }
+#endif
+    if (STATS) {
+        const uint32_t vals[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
+                                  wave_sum(c_hits), wave_sum(c_reps), wave_sum(c_ovf), wave_sum(c_acc)};
+        (void)d_active_lanes;
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (vals[k]) atomicAdd(&A.ctl->stats[k], (unsigned long long)vals[k]);
+            const uint32_t d[6] = {d_iter, d_node_iters, d_node_lanes, d_tri_iters, d_tri_lanes, 0u};
+#pragma unroll
+            for (int k = 0; k < 6; k++) atomicAdd(&A.ctl->diag[k], (unsigned long long)d[k]);
+        }
+    }
+}
+
+#ifndef TT_KERNEL_UNIFORM
+#define TT_KERNEL_UNIFORM 0
+#endif
+#if TT_KERNEL_UNIFORM
+#define TT_KERNEL tt_trace_kernel_u
+#define TT_LDS_ENTRIES TT_UNIFORM_STACK
+#else
+#define TT_KERNEL tt_trace_kernel
+#define TT_LDS_ENTRIES TT_LDS_STACK
+#endif
+
 // ------------------------------------------------------------------ launchers
 template <bool S, bool M, int I>
 static hipError_t launch_one(const TraceArgs& a, uint32_t grid, hipStream_t st) {
-    hipLaunchKernelGGL((tt_trace_kernel<S, M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+    hipLaunchKernelGGL((TT_KERNEL<S, M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
     return hipGetLastError();
 }
 
@@ -610,7 +1104,7 @@ hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int in
 template <bool S, bool M, int I>
 static int occ_one() {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_trace_kernel<S, M, I>, TT_BLOCK, 0) != hipSuccess) b = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, TT_KERNEL<S, M, I>, TT_BLOCK, 0) != hipSuccess) b = 1;
     return b;
 }
 hipError_t tt_trace_occupancy_table(int* out12) {
@@ -630,5 +1124,7 @@ hipError_t tt_trace_occupancy_table(int* out12) {
 }
 
 uint32_t tt_trace_block_size() { return TT_BLOCK; }
-uint32_t tt_trace_lds_bytes() { return (uint32_t)(TT_LDS_STACK * TT_BLOCK * sizeof(uint2)); }
-uint32_t tt_trace_spill_entries() { return TT_LDS_STACK >= TT_STACK_SIZE ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK); }
+uint32_t tt_trace_lds_bytes() { return (uint32_t)(TT_LDS_ENTRIES * TT_BLOCK * sizeof(uint2)); }
+uint32_t tt_trace_spill_entries() {
+    return (TT_KERNEL_UNIFORM || TT_LDS_STACK >= TT_STACK_SIZE) ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK);
+}
