@@ -240,6 +240,10 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
         why = "null or empty buffer";
         return TT_ERR_INVALID_ARG;
     }
+    if ((uint64_t)n_nodes * sizeof(tt_cwbvh_node) >= (1ull << 32) || (uint64_t)n_tris * 48u >= (1ull << 32)) {
+        why = "node or triangle array of 4 GiB or more (the trace kernel addresses them with 32-bit offsets)";
+        return TT_ERR_INVALID_ARG;
+    }
     h.nodes.assign(nodes, nodes + n_nodes);
     h.tlas.assign(tlas, tlas + n_tlas);
     h.mesh.assign(md, md + n_mesh);
@@ -610,6 +614,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
     a.n_nodes = (uint32_t)c->host.nodes.size();
     a.tris = c->tris.p;
+    a.n_tris = c->host.n_tris;
     a.tlas = c->tlas.p;
     a.mesh = c->mesh.p;
     a.mat_tag = c->mat_tag.p;

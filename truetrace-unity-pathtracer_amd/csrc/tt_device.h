@@ -46,6 +46,7 @@ struct TraceArgs {
     const uint4* nodes;          // 80 B nodes as 5 x uint4
     uint32_t n_nodes;
     const TriPos* tris;          // traversal-layout triangles
+    uint32_t n_tris;
     const int32_t* tlas;         // TLASBVH8Indices
     const MeshGpu* mesh;         // traversal-layout mesh records
     const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)

@@ -42,12 +42,6 @@
 #ifndef TT_WAVES_PER_EU
 #define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
 #endif
-#ifndef TT_TRI_LOOP
-#define TT_TRI_LOOP 0     // 0: one triangle per lane per pass; 1: drain the lane's triangles
-#endif
-#ifndef TT_PREFETCH
-#define TT_PREFETCH 0     // 1: issue the next node's loads as soon as its index is known
-#endif
 #ifndef TT_WRAY_RELOAD
 #define TT_WRAY_RELOAD 0  // 1: re-read the world-space ray from GlobalRays on BLAS exit
 #endif
@@ -73,7 +67,22 @@ __device__ __forceinline__ uint32_t octant_inv4(const LaneRay& r) {
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+[[maybe_unused]] __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Node / triangle fetches are raw buffer loads: a 32-bit byte offset per lane (two full-rate
+// shift-adds) instead of a 64-bit address (v_mad_u64_u32), and a bounded descriptor, so an
+// out-of-range offset reads zeros instead of faulting. Offsets stay below 2^32 because
+// tt_scene_upload rejects node / triangle arrays of 4 GiB or more.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buffer_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t node_offset(uint32_t i) { return (i + (i << 2)) << 4; }  // i * 80
+__device__ __forceinline__ uint32_t tri_offset(uint32_t i) { return (i + (i << 1)) << 4; }   // i * 48
 
 // cwbvh_node_intersect — CommonData.cginc:641-707
 __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n1, const uint4 n2,
@@ -157,11 +166,11 @@ struct Best {
 // IntersectTriangle — IntersectionKernels.compute:14-57 (Moller-Trumbore on pos0/edges).
 // Evaluated branch-free; the accept predicate is exactly the reference's nested conditions.
 template <bool MATCHECK>
-__device__ __forceinline__ bool intersect_triangle(const TriPos* __restrict__ tris, const uint32_t* __restrict__ mat_tag,
+__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const uint32_t* __restrict__ mat_tag,
                                                    uint32_t n_mat, int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
                                                    const LaneRay& r, Best& best) {
-    const uint4* tp = reinterpret_cast<const uint4*>(tris + tri_id);
-    const uint4 a = tp[0], b = tp[1], c = tp[2];
+    const uint32_t to = tri_offset((uint32_t)tri_id);
+    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
     const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
     const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);
@@ -299,6 +308,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
     SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
     const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
+    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
+    const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
     // lane traversal state (IntersectionKernels.compute:62-77)
     bool active = false;
@@ -316,27 +327,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
 #ifdef TT_DIAG_RAYS  // per-ray (start, end, iterations, node visits): diag_times -> uint4[n_rays]
     uint32_t r_t0 = 0, r_iter = 0, r_nodes = 0;
-#endif
-#if TT_PREFETCH
-    // next node of this lane, loaded as soon as its index is known (the group on top decides it:
-    // IntersectionKernels.compute:158-161), so its latency overlaps the leaf triangle tests
-    uint32_t pf_idx = 0xffffffffu;
-    uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0, pf2 = pf0, pf3 = pf0, pf4 = pf0;
-#define TT_PREFETCH_NEXT()                                                             \
-    do {                                                                               \
-        if (active && (cg.y & 0xff000000u)) {                                          \
-            const uint32_t pcio = firstbithigh(cg.y);                                  \
-            const uint32_t pslot = (pcio - 24u) ^ (oct & 0xffu);                       \
-            const uint32_t pchild = cg.x + __builtin_popcount(cg.y & ~(0xffffffffu << pslot)); \
-            if (pchild != pf_idx) {                                                    \
-                const uint4* pp = A.nodes + (size_t)pchild * 5u;                       \
-                pf0 = pp[0]; pf1 = pp[1]; pf2 = pp[2]; pf3 = pp[3]; pf4 = pp[4];       \
-                pf_idx = pchild;                                                       \
-            }                                                                          \
-        }                                                                              \
-    } while (0)
-#else
-#define TT_PREFETCH_NEXT() do {} while (0)
 #endif
     // world-space ray (ray2, IntersectionKernels.compute:151): kept in registers, or re-read from
     // GlobalRays with the same correctly rounded reciprocals (bit-identical either way)
@@ -466,7 +456,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
 #endif
         // ------------------------------------------------------------- node phase
-        bool finish = false;
 #ifdef TT_DIAG_RAYS
         r_iter += active ? 1u : 0u;
 #endif
@@ -479,114 +468,80 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 d_active_lanes += (uint32_t)__popcll(__ballot(active));
             }
         }
+        // A lane is at the top of the reference's loop exactly when no leaf triangles are pending.
         if (active && tg.y == 0u) {
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
-            } else {
-                if (cg.y & 0xff000000u) {  // IntersectionKernels.compute:157-187
-                    const uint32_t cio = firstbithigh(cg.y);
-                    const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
-                    const uint32_t rel = __builtin_popcount(cg.y & ~(0xffffffffu << slot));
-                    const uint32_t child = cg.x + rel;
-                    cg.y &= ~(1u << cio);
-                    bool ok = true;
-                    if (cg.y & 0xff000000u) TT_PUSH(cg, ok);
-                    if (ok) {
-#if TT_PREFETCH
-                        uint4 n0, n1, n2, n3, n4;
-                        if (pf_idx == child) {
-                            n0 = pf0; n1 = pf1; n2 = pf2; n3 = pf3; n4 = pf4;
-                        } else {
-                            const uint4* np = A.nodes + (size_t)child * 5u;
-                            n0 = np[0]; n1 = np[1]; n2 = np[2]; n3 = np[3]; n4 = np[4];
-                        }
-#else
-                        const uint4* np = A.nodes + (size_t)child * 5u;
-#ifdef TT_EXP_DOUBLE_FETCH  // diagnostic: a second, redundant fetch of the same node (same lines)
-                        uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
-                        const uint4* np2 = A.nodes + (size_t)((child ^ 1u) < A.n_nodes ? (child ^ 1u) : child) * 5u;
-                        const uint4 m0 = np2[0], m1 = np2[1], m2 = np2[2], m3 = np2[3], m4 = np2[4];
-                        if ((m0.x ^ m1.y ^ m2.z ^ m3.w ^ m4.x) == 0x9E3779B9u && m0.y == 0x7F7F7F7Fu) n0.w ^= 1u;
-#else
-                        const uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
-#endif
-#endif
-                        const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
-                        cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
-                        tg.y = hitmask & 0x00ffffffu;
-                        cg.x = n1.x + (uint32_t)NodeOffset;
-                        tg.x = n1.y + (uint32_t)TriOffset;
-                        Reps++;
-                        if (STATS) c_nodes++;
+            } else if (cg.y & 0xff000000u) {  // IntersectionKernels.compute:157-187
+                const uint32_t cio = firstbithigh(cg.y);
+                const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
+                const uint32_t rel = __builtin_popcount(cg.y & ~(0xffffffffu << slot));
+                const uint32_t child = cg.x + rel;
+                cg.y &= ~(1u << cio);
+                bool ok = true;
+                if (cg.y & 0xff000000u) TT_PUSH(cg, ok);
+                if (ok) {
+                    const uint32_t no = node_offset(child);
+                    const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
+                                n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
+                                n4 = buffer_load16(nodes, no + 64u);
+                    const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
+                    cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
+                    tg.y = hitmask & 0x00ffffffu;
+                    cg.x = n1.x + (uint32_t)NodeOffset;
+                    tg.x = n1.y + (uint32_t)TriOffset;
+                    Reps++;
+                    if (STATS) c_nodes++;
 #ifdef TT_DIAG_RAYS
-                        r_nodes++;
+                    r_nodes++;
 #endif
-                    } else {
-                        active = false;
-                        tg.y = 0u;
-                        if (STATS) c_ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
-                    }
-                } else {  // :188-191
-                    tg = cg;
-                    cg = make_uint2(0u, 0u);
+                } else {
+                    active = false;
+                    if (STATS) c_ovf++;
+                    atomicAdd(&A.ctl->err_overflow, 1u);
                 }
-                if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
-                    const uint32_t mo = firstbithigh(tg.y);
-                    tg.y &= ~(1u << mo);
-                    mesh_id = A.tlas[tg.x + mo];
-                    const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
-                    const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                    const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
-                    NodeOffset = mo4.y;
-                    TriOffset = mo4.x;
-                    bool ok = true;
-                    if (tg.y != 0u) TT_PUSH(tg, ok);
-                    if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
-                    if (ok) {
-                        tlas_ss = stack_size;
-                        MatOffset = mo4.z;
-                        LaneRay nr;
-                        nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
-                        nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
-                        nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
-                        nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
-                        nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
-                        nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                        nr.ix = 1.0f / nr.dx;
-                        nr.iy = 1.0f / nr.dy;
-                        nr.iz = 1.0f / nr.dz;
-                        ray = nr;
-                        oct = octant_inv4(ray);
-                        cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
-                        if (STATS) c_blas++;
-                    } else {
-                        active = false;
-                        if (STATS) c_ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
-                    }
-                    tg.y = 0u;
+            } else {  // :188-191
+                tg = cg;
+                cg = make_uint2(0u, 0u);
+            }
+            if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
+                const uint32_t mo = firstbithigh(tg.y);
+                tg.y &= ~(1u << mo);
+                mesh_id = A.tlas[tg.x + mo];
+                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
+                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                NodeOffset = mo4.y;
+                TriOffset = mo4.x;
+                bool ok = true;
+                if (tg.y != 0u) TT_PUSH(tg, ok);
+                if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
+                if (ok) {
+                    tlas_ss = stack_size;
+                    MatOffset = mo4.z;
+                    LaneRay nr;
+                    nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
+                    nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
+                    nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
+                    nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
+                    nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
+                    nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
+                    nr.ix = 1.0f / nr.dx;
+                    nr.iy = 1.0f / nr.dy;
+                    nr.iz = 1.0f / nr.dz;
+                    ray = nr;
+                    oct = octant_inv4(ray);
+                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                    if (STATS) c_blas++;
+                } else {
+                    active = false;
+                    if (STATS) c_ovf++;
+                    atomicAdd(&A.ctl->err_overflow, 1u);
                 }
-                // :228-251 pop / finish when no leaf triangles are pending
-                if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
-                    if (stack_size == 0) {
-                        finish = true;
-                    } else {
-                        if (stack_size == tlas_ss) {
-                            NodeOffset = 0;
-                            TriOffset = 0;
-                            tlas_ss = -1;
-                            ray = world_ray();
-                            oct = octant_inv4(ray);
-                        }
-                        TT_POP(cg);
-                    }
-                }
+                tg.y = 0u;
             }
         }
-
-        TT_PREFETCH_NEXT();
 
         if (STATS) {
             const uint64_t tm = __ballot(active && tg.y != 0u);
@@ -596,95 +551,80 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             }
         }
         // --------------------------------------------------------- triangle phase
-#if TT_TRI_LOOP
-        while (active && tg.y != 0u) {  // :220-226, highest bit first, drain the lane's leaf bits
-#else
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
-#endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
-#ifdef TT_EXP_NO_TRI
-            const bool acc = false;
-            if (best.t == -1.0f) best.tri_id = (int32_t)(tg.x + ti);
-#else
-            const bool acc = intersect_triangle<MATCHECK>(A.tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), mesh_id,
+            const bool acc = intersect_triangle<MATCHECK>(tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), mesh_id,
                                                           MatOffset, ray, best);
-#endif
             if (STATS) {
                 c_tris++;
                 c_acc += acc ? 1u : 0u;
             }
-            if (tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
-                if (stack_size == 0) {
-                    finish = true;
-                } else {
-                    if (stack_size == tlas_ss) {
-                        NodeOffset = 0;
-                        TriOffset = 0;
-                        tlas_ss = -1;
-                        ray = world_ray();
-                        oct = octant_inv4(ray);
-                    }
-                    TT_POP(cg);
-                }
-                TT_PREFETCH_NEXT();
-            }
         }
 
-        // ------------------------------------------------------------------ finish
-        if (finish) {  // :229-241 + set() CommonData.cginc:430-434
-            tt_ray_data* R = A.rays + ray_index;
-            if (INFO != 0) {
-                const uint32_t pix = R->PixelIndex;
-                const uint32_t tx = pix % A.width, ty = pix / A.width;
-                if (ty < A.height) {
-                    uint4 o;
-                    bool write = false;
-                    if (INFO == 1) {
-                        const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                        o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to), __float_as_uint(best.u),
-                                       __float_as_uint(best.v));
-                        write = true;
-                    } else {
-                        const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
-                        if (w == -1.0f || (float)A.bounce == w) {
-                            const LaneRay wr = world_ray();
-                            write = true;
-                            const bool miss = best.t == A.far_plane;
-                            if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
-                                const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                                o.x = (uint32_t)best.mesh_id;
-                                o.y = (uint32_t)(best.tri_id - to);
-                                o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-                            } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
-                                o.x = __float_as_uint(wr.dx);
-                                o.y = __float_as_uint(wr.dy);
-                                o.z = __float_as_uint(wr.dz);
-                            } else {
-                                o.x = __float_as_uint(wr.dx * best.t + wr.ox);
-                                o.y = __float_as_uint(wr.dy * best.t + wr.oy);
-                                o.z = __float_as_uint(wr.dz * best.t + wr.oz);
-                            }
-                            o.w = miss ? 1u : 0u;
-                        }
-                    }
-                    if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+        // ----------------------------------------- advance: pop / finish (:228-251)
+        // One place for every lane whose group is used up, whether it came from a node step or
+        // from its last triangle this pass (equivalent order: the reference pops right after).
+        if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+            if (stack_size != 0) {
+                if (stack_size == tlas_ss) {
+                    NodeOffset = 0;
+                    TriOffset = 0;
+                    tlas_ss = -1;
+                    ray = world_ray();
+                    oct = octant_inv4(ray);
                 }
-            }
-            const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-#ifndef TT_EXP_NO_STORE
-            reinterpret_cast<uint4*>(R)[2] =
-                make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
-#else
-            if (best.t == -12345.0f) reinterpret_cast<uint4*>(R)[2] = make_uint4(0, 0, 0, uv);
-#endif
-            if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
+                TT_POP(cg);
+            } else {  // :229-241 + set() CommonData.cginc:430-434
+                tt_ray_data* R = A.rays + ray_index;
+                if (INFO != 0) {
+                    const uint32_t pix = R->PixelIndex;
+                    const uint32_t tx = pix % A.width, ty = pix / A.width;
+                    if (ty < A.height) {
+                        uint4 o;
+                        bool write = false;
+                        if (INFO == 1) {
+                            const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                            o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to),
+                                           __float_as_uint(best.u), __float_as_uint(best.v));
+                            write = true;
+                        } else {
+                            const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
+                            if (w == -1.0f || (float)A.bounce == w) {
+                                const LaneRay wr = world_ray();
+                                write = true;
+                                const bool miss = best.t == A.far_plane;
+                                if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
+                                    const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                                    o.x = (uint32_t)best.mesh_id;
+                                    o.y = (uint32_t)(best.tri_id - to);
+                                    o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                                } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
+                                    o.x = __float_as_uint(wr.dx);
+                                    o.y = __float_as_uint(wr.dy);
+                                    o.z = __float_as_uint(wr.dz);
+                                } else {
+                                    o.x = __float_as_uint(wr.dx * best.t + wr.ox);
+                                    o.y = __float_as_uint(wr.dy * best.t + wr.oy);
+                                    o.z = __float_as_uint(wr.dz * best.t + wr.oz);
+                                }
+                                o.w = miss ? 1u : 0u;
+                            }
+                        }
+                        if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+                    }
+                }
+                const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                reinterpret_cast<uint4*>(R)[2] =
+                    make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+                if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
 #ifdef TT_DIAG_RAYS
-            if (A.diag_times)
-                reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
-                    make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
+                if (A.diag_times)
+                    reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
+                        make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
 #endif
-            active = false;
+                active = false;
+            }
         }
     }
 
@@ -739,6 +679,8 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
     const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
     SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
     const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
+    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
+    const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
     bool active = false;
     uint32_t ray_index = 0;
@@ -837,8 +779,9 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
         const bool overflow = push && stack_size == TT_STACK_SIZE;
         s_stack[stack_size][tid] = make_uint2(cg.x, rem);  // above the top unless pushed
         const uint32_t child = do_node ? cg.x + rel : 0u;
-        const uint4* np = A.nodes + (size_t)child * 5u;
-        const uint4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3], n4 = np[4];
+        const uint32_t no = node_offset(child);
+        const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u), n2 = buffer_load16(nodes, no + 32u),
+                    n3 = buffer_load16(nodes, no + 48u), n4 = buffer_load16(nodes, no + 64u);
         const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
         const bool commit = do_node && !overflow;
         {
@@ -927,8 +870,8 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
             const bool do_tri = active && tg.y != 0u;
             const uint32_t ti = firstbithigh(tg.y | 1u);
             const int32_t tri_id = do_tri ? (int32_t)(tg.x + ti) : 0;
-            const uint4* tp = reinterpret_cast<const uint4*>(A.tris + tri_id);
-            const uint4 ta = tp[0], tb = tp[1], tc = tp[2];
+            const uint32_t to = tri_offset((uint32_t)tri_id);
+            const uint4 ta = buffer_load16(tris, to), tb = buffer_load16(tris, to + 16u), tc = buffer_load16(tris, to + 32u);
             const float p0x = __uint_as_float(ta.x), p0y = __uint_as_float(ta.y), p0z = __uint_as_float(ta.z);
             const float e1x = __uint_as_float(ta.w), e1y = __uint_as_float(tb.x), e1z = __uint_as_float(tb.y);
             const float e2x = __uint_as_float(tb.z), e2y = __uint_as_float(tb.w), e2z = __uint_as_float(tc.x);
