@@ -177,6 +177,16 @@ def main():
                          f"C# scalar baseline not run: no .NET runtime on the box"}
         log(f"cpu baseline {cpu['value']} Mrays/s ({reps} reps, {tcpu:.1f}s)")
 
+    # fabric traffic per launch from the round's separate rocprofv3 --pmc pass of this same command
+    # (tools/profile_round.sh -> profiles/traffic_latest.json); null when no such pass was committed
+    traffic, traffic_src = None, None
+    tpath = os.path.join(REPO, "profiles", "traffic_latest.json")
+    if os.path.exists(tpath) and (W, H, args.tris) == (1920, 1080, 262267):
+        with open(tpath) as f:
+            tj = json.load(f)
+        traffic = round(float(tj["mean_bytes_per_launch"]))
+        traffic_src = "profiles/" + os.path.basename(tj.get("file", "traffic_latest.json"))
+
     ms_per_step = elapsed * 1e3 / args.steps
     result = {
         "metric": METRIC,
@@ -200,9 +210,13 @@ def main():
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
                    "gather_ms": None if gather_ms is None else round(gather_ms, 3)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),
                      "note": "achieved = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean HIP-event "
-                             "launch time; bytes are served mostly from L2/MALL, see DESIGN.md"},
+                             "launch time; bytes are served mostly from L2/MALL, so the loop is bound by VALU issue "
+                             "and load latency, not HBM (DESIGN.md §5). traffic = fabric bytes per launch from "
+                             + (traffic_src or "no PMC pass") + " (2 x FETCH_SIZE + WRITE_SIZE, includes "
+                             "Infinity-Cache hits)"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(result), flush=True)

@@ -22,7 +22,9 @@ c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0)
 eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
 eng.trace(rays, W * H, 0, far, W, H, info=info, device=True)
 nb = eng.enqueue_bounce(rays, W * H, 0, far, W, H, frames=0, max_bounce=1, device=True)
-eng.trace(rays, nb, 1, far, W, H, device=True)
+colors = np.zeros(W * H, tthip.COL_DTYPE); colors["Data"][:, 3] = 1.0  # as bench.py: info written at bounce 1
+colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True)
 host = rays.cpu().numpy().view(tthip.RAY_DTYPE).copy()
 ok = True
 for off, n, b in ((0, W * H, 0), (W * H, nb, 1)):
@@ -32,11 +34,11 @@ for off, n, b in ((0, W * H, 0), (W * H, nb, 1)):
     ok &= bool(np.array_equal(s["hits"][:len(idx)], host["hits"][idx]))
 for _ in range(3):
     eng.trace(rays, W * H, 0, far, W, H, info=info, device=True, asynchronous=True)
-    eng.trace(rays, nb, 1, far, W, H, device=True, asynchronous=True)
+    eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
 eng.timing_reset()
 for _ in range(10):
     eng.trace(rays, W * H, 0, far, W, H, info=info, device=True, asynchronous=True)
-    eng.trace(rays, nb, 1, far, W, H, device=True, asynchronous=True)
+    eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
 ms = eng.timing_read()
 p, b = float(np.median(ms[0::2])), float(np.median(ms[1::2]))
 print(json.dumps({"ok": ok, "primary_ms": round(p, 4), "bounce_ms": round(b, 4), "grays": round((W * H + nb) / (p + b) / 1e6, 3)}))

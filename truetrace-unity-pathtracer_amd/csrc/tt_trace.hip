@@ -24,6 +24,12 @@
 #ifndef TT_SDWA_BITS
 #define TT_SDWA_BITS 1    // 1: per-child hit bits with one byte-selecting SDWA shift
 #endif
+#ifndef TT_DEFER_FINISH
+#define TT_DEFER_FINISH 1 // 1: write finished rays' records in batches at refill time
+#endif
+#ifndef TT_TRI_MIN
+#define TT_TRI_MIN 1      // >1: run the triangle pass only when at least this many lanes need it
+#endif
 #ifndef TT_NODE_PK
 #define TT_NODE_PK 0      // 1: node slab fmas as v_pk_fma_f32 pairs (measured ~2% slower on C2)
 #endif
@@ -314,6 +320,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     // lane traversal state (IntersectionKernels.compute:62-77)
     bool active = false;
     uint32_t ray_index = 0;
+    uint32_t pix = 0;    // RayData.PixelIndex, kept from the ray load
+    float col_w = 0.0f;  // GlobalColors[pix].Data.w (INFO == 2), loaded when the ray starts
+    bool pending = false;  // finished, record not yet written (TT_DEFER_FINISH)
     LaneRay ray{}, wray{};
     Best best{};
     uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
@@ -350,6 +359,55 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
     };
 
+    // :229-241 + set() CommonData.cginc:430-434: hit record and _PrimaryTriangleInfo of a finished ray
+    auto finish_ray = [&]() {
+        tt_ray_data* R = A.rays + ray_index;
+        if (INFO != 0) {
+            const uint32_t tx = pix % A.width, ty = pix / A.width;
+            if (ty < A.height) {
+                uint4 o;
+                bool write = false;
+                if (INFO == 1) {
+                    const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                    o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to),
+                                   __float_as_uint(best.u), __float_as_uint(best.v));
+                    write = true;
+                } else {
+                    const float w = col_w;
+                    if (w == -1.0f || (float)A.bounce == w) {
+                        const LaneRay wr = world_ray();
+                        write = true;
+                        const bool miss = best.t == A.far_plane;
+                        if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
+                            const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                            o.x = (uint32_t)best.mesh_id;
+                            o.y = (uint32_t)(best.tri_id - to);
+                            o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                        } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
+                            o.x = __float_as_uint(wr.dx);
+                            o.y = __float_as_uint(wr.dy);
+                            o.z = __float_as_uint(wr.dz);
+                        } else {
+                            o.x = __float_as_uint(wr.dx * best.t + wr.ox);
+                            o.y = __float_as_uint(wr.dy * best.t + wr.oy);
+                            o.z = __float_as_uint(wr.dz * best.t + wr.oz);
+                        }
+                        o.w = miss ? 1u : 0u;
+                    }
+                }
+                if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+            }
+        }
+        const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+        reinterpret_cast<uint4*>(R)[2] =
+            make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+        if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
+#ifdef TT_DIAG_RAYS
+        if (A.diag_times)
+            reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
+                make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
+#endif
+    };
 #ifdef TT_DIAG_TIMES
     const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
     const uint64_t c_begin = __builtin_amdgcn_s_memtime();
@@ -359,6 +417,15 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
         const bool pool_dry = !more && pool_next >= pool_end;
+#if TT_DEFER_FINISH
+        // finished rays write their records in batches, right before their lanes are refilled
+        if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry)) {
+            if (pending) {
+                finish_ray();
+                pending = false;
+            }
+        }
+#endif
         if (n_idle == TT_WAVE && pool_dry) break;
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest
@@ -392,6 +459,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 ray_index = A.ray_offset + local;
                 const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
                 const uint4 r0 = rp[0], r1 = rp[1];
+                pix = r0.w;
+                if (INFO == 2) col_w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
                 ray.ox = __uint_as_float(r0.x);
                 ray.oy = __uint_as_float(r0.y);
                 ray.oz = __uint_as_float(r0.z);
@@ -551,7 +620,19 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             }
         }
         // --------------------------------------------------------- triangle phase
+#if TT_TRI_MIN > 1
+        // postpone the pass while few lanes have a triangle pending and others still traverse
+        // (per-ray order is unchanged: a lane with pending triangles takes no node step)
+        bool tri_pass = true;
+        {
+            const uint32_t n_tri = (uint32_t)__popcll(__ballot(active && tg.y != 0u));
+            const uint32_t n_act = (uint32_t)__popcll(__ballot(active));
+            tri_pass = n_tri >= TT_TRI_MIN || n_tri == n_act;
+        }
+        if (tri_pass && active && tg.y != 0u) {
+#else
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
+#endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool acc = intersect_triangle<MATCHECK>(tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), mesh_id,
@@ -575,53 +656,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     oct = octant_inv4(ray);
                 }
                 TT_POP(cg);
-            } else {  // :229-241 + set() CommonData.cginc:430-434
-                tt_ray_data* R = A.rays + ray_index;
-                if (INFO != 0) {
-                    const uint32_t pix = R->PixelIndex;
-                    const uint32_t tx = pix % A.width, ty = pix / A.width;
-                    if (ty < A.height) {
-                        uint4 o;
-                        bool write = false;
-                        if (INFO == 1) {
-                            const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                            o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to),
-                                           __float_as_uint(best.u), __float_as_uint(best.v));
-                            write = true;
-                        } else {
-                            const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
-                            if (w == -1.0f || (float)A.bounce == w) {
-                                const LaneRay wr = world_ray();
-                                write = true;
-                                const bool miss = best.t == A.far_plane;
-                                if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
-                                    const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                                    o.x = (uint32_t)best.mesh_id;
-                                    o.y = (uint32_t)(best.tri_id - to);
-                                    o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-                                } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
-                                    o.x = __float_as_uint(wr.dx);
-                                    o.y = __float_as_uint(wr.dy);
-                                    o.z = __float_as_uint(wr.dz);
-                                } else {
-                                    o.x = __float_as_uint(wr.dx * best.t + wr.ox);
-                                    o.y = __float_as_uint(wr.dy * best.t + wr.oy);
-                                    o.z = __float_as_uint(wr.dz * best.t + wr.oz);
-                                }
-                                o.w = miss ? 1u : 0u;
-                            }
-                        }
-                        if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
-                    }
-                }
-                const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-                reinterpret_cast<uint4*>(R)[2] =
-                    make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
-                if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
-#ifdef TT_DIAG_RAYS
-                if (A.diag_times)
-                    reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
-                        make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
+            } else {
+#if TT_DEFER_FINISH
+                pending = true;  // written at the next refill (or when the wave drains)
+#else
+                finish_ray();
 #endif
                 active = false;
             }
