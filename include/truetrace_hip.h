@@ -171,6 +171,22 @@ typedef struct tt_col_data {
 } tt_col_data;
 TT_STATIC_ASSERT(sizeof(tt_col_data) == 64, "ColData is 64 bytes");
 
+/* ShadowRayData, 48 B (CommonData.cginc:116-123). t > 0 / t < 0 selects the Direct vs
+ * PrimaryNEERay/Indirect accumulation in the reference; max distance = |t|; t is set to 0 in
+ * place when the ray is occluded (IntersectionKernels.compute:449-454). */
+typedef struct tt_shadow_ray {
+    float origin[3];
+    float LuminanceIncomming;
+    float direction[3];
+    float t;
+    float illumination[3];
+    uint32_t PixelIndex;
+} tt_shadow_ray;
+TT_STATIC_ASSERT(sizeof(tt_shadow_ray) == 48, "ShadowRayData is 48 bytes");
+
+#define TT_FLAG_IS_BACKGROUND 5 /* GlobalDefines.cginc:41 */
+#define TT_FLAG_SHADOW_CASTER 6 /* GlobalDefines.cginc:42 */
+
 /* --------------------------------------------------------- context */
 typedef struct tt_ctx tt_ctx;
 
@@ -275,6 +291,32 @@ tt_status tt_trace_diagnostics(const tt_ctx* ctx, uint64_t* out8);
 tt_status tt_sync(tt_ctx* ctx);
 /* The hipStream_t the context issues on. */
 void* tt_ctx_stream(tt_ctx* ctx);
+
+/* --------------------------------------- any-hit visibility */
+typedef struct tt_shadow_params {
+    uint32_t n_rays;         /* BufferSizes[CurBounce].shadow_rays                      */
+    int32_t bounce;          /* CurBounce                                               */
+    uint32_t screen_width;   /* NEEPosA pixel decode                                    */
+    uint32_t screen_height;
+    uint32_t flags;          /* TT_TRACE_DEVICE_PTRS | TT_TRACE_STATS | TT_TRACE_ASYNC  */
+} tt_shadow_params;
+
+/* Replaces one kernel_shadow dispatch (IntersectionKernels.compute:264-505, HardwareRT off,
+ * AdvancedAlphaMapped / IgnoreGlassShadow / StainedGlassShadows on): any-hit CWBVH8 traversal of
+ * shadow_rays[0, n_rays) against max distance |t|, skipping IsBackground / ShadowCaster
+ * materials (triangle_intersect_shadow, CommonData.cginc:593-634). Outputs:
+ *   shadow_rays    : t = 0 in place for occluded rays (as the reference);
+ *   visibility     : nullable float4[n_rays] = (throughput.xyz, 1) for rays that reached |t|,
+ *                    (0,0,0,0) occluded, (0,0,0,-1) Reps bound hit (the reference writes nothing);
+ *   global_colors  : nullable ColData[W*H]; at bounce 0, for unoccluded rays with t >= 0,
+ *                    Direct += illumination * throughput (:466-470);
+ *   nee_pos        : nullable float4[W*H]; at bounce 0, unoccluded rays write
+ *                    (origin + direction * |t|, 0) to NEEPosA[pixel] (:461).
+ * The radiance-cache, PrimaryNEERay and bounce > 0 Indirect accumulations (RGBE / log-luminance
+ * encodings) stay with the caller, driven by `visibility`. Scenes with Cutout materials or
+ * specTrans == 1 (glass tint samples the texture atlas) return TT_ERR_UNSUPPORTED. */
+tt_status tt_trace_shadow(tt_ctx* ctx, const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
+                          tt_col_data* global_colors, float* nee_pos, tt_stats* stats);
 
 /* ------------------------------------------------- attribute resolve */
 /* Parity aid for "normals within 1e-5": per hit, the interpolated shading normal

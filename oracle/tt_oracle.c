@@ -391,6 +391,259 @@ tt_status tt_oracle_trace(const tt_cwbvh_node* nodes, uint32_t n_nodes,
     return TT_OK;
 }
 
+/* ------------------------------------------------------ any-hit (kernel_shadow) */
+/* triangle_intersect_shadow — CommonData.cginc:593-634 with AdvancedAlphaMapped,
+ * IgnoreGlassShadow and StainedGlassShadows on (GlobalDefines.cginc:1-8). The material checks run
+ * BEFORE the t-range test (:611-629). Returns 1 = occluder, 0 = not, 3 = a material that needs
+ * the alpha / texture atlases (Cutout, specTrans == 1: unsupported). */
+static int intersect_triangle_shadow(const scene* s, int tri_id, const Ray* ray, float max_distance,
+                                     int MatOffset, uint32_t* accepts) {
+    const tt_cuda_triangle* T = &s->tris[tri_id];
+    const int MaterialIndex = MatOffset + (int)T->MatDat;
+    const v3 pos0 = ld3(T->pos0), posedge1 = ld3(T->posedge1), posedge2 = ld3(T->posedge2);
+    const v3 h = vcross(ray->direction, posedge2);
+    const float a = vdot(posedge1, h);
+    const float f = 1.0f / a;
+    const v3 sv = vsub(ray->origin, pos0);
+    const float u = f * vdot(sv, h);
+    if (u >= 0.0f && u <= 1.0f) {
+        const v3 q = vcross(sv, posedge1);
+        const float v = f * vdot(ray->direction, q);
+        if (v >= 0.0f && u + v <= 1.0f) {
+            const float t = f * vdot(posedge2, q);
+            /* out-of-range _Materials reads return zeros (no flags, MatType 0, specTrans 0) */
+            if (MaterialIndex >= 0 && (uint32_t)MaterialIndex < s->n_mat) {
+                const tt_material* m = &s->mats[MaterialIndex];
+                const int tag = (int)m->Tag;
+                if (((tag >> TT_FLAG_IS_BACKGROUND) & 1) || ((tag >> TT_FLAG_SHADOW_CASTER) & 1)) return 0;
+                if (m->MatType == TT_MAT_CUTOUT_INDEX || m->specTrans == 1.0f) return 3;
+            }
+            if (t > 0.0f && t < max_distance) {
+                ++*accepts;
+                return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+typedef struct shadow_job {
+    const scene* s;
+    const tt_shadow_params* p;
+    tt_shadow_ray* rays;
+    float* visibility;
+    tt_col_data* colors;
+    float* nee_pos;
+    tt_oracle_ray_counts* counts;
+} shadow_job;
+
+/* IntersectBVHShadow — IntersectionKernels.compute:264-500 (HardwareRT off, TerrainExists false).
+ * status: 0 = reached |t| (outputs written), 4 = occluded (t = 0 written), 1 = Reps exhausted,
+ * 2 = stack overflow, 3 = unsupported material. */
+static int intersect_bvh_shadow(const shadow_job* J, uint32_t i) {
+    const scene* s = J->s;
+    const tt_shadow_params* P = J->p;
+    const int CurBounce = P->bounce;
+    tt_oracle_ray_counts cnt = {0, 0, 0, 0, 0, 0};
+    uint2 stack[TT_STACK_SIZE];
+    int stack_size = 0;
+    uint2 current_group, triangle_group = {0u, 0u};
+    uint32_t oct_inv4;
+    int tlas_stack_size;
+    Ray ray, ray2;
+    int NodeOffset, TriOffset, MatOffset;
+    int mesh_id = -1;
+    int Reps;
+    tt_shadow_ray* SR = &J->rays[i];
+    const float max_distance = fabsf(SR->t);
+    ray.origin = ld3(SR->origin);
+    ray.direction = ld3(SR->direction);
+    ray.direction_inv = vrcp(ray.direction);
+    ray2 = ray;
+    const float throughput[3] = {1.0f, 1.0f, 1.0f};
+    TriOffset = 0;
+    MatOffset = 0;
+    Reps = 0;
+    NodeOffset = 0;
+    oct_inv4 = ray_get_octant_inv4(ray.direction);
+    current_group.x = 0u;
+    current_group.y = 0x80000000u;
+    tlas_stack_size = -1;
+    int status = 1;
+    (void)mesh_id;
+
+    while (Reps < TT_MAX_REPS) {
+        if (current_group.y & 0xff000000u) { /* :374-403 */
+            const uint32_t child_index_offset = firstbithigh(current_group.y);
+            const uint32_t slot_index = (child_index_offset - 24) ^ (oct_inv4 & 0xff);
+            const uint32_t relative_index = countbits(current_group.y & ~(0xffffffffu << slot_index));
+            const uint32_t child_node_index = current_group.x + relative_index;
+            current_group.y &= ~(1u << child_index_offset);
+            if (current_group.y & 0xff000000u) {
+                if (stack_size == TT_STACK_SIZE) { status = 2; goto done; }
+                stack[stack_size++] = current_group;
+                if ((uint32_t)stack_size > cnt.max_stack) cnt.max_stack = (uint32_t)stack_size;
+            }
+            const tt_cwbvh_node* TempNode = &s->nodes[child_node_index];
+            const uint32_t hitmask = cwbvh_node_intersect(&ray, oct_inv4, max_distance, TempNode);
+            current_group.y = (hitmask & 0xff000000u) | ((TempNode->e_imask >> 24) & 0xff);
+            triangle_group.y = (hitmask & 0x00ffffffu);
+            current_group.x = TempNode->base_child + (uint32_t)NodeOffset;
+            triangle_group.x = TempNode->base_tri + (uint32_t)TriOffset;
+            Reps++;
+            cnt.node_visits++;
+        } else { /* :404-407 */
+            triangle_group = current_group;
+            current_group.x = 0u;
+            current_group.y = 0u;
+        }
+        int hit = 0;
+        if (triangle_group.y != 0) {
+            if (tlas_stack_size == -1) { /* :411-435 TLAS leaf -> enter BLAS */
+                const uint32_t mesh_offset = firstbithigh(triangle_group.y);
+                triangle_group.y &= ~(1u << mesh_offset);
+                mesh_id = s->tlas[triangle_group.x + mesh_offset];
+                const tt_mesh_data* MD = &s->md[mesh_id];
+                NodeOffset = MD->NodeOffset;
+                TriOffset = MD->TriOffset;
+                if (triangle_group.y != 0) {
+                    if (stack_size == TT_STACK_SIZE) { status = 2; goto done; }
+                    stack[stack_size++] = triangle_group;
+                }
+                if (current_group.y & 0xff000000u) {
+                    if (stack_size == TT_STACK_SIZE) { status = 2; goto done; }
+                    stack[stack_size++] = current_group;
+                }
+                if ((uint32_t)stack_size > cnt.max_stack) cnt.max_stack = (uint32_t)stack_size;
+                tlas_stack_size = stack_size;
+                const int root_index = (MD->mesh_data_bvh_offsets & 0x7fffffff);
+                MatOffset = MD->MaterialOffset;
+                ray.direction = mul33(MD->W2L, ray.direction);
+                ray.origin = mul34(MD->W2L, ray.origin);
+                ray.direction_inv = vrcp(ray.direction);
+                oct_inv4 = ray_get_octant_inv4(ray.direction);
+                current_group.x = (uint32_t)root_index;
+                current_group.y = 0x80000000u;
+                cnt.blas_entries++;
+            } else { /* :436-446 leaf triangles until the first occluder */
+                while (triangle_group.y != 0) {
+                    const uint32_t triangle_index = firstbithigh(triangle_group.y);
+                    triangle_group.y &= ~(1u << triangle_index);
+                    cnt.tri_tests++;
+                    const int r = intersect_triangle_shadow(s, (int)(triangle_group.x + triangle_index), &ray,
+                                                            max_distance, MatOffset, &cnt.accepts);
+                    if (r == 3) { status = 3; goto done; }
+                    if (r) { hit = 1; break; }
+                }
+            }
+        }
+        if (hit) { /* :449-454 */
+            SR->t = 0.0f;
+            if (J->visibility) for (int k = 0; k < 4; k++) J->visibility[4 * (size_t)i + k] = 0.0f;
+            status = 4;
+            goto done;
+        }
+        if ((current_group.y & 0xff000000u) == 0) {
+            if (stack_size == 0) { /* :457-485 reached the light: outputs (TerrainExists false) */
+                const uint32_t PixelIndex = SR->PixelIndex;
+                const uint32_t W = P->screen_width, H = P->screen_height;
+                if (J->visibility) {
+                    for (int k = 0; k < 3; k++) J->visibility[4 * (size_t)i + k] = throughput[k];
+                    J->visibility[4 * (size_t)i + 3] = 1.0f;
+                }
+                if (CurBounce == 0 && J->nee_pos && PixelIndex / W < H) {
+                    float* o = &J->nee_pos[4 * (size_t)PixelIndex];
+                    const float d = fabsf(SR->t);
+                    o[0] = ray2.origin.x + ray2.direction.x * d;
+                    o[1] = ray2.origin.y + ray2.direction.y * d;
+                    o[2] = ray2.origin.z + ray2.direction.z * d;
+                    o[3] = 0.0f;
+                }
+                if (SR->t >= 0.0f && CurBounce == 0 && J->colors) {
+                    tt_col_data* C = &J->colors[PixelIndex];
+                    for (int k = 0; k < 3; k++) C->Direct[k] = C->Direct[k] + SR->illumination[k] * throughput[k];
+                }
+                status = 0;
+                goto done;
+            }
+            if (stack_size == tlas_stack_size) { /* :487-493 */
+                NodeOffset = 0;
+                TriOffset = 0;
+                tlas_stack_size = -1;
+                ray = ray2;
+                oct_inv4 = ray_get_octant_inv4(ray.direction);
+            }
+            current_group = stack[--stack_size];
+        }
+    }
+done:
+    if (status == 1 && J->visibility) {
+        for (int k = 0; k < 3; k++) J->visibility[4 * (size_t)i + k] = 0.0f;
+        J->visibility[4 * (size_t)i + 3] = -1.0f;
+    }
+    cnt.status = (uint32_t)status;
+    if (J->counts) J->counts[i] = cnt;
+    return status;
+}
+
+typedef struct shadow_worker {
+    const shadow_job* J;
+    uint32_t tid, nthreads;
+    int worst;
+} shadow_worker;
+
+static void* shadow_worker_main(void* arg) {
+    shadow_worker* w = (shadow_worker*)arg;
+    const uint32_t n = w->J->p->n_rays;
+    for (uint32_t base = w->tid * TT_ORACLE_CHUNK; base < n; base += w->nthreads * TT_ORACLE_CHUNK) {
+        const uint32_t end = base + TT_ORACLE_CHUNK < n ? base + TT_ORACLE_CHUNK : n;
+        for (uint32_t i = base; i < end; i++) {
+            int st = intersect_bvh_shadow(w->J, i);
+            if (st == 4) st = 0;
+            if (st > w->worst) w->worst = st;
+        }
+    }
+    return NULL;
+}
+
+tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                           const tt_cuda_triangle* tris, uint32_t n_tris,
+                           const int32_t* tlas_indices, uint32_t n_tlas,
+                           const tt_mesh_data* meshdata, uint32_t n_mesh,
+                           const tt_material* materials, uint32_t n_mat,
+                           const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
+                           tt_col_data* global_colors, float* nee_pos,
+                           tt_oracle_ray_counts* counts, int32_t nthreads) {
+    if (!nodes || !tris || !tlas_indices || !meshdata || !p || !shadow_rays) return TT_ERR_INVALID_ARG;
+    if (n_mat && !materials) return TT_ERR_INVALID_ARG;
+    if (p->screen_width == 0 || p->screen_height == 0) return TT_ERR_INVALID_ARG;
+    scene s = {nodes, n_nodes, tris, n_tris, tlas_indices, n_tlas, meshdata, n_mesh, materials, n_mat};
+    for (uint32_t m = 0; m < n_mat; m++)
+        if (materials[m].MatType == TT_MAT_CUTOUT_INDEX || materials[m].specTrans == 1.0f) return TT_ERR_UNSUPPORTED;
+    shadow_job J = {&s, p, shadow_rays, visibility, global_colors, nee_pos, counts};
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    shadow_worker ws[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) {
+        ws[t].J = &J;
+        ws[t].tid = (uint32_t)t;
+        ws[t].nthreads = (uint32_t)nthreads;
+        ws[t].worst = 0;
+    }
+    if (nthreads == 1) {
+        shadow_worker_main(&ws[0]);
+    } else {
+        for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, shadow_worker_main, &ws[t]);
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    }
+    int worst = 0;
+    for (int t = 0; t < nthreads; t++) if (ws[t].worst > worst) worst = ws[t].worst;
+    if (worst == 2) return TT_ERR_STACK_OVERFLOW;
+    if (worst == 3) return TT_ERR_UNSUPPORTED;
+    return TT_OK;
+}
+
 /* ------------------------------------------------------------ normal resolve */
 /* i_octahedral_32 — CommonData.cginc:849-857 (normalize pinned as v * (1/sqrt(dot))). */
 static v3 vnormalize(v3 v) {

@@ -46,6 +46,18 @@ tt_status tt_oracle_trace(const tt_cwbvh_node* nodes, uint32_t n_nodes,
                           uint32_t* primary_info, const tt_col_data* global_colors,
                           tt_oracle_ray_counts* counts, int32_t nthreads);
 
+/* Any-hit visibility (kernel_shadow / IntersectBVHShadow, IntersectionKernels.compute:264-505);
+ * outputs as tt_trace_shadow. counts[i].status: 0 reached |t|, 4 occluded, 1 Reps exhausted,
+ * 2 stack overflow, 3 unsupported material. */
+tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                           const tt_cuda_triangle* tris, uint32_t n_tris,
+                           const int32_t* tlas_indices, uint32_t n_tlas,
+                           const tt_mesh_data* meshdata, uint32_t n_mesh,
+                           const tt_material* materials, uint32_t n_mat,
+                           const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
+                           tt_col_data* global_colors, float* nee_pos,
+                           tt_oracle_ray_counts* counts, int32_t nthreads);
+
 /* Shading / geometric normal for the hit stored in GlobalRays (see tt_resolve_normals). */
 tt_status tt_oracle_resolve_normals(const tt_cuda_triangle* tris, uint32_t n_tris,
                                     const tt_mesh_data* meshdata, uint32_t n_mesh,

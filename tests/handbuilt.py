@@ -100,3 +100,37 @@ def rays_buffer(origins, dirs, far=1000.0, width=None, height=1):
 def expected_hit(mesh_id, tri_id, t, u, v):
     uv = int(np.uint32(np.float32(u) * np.float32(65535.0))) | (int(np.uint32(np.float32(v) * np.float32(65535.0))) << 16)
     return [mesh_id, tri_id & 0xFFFFFFFF, int(np.float32(t).view(np.uint32)), uv]
+
+
+def shadow_rays(origins, dirs, ts, illum=(1.0, 2.0, 4.0)):
+    """ShadowRayData array (CommonData.cginc:116-123), PixelIndex = ray index."""
+    n = len(origins)
+    r = np.zeros(n, tthip.SHADOW_DTYPE)
+    r["origin"] = origins
+    r["direction"] = dirs
+    r["t"] = ts
+    r["illumination"] = illum
+    r["PixelIndex"] = np.arange(n)
+    return r
+
+
+def nee_rays_from_hits(rays, n, light, seed=0, far=1000.0):
+    """Shadow rays toward a point light from the hit points of the first n traced rays (misses
+    skipped): origin backed off 1e-3 along the incoming direction, t = +-distance with a random
+    sign (the reference uses the sign to pick the accumulation target). Test input only."""
+    rng = np.random.default_rng(seed)
+    h = rays["hits"][:n]
+    t = h[:, 2].view(np.float32)
+    hit = t < np.float32(far)
+    o = rays["origin"][:n][hit].astype(np.float32)
+    d = rays["direction"][:n][hit].astype(np.float32)
+    p = o + d * t[hit][:, None] - d * np.float32(1e-3)
+    to = np.asarray(light, np.float32)[None, :] - p
+    dist = np.sqrt((to * to).sum(1)).astype(np.float32)
+    sr = np.zeros(int(hit.sum()), tthip.SHADOW_DTYPE)
+    sr["origin"] = p
+    sr["direction"] = to / dist[:, None]
+    sr["t"] = dist * np.where(rng.random(len(sr)) < 0.75, 1.0, -1.0).astype(np.float32)
+    sr["illumination"] = rng.random((len(sr), 3)).astype(np.float32)
+    sr["PixelIndex"] = rays["PixelIndex"][:n][hit]
+    return sr

@@ -152,3 +152,47 @@ def case_invisible_bounce0():
 
 ALL_CASES = [case_single_triangle, case_tie_first_found_wins, case_octant_order_and_culling, case_reps_exhausted,
              case_chain_within_bound, case_two_instances]
+
+
+# ------------------------------------------------------------------- any-hit (kernel_shadow)
+def shadow_case_single_triangle():
+    """Unit triangle at z = 0, rays straight down from z = 1 (the hit is at t = 1 exactly).
+    Returns (scene, shadow rays, expected status per ray: 0 reached |t|, 4 occluded)."""
+    sc = hb.scene([_leaf_root()], [UNIT_TRI])
+    o, d = (0.25, 0.25, 1.0), (0.0, 0.0, -1.0)
+    rays = hb.shadow_rays([o, o, o, o, (2.0, 2.0, 1.0), o, (0.25, 0.25, -1.0)],
+                          [d, d, d, d, d, d, d],
+                          [2.0, 0.5, -2.0, -0.5, 2.0, 1.0, 2.0])
+    # t = 2 occluded; 0.5 short of the surface; -2 occluded (|t|); -0.5 short; miss in x,y;
+    # |t| = 1 exactly: strict t < max_distance keeps it visible; origin below, t = -1 behind
+    return "shadow_single_triangle", sc, rays, [4, 0, 4, 0, 0, 0, 0]
+
+
+def shadow_case_flags():
+    """A ShadowCaster and an IsBackground surface never occlude (CommonData.cginc:612); a plain
+    one behind them does."""
+    tris = [hb.tri((0.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=1),
+            hb.tri((0.0, 0.0, -0.25), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=2),
+            hb.tri((0.0, 0.0, -0.5), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=0)]
+    root = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0,
+                        [(0, "leaf", (64, 64, 31), (128, 128, 65), (0, 3))])
+    mats = np.zeros(3, tthip.MAT_DTYPE)
+    mats[1]["Tag"] = 1 << tthip.TT_FLAG_SHADOW_CASTER
+    mats[2]["Tag"] = 1 << tthip.TT_FLAG_IS_BACKGROUND
+    sc = hb.scene([root], tris, materials=mats)
+    o, d = (0.25, 0.25, 1.0), (0.0, 0.0, -1.0)
+    rays = hb.shadow_rays([o, o, o], [d, d, d], [1.4, 1.6, 1.2])
+    # 1.4: only the flagged surfaces lie within |t| -> reaches the light; 1.6: the plain one at
+    # t = 1.5 occludes; 1.2: flagged surfaces only
+    return "shadow_flags", sc, rays, [0, 4, 0]
+
+
+def shadow_case_two_instances():
+    name, sc, _, _, _ = case_two_instances()
+    d = (0.0, 0.0, -1.0)
+    rays = hb.shadow_rays([(4.25, 0.25, 1.0), (0.25, 0.25, 1.0), (2.25, 0.25, 1.0), (0.25, 0.25, 1.0)],
+                          [d, d, d, d], [3.0, 3.0, 3.0, 0.75])
+    return "shadow_two_instances", sc, rays, [4, 4, 0, 0]
+
+
+SHADOW_CASES = [shadow_case_single_triangle, shadow_case_flags, shadow_case_two_instances]

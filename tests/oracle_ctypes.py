@@ -48,6 +48,9 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_generate.argtypes = [vp, vp, u32, u32, C.c_float, C.c_float, i32, i32, i32, vp]
         L.tt_oracle_generate.restype = i32
         L.tt_oracle_hardware_threads.restype = i32
+        L.tt_oracle_shadow.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, C.POINTER(tthip.ShadowParams), vp,
+                                       vp, vp, vp, vp, i32]
+        L.tt_oracle_shadow.restype = i32
         L._path = path
         _LIB = L
     return _LIB
@@ -68,6 +71,25 @@ def trace(scene: "tthip.Scene", rays: np.ndarray, n_rays: int, bounce: int, far_
                            rays.ctypes.data, None if info is None else info.ctypes.data,
                            None if colors is None else colors.ctypes.data,
                            None if cnt is None else cnt.ctypes.data, nthreads)
+    return st, cnt
+
+
+def shadow(scene: "tthip.Scene", srays: np.ndarray, n_rays: int, bounce: int, width: int, height: int,
+           visibility=None, colors=None, nee_pos=None, counts: bool = False, nthreads: int = 1):
+    """Any-hit oracle in place on ``srays`` (SHADOW_DTYPE) and the optional outputs.
+    Returns (status, counts or None); counts.status 0 reached |t|, 4 occluded, 1 Reps exhausted."""
+    L = lib()
+    p = tthip.ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height, flags=0)
+    cnt = np.zeros(n_rays, COUNTS_DTYPE) if counts else None
+    mats = scene.materials
+    st = L.tt_oracle_shadow(scene.nodes.ctypes.data, len(scene.nodes), scene.tris.ctypes.data, len(scene.tris),
+                            scene.tlas.ctypes.data, len(scene.tlas), scene.meshdata.ctypes.data, len(scene.meshdata),
+                            None if mats is None or len(mats) == 0 else mats.ctypes.data,
+                            0 if mats is None else len(mats), C.byref(p), srays.ctypes.data,
+                            None if visibility is None else visibility.ctypes.data,
+                            None if colors is None else colors.ctypes.data,
+                            None if nee_pos is None else nee_pos.ctypes.data,
+                            None if cnt is None else cnt.ctypes.data, nthreads)
     return st, cnt
 
 

@@ -316,3 +316,115 @@ def test_sponza_4k_properties(engine, sponza):
     st, _ = O.trace(sponza, sample, len(idx), 0, FAR, len(idx), 1, nthreads=CPU_THREADS)
     assert st == 0
     assert np.array_equal(sample["hits"][: len(idx)], a["hits"][idx])
+
+
+# ------------------------------------------------------------------ any-hit (kernel_shadow, §8 f1)
+def shadow_both(engine, sc, srays, bounce, W, H, upload=True):
+    if upload:
+        engine.upload(sc)
+    n = len(srays)
+    out = []
+    for side in ("gpu", "cpu"):
+        r = srays.copy()
+        vis = np.full((n, 4), 7.0, np.float32)
+        col = np.zeros(W * H, tthip.COL_DTYPE)
+        col["Direct"] = 0.5
+        nee = np.full((W * H, 4), 9.0, np.float32)
+        if side == "gpu":
+            s = engine.trace_shadow(r, n, bounce, W, H, visibility=vis, colors=col, nee_pos=nee, stats=True)
+            out.append((r, vis, col, nee, s))
+        else:
+            st, cnt = O.shadow(sc, r, n, bounce, W, H, visibility=vis, colors=col, nee_pos=nee, counts=True,
+                               nthreads=CPU_THREADS)
+            assert st == 0
+            out.append((r, vis, col, nee, cnt))
+    (rg, vg, cg, ng, s), (rc, vc, cc, nc, cnt) = out
+    assert np.array_equal(rg, rc), f"{int((rg['t'] != rc['t']).sum())} shadow t values differ"
+    assert np.array_equal(vg, vc), "visibility differs"
+    assert np.array_equal(cg, cc), "GlobalColors differ"
+    assert np.array_equal(ng, nc), "NEEPosA differs"
+    assert s.node_visits == int(cnt["node_visits"].sum()) and s.tri_tests == int(cnt["tri_tests"].sum())
+    assert s.hits == int((cnt["status"] == 4).sum())
+    return rg, vg, s, cnt
+
+
+@pytest.mark.parametrize("case", K.SHADOW_CASES, ids=lambda c: c.__name__)
+def test_shadow_kat_on_gpu(engine, case):
+    name, sc, rays, expected = case()
+    n = len(rays)
+    rg, vg, s, cnt = shadow_both(engine, sc, rays, 0, n, 1)
+    assert cnt["status"].tolist() == expected, name
+    assert [0 if v[3] == 1.0 else 4 for v in vg] == expected
+
+
+def test_shadow_reps_and_glass_on_gpu(engine):
+    _, sc, _, _, _ = K.case_reps_exhausted()
+    rays = hb.shadow_rays([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)], [2.0])
+    engine.upload(sc)
+    vis = np.zeros((1, 4), np.float32)
+    s = engine.trace_shadow(rays, 1, 0, 1, 1, visibility=vis, stats=True)
+    assert rays["t"][0] == 2.0 and vis[0].tolist() == [0, 0, 0, -1] and s.reps_exhausted == 1
+    _, sc, rays, _ = K.shadow_case_single_triangle()
+    sc.materials[0]["specTrans"] = 1.0
+    engine.upload(sc)
+    s, st = engine.trace_shadow(rays, len(rays), 0, len(rays), 1, check=False)
+    assert st == tthip.TT_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_shadow_random_soup(engine, seed):
+    rng = np.random.default_rng(seed)
+    sc = tthip.single_object_scene(tthip.Mesh.soup(seed, int(rng.integers(2000, 40000)), 1.0,
+                                                   float(rng.uniform(0.02, 0.2))))
+    W, H = int(rng.integers(40, 200)), int(rng.integers(20, 120))
+    pos = rng.uniform(-2.5, 2.5, 3)
+    c2w, ip = tthip.unity_camera(pos, -pos, (0, 1, 0), 60.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    engine.upload(sc)
+    engine.trace(rays, W * H, 0, FAR, W, H)
+    sr = hb.nee_rays_from_hits(rays, W * H, pos * 1.2 + rng.normal(0, 0.3, 3), seed)  # light near the eye
+    assert len(sr) > 0
+    _, vg, s, cnt = shadow_both(engine, sc, sr, 0, W, H, upload=False)
+    assert 0 < s.hits < len(sr)  # some occluded, some not
+
+
+@pytest.mark.parametrize("seed", [15])
+def test_shadow_instanced_bounce1(engine, seed):
+    sc = instanced_scene(seed)
+    W, H = 160, 90
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    engine.upload(sc)
+    engine.trace(rays, W * H, 0, FAR, W, H)
+    sr = hb.nee_rays_from_hits(rays, W * H, (5.0, 30.0, 10.0), seed)
+    for bounce in (0, 1):
+        _, _, s, cnt = shadow_both(engine, sc, sr, bounce, W, H, upload=False)
+        assert s.blas_entries > len(sr)
+
+
+def test_shadow_sponza_1080p_full_parity(engine, sponza):
+    W, H = 1920, 1080
+    c2w, ip = tthip.unity_camera((-10, 2, 0), (1, 0, 0), (0, 1, 0), 60, W, H, 0.3, FAR)
+    engine.upload(sponza)
+    rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+    engine.generate(rays, c2w, ip, W, H, 0.3, FAR, jitter=1)
+    engine.trace(rays, W * H, 0, FAR, W, H)
+    sr = hb.nee_rays_from_hits(rays, W * H, (0.0, 9.0, 0.5), 3)
+    assert len(sr) > 0.9 * W * H
+    _, _, s, cnt = shadow_both(engine, sponza, sr, 0, W, H, upload=False)
+    assert 0 < s.hits < len(sr)
+
+
+def test_shadow_device_pointers(engine):
+    import torch
+    _, sc, rays, expected = K.shadow_case_flags()
+    engine.upload(sc)
+    n = len(rays)
+    dev = torch.device("cuda:0")
+    rt = torch.from_numpy(rays.view(np.uint8).copy()).to(dev)
+    vt = torch.zeros((n, 4), dtype=torch.float32, device=dev)
+    engine.trace_shadow(rt, n, 0, n, 1, visibility=vt, device=True)
+    torch.cuda.synchronize()
+    back = rt.cpu().numpy().view(tthip.SHADOW_DTYPE)
+    assert [0 if v == 1.0 else 4 for v in vt[:, 3].cpu().tolist()] == expected
+    assert [int(t == 0.0) * 4 for t in back["t"]] == expected

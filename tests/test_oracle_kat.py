@@ -115,3 +115,52 @@ def test_out_of_range_material_reads_as_zero():
     r = rays.copy()
     assert O.trace(sc, r, 1, 0, 1000.0, 1, 1)[0] == 0
     assert r["hits"][0].tolist() == exp1
+
+
+# ------------------------------------------------------------------- any-hit (kernel_shadow)
+@pytest.mark.parametrize("case", K.SHADOW_CASES, ids=lambda c: c.__name__)
+def test_shadow_kat(case):
+    name, sc, rays, expected = case()
+    n = len(rays)
+    t_in = rays["t"].copy()
+    vis = np.full((n, 4), 7.0, np.float32)
+    colors = np.zeros(n, tthip.COL_DTYPE)
+    nee = np.full((n, 4), 9.0, np.float32)
+    st, cnt = O.shadow(sc, rays, n, 0, n, 1, visibility=vis, colors=colors, nee_pos=nee, counts=True)
+    assert st == tthip.TT_OK, name
+    assert cnt["status"].tolist() == expected, name
+    for i, e in enumerate(expected):
+        if e == 4:  # occluded: t = 0 in place (IntersectionKernels.compute:449-454), nothing else
+            assert rays["t"][i] == 0.0 and vis[i].tolist() == [0, 0, 0, 0]
+            assert colors["Direct"][i].tolist() == [0, 0, 0] and nee[i].tolist() == [9, 9, 9, 9]
+        else:       # reached |t|: NEEPosA, Direct only for t >= 0 (:461-470)
+            assert rays["t"][i] == t_in[i] and vis[i].tolist() == [1, 1, 1, 1]
+            o, d = rays["origin"][i], rays["direction"][i]
+            assert nee[i].tolist() == (o + d * np.float32(abs(t_in[i]))).tolist() + [0.0]
+            want = [1.0, 2.0, 4.0] if t_in[i] >= 0 else [0.0, 0.0, 0.0]
+            assert colors["Direct"][i].tolist() == want
+
+
+def test_shadow_bounce1_no_color_outputs():
+    _, sc, rays, expected = K.shadow_case_single_triangle()
+    n = len(rays)
+    colors = np.zeros(n, tthip.COL_DTYPE)
+    nee = np.full((n, 4), 9.0, np.float32)
+    st, cnt = O.shadow(sc, rays, n, 1, n, 1, colors=colors, nee_pos=nee, counts=True)
+    assert st == 0 and cnt["status"].tolist() == expected
+    assert not colors["Direct"].any() and (nee == 9.0).all()
+
+
+def test_shadow_reps_exhausted_writes_nothing():
+    _, sc, _, _, _ = K.case_reps_exhausted()
+    rays = hb.shadow_rays([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)], [2.0])
+    vis = np.zeros((1, 4), np.float32)
+    st, cnt = O.shadow(sc, rays, 1, 0, 1, 1, visibility=vis, counts=True)
+    assert st == 0 and cnt["status"][0] == 1 and rays["t"][0] == 2.0 and vis[0].tolist() == [0, 0, 0, -1]
+
+
+def test_shadow_glass_unsupported():
+    _, sc, rays, _ = K.shadow_case_single_triangle()
+    sc.materials[0]["specTrans"] = 1.0
+    st, _ = O.shadow(sc, rays, len(rays), 0, len(rays), 1)
+    assert st == tthip.TT_ERR_UNSUPPORTED

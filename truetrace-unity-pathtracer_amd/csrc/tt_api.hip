@@ -16,6 +16,8 @@
 
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
 hipError_t tt_trace_occupancy_table(int* out12);
+hipError_t tt_launch_shadow(const ShadowArgs* a, uint32_t grid, hipStream_t st, int stats, int matcheck);
+void tt_shadow_occupancy_table(int* out4);
 uint32_t tt_trace_block_size();
 uint32_t tt_trace_spill_entries();
 uint32_t tt_trace_lds_bytes();
@@ -59,6 +61,8 @@ struct SceneHost {
     uint32_t n_tris = 0;
     uint32_t n_mat = 0;
     std::vector<uint32_t> matdat;  // only kept when a material sets the Invisible flag
+    bool any_shadow_skip = false;  // IsBackground / ShadowCaster present (shadow material checks)
+    bool any_atlas_shadow = false; // Cutout or specTrans == 1 present (shadow path unsupported)
 };
 
 }  // namespace
@@ -71,6 +75,7 @@ struct tt_ctx {
     int blocks_per_cu = 0;
     uint32_t grid = 0;
     uint32_t grid_of[12] = {};  // resident persistent grid per kernel instantiation
+    uint32_t shadow_grid_of[4] = {};  // the same for the any-hit kernel (stats * 2 + matcheck)
     TraceControl* ctl = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
     hipEvent_t ring0[256] = {}, ring1[256] = {};
@@ -79,6 +84,8 @@ struct tt_ctx {
     // scene
     bool has_scene = false;
     bool any_invisible = false;
+    bool any_shadow_skip = false;  // some material is IsBackground / ShadowCaster
+    bool any_atlas_shadow = false; // some material is Cutout or specTrans == 1 (needs the atlases)
     SceneHost host;
     DevBuf<tt_cwbvh_node> nodes;
     DevBuf<tt_cuda_triangle> tris_raw;
@@ -96,6 +103,10 @@ struct tt_ctx {
     DevBuf<float> cam;          // 32 floats: cam_to_world | cam_inv_proj
     DevBuf<uint32_t> counter;   // bounce enqueue counter
     DevBuf<uint2> spill;        // deep traversal-stack entries (tt_trace_spill_entries() per thread)
+    uint32_t spill_threads = 0; // grid threads the spill area is sized for (max over all grids)
+    DevBuf<tt_shadow_ray> st_shadow;
+    DevBuf<float4> st_vis;
+    DevBuf<float4> st_nee;
     unsigned long long last_diag[8] = {};
 };
 
@@ -259,6 +270,8 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
         }
         tags[m] = mats[m].Tag;
         any_invisible |= ((mats[m].Tag >> TT_FLAG_INVISIBLE) & 1u) != 0;
+        h.any_shadow_skip |= (((mats[m].Tag >> TT_FLAG_IS_BACKGROUND) | (mats[m].Tag >> TT_FLAG_SHADOW_CASTER)) & 1u) != 0;
+        h.any_atlas_shadow |= mats[m].specTrans == 1.0f;
     }
     if (any_invisible) {
         h.matdat.resize(n_tris);
@@ -366,8 +379,19 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
         if (knob > 0 && knob < b) b = knob;
         c->grid_of[k] = (uint32_t)(c->num_cus * b);
     }
+    int socc[4];
+    tt_shadow_occupancy_table(socc);
+    for (int k = 0; k < 4; k++) {
+        int b = std::max(1, std::min(std::min(socc[k], lds_cap), 8));
+        if (knob > 0 && knob < b) b = knob;
+        c->shadow_grid_of[k] = (uint32_t)(c->num_cus * b);
+    }
     c->blocks_per_cu = (int)(c->grid_of[1] / c->num_cus);
     c->grid = c->grid_of[1];
+    uint32_t max_grid = 0;
+    for (int k = 0; k < 12; k++) max_grid = std::max(max_grid, c->grid_of[k]);
+    for (int k = 0; k < 4; k++) max_grid = std::max(max_grid, c->shadow_grid_of[k]);
+    c->spill_threads = max_grid * tt_trace_block_size();
     if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess) {
         tt_ctx_destroy(c);
         return TT_ERR_OOM;
@@ -379,7 +403,7 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
         }
     }
     if (const uint32_t se = tt_trace_spill_entries()) {
-        if (c->spill.alloc((size_t)se * c->grid * tt_trace_block_size()) != hipSuccess) {
+        if (c->spill.alloc((size_t)se * c->spill_threads) != hipSuccess) {
             tt_ctx_destroy(c);
             return TT_ERR_OOM;
         }
@@ -499,6 +523,8 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     TT_HIP(c, hipMemcpy(c->mat_tag.p, tags.data(), sizeof(uint32_t) * tags.size(), hipMemcpyHostToDevice));
     c->host = std::move(h);
     c->any_invisible = any_invisible;
+    c->any_shadow_skip = c->host.any_shadow_skip;
+    c->any_atlas_shadow = c->host.any_atlas_shadow;
     c->has_scene = true;
     return TT_OK;
 }
@@ -674,6 +700,119 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     if (ctl.err_overflow)
         return fail(c, TT_ERR_STACK_OVERFLOW, "%u rays needed more than %d traversal stack entries", ctl.err_overflow,
                     TT_STACK_SIZE);
+    return TT_OK;
+}
+
+tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
+                          tt_col_data* colors, float* nee_pos, tt_stats* stats) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or shadow rays");
+    if (p->screen_width == 0 || p->screen_height == 0) return fail(c, TT_ERR_INVALID_ARG, "zero screen size");
+    if (p->bounce < 0) return fail(c, TT_ERR_INVALID_ARG, "negative bounce");
+    if (c->any_atlas_shadow)
+        return fail(c, TT_ERR_UNSUPPORTED,
+                    "scene has glass (specTrans == 1) materials: the shadow tint samples the texture atlas "
+                    "(CommonData.cginc:618-625), not supported");
+    const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
+    if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
+    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    const bool async = dev && (p->flags & TT_TRACE_ASYNC);
+    const bool want_stats = (p->flags & TT_TRACE_STATS) != 0;
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (p->n_rays == 0) return TT_OK;
+    if (reinterpret_cast<uintptr_t>(rays) % 16 || (visibility && reinterpret_cast<uintptr_t>(visibility) % 16) ||
+        (nee_pos && reinterpret_cast<uintptr_t>(nee_pos) % 16))
+        return fail(c, TT_ERR_INVALID_ARG, "shadow rays / visibility / NEEPosA must be 16-byte aligned");
+    TT_HIP(c, hipSetDevice(c->device));
+    tt_shadow_ray* d_rays = rays;
+    float4* d_vis = reinterpret_cast<float4*>(visibility);
+    tt_col_data* d_col = colors;
+    float4* d_nee = reinterpret_cast<float4*>(nee_pos);
+    if (dev) {
+        if (!is_device_ptr(rays)) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but rays is not device memory");
+    } else {
+        if (c->st_shadow.n < p->n_rays) TT_HIP(c, c->st_shadow.alloc(p->n_rays));
+        d_rays = c->st_shadow.p;
+        TT_HIP(c, hipMemcpyAsync(d_rays, rays, sizeof(tt_shadow_ray) * p->n_rays, hipMemcpyHostToDevice, c->stream));
+        if (visibility) {
+            if (c->st_vis.n < p->n_rays) TT_HIP(c, c->st_vis.alloc(p->n_rays));
+            d_vis = c->st_vis.p;
+        }
+        if (colors) {
+            if (c->st_colors.n < wh) TT_HIP(c, c->st_colors.alloc(wh));
+            d_col = c->st_colors.p;
+            TT_HIP(c, hipMemcpyAsync(d_col, colors, sizeof(tt_col_data) * wh, hipMemcpyHostToDevice, c->stream));
+        }
+        if (nee_pos) {
+            if (c->st_nee.n < wh) TT_HIP(c, c->st_nee.alloc(wh));
+            d_nee = c->st_nee.p;
+            TT_HIP(c, hipMemcpyAsync(d_nee, nee_pos, sizeof(float4) * wh, hipMemcpyHostToDevice, c->stream));
+        }
+    }
+    ShadowArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
+    a.n_nodes = (uint32_t)c->host.nodes.size();
+    a.tris = c->tris.p;
+    a.n_tris = c->host.n_tris;
+    a.tlas = c->tlas.p;
+    a.mesh = c->mesh.p;
+    a.mat_tag = c->mat_tag.p;
+    a.n_mat = c->host.n_mat;
+    a.rays = d_rays;
+    a.visibility = d_vis;
+    a.colors = d_col;
+    a.nee_pos = d_nee;
+    a.ctl = c->ctl;
+    a.spill = c->spill.p;
+    a.n_rays = p->n_rays;
+    a.width = p->screen_width;
+    a.height = p->screen_height;
+    a.bounce = p->bounce;
+    a.flags = p->flags;
+    const bool matcheck = c->any_shadow_skip;
+    const uint32_t blocks_needed = ((p->n_rays + 255u) / 256u + 3u) / 4u;
+    const uint32_t grid =
+        std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));
+    TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
+    const uint32_t slot = c->ring_n % TT_RING;
+    TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
+    TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
+    TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
+    c->ring_n++;
+    c->ev0 = c->ring0[slot];
+    c->ev1 = c->ring1[slot];
+    if (async) return TT_OK;
+    TraceControl ctl;
+    TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
+    if (!dev) {
+        TT_HIP(c, hipMemcpyAsync(rays, d_rays, sizeof(tt_shadow_ray) * p->n_rays, hipMemcpyDeviceToHost, c->stream));
+        if (visibility)
+            TT_HIP(c, hipMemcpyAsync(visibility, d_vis, sizeof(float4) * p->n_rays, hipMemcpyDeviceToHost, c->stream));
+        if (colors) TT_HIP(c, hipMemcpyAsync(colors, d_col, sizeof(tt_col_data) * wh, hipMemcpyDeviceToHost, c->stream));
+        if (nee_pos) TT_HIP(c, hipMemcpyAsync(nee_pos, d_nee, sizeof(float4) * wh, hipMemcpyDeviceToHost, c->stream));
+    }
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    float ms = 0.0f;
+    TT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (stats) {
+        stats->kernel_ms = ms;
+        if (want_stats) {  // hits = occluded rays, accepts = rays that reached |t|
+            stats->rays = ctl.stats[0];
+            stats->node_visits = ctl.stats[1];
+            stats->tri_tests = ctl.stats[2];
+            stats->blas_entries = ctl.stats[3];
+            stats->hits = ctl.stats[4];
+            stats->reps_exhausted = ctl.stats[5];
+            stats->stack_overflows = ctl.stats[6];
+            stats->accepts = ctl.stats[7];
+        }
+        stats->stack_overflows = std::max<uint64_t>(stats->stack_overflows, ctl.err_overflow);
+    }
+    if (ctl.err_overflow)
+        return fail(c, TT_ERR_STACK_OVERFLOW, "%u shadow rays needed more than %d traversal stack entries",
+                    ctl.err_overflow, TT_STACK_SIZE);
     return TT_OK;
 }
 

@@ -66,4 +66,26 @@ struct TraceArgs {
     uint32_t tile_swizzle;       // 1: work index -> 8x8 screen tiles (n_rays == W*H, W,H % 8 == 0)
 };
 
+// Any-hit visibility launch (tt_shadow.hip, kernel_shadow replacement).
+struct ShadowArgs {
+    const uint4* nodes;
+    uint32_t n_nodes;
+    const TriPos* tris;
+    uint32_t n_tris;
+    const int32_t* tlas;
+    const MeshGpu* mesh;
+    const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
+    uint32_t n_mat;
+    tt_shadow_ray* rays;         // ShadowRaysBuffer (t = 0 written for occluded rays)
+    float4* visibility;          // nullable, per ray
+    tt_col_data* colors;         // nullable, GlobalColors (Direct += at bounce 0)
+    float4* nee_pos;             // nullable, NEEPosA (bounce 0)
+    TraceControl* ctl;
+    uint2* spill;
+    uint32_t n_rays;
+    uint32_t width, height;
+    int32_t bounce;
+    uint32_t flags;
+};
+
 #endif

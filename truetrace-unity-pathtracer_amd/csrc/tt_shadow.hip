@@ -1,0 +1,294 @@
+// tt_shadow.hip — gfx950 any-hit CWBVH8 visibility traversal (replaces kernel_shadow,
+// TrueTrace/Resources/MainCompute/IntersectionKernels.compute:264-505, HardwareRT off).
+//
+// Same persistent-wave machinery as the closest-hit kernel (tt_trace.hip): per-XCD segment
+// dequeues, in-place lane refill, LDS traversal stack. Differences that follow the reference:
+//  * the culling distance is the fixed |t| of the shadow ray (max_distance, :366), not a
+//    shrinking best hit;
+//  * the first occluder ends the ray (:441-454): t = 0 is written back to ShadowRaysBuffer;
+//  * triangle_intersect_shadow (CommonData.cginc:593-634) reads the material BEFORE the t-range
+//    test and ignores IsBackground / ShadowCaster surfaces; Cutout and glass (specTrans == 1)
+//    need the texture atlases and are rejected on the host (TT_ERR_UNSUPPORTED);
+//  * a ray that reaches |t| writes NEEPosA (bounce 0) and GlobalColors.Direct (bounce 0, t >= 0),
+//    the radiance-cache paths stay with the caller (see include/truetrace_hip.h).
+#include "tt_traverse.h"
+
+namespace {
+
+// triangle_intersect_shadow — CommonData.cginc:593-634. Returns true for an occluder.
+template <bool MATCHECK>
+__device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, const uint32_t* __restrict__ mat_tag,
+                                                uint32_t n_mat, int32_t tri_id, int32_t mat_offset, const LaneRay& r,
+                                                float max_distance) {
+    const uint32_t to = tri_offset((uint32_t)tri_id);
+    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
+    const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
+    const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
+    const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);
+    const float hx = fma_(r.dy, e2z, -(r.dz * e2y));
+    const float hy = fma_(r.dz, e2x, -(r.dx * e2z));
+    const float hz = fma_(r.dx, e2y, -(r.dy * e2x));
+    const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
+    const float f = 1.0f / aa;
+    const float sx = r.ox - p0x, sy = r.oy - p0y, sz = r.oz - p0z;
+    const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
+    const float qx = fma_(sy, e1z, -(sz * e1y));
+    const float qy = fma_(sz, e1x, -(sx * e1z));
+    const float qz = fma_(sx, e1y, -(sy * e1x));
+    const float v = f * fma_(r.dz, qz, fma_(r.dy, qy, r.dx * qx));
+    const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
+    const bool in_tri = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f);
+    bool occ = in_tri && (t > 0.0f && t < max_distance);
+    if (MATCHECK && in_tri) {
+        // IsBackground / ShadowCaster surfaces never occlude (:612); out-of-range material = zeros
+        const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
+        const uint32_t tag = mi < n_mat ? mat_tag[mi] : 0u;
+        if (((tag >> TT_FLAG_IS_BACKGROUND) | (tag >> TT_FLAG_SHADOW_CASTER)) & 1u) occ = false;
+    }
+    return occ;
+}
+
+}  // namespace
+
+template <bool STATS, bool MATCHECK>
+__global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
+    __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gtid = blockIdx.x * TT_BLOCK + tid;
+    const uint32_t spill_stride = gridDim.x * TT_BLOCK;
+    uint2* __restrict__ spill = A.spill;
+    (void)gtid;
+    (void)spill_stride;
+    (void)spill;
+    const uint32_t lane = tid & (TT_WAVE - 1);
+
+    uint32_t pool_next = 0, pool_end = 0, more = 1;
+    const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
+    SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
+    const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
+    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
+    const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
+
+    bool active = false;
+    uint32_t ray_index = 0;
+    LaneRay ray{}, wray{};
+    float max_distance = 0.0f;
+    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
+    uint32_t oct = 0;
+    int32_t stack_size = 0, tlas_ss = -1;
+    int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, Reps = 0;
+    uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_occ = 0, c_rays = 0, c_vis = 0, c_reps = 0, c_ovf = 0;
+
+    while (true) {
+        // ---------------------------------------------------------------- refill
+        const uint64_t idle = __ballot(!active);
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        const bool pool_dry = !more && pool_next >= pool_end;
+        if (n_idle == TT_WAVE && pool_dry) break;
+        if (n_idle >= TT_REFILL_MIN && !pool_dry) {
+            const uint32_t avail = pool_end - pool_next;
+            uint32_t new_base = 0, new_count = 0;
+            if (avail < n_idle && more) {
+                new_count = sched_reserve(A.ctl, A.n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
+                more = new_count > 0 ? 1u : 0u;
+            }
+            const uint32_t take_old = min(avail, n_idle);
+            const uint32_t take_new = min(n_idle - take_old, new_count);
+            const uint32_t rank = lane_prefix(idle);
+            uint32_t widx = 0xffffffffu;
+            if (rank < take_old) widx = pool_next + rank;
+            else if (rank - take_old < take_new) widx = new_base + (rank - take_old);
+            if (new_count > 0) {
+                pool_next = new_base + take_new;
+                pool_end = new_base + new_count;
+            } else {
+                pool_next += take_old;
+            }
+            if (!active && widx != 0xffffffffu) {  // :355-371
+                ray_index = widx;
+                const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
+                const uint4 r0 = rp[0], r1 = rp[1];
+                ray.ox = __uint_as_float(r0.x);
+                ray.oy = __uint_as_float(r0.y);
+                ray.oz = __uint_as_float(r0.z);
+                ray.dx = __uint_as_float(r1.x);
+                ray.dy = __uint_as_float(r1.y);
+                ray.dz = __uint_as_float(r1.z);
+                max_distance = fabsf(__uint_as_float(r1.w));
+                ray.ix = 1.0f / ray.dx;
+                ray.iy = 1.0f / ray.dy;
+                ray.iz = 1.0f / ray.dz;
+                wray = ray;
+                oct = octant_inv4(ray);
+                cg = make_uint2(0u, 0x80000000u);
+                tg = make_uint2(0u, 0u);
+                stack_size = 0;
+                tlas_ss = -1;
+                NodeOffset = 0;
+                TriOffset = 0;
+                MatOffset = 0;
+                Reps = 0;
+                active = true;
+                if (STATS) c_rays++;
+            }
+        }
+
+        // ------------------------------------------------------------- node phase
+        if (active && tg.y == 0u) {
+            if (Reps >= TT_MAX_REPS) {  // :373 loop bound: nothing is written
+                active = false;
+                if (STATS) c_reps++;
+                if (A.visibility) A.visibility[ray_index] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+            } else if (cg.y & 0xff000000u) {  // :374-403
+                const uint32_t cio = firstbithigh(cg.y);
+                const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
+                const uint32_t rel = __builtin_popcount(cg.y & ~(0xffffffffu << slot));
+                const uint32_t child = cg.x + rel;
+                cg.y &= ~(1u << cio);
+                bool ok = true;
+                if (cg.y & 0xff000000u) TT_PUSH(cg, ok);
+                if (ok) {
+                    const uint32_t no = node_offset(child);
+                    const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
+                                n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
+                                n4 = buffer_load16(nodes, no + 64u);
+                    const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, max_distance);
+                    cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
+                    tg.y = hitmask & 0x00ffffffu;
+                    cg.x = n1.x + (uint32_t)NodeOffset;
+                    tg.x = n1.y + (uint32_t)TriOffset;
+                    Reps++;
+                    if (STATS) c_nodes++;
+                } else {
+                    active = false;
+                    if (STATS) c_ovf++;
+                    atomicAdd(&A.ctl->err_overflow, 1u);
+                }
+            } else {  // :404-407
+                tg = cg;
+                cg = make_uint2(0u, 0u);
+            }
+            if (active && tg.y != 0u && tlas_ss == -1) {  // :411-435 TLAS leaf -> BLAS
+                const uint32_t mo = firstbithigh(tg.y);
+                tg.y &= ~(1u << mo);
+                const int32_t mesh_id = A.tlas[tg.x + mo];
+                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
+                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                NodeOffset = mo4.y;
+                TriOffset = mo4.x;
+                bool ok = true;
+                if (tg.y != 0u) TT_PUSH(tg, ok);
+                if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
+                if (ok) {
+                    tlas_ss = stack_size;
+                    MatOffset = mo4.z;
+                    LaneRay nr;
+                    nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
+                    nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
+                    nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
+                    nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
+                    nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
+                    nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
+                    nr.ix = 1.0f / nr.dx;
+                    nr.iy = 1.0f / nr.dy;
+                    nr.iz = 1.0f / nr.dz;
+                    ray = nr;
+                    oct = octant_inv4(ray);
+                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                    if (STATS) c_blas++;
+                } else {
+                    active = false;
+                    if (STATS) c_ovf++;
+                    atomicAdd(&A.ctl->err_overflow, 1u);
+                }
+                tg.y = 0u;
+            }
+        }
+
+        // --------------------------------------------------------- triangle phase
+        if (active && tg.y != 0u) {  // :436-446, highest bit first, until the first occluder
+            const uint32_t ti = firstbithigh(tg.y);
+            tg.y &= ~(1u << ti);
+            const bool occ =
+                shadow_triangle<MATCHECK>(tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), MatOffset, ray, max_distance);
+            if (STATS) c_tris++;
+            if (occ) {  // :449-454
+                A.rays[ray_index].t = 0.0f;
+                if (A.visibility) A.visibility[ray_index] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                active = false;
+                if (STATS) c_occ++;
+            }
+        }
+
+        // ----------------------------------------- advance: pop / finish (:456-494)
+        if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+            if (stack_size != 0) {
+                if (stack_size == tlas_ss) {
+                    NodeOffset = 0;
+                    TriOffset = 0;
+                    tlas_ss = -1;
+                    ray = wray;
+                    oct = octant_inv4(ray);
+                }
+                TT_POP(cg);
+            } else {  // reached the light (TerrainExists false): :457-485
+                const tt_shadow_ray& R = A.rays[ray_index];
+                const uint32_t pix = R.PixelIndex;
+                const float t = R.t;
+                if (A.visibility) A.visibility[ray_index] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                if (A.bounce == 0 && A.nee_pos && pix / A.width < A.height) {
+                    const float d = fabsf(t);
+                    A.nee_pos[pix] = make_float4(wray.ox + wray.dx * d, wray.oy + wray.dy * d, wray.oz + wray.dz * d, 0.0f);
+                }
+                if (A.bounce == 0 && t >= 0.0f && A.colors) {  // Direct += illumination * throughput (1)
+                    tt_col_data& C = A.colors[pix];
+                    C.Direct[0] = C.Direct[0] + R.illumination[0] * 1.0f;
+                    C.Direct[1] = C.Direct[1] + R.illumination[1] * 1.0f;
+                    C.Direct[2] = C.Direct[2] + R.illumination[2] * 1.0f;
+                }
+                active = false;
+                if (STATS) c_vis++;
+            }
+        }
+    }
+
+    if (STATS) {
+        // stats slots as the closest-hit kernel: rays, nodes, tris, blas, hits (= occluded),
+        // reps_exhausted, overflow, accepts (= reached the light)
+        const uint32_t v[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
+                               wave_sum(c_occ),  wave_sum(c_reps),  wave_sum(c_ovf),  wave_sum(c_vis)};
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (v[k]) atomicAdd(&A.ctl->stats[k], (unsigned long long)v[k]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+template <bool S, bool M>
+static hipError_t launch_shadow(const ShadowArgs& a, uint32_t grid, hipStream_t st) {
+    hipLaunchKernelGGL((tt_shadow_kernel<S, M>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t tt_launch_shadow(const ShadowArgs* a, uint32_t grid, hipStream_t st, int stats, int matcheck) {
+    if (stats) return matcheck ? launch_shadow<true, true>(*a, grid, st) : launch_shadow<true, false>(*a, grid, st);
+    return matcheck ? launch_shadow<false, true>(*a, grid, st) : launch_shadow<false, false>(*a, grid, st);
+}
+
+template <bool S, bool M>
+static int shadow_occ() {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_shadow_kernel<S, M>, TT_BLOCK, 0) != hipSuccess) b = 1;
+    return b;
+}
+
+// resident blocks per CU per instantiation, index stats * 2 + matcheck
+void tt_shadow_occupancy_table(int* out4) {
+    out4[0] = shadow_occ<false, false>();
+    out4[1] = shadow_occ<false, true>();
+    out4[2] = shadow_occ<true, false>();
+    out4[3] = shadow_occ<true, true>();
+}

@@ -14,265 +14,8 @@
 //  * the per-ray visit order, the culling distance and the strict t < best.t acceptance are
 //    exactly the reference's, so t / primID / instID are bit-identical to the oracle.
 // Numerics follow include/truetrace_hip.h (compiled with -ffp-contract=off).
-#include "tt_device.h"
+#include "tt_traverse.h"
 
-#define TT_WAVE 64
-#define TT_BLOCK 256
-#ifndef TT_SEGS
-#define TT_SEGS 8         // ray-range segments, one per XCD group (blockIdx % 8), with stealing
-#endif
-#ifndef TT_SDWA_BITS
-#define TT_SDWA_BITS 1    // 1: per-child hit bits with one byte-selecting SDWA shift
-#endif
-#ifndef TT_DEFER_FINISH
-#define TT_DEFER_FINISH 1 // 1: write finished rays' records in batches at refill time
-#endif
-#ifndef TT_TRI_MIN
-#define TT_TRI_MIN 1      // >1: run the triangle pass only when at least this many lanes need it
-#endif
-#ifndef TT_NODE_PK
-#define TT_NODE_PK 0      // 1: node slab fmas as v_pk_fma_f32 pairs (measured ~2% slower on C2)
-#endif
-#ifndef TT_EXACT_TAIL
-#define TT_EXACT_TAIL 0   // 1: exact-size dequeues over the last quarter of each segment (measured: no gain on C2)
-#endif
-#ifndef TT_CHUNK_BIG
-#define TT_CHUNK_BIG 64   // rays per dequeue over the first 3/4 of a segment (then exact)
-#endif
-#ifndef TT_REFILL_MIN
-#define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
-#endif
-#ifndef TT_LDS_STACK
-#define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
-#endif
-#ifndef TT_WAVES_PER_EU
-#define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
-#endif
-#ifndef TT_WRAY_RELOAD
-#define TT_WRAY_RELOAD 0  // 1: re-read the world-space ray from GlobalRays on BLAS exit
-#endif
-#if TT_WAVES_PER_EU > 0
-#define TT_BOUNDS __launch_bounds__(TT_BLOCK, TT_WAVES_PER_EU)
-#else
-#define TT_BOUNDS __launch_bounds__(TT_BLOCK)
-#endif
-
-namespace {
-
-struct LaneRay {
-    float ox, oy, oz, dx, dy, dz, ix, iy, iz;
-};
-
-__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ uint32_t firstbithigh(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
-
-// ray_get_octant_inv4 — CommonData.cginc:635-640
-__device__ __forceinline__ uint32_t octant_inv4(const LaneRay& r) {
-    return (r.dx < 0.0f ? 0u : 0x04040404u) | (r.dy < 0.0f ? 0u : 0x02020202u) |
-           (r.dz < 0.0f ? 0u : 0x01010101u);
-}
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-[[maybe_unused]] __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-// Node / triangle fetches are raw buffer loads: a 32-bit byte offset per lane (two full-rate
-// shift-adds) instead of a 64-bit address (v_mad_u64_u32), and a bounded descriptor, so an
-// out-of-range offset reads zeros instead of faulting. Offsets stay below 2^32 because
-// tt_scene_upload rejects node / triangle arrays of 4 GiB or more.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ uint4 buffer_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint32_t node_offset(uint32_t i) { return (i + (i << 2)) << 4; }  // i * 80
-__device__ __forceinline__ uint32_t tri_offset(uint32_t i) { return (i + (i << 1)) << 4; }   // i * 48
-
-// cwbvh_node_intersect — CommonData.cginc:641-707
-__device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n1, const uint4 n2,
-                                                   const uint4 n3, const uint4 n4, const LaneRay& r,
-                                                   uint32_t oct_inv4, float max_distance) {
-    const uint32_t w = n0.w;
-    const float adjx = __uint_as_float((w & 0xffu) << 23) * r.ix;
-    const float adjy = __uint_as_float(((w >> 8) & 0xffu) << 23) * r.iy;
-    const float adjz = __uint_as_float(((w >> 16) & 0xffu) << 23) * r.iz;
-    const float orgx = r.ix * (__uint_as_float(n0.x) - r.ox);
-    const float orgy = r.iy * (__uint_as_float(n0.y) - r.oy);
-    const float orgz = r.iz * (__uint_as_float(n0.z) - r.oz);
-    const bool nx = r.dx < 0.0f, ny = r.dy < 0.0f, nz = r.dz < 0.0f;
-    uint32_t hit_mask = 0;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const uint32_t meta4 = i == 0 ? n1.z : n1.w;
-        const uint32_t is_inner4 = (meta4 & (meta4 << 1)) & 0x10101010u;
-        // 0x07 in each inner child's byte (oct_inv4 bytes are <= 7, so 3 bits of the reference's
-        // 0xff byte mask suffice); 8 - 1 per byte, no borrow: avoids the quarter-rate v_mul_lo_u32
-        const uint32_t inner_mask4 = (is_inner4 >> 1) - (is_inner4 >> 4);
-        const uint32_t bit_index4 = (meta4 ^ (oct_inv4 & inner_mask4)) & 0x1f1f1f1fu;
-        const uint32_t child_bits4 = (meta4 >> 5) & 0x07070707u;
-        const uint32_t qlx = i == 0 ? n2.x : n2.y, qhx = i == 0 ? n2.z : n2.w;
-        const uint32_t qly = i == 0 ? n3.x : n3.y, qhy = i == 0 ? n3.z : n3.w;
-        const uint32_t qlz = i == 0 ? n4.x : n4.y, qhz = i == 0 ? n4.z : n4.w;
-        const uint32_t x_min = nx ? qhx : qlx, x_max = nx ? qlx : qhx;
-        const uint32_t y_min = ny ? qhy : qly, y_max = ny ? qly : qhy;
-        const uint32_t z_min = nz ? qhz : qlz, z_max = nz ? qlz : qhz;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-#if TT_NODE_PK
-            // (tmin, tmax) per axis as one v_pk_fma_f32: two IEEE fmas, bitwise the same as fmaf.
-            const f32x2 tx = pk_fma(f32x2{(float)((x_min >> (j * 8)) & 0xffu), (float)((x_max >> (j * 8)) & 0xffu)},
-                                    f32x2{adjx, adjx}, f32x2{orgx, orgx});
-            const f32x2 ty = pk_fma(f32x2{(float)((y_min >> (j * 8)) & 0xffu), (float)((y_max >> (j * 8)) & 0xffu)},
-                                    f32x2{adjy, adjy}, f32x2{orgy, orgy});
-            const f32x2 tz = pk_fma(f32x2{(float)((z_min >> (j * 8)) & 0xffu), (float)((z_max >> (j * 8)) & 0xffu)},
-                                    f32x2{adjz, adjz}, f32x2{orgz, orgz});
-            const float tmin = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 1e-8f));
-            const float tmax = fminf(fminf(tx.y, ty.y), fminf(tz.y, max_distance));
-#else
-            const float tminx = fma_((float)((x_min >> (j * 8)) & 0xffu), adjx, orgx);
-            const float tminy = fma_((float)((y_min >> (j * 8)) & 0xffu), adjy, orgy);
-            const float tminz = fma_((float)((z_min >> (j * 8)) & 0xffu), adjz, orgz);
-            const float tmaxx = fma_((float)((x_max >> (j * 8)) & 0xffu), adjx, orgx);
-            const float tmaxy = fma_((float)((y_max >> (j * 8)) & 0xffu), adjy, orgy);
-            const float tmaxz = fma_((float)((z_max >> (j * 8)) & 0xffu), adjz, orgz);
-            const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
-            const float tmax = fminf(fminf(tmaxx, tmaxy), fminf(tmaxz, max_distance));
-#endif
-#if TT_SDWA_BITS
-            // child_bits byte j << bit_index byte j in ONE v_lshlrev_b32_sdwa (both operands byte-selected)
-            uint32_t bits;
-            if (j == 0)
-                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0"
-                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
-            else if (j == 1)
-                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1"
-                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
-            else if (j == 2)
-                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2"
-                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
-            else
-                asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3"
-                    : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
-#else
-            const uint32_t bits = ((child_bits4 >> (j * 8)) & 0xffu) << ((bit_index4 >> (j * 8)) & 0xffu);
-#endif
-            hit_mask |= (tmin < tmax) ? bits : 0u;
-        }
-    }
-    return hit_mask;
-}
-
-struct Best {
-    float t, u, v;
-    int32_t mesh_id, tri_id;
-};
-
-// IntersectTriangle — IntersectionKernels.compute:14-57 (Moller-Trumbore on pos0/edges).
-// Evaluated branch-free; the accept predicate is exactly the reference's nested conditions.
-template <bool MATCHECK>
-__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const uint32_t* __restrict__ mat_tag,
-                                                   uint32_t n_mat, int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
-                                                   const LaneRay& r, Best& best) {
-    const uint32_t to = tri_offset((uint32_t)tri_id);
-    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
-    const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
-    const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
-    const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);
-    // h = cross(d, e2); a = dot(e1, h)
-    const float hx = fma_(r.dy, e2z, -(r.dz * e2y));
-    const float hy = fma_(r.dz, e2x, -(r.dx * e2z));
-    const float hz = fma_(r.dx, e2y, -(r.dy * e2x));
-    const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
-    const float f = 1.0f / aa;
-    const float sx = r.ox - p0x, sy = r.oy - p0y, sz = r.oz - p0z;
-    const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
-    // q = cross(s, e1)
-    const float qx = fma_(sy, e1z, -(sz * e1y));
-    const float qy = fma_(sz, e1x, -(sx * e1z));
-    const float qz = fma_(sx, e1y, -(sy * e1x));
-    const float v = f * fma_(r.dz, qz, fma_(r.dy, qy, r.dx * qx));
-    const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
-    const bool cand = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best.t);
-    bool accept = cand;
-    if (MATCHECK && accept) {
-        // GetFlag(_Materials[MatOffset + MatDat].Tag, Invisible) at CurBounce == 0 (:48); an
-        // out-of-range StructuredBuffer read returns zeros in D3D (no flags)
-        const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
-        const uint32_t tag = mi < n_mat ? mat_tag[mi] : 0u;
-        if ((tag >> TT_FLAG_INVISIBLE) & 1u) accept = false;
-    }
-    if (accept) {
-        best.t = t;
-        best.u = u;
-        best.v = v;
-        best.mesh_id = mesh_id;
-        best.tri_id = tri_id;
-    }
-    return cand;  // counted as an "accept" (candidate passed the t test) before the material check
-}
-
-// ------------------------------------------------------------------ ray scheduler
-// The work range is cut into TT_SEGS segments of whole 64-ray tiles; blocks start on segment
-// blockIdx % TT_SEGS (one per XCD under round-robin placement, for L2 locality). A dequeue is ONE
-// returning atomicAdd on the segment's counter (counted in rays). Over the first 3/4 of a
-// segment a wave reserves TT_CHUNK_BIG rays (fewer atomics; the surplus waits in the wave's pool);
-// over the last quarter exactly the lanes it can fill, so no ray waits in a busy wave's pool when
-// the launch drains. A wave whose segment is exhausted probes the others starting at an offset
-// derived from its wave id, so thieves spread over all counters instead of converging on one
-// (measured, tools/diag_tl.py: convergent stealing serialised thousands of atomics on one word).
-__device__ __forceinline__ uint32_t seg_lo(uint32_t n_tiles, uint32_t seg) {
-    return (uint32_t)(((uint64_t)n_tiles * seg / TT_SEGS) << 6);
-}
-struct SegState {
-    uint32_t seg;   // segment this wave dequeues from
-    uint32_t dead;  // bit k: segment k seen exhausted by this wave
-    uint32_t est;   // this wave's last known counter value of `seg`
-};
-// Reserves up to max(need, chunk) rays; returns the count (0 once every segment is exhausted).
-__device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_rays, uint32_t n_tiles, uint32_t lane,
-                                                  uint32_t need, uint32_t wave_id, SegState& S, uint32_t& base) {
-    while (S.dead != (1u << TT_SEGS) - 1u) {
-        const uint32_t lo = seg_lo(n_tiles, S.seg);
-        const uint32_t hi = min(seg_lo(n_tiles, S.seg + 1), n_rays);
-        const uint32_t len = hi > lo ? hi - lo : 0u;
-        const uint32_t want = (!TT_EXACT_TAIL || S.est < len - len / 4u) ? max(need, (uint32_t)TT_CHUNK_BIG) : need;
-        uint32_t off = 0;
-        if (lane == 0) off = atomicAdd(&ctl->seg_ticket[S.seg * 32u], want);
-        off = __builtin_amdgcn_readfirstlane(off);
-        if (off < len) {
-            S.est = off + want;
-            base = lo + off;
-            return min(want, len - off);
-        }
-        S.dead |= 1u << S.seg;
-        // next live segment, scanning from a per-wave offset
-        const uint32_t start = (S.seg + 1u + wave_id % (TT_SEGS - 1u)) % TT_SEGS;
-#pragma unroll
-        for (uint32_t k = 0; k < TT_SEGS; k++) {
-            const uint32_t c = (start + k) % TT_SEGS;
-            if (!((S.dead >> c) & 1u)) {
-                S.seg = c;
-                break;
-            }
-        }
-        S.est = 0;
-    }
-    return 0u;
-}
-
-__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, TT_WAVE);
-    return v;
-}
-
-}  // namespace
 
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
 template <bool STATS, bool MATCHECK, int INFO>
@@ -285,26 +28,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     (void)gtid;
     (void)spill_stride;
     (void)spill;
-#define TT_PUSH(val, ok)                                                            \
-    do {                                                                            \
-        if (stack_size == TT_STACK_SIZE) {                                          \
-            ok = false;                                                             \
-        } else {                                                                    \
-            if (TT_LDS_STACK >= TT_STACK_SIZE || stack_size < TT_LDS_STACK)         \
-                s_stack[stack_size][tid] = (val);                                   \
-            else                                                                    \
-                spill[(size_t)(stack_size - TT_LDS_STACK) * spill_stride + gtid] = (val); \
-            stack_size++;                                                           \
-        }                                                                           \
-    } while (0)
-#define TT_POP(dst)                                                                 \
-    do {                                                                            \
-        --stack_size;                                                               \
-        if (TT_LDS_STACK >= TT_STACK_SIZE || stack_size < TT_LDS_STACK)             \
-            dst = s_stack[stack_size][tid];                                         \
-        else                                                                        \
-            dst = spill[(size_t)(stack_size - TT_LDS_STACK) * spill_stride + gtid]; \
-    } while (0)
     const uint32_t lane = tid & (TT_WAVE - 1);
 
     // wave-uniform scheduler state: a private pool [pool_next, pool_end) of work indices, refilled

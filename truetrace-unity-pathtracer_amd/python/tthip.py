@@ -55,9 +55,14 @@ MAT_DTYPE = np.dtype([("AlbedoTex", "<i4", 2), ("NormalTex", "<i4", 2), ("Emissi
                       ("MetallicTex", "<i4", 2), ("RoughnessTex", "<i4", 2), ("AlphaTex", "<i4", 2),
                       ("MatCapMask", "<i4", 2), ("MatCapTex", "<i4", 2), ("surfaceColor", "<f4", 3),
                       ("emmissive", "<f4"), ("EmissionColor", "<f4", 3), ("Tag", "<u4"), ("roughness", "<f4"),
-                      ("MatType", "<i4"), ("transmittanceColor", "<f4", 3), ("ior", "<f4"), ("rest", "<f4", 12),
+                      ("MatType", "<i4"), ("transmittanceColor", "<f4", 3), ("ior", "<f4"), ("metallic", "<f4"),
+                      ("sheen", "<f4"), ("sheenTint", "<f4"), ("specularTint", "<f4"), ("clearcoat", "<f4"),
+                      ("clearcoatGloss", "<f4"), ("anisotropic", "<f4"), ("flatness", "<f4"), ("diffTrans", "<f4"),
+                      ("specTrans", "<f4"), ("Specular", "<f4"), ("scatterDistance", "<f4"),
                       ("AlbedoTexScale", "<f4", 4), ("MetallicRemap", "<f4", 2), ("RoughnessRemap", "<f4", 2),
-                      ("AlphaCutoff", "<f4"), ("tail", "<f4", 12)])
+                      ("AlphaCutoff", "<f4"), ("NormalStrength", "<f4"), ("Hue", "<f4"), ("Saturation", "<f4"),
+                      ("Contrast", "<f4"), ("Brightness", "<f4"), ("BlendColor", "<f4", 3), ("BlendFactor", "<f4"),
+                      ("SecondaryTexScale", "<f4", 2), ("Rotation", "<f4")])
 RAY_DTYPE = np.dtype([("origin", "<f4", 3), ("PixelIndex", "<u4"), ("direction", "<f4", 3), ("last_pdf", "<f4"),
                       ("hits", "<u4", 4)])
 COL_DTYPE = np.dtype([("throughput", "<f4", 3), ("Direct", "<f4", 3), ("Indirect", "<f4", 3),
@@ -73,6 +78,18 @@ FLAG_INVISIBLE = 7
 
 
 # ---------------------------------------------------------------- ctypes structs
+# ShadowRayData (CommonData.cginc:116-123)
+SHADOW_DTYPE = np.dtype([("origin", "<f4", 3), ("LuminanceIncomming", "<f4"), ("direction", "<f4", 3), ("t", "<f4"),
+                         ("illumination", "<f4", 3), ("PixelIndex", "<u4")])
+assert SHADOW_DTYPE.itemsize == 48
+TT_FLAG_IS_BACKGROUND, TT_FLAG_SHADOW_CASTER = 5, 6
+
+
+class ShadowParams(C.Structure):
+    _fields_ = [("n_rays", C.c_uint32), ("bounce", C.c_int32), ("screen_width", C.c_uint32),
+                ("screen_height", C.c_uint32), ("flags", C.c_uint32)]
+
+
 class TraceParams(C.Structure):
     _fields_ = [("n_rays", C.c_uint32), ("bounce", C.c_int32), ("far_plane", C.c_float),
                 ("screen_width", C.c_uint32), ("screen_height", C.c_uint32), ("flags", C.c_uint32)]
@@ -222,6 +239,7 @@ def hip_lib():
         L.tt_scene_update_meshdata.argtypes = [vp, u32, u32, vp]
         L.tt_scene_bytes.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
+        L.tt_trace_shadow.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, C.POINTER(Stats)]
         L.tt_sync.argtypes = [vp]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
@@ -562,6 +580,20 @@ class Engine:
         st = self.L.tt_trace_closest(self.h, C.byref(p), _ptr(rays), _ptr(info), _ptr(colors), C.byref(s))
         if check:
             self._check(st, "tt_trace_closest")
+        return (s, st) if not check else s
+
+    def trace_shadow(self, shadow_rays, n_rays: int, bounce: int, width: int, height: int, visibility=None,
+                     colors=None, nee_pos=None, device: bool = False, stats: bool = False, check: bool = True,
+                     asynchronous: bool = False):
+        """tt_trace_shadow (kernel_shadow replacement): any-hit visibility of ShadowRayData rays."""
+        p = ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height,
+                         flags=(TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0)
+                         | (TT_TRACE_ASYNC if asynchronous else 0))
+        s = Stats()
+        st = self.L.tt_trace_shadow(self.h, C.byref(p), _ptr(shadow_rays), _ptr(visibility), _ptr(colors),
+                                    _ptr(nee_pos), C.byref(s))
+        if check:
+            self._check(st, "tt_trace_shadow")
         return (s, st) if not check else s
 
     def resolve_normals(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int,
