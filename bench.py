@@ -42,6 +42,27 @@ def alg_bytes(stats, bounce: int, info_written: int) -> float:
             + 36.0 * stats.tri_tests + 8.0 * stats.accepts + 68.0 * stats.blas_entries)
 
 
+def nee_rays(torch, rays, n, far, light):
+    """ShadowRayData (48 B) toward `light` from the hit points of the first n RayData records in the
+    device buffer `rays` (uint8): origin backed off 1e-3 along the incoming ray, t = distance,
+    illumination 1. Built on the GPU with torch (setup, not timed)."""
+    r = rays[: n * 48].view(torch.float32).view(n, 12)
+    t = r[:, 10]
+    hit = t < far
+    o, d = r[hit, 0:3], r[hit, 4:7]
+    p = o + d * t[hit, None] - d * 1e-3
+    to = torch.tensor(light, dtype=torch.float32, device=rays.device)[None, :] - p
+    dist = torch.sqrt((to * to).sum(1))
+    sr = torch.zeros((p.shape[0], 12), dtype=torch.float32, device=rays.device)
+    sr[:, 0:3] = p
+    sr[:, 4:7] = to / dist[:, None]
+    sr[:, 7] = dist
+    sr[:, 8:11] = 1.0
+    sri = sr.view(torch.int32)
+    sri[:, 11] = rays[: n * 48].view(torch.int32).view(n, 12)[hit, 3]  # PixelIndex, integer copy
+    return sr.contiguous().view(torch.uint8).view(-1)
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,6 +76,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather hit records to rank 0 after timing")
+    ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -138,6 +160,31 @@ def main():
     avg_ms = float(np.mean(launch_ms))
     achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9  # GB/s per launch, averaged over both launches
 
+    # ---- auxiliary (not the metric): any-hit NEE visibility rays (tt_trace_shadow)
+    # from this rank's primary hit points toward a point light; each launch restores the pristine
+    # rays first (occluded rays get t = 0 in place), only the kernel is timed (HIP events).
+    shadow = None
+    if not args.no_shadow:
+        sr = nee_rays(torch, rays, WH, far, light=(0.0, 9.0, 0.5))
+        ns = int(sr.shape[0]) // 48
+        work = torch.empty_like(sr)
+        s_sh = None
+        for k in range(args.warmup + args.steps):
+            if k == args.warmup:
+                torch.cuda.synchronize(dev)
+                eng.timing_reset()
+            work.copy_(sr)
+            if k == 0:
+                s_sh = eng.trace_shadow(work, ns, 0, W, H, device=True, stats=True)
+            else:
+                eng.trace_shadow(work, ns, 0, W, H, device=True, asynchronous=True)
+        sh_ms = eng.timing_read()
+        shadow = {"rays": ns, "trace_ms": round(float(np.mean(sh_ms)), 4),
+                  "mrays_s": round(ns / float(np.mean(sh_ms)) / 1e3, 1),
+                  "occluded": int(s_sh.hits), "nodes_per_ray": round(s_sh.node_visits / max(ns, 1), 2)}
+        log(f"shadow: {ns} NEE rays {shadow['trace_ms']} ms/launch = {shadow['mrays_s']} Mrays/s, "
+            f"{shadow['occluded']} occluded")
+
     gather_ms = None
     if args.gather and world > 1:
         hits = rays[: WH * 48].view(WH, 48)[:, 32:48].contiguous()
@@ -185,7 +232,7 @@ def main():
         with open(tpath) as f:
             tj = json.load(f)
         traffic = round(float(tj["mean_bytes_per_launch"]))
-        traffic_src = "profiles/" + os.path.basename(tj.get("file", "traffic_latest.json"))
+        traffic_src = "profiles/traffic_latest.json <- " + tj.get("source", "?").split(" ")[0]
 
     ms_per_step = elapsed * 1e3 / args.steps
     result = {
@@ -208,7 +255,8 @@ def main():
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
-                   "gather_ms": None if gather_ms is None else round(gather_ms, 3)},
+                   "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                   "aux_shadow_nee": shadow},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),
