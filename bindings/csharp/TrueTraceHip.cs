@@ -50,6 +50,16 @@ namespace TrueTrace.Hip
         public uint pad;
     }
 
+    [StructLayout(LayoutKind.Sequential)]
+    public struct TTShadowParams
+    {
+        public uint nRays;        // BufferSizes[CurBounce].shadow_rays
+        public int bounce;        // CurBounce
+        public uint screenWidth;
+        public uint screenHeight;
+        public TTTraceFlags flags;
+    }
+
     public static class Native
     {
         const string Lib = "truetrace_hip";
@@ -68,6 +78,10 @@ namespace TrueTrace.Hip
         // GlobalColors (ColData, 64 B).
         [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_closest(IntPtr ctx, ref TTTraceParams p,
             void* globalRays, uint* primaryInfo, void* globalColors, out TTStats stats);
+        // ShadowRayData (48 B, t = 0 written for occluded rays), float4 visibility per ray,
+        // GlobalColors (ColData, 64 B), NEEPosA (float4 per pixel); the last three nullable.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_shadow(IntPtr ctx, ref TTShadowParams p,
+            void* shadowRays, float* visibility, void* globalColors, float* neePos, out TTStats stats);
         [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
     }
 
@@ -110,6 +124,21 @@ namespace TrueTrace.Hip
             TTStats s;
             fixed (TRay* r = globalRays) fixed (uint* info = primaryInfo) fixed (TCol* col = globalColors)
                 Check(Native.tt_trace_closest(m_ctx, ref p, r, info, col, out s));
+            return s;
+        }
+
+        /// One kernel_shadow dispatch (IntersectionKernels.compute:264-505) for bounce `curBounce`.
+        public unsafe TTStats TraceShadow<TShadow, TCol>(TShadow[] shadowRays, uint nRays, int curBounce, int width,
+                                                         int height, float[] visibility = null,
+                                                         TCol[] globalColors = null, float[] neePos = null)
+            where TShadow : unmanaged where TCol : unmanaged
+        {
+            var p = new TTShadowParams { nRays = nRays, bounce = curBounce, screenWidth = (uint)width,
+                                         screenHeight = (uint)height, flags = 0 };
+            TTStats s;
+            fixed (TShadow* r = shadowRays) fixed (float* vis = visibility) fixed (TCol* col = globalColors)
+            fixed (float* nee = neePos)
+                Check(Native.tt_trace_shadow(m_ctx, ref p, r, vis, col, nee, out s));
             return s;
         }
 
