@@ -234,6 +234,16 @@ tt_status tt_scene_update_nodes(tt_ctx* ctx, uint32_t first, uint32_t count,
 /* Per-frame transform update (MeshDataBuffer.SetData, AssetManager.cs:1825). */
 tt_status tt_scene_update_meshdata(tt_ctx* ctx, uint32_t first, uint32_t count,
                                    const tt_mesh_data* meshdata);
+/* _AlphaAtlas (AssetManager.cs:260-262, :309): the R8 alpha atlas Cutout materials sample
+ * (IntersectionKernels.compute:35-40 with my_linear_clamp_sampler; CommonData.cginc:616 with
+ * my_point_clamp_sampler in the shadow path). texels: width*height bytes, row 0 = v in [0, 1/height)
+ * (the sampling orientation, i.e. D3D texture rows). Copied to HBM; replaces any previous atlas.
+ * Without an atlas, a scene with Cutout materials traces with TT_ERR_UNSUPPORTED.
+ * Filtering is pinned (the reference leaves it to the texture unit): point = texel
+ * clamp(floor(uv*size)); linear = taps at floor(uv*size - 0.5) and +1, clamped, weights
+ * f = x - floor(x), lerp(a,b,f) = a*(1-f) + b*f in x then y, texel value = byte / 255.0f. */
+tt_status tt_scene_upload_alpha_atlas(tt_ctx* ctx, const uint8_t* texels, uint32_t width, uint32_t height);
+
 /* Bytes of HBM the scene occupies (device copies + derived traversal layouts). */
 tt_status tt_scene_bytes(const tt_ctx* ctx, uint64_t* bytes);
 

@@ -108,9 +108,67 @@ static uint32_t cwbvh_node_intersect(const Ray* ray, uint32_t oct_inv4, float ma
     return hit_mask;
 }
 
+/* ------------------------------------------------------------ alpha atlas (f3) */
+static const uint8_t* g_atlas = NULL;
+static uint32_t g_atlas_w = 0, g_atlas_h = 0;
+
+void tt_oracle_set_alpha_atlas(const uint8_t* texels, uint32_t width, uint32_t height) {
+    g_atlas = texels;
+    g_atlas_w = texels ? width : 0;
+    g_atlas_h = texels ? height : 0;
+}
+
+/* AlignUV — CommonData.cginc:569-591 (Rotation 0, IsAlbedo false); AlphaTex packs the atlas
+ * rectangle as 15-bit fixed point /16384 (max corner in .x, min corner in .y). */
+static void align_uv(float bu, float bv, const float scale[4], const int32_t tex[2], float* ou, float* ov) {
+    if (tex[0] <= 0) {
+        *ou = -1.0f;
+        *ov = -1.0f;
+        return;
+    }
+    const float dx = (float)(((uint32_t)tex[0]) & 0x7FFFu) / 16384.0f;
+    const float dy = (float)(((uint32_t)tex[0]) >> 15) / 16384.0f;
+    const float dz = (float)(((uint32_t)tex[1]) & 0x7FFFu) / 16384.0f;
+    const float dw = (float)(((uint32_t)tex[1]) >> 15) / 16384.0f;
+    float x = bu * scale[0] + scale[2];
+    float y = bv * scale[1] + scale[3];
+    x = x < 0.0f ? 1.0f - fmodf(fabsf(x), 1.0f) : fmodf(fabsf(x), 1.0f);
+    y = y < 0.0f ? 1.0f - fmodf(fabsf(y), 1.0f) : fmodf(fabsf(y), 1.0f);
+    *ou = x * (dx - dz) + dz;
+    *ov = y * (dy - dw) + dw;
+}
+
+static int atlas_clamp(float c, uint32_t n) { return (int)fminf(fmaxf(c, 0.0f), (float)(n - 1)); }
+static float atlas_texel(int x, int y) { return (float)g_atlas[(size_t)y * g_atlas_w + (size_t)x] / 255.0f; }
+
+/* SampleLevel(my_point_clamp_sampler, uv, 0) on the R8 atlas (pinned point filter) */
+static float sample_point(float u, float v) {
+    return atlas_texel(atlas_clamp(floorf(u * (float)g_atlas_w), g_atlas_w),
+                       atlas_clamp(floorf(v * (float)g_atlas_h), g_atlas_h));
+}
+
+/* SampleLevel(my_linear_clamp_sampler, uv, 0) on the R8 atlas (pinned bilinear filter) */
+static float sample_linear(float u, float v) {
+    const float x = u * (float)g_atlas_w - 0.5f, y = v * (float)g_atlas_h - 0.5f;
+    const float x0 = floorf(x), y0 = floorf(y);
+    const float fx = x - x0, fy = y - y0;
+    const int ix0 = atlas_clamp(x0, g_atlas_w), ix1 = atlas_clamp(x0 + 1.0f, g_atlas_w);
+    const int iy0 = atlas_clamp(y0, g_atlas_h), iy1 = atlas_clamp(y0 + 1.0f, g_atlas_h);
+    const float a = atlas_texel(ix0, iy0) * (1.0f - fx) + atlas_texel(ix1, iy0) * fx;
+    const float b = atlas_texel(ix0, iy1) * (1.0f - fx) + atlas_texel(ix1, iy1) * fx;
+    return a * (1.0f - fy) + b * fy;
+}
+
+/* BaseUv = tex0 * (1 - u - v) + texedge1 * u + texedge2 * v (raw vertex UVs, ParentObject.cs:1039-1041) */
+static void base_uv(const tt_cuda_triangle* T, float u, float v, float* bu, float* bv) {
+    const float w = 1.0f - u - v;
+    *bu = T->tex0[0] * w + T->texedge1[0] * u + T->texedge2[0] * v;
+    *bv = T->tex0[1] * w + T->texedge1[1] * u + T->texedge2[1] * v;
+}
+
 /* IntersectTriangle — IntersectionKernels.compute:14-57 (AdvancedAlphaMapped on,
  * IgnoreGlassMain off, IgnoreBackfacing off; GlobalDefines.cginc:1-11). Returns 0, or 3
- * when a Cutout material would need the alpha atlas (unsupported). */
+ * when a Cutout material is reached without an alpha atlas (unsupported). */
 static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray* ray,
                               RayHit* ray_hit, int MatOffset, int CurBounce, uint32_t* accepts) {
     const tt_cuda_triangle* T = &s->tris[tri_id];
@@ -132,7 +190,13 @@ static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray
                 const int MaterialIndex = MatOffset + (int)T->MatDat;
                 if (MaterialIndex >= 0 && (uint32_t)MaterialIndex < s->n_mat) {
                     const tt_material* m = &s->mats[MaterialIndex];
-                    if (m->MatType == TT_MAT_CUTOUT_INDEX) return 3;
+                    if (m->MatType == TT_MAT_CUTOUT_INDEX) { /* :35-40 */
+                        if (!g_atlas) return 3;
+                        float bu, bv, au, av;
+                        base_uv(T, u, v, &bu, &bv);
+                        align_uv(bu, bv, m->AlbedoTexScale, m->AlphaTex, &au, &av);
+                        if (sample_linear(au, av) < m->AlphaCutoff) return 0;
+                    }
                     if (CurBounce == 0 && ((((int)m->Tag) >> TT_FLAG_INVISIBLE) & 1) == 1) return 0;
                 }
                 ray_hit->t = t;
@@ -348,7 +412,7 @@ static void* worker_main(void* arg) {
 
 static tt_status check_scene(const scene* s) {
     for (uint32_t m = 0; m < s->n_mat; m++)
-        if (s->mats[m].MatType == TT_MAT_CUTOUT_INDEX) return TT_ERR_UNSUPPORTED;
+        if (s->mats[m].MatType == TT_MAT_CUTOUT_INDEX && !g_atlas) return TT_ERR_UNSUPPORTED;
     return TT_OK;
 }
 
@@ -416,7 +480,14 @@ static int intersect_triangle_shadow(const scene* s, int tri_id, const Ray* ray,
                 const tt_material* m = &s->mats[MaterialIndex];
                 const int tag = (int)m->Tag;
                 if (((tag >> TT_FLAG_IS_BACKGROUND) & 1) || ((tag >> TT_FLAG_SHADOW_CASTER) & 1)) return 0;
-                if (m->MatType == TT_MAT_CUTOUT_INDEX || m->specTrans == 1.0f) return 3;
+                if (m->specTrans == 1.0f) return 3; /* glass tint samples the texture atlas */
+                if (m->MatType == TT_MAT_CUTOUT_INDEX) { /* :613-616, point sampler */
+                    if (!g_atlas) return 3;
+                    float bu, bv, au, av;
+                    base_uv(T, u, v, &bu, &bv);
+                    align_uv(bu, bv, m->AlbedoTexScale, m->AlphaTex, &au, &av);
+                    if (sample_point(au, av) < m->AlphaCutoff) return 0;
+                }
             }
             if (t > 0.0f && t < max_distance) {
                 ++*accepts;
@@ -619,7 +690,8 @@ tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
     if (p->screen_width == 0 || p->screen_height == 0) return TT_ERR_INVALID_ARG;
     scene s = {nodes, n_nodes, tris, n_tris, tlas_indices, n_tlas, meshdata, n_mesh, materials, n_mat};
     for (uint32_t m = 0; m < n_mat; m++)
-        if (materials[m].MatType == TT_MAT_CUTOUT_INDEX || materials[m].specTrans == 1.0f) return TT_ERR_UNSUPPORTED;
+        if ((materials[m].MatType == TT_MAT_CUTOUT_INDEX && !g_atlas) || materials[m].specTrans == 1.0f)
+            return TT_ERR_UNSUPPORTED;
     shadow_job J = {&s, p, shadow_rays, visibility, global_colors, nee_pos, counts};
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;

@@ -75,6 +75,10 @@ tt_status tt_oracle_generate(const float* cam_to_world, const float* cam_inv_pro
 
 int32_t tt_oracle_hardware_threads(void);
 
+/* The R8 alpha atlas Cutout materials sample (see tt_scene_upload_alpha_atlas); NULL clears it.
+ * Process-global (test infrastructure): set it before tracing a scene with Cutout materials. */
+void tt_oracle_set_alpha_atlas(const uint8_t* texels, uint32_t width, uint32_t height);
+
 #ifdef __cplusplus
 }
 #endif

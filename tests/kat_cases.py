@@ -196,3 +196,55 @@ def shadow_case_two_instances():
 
 
 SHADOW_CASES = [shadow_case_single_triangle, shadow_case_flags, shadow_case_two_instances]
+
+
+# ------------------------------------------------------------------ Cutout alpha test (§8 f3)
+def _cutout_scene(scale=(1.0, 1.0, 0.0, 0.0), alpha_tex=(16384 | (16384 << 15), 0)):
+    """Cutout unit triangle at z = 0 (material 1, UVs = barycentrics) over an opaque one at
+    z = -0.5. Alpha atlas 4x4: columns 0-1 transparent (0), columns 2-3 opaque (255)."""
+    tris = [hb.tri((0.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=1),
+            hb.tri((0.0, 0.0, -0.5), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=0)]
+    tris[0]["tex0"], tris[0]["texedge1"], tris[0]["texedge2"] = (0.0, 0.0), (1.0, 0.0), (0.0, 1.0)
+    root = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0,
+                        [(0, "leaf", (64, 64, 31), (128, 128, 65), (0, 2))])
+    mats = np.zeros(2, tthip.MAT_DTYPE)
+    mats[1]["MatType"] = tthip.MAT_CUTOUT_INDEX
+    mats[1]["AlphaCutoff"] = 0.5
+    mats[1]["AlbedoTexScale"] = scale
+    mats[1]["AlphaTex"] = alpha_tex
+    sc = hb.scene([root], tris, materials=mats)
+    atlas = np.zeros((4, 4), np.uint8)
+    atlas[:, 2:] = 255
+    sc.alpha_atlas = atlas
+    return sc
+
+
+def case_cutout():
+    """IntersectionKernels.compute:35-40 with the pinned bilinear filter: at uv (0.25, 0.25) all four
+    taps are transparent (alpha 0 < 0.5: the cutout triangle is skipped and the opaque one behind is
+    hit); at uv (0.6, 0.2) the taps are columns 1 and 2 with weight 0.9 on the opaque one."""
+    sc = _cutout_scene()
+    rays = hb.rays_buffer([(0.25, 0.25, 1.0), (0.6, 0.2, 1.0)], [(0.0, 0.0, -1.0), (0.0, 0.0, -1.0)])
+    return "cutout", sc, rays, 2, [hb.expected_hit(0, 1, 1.5, 0.25, 0.25), hb.expected_hit(0, 0, 1.0, 0.6, 0.2)]
+
+
+def case_cutout_wrap_and_no_texture():
+    """AlignUV (CommonData.cginc:569-591): TexScale offset -0.5 wraps u = 0.25 to 0.75 (opaque);
+    AlphaTex.x <= 0 samples uv (-1, -1), i.e. the clamped corner texel (transparent)."""
+    wrap = _cutout_scene(scale=(1.0, 1.0, -0.5, 0.0))
+    none = _cutout_scene(alpha_tex=(0, 0))
+    r = hb.rays_buffer([(0.25, 0.25, 1.0)], [(0.0, 0.0, -1.0)])
+    return wrap, none, r, hb.expected_hit(0, 0, 1.0, 0.25, 0.25), hb.expected_hit(0, 1, 1.5, 0.25, 0.25)
+
+
+def shadow_case_cutout():
+    """Point-sampled cutout in the shadow test (CommonData.cginc:613-616): uv (0.25, 0.25) -> texel
+    (1, 1) transparent, the opaque triangle at t = 1.5 decides; uv (0.6, 0.2) -> texel (2, 0) opaque."""
+    sc = _cutout_scene()
+    d = (0.0, 0.0, -1.0)
+    rays = hb.shadow_rays([(0.25, 0.25, 1.0), (0.25, 0.25, 1.0), (0.6, 0.2, 1.0)], [d, d, d], [1.25, 2.0, 1.25])
+    return "shadow_cutout", sc, rays, [0, 4, 4]
+
+
+ALL_CASES.append(case_cutout)
+SHADOW_CASES.append(shadow_case_cutout)

@@ -51,9 +51,26 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_shadow.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, C.POINTER(tthip.ShadowParams), vp,
                                        vp, vp, vp, vp, i32]
         L.tt_oracle_shadow.restype = i32
+        L.tt_oracle_set_alpha_atlas.argtypes = [vp, u32, u32]
+        L.tt_oracle_set_alpha_atlas.restype = None
         L._path = path
         _LIB = L
     return _LIB
+
+
+_ATLAS_KEEP = None
+
+
+def _set_atlas(scene):
+    """The oracle's alpha atlas is process-global: point it at the scene's (or clear it)."""
+    global _ATLAS_KEEP
+    a = getattr(scene, "alpha_atlas", None)
+    if a is None:
+        _ATLAS_KEEP = None
+        lib().tt_oracle_set_alpha_atlas(None, 0, 0)
+    else:
+        _ATLAS_KEEP = np.ascontiguousarray(a, np.uint8)
+        lib().tt_oracle_set_alpha_atlas(_ATLAS_KEEP.ctypes.data, _ATLAS_KEEP.shape[1], _ATLAS_KEEP.shape[0])
 
 
 def trace(scene: "tthip.Scene", rays: np.ndarray, n_rays: int, bounce: int, far_plane: float, width: int,
@@ -65,6 +82,7 @@ def trace(scene: "tthip.Scene", rays: np.ndarray, n_rays: int, bounce: int, far_
                           screen_height=height, flags=flags)
     cnt = np.zeros(n_rays, COUNTS_DTYPE) if counts else None
     mats = scene.materials if materials else None
+    _set_atlas(scene)
     st = L.tt_oracle_trace(scene.nodes.ctypes.data, len(scene.nodes), scene.tris.ctypes.data, len(scene.tris),
                            scene.tlas.ctypes.data, len(scene.tlas), scene.meshdata.ctypes.data, len(scene.meshdata),
                            None if mats is None else mats.ctypes.data, 0 if mats is None else len(mats), C.byref(p),
@@ -82,6 +100,7 @@ def shadow(scene: "tthip.Scene", srays: np.ndarray, n_rays: int, bounce: int, wi
     p = tthip.ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height, flags=0)
     cnt = np.zeros(n_rays, COUNTS_DTYPE) if counts else None
     mats = scene.materials
+    _set_atlas(scene)
     st = L.tt_oracle_shadow(scene.nodes.ctypes.data, len(scene.nodes), scene.tris.ctypes.data, len(scene.tris),
                             scene.tlas.ctypes.data, len(scene.tlas), scene.meshdata.ctypes.data, len(scene.meshdata),
                             None if mats is None or len(mats) == 0 else mats.ctypes.data,

@@ -191,8 +191,8 @@ def test_validator_rejects_malformed():
     bad = tthip.Scene(sc.nodes, sc.tris, np.array([5], np.int32), sc.meshdata, sc.materials)
     assert tthip.validate(bad)[0] == tthip.TT_ERR_INVALID_ARG
     bad = tthip.Scene(sc.nodes, sc.tris, sc.tlas, sc.meshdata, sc.materials.copy())
-    bad.materials[0]["MatType"] = tthip.MAT_CUTOUT_INDEX
-    assert tthip.validate(bad)[0] == tthip.TT_ERR_UNSUPPORTED
+    bad.materials[0]["MatType"] = tthip.MAT_CUTOUT_INDEX  # structurally valid (needs an atlas to trace)
+    assert tthip.validate(bad)[0] == tthip.TT_OK
     # a leaf meta whose triangle bits would spill into the internal-child bits 24..31
     nodes = sc.nodes.copy()
     meta = int(nodes[2]["meta"][0]) & ~0xFF

@@ -78,12 +78,22 @@ def test_kat_invisible_on_gpu(engine):
     assert r1["hits"][1].tolist() == exp1
 
 
-def test_cutout_material_is_refused(engine):
-    sc, _, _, _ = K.case_invisible_bounce0()
+def test_cutout_without_atlas_is_refused():
+    sc, rays, _, _ = K.case_invisible_bounce0()
     sc.materials[0]["MatType"] = tthip.MAT_CUTOUT_INDEX
-    with pytest.raises(tthip.TTError) as e:
+    fresh = tthip.Engine(0)  # no alpha atlas uploaded on this context
+    fresh.upload(sc)
+    s, st = fresh.trace(rays.copy(), 1, 0, FAR, 1, 1, check=False)
+    assert st == tthip.TT_ERR_UNSUPPORTED
+
+
+def test_cutout_wrap_and_no_texture_on_gpu(engine):
+    wrap, none, rays, exp_wrap, exp_none = K.case_cutout_wrap_and_no_texture()
+    for sc, exp in ((wrap, exp_wrap), (none, exp_none)):
         engine.upload(sc)
-    assert e.value.status == tthip.TT_ERR_UNSUPPORTED
+        r = rays.copy()
+        engine.trace(r, 1, 0, FAR, 1, 1)
+        assert r["hits"][0].tolist() == exp
 
 
 def test_malformed_scene_is_refused(engine):
@@ -428,3 +438,45 @@ def test_shadow_device_pointers(engine):
     back = rt.cpu().numpy().view(tthip.SHADOW_DTYPE)
     assert [0 if v == 1.0 else 4 for v in vt[:, 3].cpu().tolist()] == expected
     assert [int(t == 0.0) * 4 for t in back["t"]] == expected
+
+
+# ------------------------------------------------------------------ Cutout alpha test (§8 f3)
+def cutout_soup(seed):
+    """Random soup where every other triangle uses a Cutout material with a random atlas rectangle,
+    random UVs (including negative / > 1 to exercise AlignUV's wrap) and a noisy 64x32 alpha atlas."""
+    rng = np.random.default_rng(seed)
+    sc = tthip.single_object_scene(tthip.Mesh.soup(seed, 6000, 1.0, 0.15))
+    n = len(sc.tris)
+    sc.tris["tex0"] = rng.uniform(-1.5, 1.5, (n, 2))
+    sc.tris["texedge1"] = rng.uniform(-1.5, 1.5, (n, 2))
+    sc.tris["texedge2"] = rng.uniform(-1.5, 1.5, (n, 2))
+    sc.tris["MatDat"] = np.arange(n) % 3
+    mats = np.zeros(3, tthip.MAT_DTYPE)
+    for m in (1, 2):
+        mats[m]["MatType"] = tthip.MAT_CUTOUT_INDEX
+        mats[m]["AlphaCutoff"] = rng.uniform(0.2, 0.8)
+        mats[m]["AlbedoTexScale"] = [rng.uniform(0.5, 2), rng.uniform(0.5, 2), rng.uniform(-1, 1), rng.uniform(-1, 1)]
+        lo = rng.integers(0, 8000, 2)
+        hi = lo + rng.integers(1000, 8000, 2)
+        mats[m]["AlphaTex"] = [int(hi[0]) | (int(hi[1]) << 15), int(lo[0]) | (int(lo[1]) << 15)]
+    sc.materials = mats
+    sc.alpha_atlas = rng.integers(0, 256, (32, 64)).astype(np.uint8)
+    return sc
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_cutout_random_soup_closest_and_shadow(engine, seed):
+    sc = cutout_soup(seed)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    # the alpha test must actually reject some candidates: closest hits differ from an opaque trace
+    opaque = rays.copy()
+    sc_opaque = cutout_soup(seed)
+    sc_opaque.materials["MatType"] = 0
+    st, _ = O.trace(sc_opaque, opaque, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)
+    assert st == 0 and (opaque["hits"][: W * H] != rg["hits"][: W * H]).any(1).sum() > 50
+    sr = hb.nee_rays_from_hits(rg, W * H, (0.5, 2.0, 2.5), seed)
+    shadow_both(engine, sc, sr, 0, W, H, upload=False)

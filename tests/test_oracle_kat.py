@@ -57,10 +57,18 @@ def test_kat_invisible_only_at_bounce0():
     assert r1["hits"][1].tolist() == exp1
 
 
-def test_cutout_unsupported():
+def test_cutout_without_atlas_unsupported():
     sc, rays, _, _ = K.case_invisible_bounce0()
     sc.materials[0]["MatType"] = tthip.MAT_CUTOUT_INDEX
     assert O.trace(sc, rays, 1, 0, 1000.0, 1, 1)[0] == tthip.TT_ERR_UNSUPPORTED
+
+
+def test_cutout_wrap_and_no_texture():
+    wrap, none, rays, exp_wrap, exp_none = K.case_cutout_wrap_and_no_texture()
+    r = rays.copy()
+    assert O.trace(wrap, r, 1, 0, 1000.0, 1, 1)[0] == 0 and r["hits"][0].tolist() == exp_wrap
+    r = rays.copy()
+    assert O.trace(none, r, 1, 0, 1000.0, 1, 1)[0] == 0 and r["hits"][0].tolist() == exp_none
 
 
 def test_primary_info_bounce0_and_miss():

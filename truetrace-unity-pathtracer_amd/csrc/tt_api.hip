@@ -62,7 +62,9 @@ struct SceneHost {
     uint32_t n_mat = 0;
     std::vector<uint32_t> matdat;  // only kept when a material sets the Invisible flag
     bool any_shadow_skip = false;  // IsBackground / ShadowCaster present (shadow material checks)
-    bool any_atlas_shadow = false; // Cutout or specTrans == 1 present (shadow path unsupported)
+    bool any_atlas_shadow = false; // specTrans == 1 present (shadow glass tint: unsupported)
+    bool any_cutout = false;       // Cutout materials present (need the alpha atlas)
+    std::vector<CutoutMat> cut;    // per material, when any_cutout
 };
 
 }  // namespace
@@ -85,7 +87,8 @@ struct tt_ctx {
     bool has_scene = false;
     bool any_invisible = false;
     bool any_shadow_skip = false;  // some material is IsBackground / ShadowCaster
-    bool any_atlas_shadow = false; // some material is Cutout or specTrans == 1 (needs the atlases)
+    bool any_atlas_shadow = false; // some material has specTrans == 1 (shadow tint needs the texture atlas)
+    bool any_cutout = false;       // some material is Cutout (needs the alpha atlas)
     SceneHost host;
     DevBuf<tt_cwbvh_node> nodes;
     DevBuf<tt_cuda_triangle> tris_raw;
@@ -94,6 +97,9 @@ struct tt_ctx {
     DevBuf<tt_mesh_data> mesh_raw;
     DevBuf<MeshGpu> mesh;
     DevBuf<uint32_t> mat_tag;
+    DevBuf<CutoutMat> mat_cut;
+    DevBuf<uint8_t> atlas;      // _AlphaAtlas (R8)
+    uint32_t atlas_w = 0, atlas_h = 0;
     // host-pointer staging
     uint64_t max_rays = 0;
     DevBuf<tt_ray_data> st_rays;
@@ -263,15 +269,24 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
     any_invisible = false;
     tags.assign(std::max<uint32_t>(n_mat, 1u), 0u);
     for (uint32_t m = 0; m < n_mat; m++) {
-        if (mats[m].MatType == TT_MAT_CUTOUT_INDEX) {
-            why = "material " + std::to_string(m) +
-                  " is Cutout (alpha-atlas test, IntersectionKernels.compute:35-40): not supported";
-            return TT_ERR_UNSUPPORTED;
+        tags[m] = mats[m].Tag & ~(1u << TT_MATWORD_CUTOUT);
+        if (mats[m].MatType == TT_MAT_CUTOUT_INDEX) {  // alpha test, IntersectionKernels.compute:35-40
+            tags[m] |= 1u << TT_MATWORD_CUTOUT;
+            h.any_cutout = true;
         }
-        tags[m] = mats[m].Tag;
         any_invisible |= ((mats[m].Tag >> TT_FLAG_INVISIBLE) & 1u) != 0;
         h.any_shadow_skip |= (((mats[m].Tag >> TT_FLAG_IS_BACKGROUND) | (mats[m].Tag >> TT_FLAG_SHADOW_CASTER)) & 1u) != 0;
         h.any_atlas_shadow |= mats[m].specTrans == 1.0f;
+    }
+    if (h.any_cutout) {
+        h.cut.assign(n_mat, CutoutMat{});
+        for (uint32_t m = 0; m < n_mat; m++) {
+            CutoutMat& r = h.cut[m];
+            r.alpha_tex[0] = mats[m].AlphaTex[0];
+            r.alpha_tex[1] = mats[m].AlphaTex[1];
+            r.cutoff = mats[m].AlphaCutoff;
+            for (int k = 0; k < 4; k++) r.scale[k] = mats[m].AlbedoTexScale[k];
+        }
     }
     if (any_invisible) {
         h.matdat.resize(n_tris);
@@ -430,7 +445,12 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->mesh_raw.release();
     c->mesh.release();
     c->mat_tag.release();
+    c->mat_cut.release();
+    c->atlas.release();
     c->st_rays.release();
+    c->st_shadow.release();
+    c->st_vis.release();
+    c->st_nee.release();
     c->st_info.release();
     c->st_colors.release();
     c->st_normals.release();
@@ -508,6 +528,7 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->mesh_raw.release();
     c->mesh.release();
     c->mat_tag.release();
+    c->mat_cut.release();
     hipError_t e;
     if ((e = c->nodes.alloc(n_nodes)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
         (e = c->tris.alloc(n_tris)) != hipSuccess || (e = c->tlas.alloc(n_tlas)) != hipSuccess ||
@@ -521,11 +542,30 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     TT_HIP(c, hipMemcpy(c->mesh_raw.p, md, sizeof(tt_mesh_data) * n_mesh, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->mesh.p, mg.data(), sizeof(MeshGpu) * n_mesh, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->mat_tag.p, tags.data(), sizeof(uint32_t) * tags.size(), hipMemcpyHostToDevice));
+    if (h.any_cutout) {
+        if ((e = c->mat_cut.alloc(h.cut.size())) != hipSuccess) return hip_fail(c, e, "cutout records");
+        TT_HIP(c, hipMemcpy(c->mat_cut.p, h.cut.data(), sizeof(CutoutMat) * h.cut.size(), hipMemcpyHostToDevice));
+    }
     c->host = std::move(h);
     c->any_invisible = any_invisible;
     c->any_shadow_skip = c->host.any_shadow_skip;
+    c->any_cutout = c->host.any_cutout;
     c->any_atlas_shadow = c->host.any_atlas_shadow;
     c->has_scene = true;
+    return TT_OK;
+}
+
+tt_status tt_scene_upload_alpha_atlas(tt_ctx* c, const uint8_t* texels, uint32_t width, uint32_t height) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!texels || width == 0 || height == 0 || (uint64_t)width * height > 0x7fffffffull)
+        return fail(c, TT_ERR_INVALID_ARG, "tt_scene_upload_alpha_atlas: empty or oversized atlas");
+    TT_HIP(c, hipSetDevice(c->device));
+    c->atlas.release();
+    c->atlas_w = c->atlas_h = 0;
+    TT_HIP(c, c->atlas.alloc((size_t)width * height));
+    TT_HIP(c, hipMemcpy(c->atlas.p, texels, (size_t)width * height, hipMemcpyHostToDevice));
+    c->atlas_w = width;
+    c->atlas_h = height;
     return TT_OK;
 }
 
@@ -591,6 +631,20 @@ tt_status tt_scene_bytes(const tt_ctx* c, uint64_t* bytes) {
     return TT_OK;
 }
 
+namespace {
+MatView mat_view(const tt_ctx* c) {
+    MatView m;
+    m.word = c->mat_tag.p;
+    m.cut = c->mat_cut.p;
+    m.raw = c->tris_raw.p;
+    m.atlas = c->atlas.p;
+    m.n_mat = c->host.n_mat;
+    m.atlas_w = c->atlas_w;
+    m.atlas_h = c->atlas_h;
+    return m;
+}
+}  // namespace
+
 tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
                            const tt_col_data* colors, tt_stats* stats) {
     if (!c) return TT_ERR_INVALID_ARG;
@@ -600,6 +654,9 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     if (p->bounce < 0) return fail(c, TT_ERR_INVALID_ARG, "negative bounce");
     if (info && p->bounce > 0 && !colors)
         return fail(c, TT_ERR_INVALID_ARG, "GlobalColors required for _PrimaryTriangleInfo at bounce > 0");
+    if (c->any_cutout && !c->atlas.p)
+        return fail(c, TT_ERR_UNSUPPORTED,
+                    "scene has Cutout materials but no alpha atlas was uploaded (tt_scene_upload_alpha_atlas)");
     const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
     if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
     const uint32_t off = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u;
@@ -645,6 +702,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.mesh = c->mesh.p;
     a.mat_tag = c->mat_tag.p;
     a.n_mat = c->host.n_mat;
+    a.mat = mat_view(c);
     a.rays = d_rays;
     a.info = d_info;
     a.colors = d_colors;
@@ -659,7 +717,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.bounce = p->bounce;
     a.flags = p->flags;
     a.tile_swizzle = (p->n_rays == wh && p->screen_width % 8 == 0 && p->screen_height % 8 == 0) ? 1u : 0u;
-    const bool matcheck = c->any_invisible && p->bounce == 0;
+    const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout;
     const uint32_t waves_needed = (p->n_rays + 255u) / 256u;  // one TT_CHUNK per wave at least
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
     const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],
@@ -714,6 +772,9 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
         return fail(c, TT_ERR_UNSUPPORTED,
                     "scene has glass (specTrans == 1) materials: the shadow tint samples the texture atlas "
                     "(CommonData.cginc:618-625), not supported");
+    if (c->any_cutout && !c->atlas.p)
+        return fail(c, TT_ERR_UNSUPPORTED,
+                    "scene has Cutout materials but no alpha atlas was uploaded (tt_scene_upload_alpha_atlas)");
     const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
     if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
     const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
@@ -760,6 +821,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     a.mesh = c->mesh.p;
     a.mat_tag = c->mat_tag.p;
     a.n_mat = c->host.n_mat;
+    a.mat = mat_view(c);
     a.rays = d_rays;
     a.visibility = d_vis;
     a.colors = d_col;
@@ -771,7 +833,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     a.height = p->screen_height;
     a.bounce = p->bounce;
     a.flags = p->flags;
-    const bool matcheck = c->any_shadow_skip;
+    const bool matcheck = c->any_shadow_skip || c->any_cutout;
     const uint32_t blocks_needed = ((p->n_rays + 255u) / 256u + 3u) / 4u;
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));

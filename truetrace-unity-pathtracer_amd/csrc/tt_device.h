@@ -42,6 +42,27 @@ struct TraceControl {
                                   // node-phase lanes, tri-phase iterations, tri-phase lanes, active lanes
 };
 
+// Per-material record for the Cutout alpha test (row f3), 32 B; only uploaded when a Cutout
+// material exists. The per-material word in mat_tag carries MaterialData.Tag plus bit 31 = Cutout.
+struct CutoutMat {
+    int32_t alpha_tex[2];   // MaterialData.AlphaTex (atlas rectangle, 15-bit fixed point)
+    float cutoff;           // MaterialData.AlphaCutoff
+    uint32_t pad;
+    float scale[4];         // MaterialData.AlbedoTexScale
+};
+static_assert(sizeof(CutoutMat) == 32, "CutoutMat is 32 bytes");
+#define TT_MATWORD_CUTOUT 31u
+
+// Everything the material checks of the triangle tests read (IntersectionKernels.compute:35-48,
+// CommonData.cginc:611-617).
+struct MatView {
+    const uint32_t* word;         // Tag | Cutout << 31, per material
+    const CutoutMat* cut;         // per material (nullptr without Cutout materials)
+    const tt_cuda_triangle* raw;  // AggTris (raw UVs for the cutout sample)
+    const uint8_t* atlas;         // _AlphaAtlas, R8
+    uint32_t n_mat, atlas_w, atlas_h;
+};
+
 struct TraceArgs {
     const uint4* nodes;          // 80 B nodes as 5 x uint4
     uint32_t n_nodes;
@@ -51,6 +72,7 @@ struct TraceArgs {
     const MeshGpu* mesh;         // traversal-layout mesh records
     const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
     uint32_t n_mat;
+    MatView mat;                 // material checks (Invisible, Cutout)
     tt_ray_data* rays;           // GlobalRays
     uint32_t* info;              // _PrimaryTriangleInfo (uint4 per pixel), nullable
     const tt_col_data* colors;   // GlobalColors (bounce > 0 with info)
@@ -76,6 +98,7 @@ struct ShadowArgs {
     const MeshGpu* mesh;
     const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
     uint32_t n_mat;
+    MatView mat;                 // material checks (IsBackground / ShadowCaster, Cutout)
     tt_shadow_ray* rays;         // ShadowRaysBuffer (t = 0 written for occluded rays)
     float4* visibility;          // nullable, per ray
     tt_col_data* colors;         // nullable, GlobalColors (Direct += at bounce 0)

@@ -17,9 +17,8 @@ namespace {
 
 // triangle_intersect_shadow — CommonData.cginc:593-634. Returns true for an occluder.
 template <bool MATCHECK>
-__device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, const uint32_t* __restrict__ mat_tag,
-                                                uint32_t n_mat, int32_t tri_id, int32_t mat_offset, const LaneRay& r,
-                                                float max_distance) {
+__device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, int32_t tri_id,
+                                                int32_t mat_offset, const LaneRay& r, float max_distance) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
     const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
@@ -40,10 +39,16 @@ __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, con
     const bool in_tri = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f);
     bool occ = in_tri && (t > 0.0f && t < max_distance);
     if (MATCHECK && in_tri) {
-        // IsBackground / ShadowCaster surfaces never occlude (:612); out-of-range material = zeros
+        // IsBackground / ShadowCaster surfaces never occlude (:612); Cutout with the point sampler
+        // (:613-616); out-of-range material = zeros
         const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
-        const uint32_t tag = mi < n_mat ? mat_tag[mi] : 0u;
-        if (((tag >> TT_FLAG_IS_BACKGROUND) | (tag >> TT_FLAG_SHADOW_CASTER)) & 1u) occ = false;
+        const uint32_t w = mi < M.n_mat ? M.word[mi] : 0u;
+        if (((w >> TT_FLAG_IS_BACKGROUND) | (w >> TT_FLAG_SHADOW_CASTER)) & 1u) {
+            occ = false;
+        } else if (occ && ((w >> TT_MATWORD_CUTOUT) & 1u)) {
+            const CutoutMat cm = M.cut[mi];
+            if (sample_point(M, align_uv(base_uv(M, tri_id, u, v), cm)) < cm.cutoff) occ = false;
+        }
     }
     return occ;
 }
@@ -211,7 +216,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool occ =
-                shadow_triangle<MATCHECK>(tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), MatOffset, ray, max_distance);
+                shadow_triangle<MATCHECK>(tris, A.mat, (int32_t)(tg.x + ti), MatOffset, ray, max_distance);
             if (STATS) c_tris++;
             if (occ) {  // :449-454
                 A.rays[ray_index].t = 0.0f;

@@ -358,7 +358,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
-            const bool acc = intersect_triangle<MATCHECK>(tris, A.mat_tag, A.n_mat, (int32_t)(tg.x + ti), mesh_id,
+            const bool acc = intersect_triangle<MATCHECK>(tris, A.mat, A.bounce == 0, (int32_t)(tg.x + ti), mesh_id,
                                                           MatOffset, ray, best);
             if (STATS) {
                 c_tris++;
@@ -653,10 +653,14 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
                               (t > 0.0f && t < best.t);
             bool accept = cand;
             if (MATCHECK && __any(cand)) {
-                if (cand) {  // :48 Invisible at CurBounce == 0; out-of-range material reads as zeros
+                if (cand) {  // :35-48 Cutout, Invisible at CurBounce == 0; out-of-range material = zeros
                     const uint32_t mi = (uint32_t)(MatOffset + (int32_t)tc.y);
-                    const uint32_t tag = mi < A.n_mat ? A.mat_tag[mi] : 0u;
-                    if ((tag >> TT_FLAG_INVISIBLE) & 1u) accept = false;
+                    const uint32_t w = mi < A.mat.n_mat ? A.mat.word[mi] : 0u;
+                    if ((w >> TT_MATWORD_CUTOUT) & 1u) {
+                        const CutoutMat cm = A.mat.cut[mi];
+                        if (sample_linear(A.mat, align_uv(base_uv(A.mat, tri_id, u, v), cm)) < cm.cutoff) accept = false;
+                    }
+                    if (A.bounce == 0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) accept = false;
                 }
             }
             best.t = accept ? t : best.t;

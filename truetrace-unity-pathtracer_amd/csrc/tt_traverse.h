@@ -161,9 +161,52 @@ struct Best {
 
 // IntersectTriangle — IntersectionKernels.compute:14-57 (Moller-Trumbore on pos0/edges).
 // Evaluated branch-free; the accept predicate is exactly the reference's nested conditions.
+// ------------------------------------------------------- alpha atlas (row f3, pinned filtering)
+// AlignUV — CommonData.cginc:569-591 (Rotation 0, IsAlbedo false)
+__device__ __forceinline__ float2 align_uv(float bu, float bv, const CutoutMat& m) {
+    if (m.alpha_tex[0] <= 0) return make_float2(-1.0f, -1.0f);
+    const float dx = (float)(((uint32_t)m.alpha_tex[0]) & 0x7FFFu) / 16384.0f;
+    const float dy = (float)(((uint32_t)m.alpha_tex[0]) >> 15) / 16384.0f;
+    const float dz = (float)(((uint32_t)m.alpha_tex[1]) & 0x7FFFu) / 16384.0f;
+    const float dw = (float)(((uint32_t)m.alpha_tex[1]) >> 15) / 16384.0f;
+    float x = bu * m.scale[0] + m.scale[2];
+    float y = bv * m.scale[1] + m.scale[3];
+    x = x < 0.0f ? 1.0f - fmodf(fabsf(x), 1.0f) : fmodf(fabsf(x), 1.0f);
+    y = y < 0.0f ? 1.0f - fmodf(fabsf(y), 1.0f) : fmodf(fabsf(y), 1.0f);
+    return make_float2(x * (dx - dz) + dz, y * (dy - dw) + dw);
+}
+__device__ __forceinline__ float2 align_uv(float2 b, const CutoutMat& m) { return align_uv(b.x, b.y, m); }
+__device__ __forceinline__ int atlas_clamp(float c, uint32_t n) { return (int)fminf(fmaxf(c, 0.0f), (float)(n - 1u)); }
+__device__ __forceinline__ float atlas_texel(const MatView& M, int x, int y) {
+    return (float)M.atlas[(size_t)y * M.atlas_w + (size_t)x] / 255.0f;
+}
+// SampleLevel(my_point_clamp_sampler, uv, 0)
+__device__ __forceinline__ float sample_point(const MatView& M, float2 uv) {
+    return atlas_texel(M, atlas_clamp(floorf(uv.x * (float)M.atlas_w), M.atlas_w),
+                       atlas_clamp(floorf(uv.y * (float)M.atlas_h), M.atlas_h));
+}
+// SampleLevel(my_linear_clamp_sampler, uv, 0)
+__device__ __forceinline__ float sample_linear(const MatView& M, float2 uv) {
+    const float x = uv.x * (float)M.atlas_w - 0.5f, y = uv.y * (float)M.atlas_h - 0.5f;
+    const float x0 = floorf(x), y0 = floorf(y);
+    const float fx = x - x0, fy = y - y0;
+    const int ix0 = atlas_clamp(x0, M.atlas_w), ix1 = atlas_clamp(x0 + 1.0f, M.atlas_w);
+    const int iy0 = atlas_clamp(y0, M.atlas_h), iy1 = atlas_clamp(y0 + 1.0f, M.atlas_h);
+    const float a = atlas_texel(M, ix0, iy0) * (1.0f - fx) + atlas_texel(M, ix1, iy0) * fx;
+    const float b = atlas_texel(M, ix0, iy1) * (1.0f - fx) + atlas_texel(M, ix1, iy1) * fx;
+    return a * (1.0f - fy) + b * fy;
+}
+// BaseUv = tex0 * (1 - u - v) + texedge1 * u + texedge2 * v (IntersectionKernels.compute:37)
+__device__ __forceinline__ float2 base_uv(const MatView& M, int32_t tri_id, float u, float v) {
+    const float2* t = reinterpret_cast<const float2*>(reinterpret_cast<const char*>(M.raw + tri_id) + 60);
+    const float2 t0 = t[0], t1 = t[1], t2 = t[2];
+    const float w = 1.0f - u - v;
+    return make_float2(t0.x * w + t1.x * u + t2.x * v, t0.y * w + t1.y * u + t2.y * v);
+}
+
 template <bool MATCHECK>
-__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const uint32_t* __restrict__ mat_tag,
-                                                   uint32_t n_mat, int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
+__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
+                                                   int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
                                                    const LaneRay& r, Best& best) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
     const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
@@ -187,11 +230,15 @@ __device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, 
     const bool cand = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best.t);
     bool accept = cand;
     if (MATCHECK && accept) {
-        // GetFlag(_Materials[MatOffset + MatDat].Tag, Invisible) at CurBounce == 0 (:48); an
-        // out-of-range StructuredBuffer read returns zeros in D3D (no flags)
+        // _Materials[MatOffset + MatDat]; an out-of-range StructuredBuffer read returns zeros in
+        // D3D (no flags, MatType 0). Cutout alpha test (:35-40), then Invisible at CurBounce == 0 (:48).
         const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
-        const uint32_t tag = mi < n_mat ? mat_tag[mi] : 0u;
-        if ((tag >> TT_FLAG_INVISIBLE) & 1u) accept = false;
+        const uint32_t w = mi < M.n_mat ? M.word[mi] : 0u;
+        if ((w >> TT_MATWORD_CUTOUT) & 1u) {
+            const CutoutMat cm = M.cut[mi];
+            if (sample_linear(M, align_uv(base_uv(M, tri_id, u, v), cm)) < cm.cutoff) accept = false;
+        }
+        if (bounce0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) accept = false;
     }
     if (accept) {
         best.t = t;

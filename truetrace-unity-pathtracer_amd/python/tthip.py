@@ -240,6 +240,7 @@ def hip_lib():
         L.tt_scene_bytes.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
         L.tt_trace_shadow.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, C.POINTER(Stats)]
+        L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_sync.argtypes = [vp]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
@@ -399,6 +400,7 @@ class Scene:
     materials: np.ndarray
     tlas_nodes: int = 0
     meta: dict = field(default_factory=dict)
+    alpha_atlas: Optional[np.ndarray] = None  # _AlphaAtlas, uint8 [height, width] (Cutout materials)
 
     def save(self, path: str):
         np.savez_compressed(path, nodes=self.nodes.view(np.uint8), tris=self.tris.view(np.uint8),
@@ -540,6 +542,14 @@ class Engine:
                                     len(s.tlas), _ptr(s.meshdata), len(s.meshdata), _ptr(s.materials),
                                     len(s.materials))
         self._check(st, "tt_scene_upload")
+        if s.alpha_atlas is not None:
+            self.upload_alpha_atlas(s.alpha_atlas)
+
+    def upload_alpha_atlas(self, atlas: np.ndarray):
+        """_AlphaAtlas (AssetManager.cs:260-262): R8 texels, row 0 = v in [0, 1/height)."""
+        a = np.ascontiguousarray(atlas, np.uint8)
+        self._check(self.L.tt_scene_upload_alpha_atlas(self.h, _ptr(a), a.shape[1], a.shape[0]),
+                    "tt_scene_upload_alpha_atlas")
 
     def update_nodes(self, first: int, nodes: np.ndarray):
         self._check(self.L.tt_scene_update_nodes(self.h, first, len(nodes), _ptr(nodes)), "tt_scene_update_nodes")
