@@ -244,6 +244,23 @@ tt_status tt_scene_update_meshdata(tt_ctx* ctx, uint32_t first, uint32_t count,
  * f = x - floor(x), lerp(a,b,f) = a*(1-f) + b*f in x then y, texel value = byte / 255.0f. */
 tt_status tt_scene_upload_alpha_atlas(tt_ctx* ctx, const uint8_t* texels, uint32_t width, uint32_t height);
 
+/* Per-frame TLAS refit on the GPU: AssetManager.RefitTLAS
+ * (AssetManager.cs:1473-1548) with BVHRefitter.compute's RefitBVHLayer / NodeUpdate / NodeCompress
+ * (:220-371). Re-quantizes p, e and the child boxes of the uploaded nodes [0, n_tlas_nodes) from
+ * per-mesh world AABBs (mesh_aabbs: n_mesh x {BBMax[3], BBMin[3]}, the reference's AABB order,
+ * indexed like _MeshData). The TLAS topology (meta, imask, base indices) is the uploaded one; its
+ * NodePair / layer plan (ConstructNewTLAS, :1256-1390) is rebuilt on the host only when the scene
+ * or its nodes change. Runs on the context stream: a later trace sees the refit TLAS. Numerics
+ * pinned: e = 2^ceil(log2(extent * 0.003921569f)) exactly, float -> uint as D3D (NaN -> 0,
+ * saturating). flags: TT_TRACE_DEVICE_PTRS (mesh_aabbs in HBM), TT_TRACE_ASYNC. */
+tt_status tt_tlas_refit(tt_ctx* ctx, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh,
+                        uint32_t flags);
+
+/* Copies nodes [first, first+count) of the scene in HBM back to the host (e.g. the TLAS after
+ * tt_tlas_refit; the reference reads its refit TLAS back for nothing, but editors and tests do).
+ * Synchronizes the context stream. */
+tt_status tt_scene_read_nodes(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cwbvh_node* out);
+
 /* Bytes of HBM the scene occupies (device copies + derived traversal layouts). */
 tt_status tt_scene_bytes(const tt_ctx* ctx, uint64_t* bytes);
 

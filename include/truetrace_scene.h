@@ -92,6 +92,9 @@ tt_status tt_scene_build_get_info(const tt_scene_build* s, tt_scene_build_info* 
 tt_status tt_scene_build_copy(const tt_scene_build* s, tt_cwbvh_node* nodes,
                               tt_cuda_triangle* tris, int32_t* tlas_indices,
                               tt_mesh_data* meshdata);
+/* The per-mesh world AABBs the TLAS was built over (AssetManager MeshAABBs, CreateAABB
+ * :1239-1249), n_mesh x {BBMax[3], BBMin[3]} — the input tt_tlas_refit takes per frame. */
+tt_status tt_scene_build_copy_mesh_aabbs(const tt_scene_build* s, float* out6);
 void tt_scene_build_free(tt_scene_build* s);
 
 /* Standalone pieces, exposed for unit tests. */

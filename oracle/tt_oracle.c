@@ -8,6 +8,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -846,4 +847,216 @@ tt_status tt_oracle_generate(const float* c2w, const float* ip, uint32_t width, 
 int32_t tt_oracle_hardware_threads(void) {
     const long n = sysconf(_SC_NPROCESSORS_ONLN);
     return n > 0 ? (int32_t)n : 1;
+}
+
+/* ------------------------------------------------------------ TLAS refit (f4) */
+/* AssetManager.ConstructNewTLAS / CorrectRefit (AssetManager.cs:1256-1297 DocumentNodes,
+ * :1353-1390 ForwardStack / LayerStack, :1420-1456) and the per-frame GPU refit RefitTLAS
+ * (:1473-1548): BVHRefitter.compute NodeInitializer (:386-394), RefitBVHLayer (:220-252),
+ * NodeUpdate (:277-317), NodeCompress (:344-371). */
+typedef struct refit_pairs {
+    uint32_t n, cap;
+    int32_t* bvh;    /* NodeIndexPairData.BVHNode   */
+    int32_t* slot;   /* NodeIndexPairData.InNodeOffset */
+    int32_t* leaf;   /* IsLeafList.x */
+    int32_t* depth;  /* IsLeafList.y */
+    int32_t* parent; /* IsLeafList.z */
+    int32_t* to_bvh; /* ToBVHIndex[bvh8 node] */
+    int32_t max_depth;
+    const tt_cwbvh_node* nodes;
+} refit_pairs;
+
+static void rp_push(refit_pairs* R, int32_t bvh, int32_t slot) {
+    if (R->n == R->cap) {
+        R->cap = R->cap ? 2 * R->cap : 64;
+        R->bvh = (int32_t*)realloc(R->bvh, sizeof(int32_t) * R->cap);
+        R->slot = (int32_t*)realloc(R->slot, sizeof(int32_t) * R->cap);
+        R->leaf = (int32_t*)realloc(R->leaf, sizeof(int32_t) * R->cap);
+        R->depth = (int32_t*)realloc(R->depth, sizeof(int32_t) * R->cap);
+        R->parent = (int32_t*)realloc(R->parent, sizeof(int32_t) * R->cap);
+    }
+    R->bvh[R->n] = bvh;
+    R->slot[R->n] = slot;
+    R->leaf[R->n] = 0;
+    R->depth[R->n] = 0;
+    R->parent[R->n] = 0;
+    R->n++;
+}
+
+static uint8_t node_meta(const tt_cwbvh_node* n, int k) { return (uint8_t)(n->meta[k >> 2] >> (8 * (k & 3))); }
+
+/* DocumentNodes — AssetManager.cs:1257-1297 (the NodePair AABBs it computes are reset by
+ * NodeInitializer every frame, so they are not kept) */
+static void document_nodes(refit_pairs* R, int current, int parent, int next_bvh8, int is_leaf, int recur) {
+    if (recur > R->max_depth) R->max_depth = recur;
+    R->depth[current] = recur;
+    R->parent[current] = parent;
+    if (!is_leaf) {
+        R->to_bvh[next_bvh8] = current;
+        R->leaf[current] = 0;
+        const tt_cwbvh_node* node = &R->nodes[next_bvh8];
+        for (int i = 0; i < 8; i++) {
+            rp_push(R, next_bvh8, i);
+            const uint8_t m = node_meta(node, i);
+            if ((m & 0x1f) < 24) {
+                document_nodes(R, (int)R->n - 1, current, -1, 1, recur + 1);
+            } else {
+                const int child_index = (int)node->base_child + (m & 31) - 24;
+                document_nodes(R, (int)R->n - 1, current, child_index, 0, recur + 1);
+            }
+        }
+    } else {
+        R->leaf[current] = 1;
+    }
+}
+
+/* pow(2, ceil(log2(x))) pinned exactly (frexp); log2(0) = -inf -> 0, NaN / negative -> NaN */
+static float pow2_ceil_log2(float x) {
+    if (isnan(x) || x < 0.0f) return NAN;
+    if (x == 0.0f) return 0.0f;
+    if (isinf(x)) return INFINITY;
+    int k;
+    const float m = frexpf(x, &k);
+    return ldexpf(1.0f, m == 0.5f ? k - 1 : k);
+}
+
+/* HLSL float -> uint conversion (D3D: NaN -> 0, saturating) */
+static uint32_t ftou_d3d(float f) {
+    if (isnan(f) || f <= 0.0f) return 0u;
+    if (f >= 4294967296.0f) return 0xffffffffu;
+    return (uint32_t)f;
+}
+
+tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, const int32_t* tlas_indices,
+                               uint32_t n_tlas_indices, const float* mesh_aabbs, uint32_t n_mesh) {
+    if (!nodes || !n_tlas_nodes || !tlas_indices || !mesh_aabbs) return TT_ERR_INVALID_ARG;
+    refit_pairs R;
+    memset(&R, 0, sizeof(R));
+    R.nodes = nodes;
+    R.to_bvh = (int32_t*)calloc(n_tlas_nodes, sizeof(int32_t));
+    rp_push(&R, 0, 0); /* NodePair[0]: the root's dummy entry */
+    document_nodes(&R, 0, 0, 0, 0, 0);
+    const uint32_t N = R.n;
+    /* ForwardStack — :1370-1380 */
+    int32_t* fwd = (int32_t*)calloc((size_t)N * 8, sizeof(int32_t));
+    for (uint32_t i = 0; i < N; i++) {
+        const tt_cwbvh_node* node = &nodes[R.bvh[i]];
+        if (R.leaf[i]) {
+            const uint8_t m = node_meta(node, R.slot[i]);
+            const int first_triangle = m & 0x1f;
+            const int num_bits = __builtin_popcount((unsigned)(m >> 5));
+            fwd[(size_t)i * 8 + R.slot[i]] = num_bits + ((int)node->base_tri + first_triangle) * 24 + 1;
+        } else {
+            fwd[(size_t)i * 8 + R.slot[i]] = -(int)i - 1;
+        }
+        fwd[(size_t)R.parent[i] * 8 + R.slot[i]] = -(int)i - 1;
+    }
+    /* NodeInitializer + RefitBVHLayer, deepest layer first */
+    float* mx = (float*)malloc(sizeof(float) * 3 * N);
+    float* mn = (float*)malloc(sizeof(float) * 3 * N);
+    for (uint32_t i = 0; i < N; i++)
+        for (int a = 0; a < 3; a++) {
+            mx[3 * i + a] = -9999999999.0f;
+            mn[3 * i + a] = 9999999999.0f;
+        }
+    tt_status st = TT_OK;
+    for (int d = R.max_depth; d >= 0 && st == TT_OK; d--) {
+        for (uint32_t i = 0; i < N; i++) {
+            if (R.depth[i] != d) continue;
+            float rmx[3] = {-99999999.0f, -99999999.0f, -99999999.0f};
+            float rmn[3] = {99999999.0f, 99999999.0f, 99999999.0f};
+            for (int k = 0; k < 8; k++) {
+                const int leaf = fwd[(size_t)i * 8 + k];
+                if (leaf == 0) continue;
+                if (leaf < 0) {
+                    const int c = -leaf - 1;
+                    for (int a = 0; a < 3; a++) {
+                        rmx[a] = fmaxf(rmx[a], mx[3 * c + a]);
+                        rmn[a] = fminf(rmn[a], mn[3 * c + a]);
+                    }
+                } else {
+                    const int v = leaf - 1;
+                    const int start = v / 24, end = start + v % 24;
+                    for (int i4 = start; i4 < end; i4++) {
+                        if ((uint32_t)i4 >= n_tlas_indices || (uint32_t)tlas_indices[i4] >= n_mesh) {
+                            st = TT_ERR_INVALID_ARG;
+                            break;
+                        }
+                        const float* b = &mesh_aabbs[6 * (size_t)tlas_indices[i4]]; /* AABB {BBMax, BBMin} */
+                        for (int a = 0; a < 3; a++) {
+                            rmx[a] = fmaxf(rmx[a], b[a]);
+                            rmn[a] = fminf(rmn[a], b[3 + a]);
+                        }
+                    }
+                }
+            }
+            for (int a = 0; a < 3; a++) {
+                mx[3 * i + a] = rmx[a];
+                mn[3 * i + a] = rmn[a];
+            }
+        }
+    }
+    if (st == TT_OK) {
+        /* NodeUpdate into the fixed-layout nodes (p, e, per-slot quantized uints) */
+        float* P = (float*)malloc(sizeof(float) * 3 * n_tlas_nodes);
+        uint32_t* E = (uint32_t*)malloc(sizeof(uint32_t) * 3 * n_tlas_nodes);
+        uint32_t* Q = (uint32_t*)malloc(sizeof(uint32_t) * 48 * n_tlas_nodes); /* [node][axis-min/max][slot] */
+        for (uint32_t n = 0; n < n_tlas_nodes; n++) {
+            const tt_cwbvh_node* s = &nodes[n];
+            for (int a = 0; a < 3; a++) {
+                P[3 * n + a] = s->p[a];
+                E[3 * n + a] = (s->e_imask >> (8 * a)) & 0xff;
+            }
+            const uint32_t* words[6] = {s->qlo_x, s->qhi_x, s->qlo_y, s->qhi_y, s->qlo_z, s->qhi_z};
+            for (int w = 0; w < 6; w++)
+                for (int k = 0; k < 8; k++) Q[48 * n + 8 * w + k] = (words[w][k >> 2] >> (8 * (k & 3))) & 0xff;
+        }
+        for (uint32_t i = 1; i < N; i++) {
+            const int node = R.bvh[i];
+            const int link = R.to_bvh[node];
+            float tmx[3], tmn[3];
+            for (int a = 0; a < 3; a++) {
+                tmx[a] = mx[3 * i + a];
+                tmn[a] = mn[3 * i + a];
+            }
+            if (tmx[0] < -10000.0f)
+                for (int a = 0; a < 3; a++) tmx[a] = tmn[a] = mn[3 * link + a];
+            for (int a = 0; a < 3; a++) {
+                const float e = pow2_ceil_log2((mx[3 * link + a] - mn[3 * link + a]) * 0.003921569f);
+                const float p = mn[3 * link + a];
+                uint32_t eu;
+                memcpy(&eu, &e, 4);
+                P[3 * node + a] = p;
+                E[3 * node + a] = eu >> 23;
+                Q[48 * node + 8 * (2 * a + 1) + R.slot[i]] = ftou_d3d(ceilf((tmx[a] - p) / e));
+                Q[48 * node + 8 * (2 * a) + R.slot[i]] = ftou_d3d(floorf((tmn[a] - p) / e));
+            }
+        }
+        /* NodeCompress — packed exactly as the reference (full uints shifted and OR-ed) */
+        for (uint32_t n = 0; n < n_tlas_nodes; n++) {
+            tt_cwbvh_node* o = &nodes[n];
+            const uint32_t imask = o->e_imask >> 24;
+            for (int a = 0; a < 3; a++) o->p[a] = P[3 * n + a];
+            o->e_imask = E[3 * n + 0] | (E[3 * n + 1] << 8) | (E[3 * n + 2] << 16) | (imask << 24);
+            uint32_t* words[6] = {o->qlo_x, o->qhi_x, o->qlo_y, o->qhi_y, o->qlo_z, o->qhi_z};
+            for (int w = 0; w < 6; w++)
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t* q = &Q[48 * n + 8 * w + 4 * h];
+                    words[w][h] = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
+                }
+        }
+        free(P);
+        free(E);
+        free(Q);
+    }
+    free(mx);
+    free(mn);
+    free(fwd);
+    free(R.bvh);
+    free(R.slot);
+    free(R.leaf);
+    free(R.depth);
+    free(R.parent);
+    free(R.to_bvh);
+    return st;
 }

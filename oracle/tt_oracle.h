@@ -75,6 +75,14 @@ tt_status tt_oracle_generate(const float* cam_to_world, const float* cam_inv_pro
 
 int32_t tt_oracle_hardware_threads(void);
 
+/* TLAS refit (AssetManager.RefitTLAS, AssetManager.cs:1473-1548, with the NodePair / layer
+ * structures of ConstructNewTLAS :1256-1390 and BVHRefitter.compute RefitBVHLayer / NodeUpdate /
+ * NodeCompress): rewrites p, e and the quantized boxes of nodes[0, n_tlas_nodes) in place from
+ * per-mesh world AABBs (mesh_aabbs: n_mesh x {BBMax[3], BBMin[3]}). Topology (meta, imask, base
+ * indices) is read from the nodes and left unchanged. */
+tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, const int32_t* tlas_indices,
+                               uint32_t n_tlas_indices, const float* mesh_aabbs, uint32_t n_mesh);
+
 /* The R8 alpha atlas Cutout materials sample (see tt_scene_upload_alpha_atlas); NULL clears it.
  * Process-global (test infrastructure): set it before tracing a scene with Cutout materials. */
 void tt_oracle_set_alpha_atlas(const uint8_t* texels, uint32_t width, uint32_t height);

@@ -53,6 +53,8 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_shadow.restype = i32
         L.tt_oracle_set_alpha_atlas.argtypes = [vp, u32, u32]
         L.tt_oracle_set_alpha_atlas.restype = None
+        L.tt_oracle_tlas_refit.argtypes = [vp, u32, vp, u32, vp, u32]
+        L.tt_oracle_tlas_refit.restype = i32
         L._path = path
         _LIB = L
     return _LIB
@@ -132,3 +134,13 @@ def generate(cam_to_world, cam_inv_proj, width, height, near, far, jitter=0, fra
                               max_bounce, rays.ctypes.data)
     assert st == 0
     return rays
+
+
+def tlas_refit(scene: "tthip.Scene", mesh_aabbs: np.ndarray, n_tlas_nodes=None):
+    """Oracle TLAS refit: returns (status, nodes) with nodes[0, n_tlas) rewritten."""
+    nodes = scene.nodes.copy()
+    n = scene.tlas_nodes if n_tlas_nodes is None else n_tlas_nodes
+    boxes = np.ascontiguousarray(mesh_aabbs, np.float32)
+    st = lib().tt_oracle_tlas_refit(nodes.ctypes.data, n, scene.tlas.ctypes.data, len(scene.tlas), boxes.ctypes.data,
+                                    boxes.shape[0])
+    return st, nodes

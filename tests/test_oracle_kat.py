@@ -172,3 +172,91 @@ def test_shadow_glass_unsupported():
     sc.materials[0]["specTrans"] = 1.0
     st, _ = O.shadow(sc, rays, len(rays), 0, len(rays), 1)
     assert st == tthip.TT_ERR_UNSUPPORTED
+
+
+# ------------------------------------------------------------------ TLAS refit (§8 f4)
+def _decode_slot_boxes(node):
+    """World boxes of the 8 child slots of an 80-B node: p + q * 2^(e-127) per axis."""
+    e = [(int(node["e_imask"]) >> (8 * a)) & 0xff for a in range(3)]
+    scale = [np.float32(2.0) ** (ea - 127) for ea in e]
+    q = {}
+    for name in ("qlo_x", "qhi_x", "qlo_y", "qhi_y", "qlo_z", "qhi_z"):
+        w = node[name]
+        q[name] = [(int(w[k >> 2]) >> (8 * (k & 3))) & 0xff for k in range(8)]
+    lo = np.array([[node["p"][0] + q["qlo_x"][k] * scale[0], node["p"][1] + q["qlo_y"][k] * scale[1],
+                    node["p"][2] + q["qlo_z"][k] * scale[2]] for k in range(8)])
+    hi = np.array([[node["p"][0] + q["qhi_x"][k] * scale[0], node["p"][1] + q["qhi_y"][k] * scale[1],
+                    node["p"][2] + q["qhi_z"][k] * scale[2]] for k in range(8)])
+    return lo, hi
+
+
+def _refit_scene(seed, n_inst=60):
+    rng = np.random.default_rng(seed)
+    am = tthip.AssetManager()
+    am.add_parent(tthip.Blas(tthip.Mesh.soup(seed, 800, 10.0, 0.5)), tthip.trs_matrix((0, 0, 0)),
+                  np.zeros(1, tthip.MAT_DTYPE))
+    props = [am.add_instance_parent(tthip.Blas(tthip.Mesh.prop(seed * 10 + k, 300)), np.zeros(1, tthip.MAT_DTYPE))
+             for k in range(4)]
+    for i in range(n_inst):
+        am.add_instance(props[i % 4], tthip.trs_matrix(rng.uniform(-30, 30, 3), float(rng.uniform(0, 360)),
+                                                       float(rng.uniform(0.5, 2))))
+    return am.build()
+
+
+def test_refit_bounds_every_instance():
+    """After the refit (AssetManager.RefitTLAS) every TLAS slot box contains the AABBs of all the
+    instances below it (the quantization rounds outward), and BLAS nodes are untouched."""
+    sc = _refit_scene(3)
+    boxes = sc.meta["mesh_aabbs"].copy()
+    boxes[:, :3] += 1.5  # moved: every instance shifted by +1.5 in x, y, z
+    boxes[:, 3:] += 1.5
+    st, nodes = O.tlas_refit(sc, boxes)
+    assert st == 0
+    assert np.array_equal(nodes[sc.tlas_nodes:], sc.nodes[sc.tlas_nodes:])
+
+    def meta_of(node):
+        return [(int(node["meta"][k >> 2]) >> (8 * (k & 3))) & 0xff for k in range(8)]
+
+    def instances_below(n):
+        node, out = nodes[n], []
+        for m in meta_of(node):
+            if m and (m & 0x1f) >= 24:
+                out += instances_below(int(node["base_child"]) + (m & 0x1f) - 24)
+            elif m:
+                first, cnt = m & 0x1f, bin(m >> 5).count("1")
+                out += [int(sc.tlas[t]) for t in range(int(node["base_tri"]) + first, int(node["base_tri"]) + first + cnt)]
+        return out
+
+    checked = 0
+    for n in range(sc.tlas_nodes):
+        node = nodes[n]
+        lo, hi = _decode_slot_boxes(node)
+        for k, m in enumerate(meta_of(node)):
+            if m == 0:
+                continue
+            if (m & 0x1f) >= 24:
+                ids = instances_below(int(node["base_child"]) + (m & 0x1f) - 24)
+            else:
+                first, cnt = m & 0x1f, bin(m >> 5).count("1")
+                ids = [int(sc.tlas[t]) for t in range(int(node["base_tri"]) + first, int(node["base_tri"]) + first + cnt)]
+            for i in ids:
+                assert (boxes[i, 3:] >= lo[k]).all() and (boxes[i, :3] <= hi[k]).all(), (n, k, i)
+                checked += 1
+    assert checked >= len(boxes)
+
+
+def test_refit_traces_like_a_fresh_build():
+    """Refit TLAS (reference topology, new boxes) finds the same closest hits as tracing with the
+    TLAS built for the same boxes; both are the oracle."""
+    sc = _refit_scene(4)
+    st, nodes = O.tlas_refit(sc, sc.meta["mesh_aabbs"])
+    assert st == 0
+    refit = tthip.Scene(nodes, sc.tris, sc.tlas, sc.meshdata, sc.materials, tlas_nodes=sc.tlas_nodes)
+    W, H = 64, 48
+    c2w, ip = tthip.unity_camera((0, 10, 50), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, 1000.0)
+    a = O.generate(c2w, ip, W, H, 0.3, 1000.0)
+    b = a.copy()
+    assert O.trace(sc, a, W * H, 0, 1000.0, W, H, nthreads=8)[0] == 0
+    assert O.trace(refit, b, W * H, 0, 1000.0, W, H, nthreads=8)[0] == 0
+    assert np.array_equal(a["hits"][: W * H, :3], b["hits"][: W * H, :3])
+    assert (a["hits"][: W * H, 1] != 0xFFFFFFFF).sum() > W * H // 4

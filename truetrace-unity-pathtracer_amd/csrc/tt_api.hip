@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "tt_device.h"
+#include "tt_refit.h"
 
 #define TT_RING 256u
 
@@ -100,6 +101,11 @@ struct tt_ctx {
     DevBuf<CutoutMat> mat_cut;
     DevBuf<uint8_t> atlas;      // _AlphaAtlas (R8)
     uint32_t atlas_w = 0, atlas_h = 0;
+    // TLAS refit (f4): plan valid for (scene generation, n_tlas_nodes)
+    RefitDev refit;
+    uint64_t scene_gen = 0, refit_gen = ~0ull;
+    uint32_t refit_n_tlas = 0;
+    DevBuf<float> st_boxes;
     // host-pointer staging
     uint64_t max_rays = 0;
     DevBuf<tt_ray_data> st_rays;
@@ -447,6 +453,8 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->mat_tag.release();
     c->mat_cut.release();
     c->atlas.release();
+    tt_refit_free(c->refit);
+    c->st_boxes.release();
     c->st_rays.release();
     c->st_shadow.release();
     c->st_vis.release();
@@ -548,6 +556,7 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     }
     c->host = std::move(h);
     c->any_invisible = any_invisible;
+    c->scene_gen++;
     c->any_shadow_skip = c->host.any_shadow_skip;
     c->any_cutout = c->host.any_cutout;
     c->any_atlas_shadow = c->host.any_atlas_shadow;
@@ -566,6 +575,47 @@ tt_status tt_scene_upload_alpha_atlas(tt_ctx* c, const uint8_t* texels, uint32_t
     TT_HIP(c, hipMemcpy(c->atlas.p, texels, (size_t)width * height, hipMemcpyHostToDevice));
     c->atlas_w = width;
     c->atlas_h = height;
+    return TT_OK;
+}
+
+tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh, uint32_t flags) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!mesh_aabbs || n_tlas_nodes == 0 || n_tlas_nodes > c->host.nodes.size())
+        return fail(c, TT_ERR_INVALID_ARG, "tt_tlas_refit: null boxes or n_tlas_nodes out of range");
+    if (n_mesh < c->host.mesh.size())
+        return fail(c, TT_ERR_INVALID_ARG, "tt_tlas_refit: need one AABB per _MeshData record (%zu)", c->host.mesh.size());
+    TT_HIP(c, hipSetDevice(c->device));
+    if (c->refit_gen != c->scene_gen || c->refit_n_tlas != n_tlas_nodes) {
+        RefitPlan plan;
+        if (!tt_refit_build_plan(c->host.nodes.data(), n_tlas_nodes, plan))
+            return fail(c, TT_ERR_INVALID_ARG, "tt_tlas_refit: a TLAS child index leaves [0, n_tlas_nodes)");
+        TT_HIP(c, hipStreamSynchronize(c->stream));  // the old plan's buffers may be in use
+        TT_HIP(c, tt_refit_prepare(plan, c->host.nodes.data(), n_tlas_nodes, c->refit));
+        c->refit_gen = c->scene_gen;
+        c->refit_n_tlas = n_tlas_nodes;
+    }
+    const float* d_boxes = mesh_aabbs;
+    if (flags & TT_TRACE_DEVICE_PTRS) {
+        if (!is_device_ptr(mesh_aabbs)) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but boxes are not device memory");
+    } else {
+        if (c->st_boxes.n < (size_t)6 * n_mesh) TT_HIP(c, c->st_boxes.alloc((size_t)6 * n_mesh));
+        TT_HIP(c, hipMemcpyAsync(c->st_boxes.p, mesh_aabbs, sizeof(float) * 6 * n_mesh, hipMemcpyHostToDevice, c->stream));
+        d_boxes = c->st_boxes.p;
+    }
+    TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
+    if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_scene_read_nodes(tt_ctx* c, uint32_t first, uint32_t count, tt_cwbvh_node* out) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!out || (uint64_t)first + count > c->host.nodes.size())
+        return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_nodes: range out of bounds");
+    TT_HIP(c, hipSetDevice(c->device));
+    TT_HIP(c, hipMemcpyAsync(out, c->nodes.p + first, sizeof(tt_cwbvh_node) * count, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
 
@@ -600,6 +650,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, hipSetDevice(c->device));
     TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, nodes, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
+    c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
     return TT_OK;
 }
 

@@ -655,6 +655,7 @@ struct tt_scene_build {
     std::vector<tt_cuda_triangle> tris;
     std::vector<int32_t> tlas_indices;
     std::vector<tt_mesh_data> meshdata;
+    std::vector<float> mesh_aabbs;  // MeshAABBs, n_mesh x {BBMax, BBMin}
     uint32_t tlas_nodes = 0;
 };
 
@@ -905,6 +906,12 @@ tt_status tt_scene_assemble(const tt_parent_desc* parents, uint32_t n_parents,
     }
     Aggregate(bvh8.BVH8Nodes, s->nodes.data());
     s->tlas_nodes = (uint32_t)bvh8.BVH8Nodes.size();
+    s->mesh_aabbs.resize(6 * (size_t)n_mesh);
+    for (uint32_t i = 0; i < n_mesh; i++) {
+        const AABB& b = MeshAABBs[i];
+        const float v[6] = {b.BBMax.x, b.BBMax.y, b.BBMax.z, b.BBMin.x, b.BBMin.y, b.BBMin.z};
+        std::memcpy(&s->mesh_aabbs[6 * (size_t)i], v, sizeof(v));
+    }
     s->tlas_indices.assign(bvh8.cwbvh_indices.begin(), bvh8.cwbvh_indices.end());
     *out = s;
     return TT_OK;
@@ -928,6 +935,12 @@ tt_status tt_scene_build_copy(const tt_scene_build* s, tt_cwbvh_node* nodes, tt_
     if (tris) std::memcpy(tris, s->tris.data(), s->tris.size() * sizeof(tt_cuda_triangle));
     if (tlas_indices) std::memcpy(tlas_indices, s->tlas_indices.data(), s->tlas_indices.size() * sizeof(int32_t));
     if (meshdata) std::memcpy(meshdata, s->meshdata.data(), s->meshdata.size() * sizeof(tt_mesh_data));
+    return TT_OK;
+}
+
+tt_status tt_scene_build_copy_mesh_aabbs(const tt_scene_build* s, float* out6) {
+    if (!s || !out6) return TT_ERR_INVALID_ARG;
+    std::memcpy(out6, s->mesh_aabbs.data(), s->mesh_aabbs.size() * sizeof(float));
     return TT_OK;
 }
 

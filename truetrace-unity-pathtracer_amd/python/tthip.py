@@ -189,6 +189,7 @@ def scene_lib():
         L.tt_scene_build_get_info.argtypes = [vp, C.POINTER(SceneBuildInfo)]
         L.tt_scene_build_copy.argtypes = [vp, vp, vp, vp, vp]
         L.tt_scene_build_free.argtypes = [vp]
+        L.tt_scene_build_copy_mesh_aabbs.argtypes = [vp, vp]
         L.tt_scene_build_free.restype = None
         L.tt_pack_octahedral.argtypes = [C.c_float, C.c_float, C.c_float]
         L.tt_pack_octahedral.restype = u32
@@ -241,6 +242,8 @@ def hip_lib():
         L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
         L.tt_trace_shadow.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, C.POINTER(Stats)]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
+        L.tt_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
+        L.tt_scene_read_nodes.argtypes = [vp, u32, u32, vp]
         L.tt_sync.argtypes = [vp]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
@@ -472,11 +475,13 @@ class AssetManager:
             tlas = np.zeros(info.n_tlas_indices, np.int32)
             md = np.zeros(info.n_mesh, MESH_DTYPE)
             L.tt_scene_build_copy(h, nodes.ctypes.data, tris.ctypes.data, tlas.ctypes.data, md.ctypes.data)
+            aabbs = np.zeros((info.n_mesh, 6), np.float32)
+            L.tt_scene_build_copy_mesh_aabbs(h, aabbs.ctypes.data)
         finally:
             L.tt_scene_build_free(h)
         mats = self.materials + getattr(self, "_ip_mats", [])
         materials = np.concatenate(mats) if mats else np.zeros(1, MAT_DTYPE)
-        return Scene(nodes, tris, tlas, md, materials, tlas_nodes=info.tlas_nodes)
+        return Scene(nodes, tris, tlas, md, materials, tlas_nodes=info.tlas_nodes, meta={"mesh_aabbs": aabbs})
 
 
 def single_object_scene(mesh: Mesh, local_to_world=None, n_materials: int = 8) -> Scene:
@@ -591,6 +596,19 @@ class Engine:
         if check:
             self._check(st, "tt_trace_closest")
         return (s, st) if not check else s
+
+    def tlas_refit(self, n_tlas_nodes: int, mesh_aabbs, device: bool = False, asynchronous: bool = False):
+        """tt_tlas_refit (AssetManager.RefitTLAS): re-quantize TLAS nodes [0, n_tlas_nodes) in HBM from
+        per-mesh world AABBs (n_mesh x {BBMax, BBMin})."""
+        n = int(mesh_aabbs.shape[0]) if hasattr(mesh_aabbs, "shape") else len(mesh_aabbs) // 6
+        flags = (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_ASYNC if asynchronous else 0)
+        self._check(self.L.tt_tlas_refit(self.h, n_tlas_nodes, _ptr(mesh_aabbs), n, flags), "tt_tlas_refit")
+
+    def scene_nodes(self, first: int, count: int) -> np.ndarray:
+        """Reads nodes [first, first+count) back from HBM (parity checks of the refit)."""
+        out = np.zeros(count, NODE_DTYPE)
+        self._check(self.L.tt_scene_read_nodes(self.h, first, count, _ptr(out)), "tt_scene_read_nodes")
+        return out
 
     def trace_shadow(self, shadow_rays, n_rays: int, bounce: int, width: int, height: int, visibility=None,
                      colors=None, nee_pos=None, device: bool = False, stats: bool = False, check: bool = True,
