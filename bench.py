@@ -63,6 +63,94 @@ def nee_rays(torch, rays, n, far, light):
     return sr.contiguous().view(torch.uint8).view(-1)
 
 
+def timed_launches(eng, launches, warmup, steps):
+    """Runs the list of launch closures warmup + steps times; returns per-launch HIP-event times
+    (ms) as an array of shape (steps, len(launches))."""
+    import torch
+
+    for _ in range(warmup):
+        for f in launches:
+            f()
+    torch.cuda.synchronize()
+    eng.timing_reset()
+    for _ in range(steps):
+        for f in launches:
+            f()
+    torch.cuda.synchronize()
+    return np.asarray(eng.timing_read(), np.float64).reshape(steps, len(launches))
+
+
+def aux_configs(torch, tthip, eng, dev, args, which):
+    """The other BASELINE.json configs, each traced by the same engine with
+    inputs resident in HBM and timed per launch with HIP events (not the metric):
+      c3  C2 geometry, primary + 3 diffuse bounces (each bounce's compacted rays kept in their own
+          buffer so every repetition traces identical rays)
+      c4  Bistro-shaped two-level instancing, 1920x1080 primary + bounce 1
+      c5  San-Miguel-shaped 10M tris, 3840x2160 primary (single GPU; 8 GPUs shard it by tiles)"""
+    import ttconfigs as T
+
+    far = T.FAR
+    out = {}
+
+    def pack(name, n_rays_per_launch, ms, extra):
+        mean = ms.mean(0)
+        rec = {"rays": [int(n) for n in n_rays_per_launch], "trace_ms": [round(float(m), 4) for m in mean],
+               "mrays_s": round(float(sum(n_rays_per_launch)) / float(mean.sum()) / 1e3, 1)}
+        rec.update(extra)
+        out[name] = rec
+        log(f"aux {name}: {rec}")
+
+    def rays_with_bounces(view, W, H, nb_max, frames):
+        WH = W * H
+        c2w, ip = view.camera(W, H)
+        base = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(base, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=frames, max_bounce=max(nb_max, 1),
+                     device=True)
+        bufs, counts = [base.clone()], [WH]
+        cur = base
+        for b in range(nb_max):
+            eng.trace(cur, counts[-1], b, far, W, H, device=True)
+            n = eng.enqueue_bounce(cur, counts[-1], b, far, W, H, frames=frames, max_bounce=max(nb_max, 1),
+                                   device=True)
+            bufs.append(cur.clone())
+            counts.append(n)
+        torch.cuda.synchronize(dev)
+        return bufs, counts
+
+    def run(name, scene_fn, view, W, H, nb, extra_fn):
+        try:
+            t0 = time.time()
+            sc = scene_fn()
+            build_s = time.time() - t0
+            eng.upload(sc)
+            bufs, counts = rays_with_bounces(view, W, H, nb, 0)
+            info = torch.zeros(W * H * 16, dtype=torch.uint8, device=dev)
+            colors = np.zeros(W * H, tthip.COL_DTYPE)
+            colors["Data"][:, 3] = 1.0  # as the metric's step: info re-written at bounce 1 only
+            colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+            launches = [(lambda b=b: eng.trace(bufs[b], counts[b], b, far, W, H, info=info,
+                                               colors=colors_t if b > 0 else None, device=True,
+                                               asynchronous=True)) for b in range(nb + 1)]
+            ms = timed_launches(eng, launches, max(1, args.warmup), max(3, args.steps // 2))
+            pack(name, counts, ms, dict(extra_fn(sc), width=W, height=H, build_s=round(build_s, 1)))
+            del bufs, info, colors_t
+        except Exception as e:  # auxiliary: record, never lose the metric line
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+            log(f"aux {name} failed: {e}")
+
+    if "c3" in which:
+        run("c3_sponza_primary_plus_3_bounces_1080p", T.c2_sponza, T.C2_VIEW, 1920, 1080, 3,
+            lambda sc: {"tris": int(len(sc.tris))})
+    if "c4" in which:
+        run("c4_bistro_primary_plus_1_bounce_1080p", T.c4_bistro, T.C4_VIEW, 1920, 1080, 1,
+            lambda sc: {"unique_tris": int(len(sc.tris)), "instanced_tris": sc.meta["instanced_tris"],
+                        "unique_blas": 600, "instances": 2400, "cwbvh_nodes": int(len(sc.nodes))})
+    if "c5" in which:
+        run("c5_san_miguel_primary_4k", T.c5_san_miguel, T.C5_VIEW, 3840, 2160, 0,
+            lambda sc: {"tris": int(len(sc.tris)), "cwbvh_nodes": int(len(sc.nodes))})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +165,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather hit records to rank 0 after timing")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
+    ap.add_argument("--aux", default="c3,c4,c5",
+                    help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,c5; '' = none)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -185,6 +275,10 @@ def main():
         log(f"shadow: {ns} NEE rays {shadow['trace_ms']} ms/launch = {shadow['mrays_s']} Mrays/s, "
             f"{shadow['occluded']} occluded")
 
+    aux = None
+    if world == 1 and args.aux:
+        aux = aux_configs(torch, tthip, eng, dev, args, set(args.aux.split(",")))
+
     gather_ms = None
     if args.gather and world > 1:
         hits = rays[: WH * 48].view(WH, 48)[:, 32:48].contiguous()
@@ -256,7 +350,7 @@ def main():
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
                    "gather_ms": None if gather_ms is None else round(gather_ms, 3),
-                   "aux_shadow_nee": shadow},
+                   "aux_shadow_nee": shadow, "aux_configs": aux},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),

@@ -16,32 +16,9 @@ import kat_cases as K
 import oracle_ctypes as O
 import tthip
 
+from parity_util import CPU_THREADS, FAR, assert_same, trace_both
+
 pytestmark = pytest.mark.gpu
-FAR = 1000.0
-CPU_THREADS = 16
-
-
-def trace_both(engine, sc, rays, n, bounce, W, H, info=True, colors=None, flags=0, upload=True):
-    if upload:
-        engine.upload(sc)
-    rg, rc = rays.copy(), rays.copy()
-    ig = np.zeros((W * H, 4), np.uint32) if info else None
-    ic = np.zeros((W * H, 4), np.uint32) if info else None
-    s = engine.trace(rg, n, bounce, FAR, W, H, info=ig, colors=colors, flags=flags, stats=True)
-    st, cnt = O.trace(sc, rc, n, bounce, FAR, W, H, info=ic, colors=colors, flags=flags, counts=True,
-                      nthreads=CPU_THREADS)
-    assert st == 0
-    return rg, rc, ig, ic, s, cnt
-
-
-def assert_same(rg, rc, ig, ic, off, n):
-    hg, hc = rg["hits"][off:off + n], rc["hits"][off:off + n]
-    bad = np.nonzero((hg != hc).any(1))[0]
-    assert len(bad) == 0, f"{len(bad)} of {n} hit records differ, first {bad[:5]}: {hg[bad[:3]]} vs {hc[bad[:3]]}"
-    assert np.array_equal(rg, rc), "bytes outside the hit records must be untouched"
-    if ig is not None:
-        badi = np.nonzero((ig != ic).any(1))[0]
-        assert len(badi) == 0, f"{len(badi)} _PrimaryTriangleInfo texels differ"
 
 
 # ------------------------------------------------------------------ known answers

@@ -10,6 +10,7 @@ __global__ __launch_bounds__(256) void k(float* out, int iters) {
     float r[16];
     unsigned u[16];
     double d[16];
+    unsigned long long sm[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 16; i++) { r[i] = threadIdx.x + i; u[i] = threadIdx.x * 77 + i; d[i] = r[i]; }
     const float a = 1.0001f, b = 0.5f;
@@ -26,12 +27,32 @@ __global__ __launch_bounds__(256) void k(float* out, int iters) {
             if (OP == 7) asm volatile("v_fma_mix_f32 %0, %0, %1, %2 op_sel_hi:[0,1,0]" : "+v"(r[i]) : "v"(u[i]), "v"(b));
             if (OP == 8) asm volatile("v_rcp_f32 %0, %0" : "+v"(r[i]));
             if (OP == 9) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(u[i]));
+            if (OP == 10) asm volatile("v_max_f32 %0, %0, %1" : "+v"(r[i]) : "v"(a));
+            if (OP == 11) asm volatile("v_min_f32 %0, %0, %1" : "+v"(r[i]) : "v"(a));
+            if (OP == 12) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(r[i]) : "v"(a));
+            if (OP == 13) asm volatile("v_add_f32 %0, %0, %1" : "+v"(r[i]) : "v"(a));
+            if (OP == 14) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(r[i]) : "v"(a), "v"(b));
+            if (OP == 15) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r[i]) : "v"(a));
+            if (OP == 16) asm volatile("v_cmp_lt_f32 vcc, %0, %1" : : "v"(r[i]), "v"(a) : "vcc");
+            if (OP == 17) asm volatile("v_and_b32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 3) & 15]));
+            if (OP == 18) asm volatile("v_or_b32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 3) & 15]));
+            if (OP == 19) asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 3) & 15]));
+            if (OP == 20) asm volatile("v_cvt_f32_u32 %0, %1" : "=v"(r[i]) : "v"(u[i]));
+            if (OP == 21) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(a), "v"(b));
+            if (OP == 22) asm volatile("v_mov_b32 %0, %1" : "=v"(r[i]) : "v"(r[(i + 1) & 15]));
+            if (OP == 23) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(u[i]) : "v"(u[(i + 3) & 15]));
+            if (OP == 24) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(d[i]) : "v"(d[(i + 1) & 15]));
+            if (OP == 25) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(d[i]) : "v"(d[(i + 1) & 15]));
+            if (OP == 26) asm volatile("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(sm[i & 3]) : "v"(r[i]), "v"(a));
+            if (OP == 27) asm volatile("v_sub_f32 %0, %1, %0" : "+v"(r[i]) : "v"(a));
+            if (OP == 28) asm volatile("v_max_i32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 3) & 15]));
+            if (OP == 29) asm volatile("v_cvt_pk_f32_fp8 %0, %1" : "=v"(d[i]) : "v"(u[i]));
         }
     }
     float s = 0;
 #pragma unroll
     for (int i = 0; i < 16; i++) s += r[i] + (float)u[i] + (float)d[i];
-    out[blockIdx.x * 256 + threadIdx.x] = s;
+    out[blockIdx.x * 256 + threadIdx.x] = s + (float)(sm[0] ^ sm[1] ^ sm[2] ^ sm[3]);
 }
 
 template <int OP>
@@ -62,5 +83,25 @@ int main() {
     run<7>("v_fma_mix_f32", out, p.multiProcessorCount, 1);
     run<8>("v_rcp_f32", out, p.multiProcessorCount, 1);
     run<9>("v_bfe_u32", out, p.multiProcessorCount, 1);
+    run<10>("v_max_f32", out, p.multiProcessorCount, 1);
+    run<11>("v_min_f32", out, p.multiProcessorCount, 1);
+    run<12>("v_mul_f32", out, p.multiProcessorCount, 1);
+    run<13>("v_add_f32", out, p.multiProcessorCount, 1);
+    run<14>("v_fmac_f32", out, p.multiProcessorCount, 1);
+    run<15>("v_cndmask_b32", out, p.multiProcessorCount, 1);
+    run<16>("v_cmp_lt_f32 (vcc)", out, p.multiProcessorCount, 1);
+    run<17>("v_and_b32", out, p.multiProcessorCount, 1);
+    run<18>("v_or_b32", out, p.multiProcessorCount, 1);
+    run<19>("v_add_u32", out, p.multiProcessorCount, 1);
+    run<20>("v_cvt_f32_u32", out, p.multiProcessorCount, 1);
+    run<21>("v_med3_f32", out, p.multiProcessorCount, 1);
+    run<22>("v_mov_b32", out, p.multiProcessorCount, 1);
+    run<23>("v_lshl_or_b32", out, p.multiProcessorCount, 1);
+    run<24>("v_pk_mul_f32", out, p.multiProcessorCount, 1);
+    run<25>("v_pk_add_f32", out, p.multiProcessorCount, 1);
+    run<26>("v_cmp_lt_f32_e64 (sgpr)", out, p.multiProcessorCount, 1);
+    run<27>("v_sub_f32", out, p.multiProcessorCount, 1);
+    run<28>("v_max_i32", out, p.multiProcessorCount, 1);
+    run<29>("v_cvt_pk_f32_fp8", out, p.multiProcessorCount, 1);
     return 0;
 }

@@ -276,6 +276,142 @@ tt_status tt_synth_sponza(uint64_t seed, uint32_t n_tris, tt_synth_mesh** out) {
     return TT_OK;
 }
 
+// Flat ground grid of nu x nv quads over [x0,x1] x [z0,z1] at y = 0 with a gentle camber
+// (C4's street plane). Material 0.
+tt_status tt_synth_ground(double x0, double x1, double z0, double z1, uint32_t nu, uint32_t nv,
+                          tt_synth_mesh** out) {
+    if (!out || !nu || !nv || !(x1 > x0) || !(z1 > z0)) return TT_ERR_INVALID_ARG;
+    tt_synth_mesh* m = new (std::nothrow) tt_synth_mesh();
+    if (!m) return TT_ERR_OOM;
+    Builder b{m};
+    b.grid((int)nu, (int)nv, 0, [&](double u, double v) {
+        return d3(x0 + (x1 - x0) * u, 0.02 * std::sin(17.0 * u) * std::cos(13.0 * v), z0 + (z1 - z0) * v);
+    });
+    *out = m;
+    return TT_OK;
+}
+
+// C5 San-Miguel-shaped courtyard: a ~44 x 14 x 32 m patio closed on three
+// sides by two-storey arcades (walls, fluted columns, arches, balcony slabs), paved floor,
+// tables and chairs, and ~60% foliage-like small triangles (tree crowns, potted plants, wall
+// ivy), padded to exactly n_tris. Tessellation of the architecture scales with n_tris so the
+// foliage share stays about the same. Materials: 0 floor, 1 walls, 2 columns, 3 arches,
+// 4 slabs, 5 furniture, 6 trunks, 7 foliage.
+tt_status tt_synth_san_miguel(uint64_t seed, uint32_t n_tris, tt_synth_mesh** out) {
+    if (!out || n_tris < 1000000) return TT_ERR_INVALID_ARG;
+    tt_synth_mesh* m = new (std::nothrow) tt_synth_mesh();
+    if (!m) return TT_ERR_OOM;
+    Builder b{m};
+    Rng r(seed);
+    const double PI = 3.141592653589793;
+    const double X0 = -22, X1 = 22, Z0 = -16, Z1 = 16, H = 14;
+    // ~730k architecture triangles at s = 1; aim for ~40% architecture
+    const double s = std::sqrt(0.4 * (double)n_tris / 730000.0);
+    auto res = [&](double base) { return std::max(2, (int)std::lround(base * s)); };
+    // paved floor with slightly raised cobbles
+    b.grid(res(400), res(300), 0, [&](double u, double v) {
+        return d3(X0 + (X1 - X0) * u, 0.004 * std::sin(310 * u) * std::sin(233 * v), Z0 + (Z1 - Z0) * v);
+    });
+    auto wall = [&](D3 o, D3 du, D3 dv, D3 nrm, int nu, int nv) {
+        b.grid(nu, nv, 1, [&](double u, double v) {
+            const double relief = 0.015 * std::sin(u * 240.0) * std::sin(v * 90.0);
+            return add(add(add(o, scl(du, u)), scl(dv, v)), scl(nrm, relief));
+        });
+    };
+    wall(d3(X0, 0, Z1), d3(0, H, 0), d3(X1 - X0, 0, 0), d3(0, 0, -1), res(100), res(300));
+    wall(d3(X0, 0, Z0), d3(0, H, 0), d3(0, 0, Z1 - Z0), d3(1, 0, 0), res(100), res(220));
+    wall(d3(X1, 0, Z0), d3(0, 0, Z1 - Z0), d3(0, H, 0), d3(-1, 0, 0), res(220), res(100));
+    // arcades 4 m deep along the back (z) and both sides (x): slabs, columns, arches
+    b.box(d3(X0, 6.5, Z1 - 4), d3(X1, 6.9, Z1), res(10), 4);
+    b.box(d3(X0, 6.5, Z0), d3(X0 + 4, 6.9, Z1 - 4), res(10), 4);
+    b.box(d3(X1 - 4, 6.5, Z0), d3(X1, 6.9, Z1 - 4), res(10), 4);
+    struct Col { double x, z; };
+    std::vector<Col> cols;
+    for (int c = 0; c < 12; c++) cols.push_back(Col{X0 + 2.0 + 3.636 * c, Z1 - 4});
+    for (int c = 0; c < 8; c++) cols.push_back(Col{X0 + 4, Z0 + 2.0 + 3.5 * c});
+    for (int c = 0; c < 8; c++) cols.push_back(Col{X1 - 4, Z0 + 2.0 + 3.5 * c});
+    const int nseg = res(32), nring = res(40);
+    for (int fl = 0; fl < 2; fl++) {
+        const double y0 = fl == 0 ? 0.0 : 6.9, y1 = fl == 0 ? 6.5 : 13.2, rad = fl == 0 ? 0.34 : 0.27;
+        for (const Col& c : cols) {
+            b.grid(nseg, nring, 2, [&](double u, double v) {
+                const double a = 2 * PI * u, rr = rad * (1.0 + 0.05 * std::cos(12 * a));
+                return d3(c.x + rr * std::cos(a), y0 + (y1 - y0) * v, c.z + rr * std::sin(a));
+            });
+        }
+        for (size_t k = 0; k + 1 < cols.size(); k++) {
+            const Col a = cols[k], c = cols[k + 1];
+            const double dx = c.x - a.x, dz = c.z - a.z, len = std::sqrt(dx * dx + dz * dz);
+            if (len > 4.0) continue;  // no arch across the corner
+            const double R = 0.5 * len, ay = y1 - R;
+            b.grid(res(48), res(16), 3, [&](double u, double v) {
+                const double th = PI * u, ph = 2 * PI * v, rt = 0.18, rr = R + rt * std::cos(ph);
+                const double along = R - rr * std::cos(th);
+                return d3(a.x + dx / len * along, ay + rr * std::sin(th) * 0.85, a.z + dz / len * along + rt * std::sin(ph));
+            });
+        }
+    }
+    // furniture: 30 tables (top + leg) with four chairs each
+    for (int t = 0; t < 30; t++) {
+        const double tx = r.uni(X0 + 6, X1 - 6), tz = r.uni(Z0 + 2, Z1 - 6);
+        b.box(d3(tx - 0.45, 0.72, tz - 0.45), d3(tx + 0.45, 0.76, tz + 0.45), res(8), 5);
+        b.box(d3(tx - 0.04, 0.0, tz - 0.04), d3(tx + 0.04, 0.72, tz + 0.04), res(4), 5);
+        for (int c = 0; c < 4; c++) {
+            const double a = PI / 2 * c + r.uni(-0.3, 0.3), cx = tx + 0.75 * std::cos(a), cz = tz + 0.75 * std::sin(a);
+            b.box(d3(cx - 0.2, 0.42, cz - 0.2), d3(cx + 0.2, 0.46, cz + 0.2), res(5), 5);
+            b.box(d3(cx - 0.2, 0.46, cz - 0.2), d3(cx + 0.2, 0.95, cz - 0.16), res(5), 5);
+        }
+    }
+    // trees: trunks now, crowns later with the leaves
+    struct Tree { double x, z, cy, rx, ry; };
+    std::vector<Tree> trees;
+    for (int t = 0; t < 10; t++) {
+        Tree tr{r.uni(X0 + 7, X1 - 7), r.uni(Z0 + 3, Z1 - 7), r.uni(6.0, 8.5), r.uni(2.5, 4.0), r.uni(2.0, 3.0)};
+        trees.push_back(tr);
+        b.grid(res(24), res(24), 6, [&](double u, double v) {
+            const double a = 2 * PI * u, rr = 0.25 * (1.2 - 0.4 * v);
+            return d3(tr.x + rr * std::cos(a), (tr.cy - 0.5 * tr.ry) * v, tr.z + rr * std::sin(a));
+        });
+    }
+    if (b.ntri() >= n_tris) {
+        delete m;
+        return TT_ERR_INVALID_ARG;
+    }
+    // foliage: 70% tree crowns, 15% potted plants along the arcades, 15% ivy on the walls
+    const size_t nleaf = n_tris - b.ntri();
+    auto leaf = [&](D3 c, double size) {
+        const D3 e1 = nrmz(d3(r.normal(), r.normal(), r.normal()));
+        const D3 e2 = nrmz(crs(e1, nrmz(d3(r.normal(), r.normal(), r.normal()))));
+        const D3 p0 = c, p1 = add(c, scl(e1, size)), p2 = add(c, add(scl(e1, 0.5 * size), scl(e2, 0.6 * size)));
+        const D3 n = nrmz(crs(sub(p1, p0), sub(p2, p0)));
+        const int32_t a = b.vert(p0, n, 0, 0), bb = b.vert(p1, n, 1, 0), cc = b.vert(p2, n, 0, 1);
+        b.tri(a, bb, cc, 7);
+    };
+    for (size_t t = 0; t < nleaf; t++) {
+        const double kind = r.u01();
+        const double size = std::min(0.25, r.lognormal(0.05, 0.5));
+        double dx, dy, dz;
+        do {
+            dx = r.uni(-1, 1); dy = r.uni(-1, 1); dz = r.uni(-1, 1);
+        } while (dx * dx + dy * dy + dz * dz > 1.0);
+        if (kind < 0.70) {
+            const Tree& tr = trees[t % trees.size()];
+            leaf(d3(tr.x + tr.rx * dx, tr.cy + tr.ry * dy, tr.z + tr.rx * dz), size);
+        } else if (kind < 0.85) {
+            const int pot = (int)(t % cols.size());
+            leaf(d3(cols[pot].x + 0.8 + 0.5 * dx, 0.9 + 0.5 * dy, cols[pot].z - 0.8 + 0.5 * dz), size);
+        } else {
+            const int w = (int)(t % 3);
+            const double u = r.u01(), v = r.u01() * 0.85, off = 0.05 + 0.1 * r.u01();
+            if (w == 0) leaf(d3(X0 + (X1 - X0) * u, H * v, Z1 - off), size);
+            else if (w == 1) leaf(d3(X0 + off, H * v, Z0 + (Z1 - Z0) * u), size);
+            else leaf(d3(X1 - off, H * v, Z0 + (Z1 - Z0) * u), size);
+        }
+    }
+    *out = m;
+    return TT_OK;
+}
+
 // C4 building block: one Bistro-shaped unique object (a facade/prop) with n_tris triangles in
 // its own object space (about 1-12 m), for two-level instancing scenes.
 tt_status tt_synth_prop(uint64_t seed, uint32_t n_tris, tt_synth_mesh** out) {

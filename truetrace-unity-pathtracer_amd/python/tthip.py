@@ -169,7 +169,8 @@ HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_des
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
-                 "tt_synth_prop", "tt_synth_mesh_view", "tt_synth_mesh_free", "tt_synth_mesh_from_arrays"]
+                 "tt_synth_prop", "tt_synth_ground", "tt_synth_san_miguel", "tt_synth_mesh_view", "tt_synth_mesh_free",
+                 "tt_synth_mesh_from_arrays"]
 
 
 def scene_lib():
@@ -200,6 +201,8 @@ def scene_lib():
         L.tt_synth_soup.argtypes = [C.c_uint64, u32, C.c_float, C.c_float, C.POINTER(vp)]
         L.tt_synth_sponza.argtypes = [C.c_uint64, u32, C.POINTER(vp)]
         L.tt_synth_prop.argtypes = [C.c_uint64, u32, C.POINTER(vp)]
+        L.tt_synth_ground.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, u32, u32, C.POINTER(vp)]
+        L.tt_synth_san_miguel.argtypes = [C.c_uint64, u32, C.POINTER(vp)]
         L.tt_synth_mesh_view.argtypes = [vp, C.POINTER(MeshInput)]
         L.tt_synth_mesh_free.argtypes = [vp]
         L.tt_synth_mesh_free.restype = None
@@ -207,7 +210,7 @@ def scene_lib():
         L.tt_synth_mesh_from_arrays.restype = vp
         for s in ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_scene_assemble", "tt_scene_build_get_info",
                   "tt_scene_build_copy", "tt_bvh2_build", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
-                  "tt_synth_prop", "tt_synth_mesh_view"]:
+                  "tt_synth_prop", "tt_synth_ground", "tt_synth_san_miguel", "tt_synth_mesh_view"]:
             getattr(L, s).restype = i32
         _SCENE = L
     return _SCENE
@@ -334,6 +337,18 @@ class Mesh:
     def prop(cls, seed: int, n_tris: int) -> "Mesh":
         h = C.c_void_p()
         cls._check(scene_lib().tt_synth_prop(seed, n_tris, C.byref(h)), "tt_synth_prop")
+        return cls(h.value)
+
+    @classmethod
+    def ground(cls, x0: float, x1: float, z0: float, z1: float, nu: int, nv: int) -> "Mesh":
+        h = C.c_void_p()
+        cls._check(scene_lib().tt_synth_ground(x0, x1, z0, z1, nu, nv, C.byref(h)), "tt_synth_ground")
+        return cls(h.value)
+
+    @classmethod
+    def san_miguel(cls, seed: int = 0x5A4E4D, n_tris: int = 10_000_000) -> "Mesh":
+        h = C.c_void_p()
+        cls._check(scene_lib().tt_synth_san_miguel(seed, n_tris, C.byref(h)), "tt_synth_san_miguel")
         return cls(h.value)
 
     @classmethod
