@@ -19,6 +19,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import sys
 import time
 
@@ -315,7 +316,9 @@ def main():
         cpu = {"value": round(done / tcpu / 1e6, 3), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
                "sample": f"full step workload ({WH} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
                          f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {nthreads} threads; "
-                         f"C# scalar baseline not run: no .NET runtime on the box"}
+                         f"C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
+                         + ("not run: no .NET runtime (dotnet) on the box" if shutil.which("dotnet") is None
+                            else "not run by bench.py: see tools/dump_scene_raw.py")}
         log(f"cpu baseline {cpu['value']} Mrays/s ({reps} reps, {tcpu:.1f}s)")
 
     # fabric traffic per launch from the round's separate rocprofv3 --pmc pass of this same command

@@ -82,6 +82,13 @@ namespace TrueTrace.Hip
         // GlobalColors (ColData, 64 B), NEEPosA (float4 per pixel); the last three nullable.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_shadow(IntPtr ctx, ref TTShadowParams p,
             void* shadowRays, float* visibility, void* globalColors, float* neePos, out TTStats stats);
+        // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload_alpha_atlas(IntPtr ctx, byte* texels,
+            uint width, uint height);
+        // RefitTLAS: MeshAABBs as {BBMax.xyz, BBMin.xyz} per mesh; flags: TT_TRACE_DEVICE_PTRS / ASYNC.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_tlas_refit(IntPtr ctx, uint nTlasNodes, float* meshAabbs,
+            uint nMesh, uint flags);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_read_nodes(IntPtr ctx, uint first, uint count, void* nodes);
         [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
     }
 
@@ -140,6 +147,22 @@ namespace TrueTrace.Hip
             fixed (float* nee = neePos)
                 Check(Native.tt_trace_shadow(m_ctx, ref p, r, vis, col, nee, out s));
             return s;
+        }
+
+        /// The _AlphaAtlas binding of SetMeshTraceBuffers (AssetManager.cs:75-88): R8 texels, once
+        /// per scene change, before tracing scenes with Cutout materials.
+        public unsafe void SetAlphaAtlas(byte[] texels, int width, int height)
+        {
+            fixed (byte* t = texels)
+                Check(Native.tt_scene_upload_alpha_atlas(m_ctx, t, (uint)width, (uint)height));
+        }
+
+        /// AssetManager.RefitTLAS(Boxes, cmd) (AssetManager.cs:1473-1548): re-quantizes the TLAS
+        /// nodes in HBM from this frame's MeshAABBs (6 floats per mesh: BBMax, BBMin).
+        public unsafe void RefitTLAS(float[] meshAabbs, int nTlasNodes)
+        {
+            fixed (float* b = meshAabbs)
+                Check(Native.tt_tlas_refit(m_ctx, (uint)nTlasNodes, b, (uint)(meshAabbs.Length / 6), 0));
         }
 
         void Check(TTStatus st)

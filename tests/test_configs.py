@@ -61,3 +61,28 @@ def test_generators_reject_bad_sizes():
         tthip.Mesh.san_miguel(1, 1000)
     with pytest.raises(tthip.TTError):
         tthip.Mesh.ground(1.0, 0.0, 0.0, 1.0, 4, 4)
+
+
+def test_raw_dump_for_csharp_baseline(tmp_path):
+    """tools/dump_scene_raw.py writes the byte-exact buffers ScalarTraversal.cs reads, and the
+    word offsets that file hard-codes match the C ABI layouts."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import dump_scene_raw as D
+
+    sc, rays, ref = D.dump(str(tmp_path), "c1", 32, 24, threads=2)
+    assert (tmp_path / "nodes.bin").stat().st_size == 80 * len(sc.nodes)
+    assert (tmp_path / "tris.bin").stat().st_size == 88 * len(sc.tris)
+    assert (tmp_path / "meshdata.bin").stat().st_size == 88 * len(sc.meshdata)
+    assert (tmp_path / "materials.bin").stat().st_size == 252 * len(sc.materials)
+    hits = np.fromfile(tmp_path / "expected_hits.bin", np.uint32).reshape(-1, 4)
+    assert np.array_equal(hits, ref["hits"][: 32 * 24])
+    assert (tmp_path / "params.txt").read_text().split()[:2] == [str(32 * 24), "0"]
+    # word offsets used by ScalarTraversal.cs
+    md, mat, tri = tthip.MESH_DTYPE, tthip.MAT_DTYPE, tthip.TRI_DTYPE
+    assert [md.fields[k][1] // 4 for k in ("TriOffset", "NodeOffset", "MaterialOffset", "mesh_data_bvh_offsets")] == \
+        [16, 17, 18, 19]
+    assert mat.fields["Tag"][1] // 4 == 23 and mat.fields["MatType"][1] // 4 == 25 and mat.itemsize == 63 * 4
+    assert tri.fields["MatDat"][1] // 4 == 21 and tri.itemsize == 22 * 4
