@@ -14,7 +14,55 @@
 //  * the per-ray visit order, the culling distance and the strict t < best.t acceptance are
 //    exactly the reference's, so t / primID / instID are bit-identical to the oracle.
 // Numerics follow include/truetrace_hip.h (compiled with -ffp-contract=off).
-#include "tt_traverse.h"
+#include "tt_wide.h"
+
+namespace {
+// :229-241 + set() CommonData.cginc:430-434: the hit record and _PrimaryTriangleInfo of a finished
+// ray (wr = the world-space ray, ray2). Returns whether the ray hit something.
+template <int INFO>
+__device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_index, uint32_t pix, float col_w,
+                                             const Best& best, const LaneRay& wr) {
+    tt_ray_data* R = A.rays + ray_index;
+    if (INFO != 0) {
+        const uint32_t tx = pix % A.width, ty = pix / A.width;
+        if (ty < A.height) {
+            uint4 o;
+            bool write = false;
+            if (INFO == 1) {
+                const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to),
+                               __float_as_uint(best.u), __float_as_uint(best.v));
+                write = true;
+            } else {
+                const float w = col_w;
+                if (w == -1.0f || (float)A.bounce == w) {
+                    write = true;
+                    const bool miss = best.t == A.far_plane;
+                    if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
+                        const int32_t to = A.mesh[best.mesh_id].TriOffset;
+                        o.x = (uint32_t)best.mesh_id;
+                        o.y = (uint32_t)(best.tri_id - to);
+                        o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+                    } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
+                        o.x = __float_as_uint(wr.dx);
+                        o.y = __float_as_uint(wr.dy);
+                        o.z = __float_as_uint(wr.dz);
+                    } else {
+                        o.x = __float_as_uint(wr.dx * best.t + wr.ox);
+                        o.y = __float_as_uint(wr.dy * best.t + wr.oy);
+                        o.z = __float_as_uint(wr.dz * best.t + wr.oz);
+                    }
+                    o.w = miss ? 1u : 0u;
+                }
+            }
+            if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+        }
+    }
+    const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
+    reinterpret_cast<uint4*>(R)[2] = make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+    return best.t != A.far_plane;
+}
+}  // namespace
 
 
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
@@ -82,54 +130,16 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
     };
 
-    // :229-241 + set() CommonData.cginc:430-434: hit record and _PrimaryTriangleInfo of a finished ray
+    // :229-241: the finished ray's hit record and _PrimaryTriangleInfo
     auto finish_ray = [&]() {
-        tt_ray_data* R = A.rays + ray_index;
-        if (INFO != 0) {
-            const uint32_t tx = pix % A.width, ty = pix / A.width;
-            if (ty < A.height) {
-                uint4 o;
-                bool write = false;
-                if (INFO == 1) {
-                    const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                    o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to),
-                                   __float_as_uint(best.u), __float_as_uint(best.v));
-                    write = true;
-                } else {
-                    const float w = col_w;
-                    if (w == -1.0f || (float)A.bounce == w) {
-                        const LaneRay wr = world_ray();
-                        write = true;
-                        const bool miss = best.t == A.far_plane;
-                        if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
-                            const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                            o.x = (uint32_t)best.mesh_id;
-                            o.y = (uint32_t)(best.tri_id - to);
-                            o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-                        } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
-                            o.x = __float_as_uint(wr.dx);
-                            o.y = __float_as_uint(wr.dy);
-                            o.z = __float_as_uint(wr.dz);
-                        } else {
-                            o.x = __float_as_uint(wr.dx * best.t + wr.ox);
-                            o.y = __float_as_uint(wr.dy * best.t + wr.oy);
-                            o.z = __float_as_uint(wr.dz * best.t + wr.oz);
-                        }
-                        o.w = miss ? 1u : 0u;
-                    }
-                }
-                if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
-            }
-        }
-        const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-        reinterpret_cast<uint4*>(R)[2] =
-            make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
-        if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
+        const bool hit = write_record<INFO>(A, ray_index, pix, col_w, best, world_ray());
+        if (STATS) c_hits += hit ? 1u : 0u;
 #ifdef TT_DIAG_RAYS
         if (A.diag_times)
             reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
                 make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
 #endif
+        (void)hit;
     };
 #ifdef TT_DIAG_TIMES
     const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
@@ -140,9 +150,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
         const bool pool_dry = !more && pool_next >= pool_end;
+        // the queue is dry and the live rays fit in 2-lane groups: cooperative drain (tt_wide.h)
+        const bool to_wide = TT_WIDE && pool_dry && n_idle < TT_WAVE && TT_WAVE - n_idle <= TT_WIDE_ENTER;
 #if TT_DEFER_FINISH
         // finished rays write their records in batches, right before their lanes are refilled
-        if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry)) {
+        if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry) || to_wide) {
             if (pending) {
                 finish_ray();
                 pending = false;
@@ -150,6 +162,21 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
 #endif
         if (n_idle == TT_WAVE && pool_dry) break;
+#if TT_WIDE
+        if (to_wide) {
+            WideState st{ray, wray, best, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset,
+                         mesh_id, Reps, ray_index, pix, col_w, tid, gtid, active};
+            regroup<2>(st, __ballot(active), lane);
+            auto finish_wide = [&](const WideState& w) {
+                const bool hit = write_record<INFO>(A, w.ray_index, w.pix, w.col_w, w.best, w.wray);
+                if (STATS) c_hits += hit ? 1u : 0u;
+            };
+            wide_phase<STATS, MATCHECK, 2>(A, st, s_stack, spill, spill_stride, nodes, tris, lane,
+                                           Counters{c_nodes, c_tris, c_blas, c_acc, c_hits, c_reps, c_ovf},
+                                           finish_wide);
+            break;
+        }
+#endif
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest
             const uint32_t avail = pool_end - pool_next;

@@ -204,10 +204,16 @@ __device__ __forceinline__ float2 base_uv(const MatView& M, int32_t tri_id, floa
     return make_float2(t0.x * w + t1.x * u + t2.x * v, t0.y * w + t1.y * u + t2.y * v);
 }
 
+// One triangle against the ray: `cand` = the reference's geometric accept (u, v range and
+// 0 < t < best_t), `accept` = cand and the material checks passed (the record is taken).
+struct TriCand {
+    float t, u, v;
+    bool cand, accept;
+};
 template <bool MATCHECK>
-__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
-                                                   int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
-                                                   const LaneRay& r, Best& best) {
+__device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
+                                                      int32_t tri_id, int32_t mat_offset, const LaneRay& r,
+                                                      float best_t) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
     const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
@@ -227,27 +233,39 @@ __device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, 
     const float qz = fma_(sx, e1y, -(sy * e1x));
     const float v = f * fma_(r.dz, qz, fma_(r.dy, qy, r.dx * qx));
     const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
-    const bool cand = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best.t);
-    bool accept = cand;
-    if (MATCHECK && accept) {
+    TriCand R;
+    R.t = t;
+    R.u = u;
+    R.v = v;
+    R.cand = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best_t);
+    R.accept = R.cand;
+    if (MATCHECK && R.accept) {
         // _Materials[MatOffset + MatDat]; an out-of-range StructuredBuffer read returns zeros in
         // D3D (no flags, MatType 0). Cutout alpha test (:35-40), then Invisible at CurBounce == 0 (:48).
         const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
         const uint32_t w = mi < M.n_mat ? M.word[mi] : 0u;
         if ((w >> TT_MATWORD_CUTOUT) & 1u) {
             const CutoutMat cm = M.cut[mi];
-            if (sample_linear(M, align_uv(base_uv(M, tri_id, u, v), cm)) < cm.cutoff) accept = false;
+            if (sample_linear(M, align_uv(base_uv(M, tri_id, u, v), cm)) < cm.cutoff) R.accept = false;
         }
-        if (bounce0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) accept = false;
+        if (bounce0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) R.accept = false;
     }
-    if (accept) {
-        best.t = t;
-        best.u = u;
-        best.v = v;
+    return R;
+}
+
+template <bool MATCHECK>
+__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
+                                                   int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
+                                                   const LaneRay& r, Best& best) {
+    const TriCand c = triangle_candidate<MATCHECK>(tris, M, bounce0, tri_id, mat_offset, r, best.t);
+    if (c.accept) {
+        best.t = c.t;
+        best.u = c.u;
+        best.v = c.v;
         best.mesh_id = mesh_id;
         best.tri_id = tri_id;
     }
-    return cand;  // counted as an "accept" (candidate passed the t test) before the material check
+    return c.cand;  // counted as an "accept" (candidate passed the t test) before the material check
 }
 
 // ------------------------------------------------------------------ ray scheduler
