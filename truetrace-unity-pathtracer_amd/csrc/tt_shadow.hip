@@ -20,7 +20,14 @@ template <bool MATCHECK>
 __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, int32_t tri_id,
                                                 int32_t mat_offset, const LaneRay& r, float max_distance) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
-    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
+    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u);
+    uint2 c;
+    if (MATCHECK) {
+        c = buffer_load8(tris, to + 32u);
+    } else {
+        c.x = buffer_load4(tris, to + 32u);
+        c.y = 0u;
+    }
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
     const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
     const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);

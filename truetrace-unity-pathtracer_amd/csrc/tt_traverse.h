@@ -77,8 +77,26 @@ __device__ __forceinline__ uint4 buffer_load16(__amdgpu_buffer_rsrc_t r, uint32_
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ uint32_t node_offset(uint32_t i) { return (i + (i << 2)) << 4; }  // i * 80
-__device__ __forceinline__ uint32_t tri_offset(uint32_t i) { return (i + (i << 1)) << 4; }   // i * 48
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 buffer_load8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint32_t buffer_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+// i * 80 and i * 48 as shift-adds: written plainly, LLVM folds them back into v_mul_lo_u32, a
+// quarter-rate instruction on the traversal's critical path
+__device__ __forceinline__ uint32_t node_offset(uint32_t i) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 2, %1\n\tv_lshlrev_b32 %0, 4, %0" : "=&v"(r) : "v"(i));
+    return r;
+}
+__device__ __forceinline__ uint32_t tri_offset(uint32_t i) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 1, %1\n\tv_lshlrev_b32 %0, 4, %0" : "=&v"(r) : "v"(i));
+    return r;
+}
 
 // cwbvh_node_intersect — CommonData.cginc:641-707
 __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n1, const uint4 n2,
@@ -215,7 +233,15 @@ __device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tri
                                                       int32_t tri_id, int32_t mat_offset, const LaneRay& r,
                                                       float best_t) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
-    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u), c = buffer_load16(tris, to + 32u);
+    // 36 B of positions (+ MatDat when materials are checked): two 16-B loads and a 4- or 8-B one
+    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u);
+    uint2 c;
+    if (MATCHECK) {
+        c = buffer_load8(tris, to + 32u);
+    } else {
+        c.x = buffer_load4(tris, to + 32u);
+        c.y = 0u;
+    }
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
     const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
     const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);
