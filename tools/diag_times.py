@@ -30,6 +30,11 @@ for b in (0, 1):
     print(f"bounce {b}: waves {used.sum()} kernel {s.kernel_ms*1e3:.0f}us span {span:.0f}us start spread {(st.max()-t0)/100:.1f}us "
           f"wave life mean {life.mean():.0f} min {life.min():.0f} p10 {np.percentile(life,10):.0f} p50 {np.percentile(life,50):.0f} p90 {np.percentile(life,90):.0f} max {life.max():.0f}us; "
           f"rays/wave mean {n.mean():.0f} min {n.min()} max {n.max()}")
-    print(f"   shader clock {np.median(cyc / ((en - st) * 10.0)):.3f} GHz (memtime ticks / memrealtime)")
+    wide = cyc > 0  # slot 3: memrealtime at entry into the cooperative drain phase (tt_wide.h)
+    if wide.any():
+        we = (cyc[wide] - t0) / 100.0
+        dur = (en[wide] - cyc[wide]) / 100.0
+        print(f"   drain phase: {wide.sum()} waves; entry percentiles", [round(float(np.percentile(we, q))) for q in (1, 10, 50, 90, 99)],
+              "us; time in drain p50/p90/max", [round(float(np.percentile(dur, q))) for q in (50, 90, 100)], "us")
     end_rel = (en - t0) / 100.0
     print("   end-time percentiles", [round(float(np.percentile(end_rel, q))) for q in (1, 10, 25, 50, 75, 90, 99, 100)])

@@ -143,7 +143,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     };
 #ifdef TT_DIAG_TIMES
     const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
-    const uint64_t c_begin = __builtin_amdgcn_s_memtime();
+    uint64_t t_wide = 0;  // when the wave entered the cooperative drain phase (0: never)
 #endif
     while (true) {
         // ---------------------------------------------------------------- refill
@@ -164,6 +164,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         if (n_idle == TT_WAVE && pool_dry) break;
 #if TT_WIDE
         if (to_wide) {
+#ifdef TT_DIAG_TIMES
+            t_wide = __builtin_amdgcn_s_memrealtime();
+#endif
             WideState st{ray, wray, best, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset,
                          mesh_id, Reps, ray_index, pix, col_w, tid, gtid, active};
             regroup<2>(st, __ballot(active), lane);
@@ -426,7 +429,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             A.diag_times[4 * w + 0] = t_begin;
             A.diag_times[4 * w + 1] = t_end;
             A.diag_times[4 * w + 2] = rays_done;
-            A.diag_times[4 * w + 3] = __builtin_amdgcn_s_memtime() - c_begin;  // shader clock ticks
+            A.diag_times[4 * w + 3] = t_wide;
         }
     }
 #endif
