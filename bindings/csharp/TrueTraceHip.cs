@@ -60,6 +60,20 @@ namespace TrueTrace.Hip
         public TTTraceFlags flags;
     }
 
+    [StructLayout(LayoutKind.Sequential)]
+    public unsafe struct TTBlasRefitParams
+    {
+        public uint meshIndex;     // _MeshData record: TriOffset, NodeOffset, BLAS root
+        public uint nTris;
+        public uint nVertices;
+        public uint vertexStride;  // VertexBuffer stride / 4; position at +0, normal at +3
+        public fixed float transform[16];
+        public uint flags;
+    }
+
+    /// Column-major 4x4 (the memory order of UnityEngine.Matrix4x4: m00, m10, m20, m30, m01, ...).
+    public struct Matrix4x4Floats { public float[] m; }
+
     public static class Native
     {
         const string Lib = "truetrace_hip";
@@ -89,6 +103,9 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern unsafe TTStatus tt_tlas_refit(IntPtr ctx, uint nTlasNodes, float* meshAabbs,
             uint nMesh, uint flags);
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_read_nodes(IntPtr ctx, uint first, uint count, void* nodes);
+        // ParentObject.RefitMesh: vertex buffer (floats), sharedMesh.triangles, CWBVHIndicesBufferInverted.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_blas_refit(IntPtr ctx, ref TTBlasRefitParams p, float* vertices,
+            int* indices, int* leafOfTriangle);
         [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
     }
 
@@ -163,6 +180,20 @@ namespace TrueTrace.Hip
         {
             fixed (float* b = meshAabbs)
                 Check(Native.tt_tlas_refit(m_ctx, (uint)nTlasNodes, b, (uint)(meshAabbs.Length / 6), 0));
+        }
+
+        /// ParentObject.RefitMesh (ParentObject.cs:750-917) for a skinned / deformable mesh: pass the
+        /// vertex buffer read back from SkinnedMeshRenderer.GetVertexBuffer (floats), the mesh's
+        /// triangles, CWBVHIndicesBufferInverted and the "Transform" matrix; RefitTLAS follows.
+        public unsafe void RefitMesh(int meshIndex, float[] vertices, int vertexStride, int[] triangles,
+                                     int[] leafOfTriangle, Matrix4x4Floats transform)
+        {
+            var p = new TTBlasRefitParams { meshIndex = (uint)meshIndex, nTris = (uint)(triangles.Length / 3),
+                                            nVertices = (uint)(vertices.Length / vertexStride),
+                                            vertexStride = (uint)vertexStride, flags = 0 };
+            for (int i = 0; i < 16; i++) p.transform[i] = transform.m[i];
+            fixed (float* v = vertices) fixed (int* t = triangles) fixed (int* l = leafOfTriangle)
+                Check(Native.tt_blas_refit(m_ctx, ref p, v, t, l));
         }
 
         void Check(TTStatus st)

@@ -256,6 +256,38 @@ tt_status tt_scene_upload_alpha_atlas(tt_ctx* ctx, const uint8_t* texels, uint32
 tt_status tt_tlas_refit(tt_ctx* ctx, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh,
                         uint32_t flags);
 
+/* Per-frame BLAS refit of a deforming or skinned mesh (row f4), replacing ParentObject.RefitMesh
+ * (ParentObject.cs:750-917): Construct (BVHRefitter.compute:72-120) re-derives each triangle of the
+ * mesh from the current vertex buffer — positions and normals transformed by `transform`, AABB
+ * padded by 1e-6 where flat, pos0 / posedge1 / posedge2 / packed normals written to AggTris at
+ * TriOffset + leaf_of_triangle[t] — then NodeInitializer, RefitLayer (:177-212, deepest layer
+ * first), NodeUpdate and NodeCompress re-quantize the mesh's CWBVH8 nodes in HBM (the plan of
+ * ParentObject.Construct, :679-730, is built once per scene and cached per mesh).
+ *   vertices: n_vertices x vertex_stride floats, position at +0 and normal at +3 (the raw
+ *             GraphicsBuffer of SkinnedMeshRenderer.GetVertexBuffer / Mesh.GetVertexBuffer(0)),
+ *   indices: 3 per triangle in Unity order (sharedMesh.triangles; submeshes concatenated, the
+ *            triangle is (i0, i2, i1) as everywhere in TrueTrace),
+ *   leaf_of_triangle: CWBVHIndicesBufferInverted (source triangle -> leaf-order position),
+ *                     from tt_blas_copy_leaf_order.
+ * Numerics pinned where the HLSL leaves them to DXC: mul as fmaf(m2, z, fmaf(m1, y, m0 * x)) (+ m3),
+ * normalize(v) = v * (1 / sqrt(dot)), octahedral round = round-half-to-even. Out-of-range vertex
+ * reads return zeros and out-of-range leaf writes are dropped (D3D semantics); host arrays are
+ * also validated up front. The caller refits the TLAS afterwards (the mesh's bounds changed).
+ * flags: TT_TRACE_DEVICE_PTRS (all three arrays in HBM), TT_TRACE_ASYNC. */
+typedef struct tt_blas_refit_params {
+    uint32_t mesh_index;     /* _MeshData record: its TriOffset, NodeOffset and BLAS root          */
+    uint32_t n_tris;         /* triangles of the mesh (= its BLAS's triangle count)               */
+    uint32_t n_vertices;
+    uint32_t vertex_stride;  /* floats per vertex (Unity vertex buffer stride / 4), >= 6           */
+    float transform[16];     /* "Transform", column-major (Unity Matrix4x4)                        */
+    uint32_t flags;
+} tt_blas_refit_params;
+tt_status tt_blas_refit(tt_ctx* ctx, const tt_blas_refit_params* p, const float* vertices, const int32_t* indices,
+                        const int32_t* leaf_of_triangle);
+
+/* Copies AggTris [first, first+count) back from HBM (e.g. after tt_blas_refit). */
+tt_status tt_scene_read_tris(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cuda_triangle* out);
+
 /* Copies nodes [first, first+count) of the scene in HBM back to the host (e.g. the TLAS after
  * tt_tlas_refit; the reference reads its refit TLAS back for nothing, but editors and tests do).
  * Synchronizes the context stream. */

@@ -54,6 +54,9 @@ tt_status tt_blas_build(const tt_mesh_input* mesh, tt_blas** out);
 tt_status tt_blas_get_info(const tt_blas* b, tt_blas_info* info);
 /* Copies the packed nodes (80 B) and the leaf-ordered triangles (88 B). */
 tt_status tt_blas_copy(const tt_blas* b, tt_cwbvh_node* nodes, tt_cuda_triangle* tris);
+/* CWBVHIndicesBufferInverted (ParentObject.cs:691-694): for each source triangle, its position in
+ * the leaf-ordered triangle array — the map tt_blas_refit's Construct writes through. */
+tt_status tt_blas_copy_leaf_order(const tt_blas* b, int32_t* leaf_of_triangle);
 void tt_blas_free(tt_blas* b);
 
 /* AssetManager aggregation. Order of meshes = RenderQue parents, then instances. */

@@ -863,6 +863,8 @@ typedef struct refit_pairs {
     int32_t* parent; /* IsLeafList.z */
     int32_t* to_bvh; /* ToBVHIndex[bvh8 node] */
     int32_t max_depth;
+    uint32_t n_nodes; /* bound on BVH8 node indices */
+    int bad;          /* a child index left [0, n_nodes) or the recursion got too deep */
     const tt_cwbvh_node* nodes;
 } refit_pairs;
 
@@ -885,7 +887,7 @@ static void rp_push(refit_pairs* R, int32_t bvh, int32_t slot) {
 
 static uint8_t node_meta(const tt_cwbvh_node* n, int k) { return (uint8_t)(n->meta[k >> 2] >> (8 * (k & 3))); }
 
-/* DocumentNodes — AssetManager.cs:1257-1297 (the NodePair AABBs it computes are reset by
+/* DocumentNodes — AssetManager.cs:1257-1297 / ParentObject.cs:638-677 (the same walk; the NodePair AABBs it computes are reset by
  * NodeInitializer every frame, so they are not kept) */
 static void document_nodes(refit_pairs* R, int current, int parent, int next_bvh8, int is_leaf, int recur) {
     if (recur > R->max_depth) R->max_depth = recur;
@@ -902,6 +904,10 @@ static void document_nodes(refit_pairs* R, int current, int parent, int next_bvh
                 document_nodes(R, (int)R->n - 1, current, -1, 1, recur + 1);
             } else {
                 const int child_index = (int)node->base_child + (m & 31) - 24;
+                if (child_index < 0 || (uint32_t)child_index >= R->n_nodes || recur > 256) {
+                    R->bad = 1;
+                    return;
+                }
                 document_nodes(R, (int)R->n - 1, current, child_index, 0, recur + 1);
             }
         }
@@ -927,15 +933,29 @@ static uint32_t ftou_d3d(float f) {
     return (uint32_t)f;
 }
 
-tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, const int32_t* tlas_indices,
-                               uint32_t n_tlas_indices, const float* mesh_aabbs, uint32_t n_mesh) {
-    if (!nodes || !n_tlas_nodes || !tlas_indices || !mesh_aabbs) return TT_ERR_INVALID_ARG;
+/* The refit shared by the TLAS (RefitBVHLayer: leaf ranges index `boxes` through `box_index`, the
+ * TLASCWBVHIndices) and a BLAS (RefitLayer: box_index NULL, leaf ranges are triangle boxes in leaf
+ * order). `nodes` is the node array whose root is node 0 (child indices local to it), `n_nodes` a
+ * bound on it; NodeCompress rewrites the nodes the plan reaches. */
+static tt_status refit_core(tt_cwbvh_node* nodes, uint32_t n_nodes, const int32_t* box_index, uint32_t n_box_index,
+                            const float* boxes, uint32_t n_boxes) {
+    const uint32_t n_tlas_nodes = n_nodes;
+    uint32_t n_tlas_nodes_used = n_nodes;
+    const int32_t* tlas_indices = box_index;
+    const uint32_t n_tlas_indices = n_box_index;
+    const float* mesh_aabbs = boxes;
+    const uint32_t n_mesh = n_boxes;
     refit_pairs R;
     memset(&R, 0, sizeof(R));
     R.nodes = nodes;
     R.to_bvh = (int32_t*)calloc(n_tlas_nodes, sizeof(int32_t));
+    R.n_nodes = n_nodes;
     rp_push(&R, 0, 0); /* NodePair[0]: the root's dummy entry */
     document_nodes(&R, 0, 0, 0, 0, 0);
+    if (R.bad) {
+        free(R.bvh); free(R.slot); free(R.leaf); free(R.depth); free(R.parent); free(R.to_bvh);
+        return TT_ERR_INVALID_ARG;
+    }
     const uint32_t N = R.n;
     /* ForwardStack — :1370-1380 */
     int32_t* fwd = (int32_t*)calloc((size_t)N * 8, sizeof(int32_t));
@@ -978,11 +998,12 @@ tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, cons
                     const int v = leaf - 1;
                     const int start = v / 24, end = start + v % 24;
                     for (int i4 = start; i4 < end; i4++) {
-                        if ((uint32_t)i4 >= n_tlas_indices || (uint32_t)tlas_indices[i4] >= n_mesh) {
+                        const int32_t bi = tlas_indices ? ((uint32_t)i4 < n_tlas_indices ? tlas_indices[i4] : -1) : i4;
+                        if (bi < 0 || (uint32_t)bi >= n_mesh) {
                             st = TT_ERR_INVALID_ARG;
                             break;
                         }
-                        const float* b = &mesh_aabbs[6 * (size_t)tlas_indices[i4]]; /* AABB {BBMax, BBMin} */
+                        const float* b = &mesh_aabbs[6 * (size_t)bi]; /* AABB {BBMax, BBMin} */
                         for (int a = 0; a < 3; a++) {
                             rmx[a] = fmaxf(rmx[a], b[a]);
                             rmn[a] = fminf(rmn[a], b[3 + a]);
@@ -996,12 +1017,16 @@ tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, cons
             }
         }
     }
+    uint32_t n_used = 0;
+    for (uint32_t i = 0; i < N; i++)
+        if ((uint32_t)R.bvh[i] + 1u > n_used) n_used = (uint32_t)R.bvh[i] + 1u;
+    if (n_used < n_tlas_nodes) n_tlas_nodes_used = n_used;
     if (st == TT_OK) {
         /* NodeUpdate into the fixed-layout nodes (p, e, per-slot quantized uints) */
-        float* P = (float*)malloc(sizeof(float) * 3 * n_tlas_nodes);
-        uint32_t* E = (uint32_t*)malloc(sizeof(uint32_t) * 3 * n_tlas_nodes);
-        uint32_t* Q = (uint32_t*)malloc(sizeof(uint32_t) * 48 * n_tlas_nodes); /* [node][axis-min/max][slot] */
-        for (uint32_t n = 0; n < n_tlas_nodes; n++) {
+        float* P = (float*)malloc(sizeof(float) * 3 * n_tlas_nodes_used);
+        uint32_t* E = (uint32_t*)malloc(sizeof(uint32_t) * 3 * n_tlas_nodes_used);
+        uint32_t* Q = (uint32_t*)malloc(sizeof(uint32_t) * 48 * n_tlas_nodes_used); /* [node][axis-min/max][slot] */
+        for (uint32_t n = 0; n < n_tlas_nodes_used; n++) {
             const tt_cwbvh_node* s = &nodes[n];
             for (int a = 0; a < 3; a++) {
                 P[3 * n + a] = s->p[a];
@@ -1033,7 +1058,7 @@ tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, cons
             }
         }
         /* NodeCompress — packed exactly as the reference (full uints shifted and OR-ed) */
-        for (uint32_t n = 0; n < n_tlas_nodes; n++) {
+        for (uint32_t n = 0; n < n_tlas_nodes_used; n++) {
             tt_cwbvh_node* o = &nodes[n];
             const uint32_t imask = o->e_imask >> 24;
             for (int a = 0; a < 3; a++) o->p[a] = P[3 * n + a];
@@ -1058,5 +1083,91 @@ tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, cons
     free(R.depth);
     free(R.parent);
     free(R.to_bvh);
+    return st;
+}
+
+tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, const int32_t* tlas_indices,
+                               uint32_t n_tlas_indices, const float* mesh_aabbs, uint32_t n_mesh) {
+    if (!nodes || !n_tlas_nodes || !tlas_indices || !mesh_aabbs) return TT_ERR_INVALID_ARG;
+    return refit_core(nodes, n_tlas_nodes, tlas_indices, n_tlas_indices, mesh_aabbs, n_mesh);
+}
+
+/* ---------------------------------------------------------------- BLAS refit (f4) */
+/* Construct — BVHRefitter.compute:72-120, with the numerics the HLSL leaves to DXC pinned as in
+ * include/truetrace_hip.h (tt_blas_refit): mul rows fmaf(m2, z, fmaf(m1, y, m0 * x)) (+ m3),
+ * normalize(v) = v * (1 / sqrt(dot)), round = round-half-to-even. */
+static v3 vtx3(const float* vertices, uint32_t n_vertices, uint32_t stride, int32_t idx, int off) {
+    if (idx < 0 || (uint32_t)idx >= n_vertices) return mk(0.0f, 0.0f, 0.0f); /* D3D: OOB reads 0 */
+    const float* v = vertices + (size_t)idx * stride + off;
+    return mk(v[0], v[1], v[2]);
+}
+static v3 xform_normal(const float* m, v3 n) {
+    const v3 v = mul33(m, n);
+    const float inv = 1.0f / sqrtf(fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x)));
+    return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+/* octahedral_32 — BVHRefitter.compute:62-68 */
+static uint32_t octahedral_32(v3 n) {
+    const float s = (fabsf(n.x) + fabsf(n.y)) + fabsf(n.z);
+    float x = n.x / s, y = n.y / s;
+    if (!(n.z >= 0.0f)) {
+        const float sx = (x >= 0.0f) ? 1.0f : -1.0f, sy = (y >= 0.0f) ? 1.0f : -1.0f;
+        const float ox = x;
+        x = (1.0f - fabsf(y)) * sx;
+        y = (1.0f - fabsf(ox)) * sy;
+    }
+    const uint32_t dx = (uint32_t)rintf(32767.5f + x * 32767.5f), dy = (uint32_t)rintf(32767.5f + y * 32767.5f);
+    return dx | (dy << 16);
+}
+
+tt_status tt_oracle_blas_refit(tt_cwbvh_node* nodes, uint32_t n_nodes, tt_cuda_triangle* tris, uint32_t n_tris,
+                               const tt_mesh_data* meshdata, uint32_t n_mesh, uint32_t mesh_index,
+                               const float* vertices, uint32_t n_vertices, uint32_t vertex_stride,
+                               const int32_t* indices, uint32_t n_mesh_tris, const int32_t* leaf_of_triangle,
+                               const float* transform) {
+    if (!nodes || !tris || !meshdata || !vertices || !indices || !leaf_of_triangle || !transform || !n_mesh_tris ||
+        vertex_stride < 6 || mesh_index >= n_mesh)
+        return TT_ERR_INVALID_ARG;
+    const tt_mesh_data* md = &meshdata[mesh_index];
+    const uint32_t node_base = (uint32_t)md->NodeOffset, tri_base = (uint32_t)md->TriOffset;
+    if ((uint32_t)(md->mesh_data_bvh_offsets & 0x7fffffff) != node_base || node_base >= n_nodes) return TT_ERR_UNSUPPORTED;
+    if ((uint64_t)tri_base + n_mesh_tris > n_tris) return TT_ERR_INVALID_ARG;
+    float* boxes = (float*)malloc(sizeof(float) * 6 * (size_t)n_mesh_tris);
+    for (size_t i = 0; i < 6 * (size_t)n_mesh_tris; i++) boxes[i] = 0.0f; /* fresh AABBBuffer */
+    for (uint32_t t = 0; t < n_mesh_tris; t++) {
+        const int32_t i0 = indices[3 * t], i1 = indices[3 * t + 1], i2 = indices[3 * t + 2];
+        /* vidx = Load3(...).xzy: p from i0, p2 from i2, p3 from i1 */
+        const v3 p = mul34(transform, vtx3(vertices, n_vertices, vertex_stride, i0, 0));
+        const v3 p2 = mul34(transform, vtx3(vertices, n_vertices, vertex_stride, i2, 0));
+        const v3 p3 = mul34(transform, vtx3(vertices, n_vertices, vertex_stride, i1, 0));
+        const v3 n1 = xform_normal(transform, vtx3(vertices, n_vertices, vertex_stride, i0, 3));
+        const v3 n2 = xform_normal(transform, vtx3(vertices, n_vertices, vertex_stride, i2, 3));
+        const v3 n3 = xform_normal(transform, vtx3(vertices, n_vertices, vertex_stride, i1, 3));
+        const int32_t leaf = leaf_of_triangle[t];
+        if (leaf < 0 || (uint32_t)leaf >= n_mesh_tris) continue; /* D3D drops out-of-range writes */
+        float mx[3] = {fmaxf(fmaxf(p.x, p2.x), p3.x), fmaxf(fmaxf(p.y, p2.y), p3.y), fmaxf(fmaxf(p.z, p2.z), p3.z)};
+        float mn[3] = {fminf(fminf(p.x, p2.x), p3.x), fminf(fminf(p.y, p2.y), p3.y), fminf(fminf(p.z, p2.z), p3.z)};
+        for (int k = 0; k < 3; k++)
+            if (mx[k] - mn[k] < 0.000001f) {
+                mn[k] -= 0.000001f;
+                mx[k] += 0.000001f;
+            }
+        float* b = &boxes[6 * (size_t)leaf];
+        for (int k = 0; k < 3; k++) {
+            b[k] = mx[k];
+            b[3 + k] = mn[k];
+        }
+        tt_cuda_triangle* T = &tris[tri_base + (uint32_t)leaf];
+        T->pos0[0] = p.x; T->pos0[1] = p.y; T->pos0[2] = p.z;
+        T->posedge1[0] = p2.x - p.x; T->posedge1[1] = p2.y - p.y; T->posedge1[2] = p2.z - p.z;
+        T->posedge2[0] = p3.x - p.x; T->posedge2[1] = p3.y - p.y; T->posedge2[2] = p3.z - p.z;
+        T->norms[0] = octahedral_32(n1);
+        T->norms[1] = octahedral_32(n2);
+        T->norms[2] = octahedral_32(n3);
+    }
+    /* NodeInitializer, RefitLayer (:177-212, deepest first), NodeUpdate, NodeCompress over the plan
+     * of ParentObject.Construct (:679-730) */
+    const tt_status st = refit_core(nodes + node_base, n_nodes - node_base, NULL, 0, boxes, n_mesh_tris);
+    free(boxes);
     return st;
 }

@@ -82,6 +82,14 @@ int32_t tt_oracle_hardware_threads(void);
  * indices) is read from the nodes and left unchanged. */
 tt_status tt_oracle_tlas_refit(tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, const int32_t* tlas_indices,
                                uint32_t n_tlas_indices, const float* mesh_aabbs, uint32_t n_mesh);
+/* BLAS refit of a deforming / skinned mesh (ParentObject.RefitMesh, ParentObject.cs:750-917):
+ * Construct (BVHRefitter.compute:72-120) into tris[TriOffset + leaf], then the refit of the mesh's
+ * BLAS nodes [NodeOffset, ...). Same contract as tt_blas_refit (include/truetrace_hip.h). */
+tt_status tt_oracle_blas_refit(tt_cwbvh_node* nodes, uint32_t n_nodes, tt_cuda_triangle* tris, uint32_t n_tris,
+                               const tt_mesh_data* meshdata, uint32_t n_mesh, uint32_t mesh_index,
+                               const float* vertices, uint32_t n_vertices, uint32_t vertex_stride,
+                               const int32_t* indices, uint32_t n_mesh_tris, const int32_t* leaf_of_triangle,
+                               const float* transform);
 
 /* The R8 alpha atlas Cutout materials sample (see tt_scene_upload_alpha_atlas); NULL clears it.
  * Process-global (test infrastructure): set it before tracing a scene with Cutout materials. */

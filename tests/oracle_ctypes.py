@@ -55,6 +55,8 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_set_alpha_atlas.restype = None
         L.tt_oracle_tlas_refit.argtypes = [vp, u32, vp, u32, vp, u32]
         L.tt_oracle_tlas_refit.restype = i32
+        L.tt_oracle_blas_refit.argtypes = [vp, u32, vp, u32, vp, u32, u32, vp, u32, u32, vp, u32, vp, vp]
+        L.tt_oracle_blas_refit.restype = i32
         L._path = path
         _LIB = L
     return _LIB
@@ -144,3 +146,19 @@ def tlas_refit(scene: "tthip.Scene", mesh_aabbs: np.ndarray, n_tlas_nodes=None):
     st = lib().tt_oracle_tlas_refit(nodes.ctypes.data, n, scene.tlas.ctypes.data, len(scene.tlas), boxes.ctypes.data,
                                     boxes.shape[0])
     return st, nodes
+
+
+def blas_refit(scene: "tthip.Scene", mesh_index: int, vertices: np.ndarray, indices: np.ndarray,
+               leaf_of_triangle: np.ndarray, transform=None):
+    """Oracle BLAS refit (ParentObject.RefitMesh): returns (status, nodes, tris) with the mesh's
+    triangles and BLAS nodes rewritten."""
+    nodes, tris = scene.nodes.copy(), scene.tris.copy()
+    v = np.ascontiguousarray(vertices, np.float32)
+    idx = np.ascontiguousarray(indices, np.int32).reshape(-1)
+    leaf = np.ascontiguousarray(leaf_of_triangle, np.int32)
+    m = tthip.unity_colmajor(np.eye(4) if transform is None else np.asarray(transform))
+    st = lib().tt_oracle_blas_refit(nodes.ctypes.data, len(nodes), tris.ctypes.data, len(tris),
+                                    scene.meshdata.ctypes.data, len(scene.meshdata), mesh_index, v.ctypes.data,
+                                    v.shape[0], v.shape[1], idx.ctypes.data, len(idx) // 3, leaf.ctypes.data,
+                                    m.ctypes.data)
+    return st, nodes, tris

@@ -522,3 +522,53 @@ def test_tlas_refit_moved_instances_then_trace(engine):
     assert O.trace(b, rf, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
     same = (rf["hits"][: W * H, :3] == rg["hits"][: W * H, :3]).all(1)
     assert same.mean() > 0.999  # ties between coincident instances may resolve differently
+
+
+# ------------------------------------------------------------------ BLAS refit (§8 f4, deforming meshes)
+@pytest.mark.parametrize("n_tris", [2000, 60000])
+def test_blas_refit_matches_oracle_and_traces(engine, n_tris):
+    from test_blas_refit import deform, two_mesh_scene, vertex_buffer
+
+    sc, mesh, blas = two_mesh_scene(seed=13, n=n_tris)
+    pos, nrm, idx = mesh.arrays()
+    leaf = blas.leaf_order()
+    engine.upload(sc)
+    W, H = 128, 96
+    c2w, ip = tthip.unity_camera((1.0, 3.0, 14.0), (0, -0.15, -1), (0, 1, 0), 60, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    for t, xf in ((0.3, np.eye(4)), (1.9, tthip.trs_matrix((0.2, -0.1, 0.3), 17.0, 1.0))):
+        V = vertex_buffer(deform(pos, t), nrm)
+        engine.blas_refit(1, V, idx, leaf, xf)
+        st, nodes, tris = O.blas_refit(sc, 1, V, idx, leaf, xf)
+        assert st == 0
+        assert np.array_equal(engine.scene_nodes(0, len(nodes)), nodes), "refit nodes differ"
+        assert np.array_equal(engine.scene_tris(0, len(tris)), tris), "re-derived triangles differ"
+        sc2 = tthip.Scene(nodes, tris, sc.tlas, sc.meshdata, sc.materials, tlas_nodes=sc.tlas_nodes)
+        rg, rc, ig, ic, _, _ = trace_both(engine, sc2, rays, W * H, 0, W, H, upload=False)
+        assert_same(rg, rc, ig, ic, 0, W * H)
+
+
+def test_blas_refit_device_pointers_and_errors(engine):
+    import torch
+
+    from test_blas_refit import deform, two_mesh_scene, vertex_buffer
+
+    sc, mesh, blas = two_mesh_scene(seed=21, n=3000)
+    pos, nrm, idx = mesh.arrays()
+    leaf = blas.leaf_order()
+    engine.upload(sc)
+    V = vertex_buffer(deform(pos, 0.8), nrm)
+    dev = torch.device("cuda", 0)
+    Vd, Id, Ld = (torch.from_numpy(a).to(dev) for a in (V, idx, leaf))
+    engine.blas_refit(1, Vd, Id, Ld, device=True)
+    torch.cuda.synchronize()
+    st, nodes, tris = O.blas_refit(sc, 1, V, idx, leaf)
+    assert st == 0
+    assert np.array_equal(engine.scene_nodes(0, len(nodes)), nodes)
+    assert np.array_equal(engine.scene_tris(0, len(tris)), tris)
+    with pytest.raises(tthip.TTError):
+        engine.blas_refit(7, V, idx, leaf)  # no such mesh
+    bad = idx.copy()
+    bad[5] = len(pos) + 3
+    with pytest.raises(tthip.TTError):
+        engine.blas_refit(1, V, bad, leaf)  # index out of range (host arrays are validated)

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -106,6 +107,15 @@ struct tt_ctx {
     uint64_t scene_gen = 0, refit_gen = ~0ull;
     uint32_t refit_n_tlas = 0;
     DevBuf<float> st_boxes;
+    // BLAS refit (f4, deforming / skinned meshes): one prepared plan + triangle boxes per mesh
+    struct BlasRefit {
+        RefitDev dev;
+        uint64_t gen = ~0ull;
+        DevBuf<float> boxes;
+    };
+    std::map<uint32_t, BlasRefit> blas_refit;
+    DevBuf<float> st_vtx;
+    DevBuf<int32_t> st_idx, st_leaf;
     // host-pointer staging
     uint64_t max_rays = 0;
     DevBuf<tt_ray_data> st_rays;
@@ -454,6 +464,13 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->mat_cut.release();
     c->atlas.release();
     tt_refit_free(c->refit);
+    for (auto& kv : c->blas_refit) {
+        tt_refit_free(kv.second.dev);
+        kv.second.boxes.release();
+    }
+    c->st_vtx.release();
+    c->st_idx.release();
+    c->st_leaf.release();
     c->st_boxes.release();
     c->st_rays.release();
     c->st_shadow.release();
@@ -605,6 +622,87 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
     }
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* vertices, const int32_t* indices,
+                        const int32_t* leaf_of_triangle) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!p || !vertices || !indices || !leaf_of_triangle || !p->n_tris || !p->n_vertices || p->vertex_stride < 6)
+        return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: null array, empty mesh or vertex_stride < 6");
+    if (p->mesh_index >= c->host.mesh.size())
+        return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: mesh_index %u out of range", p->mesh_index);
+    const tt_mesh_data& md = c->host.mesh[p->mesh_index];
+    const uint32_t node_base = (uint32_t)md.NodeOffset, tri_base = (uint32_t)md.TriOffset;
+    if ((uint32_t)(md.mesh_data_bvh_offsets & 0x7fffffff) != node_base || node_base >= c->host.nodes.size())
+        return fail(c, TT_ERR_UNSUPPORTED, "tt_blas_refit: the mesh's BLAS root is not its first node");
+    if ((uint64_t)tri_base + p->n_tris > c->host.n_tris)
+        return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: TriOffset + n_tris exceeds the scene's triangles");
+    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    if (dev && !(is_device_ptr(vertices) && is_device_ptr(indices) && is_device_ptr(leaf_of_triangle)))
+        return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but an array is not device memory");
+    if (!dev) {
+        for (uint64_t i = 0; i < 3ull * p->n_tris; i++)
+            if (indices[i] < 0 || (uint32_t)indices[i] >= p->n_vertices)
+                return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: index %d out of range", indices[i]);
+        for (uint32_t i = 0; i < p->n_tris; i++)
+            if (leaf_of_triangle[i] < 0 || (uint32_t)leaf_of_triangle[i] >= p->n_tris)
+                return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: leaf_of_triangle[%u] out of range", i);
+    }
+    TT_HIP(c, hipSetDevice(c->device));
+    tt_ctx::BlasRefit& R = c->blas_refit[p->mesh_index];
+    if (R.gen != c->scene_gen || R.boxes.n < (size_t)6 * p->n_tris) {
+        RefitPlan plan;
+        const tt_cwbvh_node* base = c->host.nodes.data() + node_base;
+        if (!tt_refit_build_plan(base, (uint32_t)(c->host.nodes.size() - node_base), plan))
+            return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: a BLAS child index leaves the node array");
+        if ((uint32_t)plan.leaf_end > p->n_tris)
+            return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: the BLAS references triangle %d beyond n_tris", plan.leaf_end - 1);
+        uint32_t n_used = 0;
+        for (int32_t b : plan.pair_bvh) n_used = std::max(n_used, (uint32_t)b + 1u);
+        TT_HIP(c, hipStreamSynchronize(c->stream));  // the old plan's buffers may be in use
+        TT_HIP(c, tt_refit_prepare(plan, base, n_used, R.dev));
+        if (R.boxes.n < (size_t)6 * p->n_tris) TT_HIP(c, R.boxes.alloc((size_t)6 * p->n_tris));
+        R.gen = c->scene_gen;
+    }
+    BlasConstructArgs a{};
+    a.vertices = vertices;
+    a.indices = indices;
+    a.leaf_of = leaf_of_triangle;
+    if (!dev) {
+        const size_t nv = (size_t)p->n_vertices * p->vertex_stride;
+        if (c->st_vtx.n < nv) TT_HIP(c, c->st_vtx.alloc(nv));
+        if (c->st_idx.n < 3ull * p->n_tris) TT_HIP(c, c->st_idx.alloc(3ull * p->n_tris));
+        if (c->st_leaf.n < p->n_tris) TT_HIP(c, c->st_leaf.alloc(p->n_tris));
+        TT_HIP(c, hipMemcpyAsync(c->st_vtx.p, vertices, sizeof(float) * nv, hipMemcpyHostToDevice, c->stream));
+        TT_HIP(c, hipMemcpyAsync(c->st_idx.p, indices, sizeof(int32_t) * 3 * p->n_tris, hipMemcpyHostToDevice, c->stream));
+        TT_HIP(c, hipMemcpyAsync(c->st_leaf.p, leaf_of_triangle, sizeof(int32_t) * p->n_tris, hipMemcpyHostToDevice, c->stream));
+        a.vertices = c->st_vtx.p;
+        a.indices = c->st_idx.p;
+        a.leaf_of = c->st_leaf.p;
+    }
+    a.n_tris = p->n_tris;
+    a.n_vertices = p->n_vertices;
+    a.vertex_stride = p->vertex_stride;
+    std::memcpy(a.m, p->transform, sizeof(a.m));
+    a.boxes = R.boxes.p;
+    a.tris88 = c->tris_raw.p + tri_base;
+    a.tripos = c->tris.p + tri_base;
+    TT_HIP(c, tt_blas_construct(a, c->stream));
+    TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
+    if (!(p->flags & TT_TRACE_ASYNC) || !dev) TT_HIP(c, hipStreamSynchronize(c->stream));
+    return TT_OK;
+}
+
+tt_status tt_scene_read_tris(tt_ctx* c, uint32_t first, uint32_t count, tt_cuda_triangle* out) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    if (!out || (uint64_t)first + count > c->host.n_tris)
+        return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_tris: range out of bounds");
+    TT_HIP(c, hipSetDevice(c->device));
+    TT_HIP(c, hipMemcpyAsync(out, c->tris_raw.p + first, sizeof(tt_cuda_triangle) * count, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
 

@@ -1,7 +1,12 @@
-// tt_refit.hip — per-frame TLAS refit on the GPU: the reference's
-// AssetManager.RefitTLAS (AssetManager.cs:1473-1548) driving BVHRefitter.compute
-// (NodeInitializer :386-394, RefitBVHLayer :220-252, NodeUpdate :277-317, NodeCompress :344-371)
-// over the NodePair / ForwardStack / layer structures of ConstructNewTLAS (:1256-1390).
+// tt_refit.hip — per-frame BVH refit on the GPU:
+//  * TLAS: the reference's AssetManager.RefitTLAS (AssetManager.cs:1473-1548) driving
+//    BVHRefitter.compute (NodeInitializer :386-394, RefitBVHLayer :220-252, NodeUpdate :277-317,
+//    NodeCompress :344-371) over the NodePair / ForwardStack / layer structures of
+//    ConstructNewTLAS (:1256-1390);
+//  * BLAS of a deforming / skinned mesh: ParentObject.RefitMesh (ParentObject.cs:750-917) —
+//    Construct (BVHRefitter.compute:72-120) re-derives the triangles and their boxes from the
+//    current vertex buffer, then the same NodeInitializer / RefitLayer (:177-212) / NodeUpdate /
+//    NodeCompress over the plan ParentObject.Construct builds (:679-730).
 //
 // MI355X shape: the refit is a few thousand tiny records per frame, latency- not bandwidth-bound;
 // it runs as one short launch per BVH depth level on the context stream (no host sync), so a
@@ -44,9 +49,10 @@ __global__ void refit_init(float* __restrict__ bb, uint32_t n) {  // NodeInitial
     }
 }
 
-// RefitBVHLayer: one NodePair of the current depth per thread
+// RefitBVHLayer (TLAS: leaf ranges index the boxes through TLASCWBVHIndices) / RefitLayer (BLAS:
+// leaf ranges are triangle boxes in leaf order, box_idx == nullptr): one NodePair per thread
 __global__ void refit_layer(const int32_t* __restrict__ layer, uint32_t n, const int32_t* __restrict__ fwd,
-                            const int32_t* __restrict__ tlas_idx, const float* __restrict__ boxes,
+                            const int32_t* __restrict__ box_idx, const float* __restrict__ boxes,
                             float* __restrict__ bb) {
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= n) return;
@@ -68,7 +74,7 @@ __global__ void refit_layer(const int32_t* __restrict__ layer, uint32_t n, const
             const int32_t v = leaf - 1;
             const int32_t start = v / 24, end = start + v % 24;
             for (int32_t i4 = start; i4 < end; i4++) {
-                const float* b = boxes + 6 * (size_t)tlas_idx[i4];  // AABB {BBMax, BBMin}
+                const float* b = boxes + 6 * (size_t)(box_idx ? box_idx[i4] : i4);  // AABB {BBMax, BBMin}
                 mx0 = fmaxf(mx0, b[0]);
                 mx1 = fmaxf(mx1, b[1]);
                 mx2 = fmaxf(mx2, b[2]);
@@ -128,6 +134,93 @@ __global__ void refit_compress(uint32_t n_nodes, const float* __restrict__ P, co
         }
 }
 
+// ------------------------------------------------------------------ Construct (BLAS refit)
+// The reference leaves normalize / round / the mul association to DXC; pinned here and in the
+// oracle: mul rows as fmaf(m2, z, fmaf(m1, y, m0 * x)) (+ m3), normalize(v) = v * (1 / sqrt(dot))
+// with dot = fmaf(z, z, fmaf(y, y, x * x)), round = round-half-to-even, no other contraction.
+__device__ __forceinline__ float3 ld_vec3(const BlasConstructArgs& a, int32_t idx, uint32_t off) {
+    if (idx < 0 || (uint32_t)idx >= a.n_vertices) return make_float3(0.0f, 0.0f, 0.0f);  // D3D: OOB reads 0
+    const float* v = a.vertices + (size_t)idx * a.vertex_stride + off;
+    return make_float3(v[0], v[1], v[2]);
+}
+__device__ __forceinline__ float M(const float* m, int r, int c) { return m[c * 4 + r]; }
+__device__ __forceinline__ float3 xform_point(const float* m, float3 p) {
+    return make_float3(__builtin_fmaf(M(m, 0, 2), p.z, __builtin_fmaf(M(m, 0, 1), p.y, M(m, 0, 0) * p.x)) + M(m, 0, 3),
+                       __builtin_fmaf(M(m, 1, 2), p.z, __builtin_fmaf(M(m, 1, 1), p.y, M(m, 1, 0) * p.x)) + M(m, 1, 3),
+                       __builtin_fmaf(M(m, 2, 2), p.z, __builtin_fmaf(M(m, 2, 1), p.y, M(m, 2, 0) * p.x)) + M(m, 2, 3));
+}
+__device__ __forceinline__ float3 xform_normal(const float* m, float3 n) {
+    const float3 v = make_float3(__builtin_fmaf(M(m, 0, 2), n.z, __builtin_fmaf(M(m, 0, 1), n.y, M(m, 0, 0) * n.x)),
+                                 __builtin_fmaf(M(m, 1, 2), n.z, __builtin_fmaf(M(m, 1, 1), n.y, M(m, 1, 0) * n.x)),
+                                 __builtin_fmaf(M(m, 2, 2), n.z, __builtin_fmaf(M(m, 2, 1), n.y, M(m, 2, 0) * n.x)));
+    const float inv = 1.0f / sqrtf(__builtin_fmaf(v.z, v.z, __builtin_fmaf(v.y, v.y, v.x * v.x)));
+    return make_float3(v.x * inv, v.y * inv, v.z * inv);
+}
+// octahedral_32 — BVHRefitter.compute:62-68
+__device__ __forceinline__ uint32_t octahedral_32(float3 n) {
+    const float s = (fabsf(n.x) + fabsf(n.y)) + fabsf(n.z);
+    float x = n.x / s, y = n.y / s;
+    if (!(n.z >= 0.0f)) {
+        const float sx = (x >= 0.0f) ? 1.0f : -1.0f, sy = (y >= 0.0f) ? 1.0f : -1.0f;
+        const float ox = x;
+        x = (1.0f - fabsf(y)) * sx;
+        y = (1.0f - fabsf(ox)) * sy;
+    }
+    const uint32_t dx = (uint32_t)rintf(32767.5f + x * 32767.5f), dy = (uint32_t)rintf(32767.5f + y * 32767.5f);
+    return dx | (dy << 16);
+}
+
+__global__ void blas_construct(BlasConstructArgs a) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= a.n_tris) return;
+    const int32_t i0 = a.indices[3 * t], i1 = a.indices[3 * t + 1], i2 = a.indices[3 * t + 2];
+    // vidx = Load3(...).xzy: p from i0, p2 from i2, p3 from i1
+    const float3 p = xform_point(a.m, ld_vec3(a, i0, 0)), p2 = xform_point(a.m, ld_vec3(a, i2, 0)),
+                 p3 = xform_point(a.m, ld_vec3(a, i1, 0));
+    const float3 n1 = xform_normal(a.m, ld_vec3(a, i0, 3)), n2 = xform_normal(a.m, ld_vec3(a, i2, 3)),
+                 n3 = xform_normal(a.m, ld_vec3(a, i1, 3));
+    const int32_t leaf = a.leaf_of[t];
+    if (leaf < 0 || (uint32_t)leaf >= a.n_tris) return;  // D3D drops out-of-range writes
+    float mx[3] = {fmaxf(fmaxf(p.x, p2.x), p3.x), fmaxf(fmaxf(p.y, p2.y), p3.y), fmaxf(fmaxf(p.z, p2.z), p3.z)};
+    float mn[3] = {fminf(fminf(p.x, p2.x), p3.x), fminf(fminf(p.y, p2.y), p3.y), fminf(fminf(p.z, p2.z), p3.z)};
+    for (int k = 0; k < 3; k++)
+        if (mx[k] - mn[k] < 0.000001f) {
+            mn[k] -= 0.000001f;
+            mx[k] += 0.000001f;
+        }
+    float* b = a.boxes + 6 * (size_t)leaf;
+    b[0] = mx[0];
+    b[1] = mx[1];
+    b[2] = mx[2];
+    b[3] = mn[0];
+    b[4] = mn[1];
+    b[5] = mn[2];
+    const float3 e1 = make_float3(p2.x - p.x, p2.y - p.y, p2.z - p.z), e2 = make_float3(p3.x - p.x, p3.y - p.y, p3.z - p.z);
+    tt_cuda_triangle& T = a.tris88[leaf];
+    T.pos0[0] = p.x;
+    T.pos0[1] = p.y;
+    T.pos0[2] = p.z;
+    T.posedge1[0] = e1.x;
+    T.posedge1[1] = e1.y;
+    T.posedge1[2] = e1.z;
+    T.posedge2[0] = e2.x;
+    T.posedge2[1] = e2.y;
+    T.posedge2[2] = e2.z;
+    T.norms[0] = octahedral_32(n1);
+    T.norms[1] = octahedral_32(n2);
+    T.norms[2] = octahedral_32(n3);
+    TriPos& q = a.tripos[leaf];
+    q.p0x = p.x;
+    q.p0y = p.y;
+    q.p0z = p.z;
+    q.e1x = e1.x;
+    q.e1y = e1.y;
+    q.e1z = e1.z;
+    q.e2x = e2.x;
+    q.e2y = e2.y;
+    q.e2z = e2.z;
+}
+
 inline uint32_t grid_of(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
 }  // namespace
@@ -155,7 +248,7 @@ static void document_nodes(const tt_cwbvh_node* nodes, RefitPlan& R, int current
                 document_nodes(nodes, R, me, current, -1, true, recur + 1);
             } else {
                 const int child = (int)node.base_child + (int)(m & 31u) - 24;
-                if (child < 0 || (uint32_t)child >= R.n_tlas || recur > 64) {
+                if (child < 0 || (uint32_t)child >= R.n_tlas || recur > 256) {
                     R.ok = false;
                     return;
                 }
@@ -186,7 +279,9 @@ bool tt_refit_build_plan(const tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, Refi
         const int slot = R.pair_slot[i];
         if (R.leaf[i]) {
             const uint32_t m = (node.meta[slot >> 2] >> (8 * (slot & 3))) & 0xffu;
-            R.fwd[i * 8 + slot] = __builtin_popcount(m >> 5) + ((int)node.base_tri + (int)(m & 0x1fu)) * 24 + 1;
+            const int nb = __builtin_popcount(m >> 5), first = (int)node.base_tri + (int)(m & 0x1fu);
+            R.fwd[i * 8 + slot] = nb + first * 24 + 1;
+            if (nb) R.leaf_end = std::max(R.leaf_end, first + nb);
         } else {
             R.fwd[i * 8 + slot] = -(int)i - 1;
         }
@@ -245,15 +340,21 @@ hipError_t tt_refit_prepare(const RefitPlan& R, const tt_cwbvh_node* host_nodes,
 }
 
 // One frame: boxes (device, n_mesh x 6 floats) -> TLAS nodes [0, n_nodes) of `nodes`.
-hipError_t tt_refit_run(RefitDev& d, const float* boxes, const int32_t* tlas_idx, tt_cwbvh_node* nodes, hipStream_t st) {
+hipError_t tt_refit_run(RefitDev& d, const float* boxes, const int32_t* box_index, tt_cwbvh_node* nodes, hipStream_t st) {
     hipLaunchKernelGGL(refit_init, dim3(grid_of(d.n_pairs)), dim3(kBlock), 0, st, d.bb, d.n_pairs);
     for (int l = (int)d.layer_n.size() - 1; l >= 0; l--) {
         if (!d.layer_n[l]) continue;
         hipLaunchKernelGGL(refit_layer, dim3(grid_of(d.layer_n[l])), dim3(kBlock), 0, st, d.layers + d.layer_off[l],
-                           d.layer_n[l], d.fwd, tlas_idx, boxes, d.bb);
+                           d.layer_n[l], d.fwd, box_index, boxes, d.bb);
     }
     hipLaunchKernelGGL(refit_update, dim3(grid_of(d.n_pairs)), dim3(kBlock), 0, st, d.n_pairs, d.pair_bvh, d.pair_slot,
                        d.to_bvh, d.bb, d.P, d.E, d.Q);
     hipLaunchKernelGGL(refit_compress, dim3(grid_of(d.n_nodes)), dim3(kBlock), 0, st, d.n_nodes, d.P, d.E, d.Q, nodes);
+    return hipGetLastError();
+}
+
+hipError_t tt_blas_construct(const BlasConstructArgs& a, hipStream_t st) {
+    if (!a.n_tris) return hipSuccess;
+    hipLaunchKernelGGL(blas_construct, dim3(grid_of(a.n_tris)), dim3(kBlock), 0, st, a);
     return hipGetLastError();
 }

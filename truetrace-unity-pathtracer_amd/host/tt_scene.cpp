@@ -645,6 +645,7 @@ static bool run_big_stack(F&& fn) {
 struct tt_blas {
     std::vector<tt_cwbvh_node> nodes;
     std::vector<tt_cuda_triangle> tris;
+    std::vector<int32_t> leaf_of;  // CWBVHIndicesBufferInverted
     AABB aabb_untransformed;
     uint32_t bvh2_depth = 0;
     double seconds = 0;
@@ -769,11 +770,21 @@ tt_status tt_blas_build(const tt_mesh_input* m, tt_blas** out) {
     }
     b->bvh2_depth = bvh2.max_depth;
     b->tris.resize(ntri);
-    for (uint32_t i = 0; i < ntri; i++) b->tris[i] = agg[bvh8.cwbvh_indices[i]];
+    b->leaf_of.assign(ntri, 0);
+    for (uint32_t i = 0; i < ntri; i++) {
+        b->tris[i] = agg[bvh8.cwbvh_indices[i]];
+        b->leaf_of[bvh8.cwbvh_indices[i]] = (int32_t)i;
+    }
     b->nodes.resize(bvh8.BVH8Nodes.size());
     Aggregate(bvh8.BVH8Nodes, b->nodes.data());
     b->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *out = b;
+    return TT_OK;
+}
+
+tt_status tt_blas_copy_leaf_order(const tt_blas* b, int32_t* out) {
+    if (!b || !out) return TT_ERR_INVALID_ARG;
+    std::copy(b->leaf_of.begin(), b->leaf_of.end(), out);
     return TT_OK;
 }
 

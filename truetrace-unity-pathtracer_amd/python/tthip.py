@@ -90,6 +90,11 @@ class ShadowParams(C.Structure):
                 ("screen_height", C.c_uint32), ("flags", C.c_uint32)]
 
 
+class BlasRefitParams(C.Structure):
+    _fields_ = [("mesh_index", C.c_uint32), ("n_tris", C.c_uint32), ("n_vertices", C.c_uint32),
+                ("vertex_stride", C.c_uint32), ("transform", C.c_float * 16), ("flags", C.c_uint32)]
+
+
 class TraceParams(C.Structure):
     _fields_ = [("n_rays", C.c_uint32), ("bounce", C.c_int32), ("far_plane", C.c_float),
                 ("screen_width", C.c_uint32), ("screen_height", C.c_uint32), ("flags", C.c_uint32)]
@@ -170,7 +175,7 @@ SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_f
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
                  "tt_synth_prop", "tt_synth_ground", "tt_synth_san_miguel", "tt_synth_mesh_view", "tt_synth_mesh_free",
-                 "tt_synth_mesh_from_arrays"]
+                 "tt_synth_mesh_from_arrays", "tt_blas_copy_leaf_order"]
 
 
 def scene_lib():
@@ -186,6 +191,8 @@ def scene_lib():
         L.tt_blas_copy.argtypes = [vp, vp, vp]
         L.tt_blas_free.argtypes = [vp]
         L.tt_blas_free.restype = None
+        L.tt_blas_copy_leaf_order.argtypes = [vp, vp]
+        L.tt_blas_copy_leaf_order.restype = i32
         L.tt_scene_assemble.argtypes = [vp, u32, vp, u32, vp, u32, C.POINTER(vp)]
         L.tt_scene_build_get_info.argtypes = [vp, C.POINTER(SceneBuildInfo)]
         L.tt_scene_build_copy.argtypes = [vp, vp, vp, vp, vp]
@@ -247,6 +254,8 @@ def hip_lib():
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
         L.tt_scene_read_nodes.argtypes = [vp, u32, u32, vp]
+        L.tt_scene_read_tris.argtypes = [vp, u32, u32, vp]
+        L.tt_blas_refit.argtypes = [vp, C.POINTER(BlasRefitParams), vp, vp, vp]
         L.tt_sync.argtypes = [vp]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
@@ -362,6 +371,17 @@ class Mesh:
             raise TTError(TT_ERR_OOM, "tt_synth_mesh_from_arrays")
         return cls(h)
 
+    def arrays(self):
+        """(positions (n,3), normals (n,3), indices (3*tris,)) copies of the mesh."""
+        v = self.view()
+        n, k = v.n_vertices, v.n_indices
+        fp, ip = C.POINTER(C.c_float), C.POINTER(C.c_int32)
+        pos = np.ctypeslib.as_array(C.cast(v.positions, fp), (3 * n,)).reshape(n, 3).copy()
+        nrm = (np.ctypeslib.as_array(C.cast(v.normals, fp), (3 * n,)).reshape(n, 3).copy() if v.normals
+               else np.tile(np.float32([0, 1, 0]), (n, 1)))
+        idx = np.ctypeslib.as_array(C.cast(v.indices, ip), (k,)).copy()
+        return pos, nrm, idx
+
     def view(self) -> MeshInput:
         v = MeshInput()
         self._check(scene_lib().tt_synth_mesh_view(self.h, C.byref(v)), "tt_synth_mesh_view")
@@ -395,6 +415,12 @@ class Blas:
     @property
     def n_tris(self):
         return self.info.n_tris
+
+    def leaf_order(self) -> np.ndarray:
+        """CWBVHIndicesBufferInverted: source triangle -> position in the leaf-ordered triangles."""
+        out = np.zeros(self.info.n_tris, np.int32)
+        scene_lib().tt_blas_copy_leaf_order(self.h, out.ctypes.data)
+        return out
 
     def arrays(self):
         nodes = np.zeros(self.info.n_nodes, NODE_DTYPE)
@@ -618,6 +644,26 @@ class Engine:
         n = int(mesh_aabbs.shape[0]) if hasattr(mesh_aabbs, "shape") else len(mesh_aabbs) // 6
         flags = (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_ASYNC if asynchronous else 0)
         self._check(self.L.tt_tlas_refit(self.h, n_tlas_nodes, _ptr(mesh_aabbs), n, flags), "tt_tlas_refit")
+
+    def blas_refit(self, mesh_index: int, vertices, indices, leaf_of_triangle, transform=None,
+                   device: bool = False, asynchronous: bool = False):
+        """tt_blas_refit (ParentObject.RefitMesh): re-derive the mesh's triangles from `vertices`
+        (n x stride floats: position at +0, normal at +3) and refit its BLAS nodes in HBM.
+        `transform` is a row-major 4x4 (identity by default)."""
+        stride = int(vertices.shape[1]) if hasattr(vertices, "shape") and len(vertices.shape) == 2 else 6
+        nv = int(vertices.shape[0]) if hasattr(vertices, "shape") and len(vertices.shape) == 2 else len(vertices) // 6
+        n_tris = int(indices.shape[0]) // 3 if len(indices.shape) == 1 else int(indices.shape[0])
+        p = BlasRefitParams(mesh_index=mesh_index, n_tris=n_tris, n_vertices=nv, vertex_stride=stride,
+                            flags=(TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_ASYNC if asynchronous else 0))
+        p.transform[:] = unity_colmajor(np.eye(4) if transform is None else np.asarray(transform))
+        self._check(self.L.tt_blas_refit(self.h, C.byref(p), _ptr(vertices), _ptr(indices), _ptr(leaf_of_triangle)),
+                    "tt_blas_refit")
+
+    def scene_tris(self, first: int, count: int) -> np.ndarray:
+        """Reads AggTris [first, first+count) back from HBM (parity checks of the BLAS refit)."""
+        out = np.zeros(count, TRI_DTYPE)
+        self._check(self.L.tt_scene_read_tris(self.h, first, count, _ptr(out)), "tt_scene_read_tris")
+        return out
 
     def scene_nodes(self, first: int, count: int) -> np.ndarray:
         """Reads nodes [first, first+count) back from HBM (parity checks of the refit)."""
