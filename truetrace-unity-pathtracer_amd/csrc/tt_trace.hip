@@ -309,6 +309,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                                 n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
                                 n4 = buffer_load16(nodes, no + 64u);
                     const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
+#ifdef TT_DIAG_NODEHIST  // diagnostic: visits per node index -> diag_times (as uint32[n_nodes])
+                    if (A.diag_times) atomicAdd(reinterpret_cast<uint32_t*>(A.diag_times) + child, 1u);
+#endif
                     cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
                     tg.y = hitmask & 0x00ffffffu;
                     cg.x = n1.x + (uint32_t)NodeOffset;

@@ -20,7 +20,7 @@
 #ifndef TT_WIDE_ENTER
 #define TT_WIDE_ENTER 32   // enter the drain phase (G = 2) once at most this many rays are live
 #endif
-#if defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || TT_WRAY_RELOAD
+#if defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST) || TT_WRAY_RELOAD
 #undef TT_WIDE
 #define TT_WIDE 0
 #endif
