@@ -25,7 +25,20 @@ def assert_same(rg, rc, ig, ic, off, n):
     hg, hc = rg["hits"][off:off + n], rc["hits"][off:off + n]
     bad = np.nonzero((hg != hc).any(1))[0]
     assert len(bad) == 0, f"{len(bad)} of {n} hit records differ, first {bad[:5]}: {hg[bad[:3]]} vs {hc[bad[:3]]}"
-    assert np.array_equal(rg, rc), "bytes outside the hit records must be untouched"
+    # byte comparison: ray fields may legitimately hold NaNs (degenerate inputs)
+    assert np.array_equal(np.ascontiguousarray(rg).view(np.uint8), np.ascontiguousarray(rc).view(np.uint8)), \
+        "bytes outside the hit records must be untouched"
     if ig is not None:
         badi = np.nonzero((ig != ic).any(1))[0]
         assert len(badi) == 0, f"{len(badi)} _PrimaryTriangleInfo texels differ"
+
+
+def same_floats(a, b) -> bool:
+    """Float outputs compare bit for bit, except that any two NaNs are equal: the NaN a CPU and a
+    GPU produce for the same invalid operation differ in sign / payload (x86 default NaN is
+    0xFFC00000, gfx950 0x7FC00000) and neither the reference nor D3D defines it."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    same_bits = a.view(np.uint32) == b.view(np.uint32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all(same_bits | both_nan))

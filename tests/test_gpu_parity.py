@@ -16,7 +16,7 @@ import kat_cases as K
 import oracle_ctypes as O
 import tthip
 
-from parity_util import CPU_THREADS, FAR, assert_same, trace_both
+from parity_util import CPU_THREADS, FAR, assert_same, same_floats, trace_both
 
 pytestmark = pytest.mark.gpu
 
@@ -326,10 +326,12 @@ def shadow_both(engine, sc, srays, bounce, W, H, upload=True):
             assert st == 0
             out.append((r, vis, col, nee, cnt))
     (rg, vg, cg, ng, s), (rc, vc, cc, nc, cnt) = out
-    assert np.array_equal(rg, rc), f"{int((rg['t'] != rc['t']).sum())} shadow t values differ"
-    assert np.array_equal(vg, vc), "visibility differs"
-    assert np.array_equal(cg, cc), "GlobalColors differ"
-    assert np.array_equal(ng, nc), "NEEPosA differs"
+    b = lambda x: np.ascontiguousarray(x).view(np.uint8)  # noqa: E731  (NaN-safe comparison)
+    assert np.array_equal(b(rg), b(rc)), f"{int((b(rg) != b(rc)).sum())} shadow ray bytes differ"
+    assert same_floats(vg, vc), "visibility differs"
+    assert same_floats(np.ascontiguousarray(cg).view(np.float32), np.ascontiguousarray(cc).view(np.float32)), \
+        "GlobalColors differ"
+    assert same_floats(ng, nc), "NEEPosA differs"
     assert s.node_visits == int(cnt["node_visits"].sum()) and s.tri_tests == int(cnt["tri_tests"].sum())
     assert s.hits == int((cnt["status"] == 4).sum())
     return rg, vg, s, cnt
@@ -572,3 +574,64 @@ def test_blas_refit_device_pointers_and_errors(engine):
     bad[5] = len(pos) + 3
     with pytest.raises(tthip.TTError):
         engine.blas_refit(1, V, bad, leaf)  # index out of range (host arrays are validated)
+
+
+# ------------------------------------------------------------------ degenerate ray inputs
+def degenerate_rays(n, seed):
+    """Normal rays mixed with the numerically hostile ones a renderer can hand over: zero, signed-zero,
+    denormal, NaN and infinite direction components, NaN / infinite origins."""
+    rng = np.random.default_rng(seed)
+    rays = np.zeros(2 * n, tthip.RAY_DTYPE)
+    o = rng.uniform(-1.5, 1.5, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    specials = np.array([0.0, -0.0, 1e-40, -1e-40, np.nan, np.inf, -np.inf, 1e-30, 1e30], np.float32)
+    k = rng.integers(0, 4, n)  # 0: normal, 1: special direction component, 2: special origin, 3: both
+    for i in range(n):
+        if k[i] in (1, 3):
+            d[i, rng.integers(0, 3)] = specials[rng.integers(0, len(specials))]
+            if rng.random() < 0.2:
+                d[i] = 0.0
+        if k[i] in (2, 3):
+            o[i, rng.integers(0, 3)] = specials[rng.integers(4, len(specials))]
+    rays["origin"][:n] = o
+    rays["direction"][:n] = d
+    rays["PixelIndex"][:n] = np.arange(n)
+    return rays
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_degenerate_rays_closest_and_shadow(engine, seed):
+    sc = tthip.single_object_scene(tthip.Mesh.soup(seed, 4000, 1.0, 0.15))
+    n = 4096
+    rays = degenerate_rays(n, seed)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, n, 0, n, 1, upload=True)
+    assert_same(rg, rc, ig, ic, 0, n)
+    assert s.node_visits == int(cnt["node_visits"].sum())
+    sh = np.zeros(n, tthip.SHADOW_DTYPE)
+    sh["origin"] = rays["origin"][:n]
+    sh["direction"] = rays["direction"][:n]
+    sh["t"] = np.where(np.arange(n) % 3 == 0, np.float32(np.inf), np.float32(2.5))
+    sh["illumination"] = 1.0
+    sh["PixelIndex"] = np.arange(n)
+    shadow_both(engine, sc, sh, 0, n, 1, upload=False)
+
+
+def test_degenerate_rays_later_bounce_info(engine):
+    """Bounce 1 with every pixel's GlobalColors.Data.w = -1: the _PrimaryTriangleInfo position /
+    direction form is written for all rays, including the NaN ones (NaN payloads may differ)."""
+    sc = tthip.single_object_scene(tthip.Mesh.soup(8, 3000, 1.0, 0.15))
+    n = 2048
+    base = degenerate_rays(n, 8)
+    rays = np.zeros(2 * n, tthip.RAY_DTYPE)
+    rays[n:] = base[:n]  # odd bounces read the second half
+    colors = np.zeros(n, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = -1.0
+    engine.upload(sc)
+    rg, rc = rays.copy(), rays.copy()
+    ig, ic = np.zeros((n, 4), np.uint32), np.zeros((n, 4), np.uint32)
+    engine.trace(rg, n, 1, FAR, n, 1, info=ig, colors=colors)
+    st, _ = O.trace(sc, rc, n, 1, FAR, n, 1, info=ic, colors=colors, nthreads=CPU_THREADS)
+    assert st == 0
+    assert np.array_equal(rg.view(np.uint8), rc.view(np.uint8))
+    assert same_floats(ig.view(np.float32), ic.view(np.float32))

@@ -260,3 +260,19 @@ def test_refit_traces_like_a_fresh_build():
     assert O.trace(refit, b, W * H, 0, 1000.0, W, H, nthreads=8)[0] == 0
     assert np.array_equal(a["hits"][: W * H, :3], b["hits"][: W * H, :3])
     assert (a["hits"][: W * H, 1] != 0xFFFFFFFF).sum() > W * H // 4
+
+
+def test_degenerate_rays_are_deterministic_on_the_oracle():
+    """Zero / NaN / infinite / denormal ray components: the oracle finishes every ray (hit, miss or
+    Reps exhaustion), single- and multi-threaded runs agree bit for bit."""
+    from test_gpu_parity import degenerate_rays
+
+    sc = tthip.single_object_scene(tthip.Mesh.soup(3, 2000, 1.0, 0.15))
+    n = 2048
+    rays = degenerate_rays(n, 5)
+    a, b = rays.copy(), rays.copy()
+    st1, c1 = O.trace(sc, a, n, 0, 1000.0, n, 1, counts=True, nthreads=1)
+    st2, c2 = O.trace(sc, b, n, 0, 1000.0, n, 1, counts=True, nthreads=4)
+    assert st1 == st2 == 0
+    assert np.array_equal(a.view(np.uint8), b.view(np.uint8)) and np.array_equal(c1, c2)
+    assert set(np.unique(c1["status"]).tolist()) <= {0, 1}
