@@ -635,3 +635,33 @@ def test_degenerate_rays_later_bounce_info(engine):
     assert st == 0
     assert np.array_equal(rg.view(np.uint8), rc.view(np.uint8))
     assert same_floats(ig.view(np.float32), ic.view(np.float32))
+
+
+# ------------------------------------------------------------------ coincident / degenerate geometry
+def duplicate_soup(seed, n_base=1500):
+    """A soup where every triangle exists 1-3 times at identical positions (exact t ties between
+    triangles in different leaves: the first found in the reference's order must win), plus
+    zero-area, collinear and far-away triangles."""
+    rng = np.random.default_rng(seed)
+    base = rng.uniform(-1, 1, (n_base, 1, 3)) + rng.normal(scale=0.08, size=(n_base, 3, 3))
+    reps = rng.integers(1, 4, n_base)
+    tris = np.repeat(base, reps, axis=0)
+    extra = [np.repeat(rng.uniform(-1, 1, (1, 3)), 3, axis=0) for _ in range(40)]            # points
+    extra += [np.outer(rng.uniform(0, 1, 3), rng.normal(size=3)) for _ in range(40)]         # collinear
+    extra += [rng.uniform(-1, 1, (1, 3)) * 1e5 + rng.normal(size=(3, 3)) for _ in range(10)]  # far away
+    tris = np.concatenate([tris, np.stack(extra)]).astype(np.float32)
+    tris = tris[rng.permutation(len(tris))]
+    pos = tris.reshape(-1, 3)
+    idx = np.arange(len(pos), dtype=np.int32)
+    return tthip.single_object_scene(tthip.Mesh.from_arrays(pos, idx))
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_coincident_triangles_tie_break(engine, seed):
+    sc = duplicate_soup(seed)
+    W, H = 200, 150
+    c2w, ip = tthip.unity_camera((0.1, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 60, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    assert s.accepts == int(cnt["accepts"].sum())
