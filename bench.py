@@ -313,7 +313,14 @@ def main():
             if time.perf_counter() - tc0 >= args.cpu_seconds:
                 break
         tcpu = time.perf_counter() - tc0
+        model = "unknown"
+        try:
+            with open("/proc/cpuinfo") as f:
+                model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+        except OSError:
+            pass
         cpu = {"value": round(done / tcpu / 1e6, 3), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+               "host_cpu": model, "hardware_threads": os.cpu_count(),
                "sample": f"full step workload ({WH} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
                          f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {nthreads} threads; "
                          f"C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
