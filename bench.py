@@ -338,6 +338,14 @@ def main():
         traffic = round(float(tj["mean_bytes_per_launch"]))
         traffic_src = "profiles/traffic_latest.json <- " + tj.get("source", "?").split(" ")[0]
 
+    # unit utilisation of the same kernels from the round's separate PMC passes (tools/pmc_units.sh
+    # -> profiles/units_latest.json): the binding units, since the scene is cache-resident
+    units = None
+    upath = os.path.join(REPO, "profiles", "units_latest.json")
+    if os.path.exists(upath) and (W, H, args.tris) == (1920, 1080, 262267):
+        with open(upath) as f:
+            units = json.load(f).get("mean")
+
     ms_per_step = elapsed * 1e3 / args.steps
     result = {
         "metric": METRIC,
@@ -364,11 +372,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),
+                     "units_busy": units,
                      "note": "achieved = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean HIP-event "
                              "launch time; bytes are served mostly from L2/MALL, so the loop is bound by VALU issue "
                              "and load latency, not HBM (DESIGN.md §5). traffic = fabric bytes per launch from "
                              + (traffic_src or "no PMC pass") + " (2 x FETCH_SIZE + WRITE_SIZE, includes "
-                             "Infinity-Cache hits)"},
+                             "Infinity-Cache hits); units_busy = VALU-issue / texture-data / texture-address "
+                             "busy fractions of the same kernels (profiles/units_latest.json, tools/pmc_units.sh)"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(result), flush=True)
