@@ -7,11 +7,16 @@
 //    shrinking best hit;
 //  * the first occluder ends the ray (:441-454): t = 0 is written back to ShadowRaysBuffer;
 //  * triangle_intersect_shadow (CommonData.cginc:593-634) reads the material BEFORE the t-range
-//    test and ignores IsBackground / ShadowCaster surfaces; Cutout and glass (specTrans == 1)
-//    need the texture atlases and are rejected on the host (TT_ERR_UNSUPPORTED);
+//    test and ignores IsBackground / ShadowCaster surfaces; Cutout runs the point-sampled alpha
+//    test; glass (specTrans == 1) tints through the BC6H texture atlas and is rejected on the host
+//    (TT_ERR_UNSUPPORTED);
+//  * the same cooperative drain phase as the closest-hit kernel (tt_wide.h): once the queue is dry
+//    the live rays regroup into 2/4/8-lane groups; a triangle pass tests up to G of the leaf's
+//    triangles and the ray is occluded if any of them occludes (what the sequential loop, which
+//    stops at the first occluder, concludes as well).
 //  * a ray that reaches |t| writes NEEPosA (bounce 0) and GlobalColors.Direct (bounce 0, t >= 0),
 //    the radiance-cache paths stay with the caller (see include/truetrace_hip.h).
-#include "tt_traverse.h"
+#include "tt_wide.h"
 
 namespace {
 
@@ -60,6 +65,209 @@ __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, con
     return occ;
 }
 
+struct ShadowWide {
+    LaneRay ray, wray;
+    float max_distance;
+    uint2 cg, tg;
+    uint32_t oct;
+    int32_t stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset, Reps;
+    uint32_t ray_index, scol, gcol;
+    bool active;
+};
+
+struct ShadowCounters {
+    uint32_t &nodes, &tris, &blas, &occ, &vis, &reps, &ovf;
+};
+
+template <int GN>
+__device__ __forceinline__ void regroup_shadow(ShadowWide& s, uint64_t lead, uint32_t lane) {
+    const uint32_t grp = lane / GN;
+    uint32_t src = 0;
+    bool has = false;
+    uint64_t m = lead;
+    for (uint32_t r = 0; m; r++) {  // wave-uniform: at most 32 leaders
+        const uint32_t b = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        if (grp == r) {
+            src = b;
+            has = true;
+        }
+    }
+    shfl_ray(s.ray, src);
+    shfl_ray(s.wray, src);
+    s.max_distance = shfl_f(s.max_distance, src);
+    s.cg.x = shfl_u(s.cg.x, src);
+    s.cg.y = shfl_u(s.cg.y, src);
+    s.tg.x = shfl_u(s.tg.x, src);
+    s.tg.y = shfl_u(s.tg.y, src);
+    s.oct = shfl_u(s.oct, src);
+    s.stack_size = shfl_i(s.stack_size, src);
+    s.tlas_ss = shfl_i(s.tlas_ss, src);
+    s.NodeOffset = shfl_i(s.NodeOffset, src);
+    s.TriOffset = shfl_i(s.TriOffset, src);
+    s.MatOffset = shfl_i(s.MatOffset, src);
+    s.Reps = shfl_i(s.Reps, src);
+    s.ray_index = shfl_u(s.ray_index, src);
+    s.scol = shfl_u(s.scol, src);
+    s.gcol = shfl_u(s.gcol, src);
+    s.active = has;
+}
+
+// The drain loop of the any-hit kernel for groups of G lanes (tt_wide.h's wide_phase with the
+// any-hit step): `occlude(st)` / `reach(st)` / `exhaust(st)` write a finished ray's outputs (group's
+// first lane only).
+template <bool STATS, bool MATCHECK, int G, class Occ, class Reach, class Exh>
+__device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s_stack)[TT_BLOCK],
+                                  uint2* __restrict__ spill, uint32_t spill_stride, __amdgpu_buffer_rsrc_t nodes,
+                                  __amdgpu_buffer_rsrc_t tris, uint32_t lane, ShadowCounters C, Occ& occlude,
+                                  Reach& reach, Exh& exhaust) {
+    const uint32_t sub = lane & (G - 1);
+    const uint32_t tid = st.scol, gtid = st.gcol;  // the stack the TT_PUSH / TT_POP macros address
+    int32_t& stack_size = st.stack_size;
+    while (true) {
+        const uint64_t lead = __ballot(st.active && sub == 0u);
+        const uint32_t n = (uint32_t)__popcll(lead);
+        if (n == 0u) return;
+        if constexpr (G < 8) {
+            if (n * (2 * G) <= TT_WAVE) {
+                regroup_shadow<2 * G>(st, lead, lane);
+                shadow_wide_phase<STATS, MATCHECK, 2 * G>(A, st, s_stack, spill, spill_stride, nodes, tris, lane, C,
+                                                          occlude, reach, exhaust);
+                return;
+            }
+        }
+        // ------------------------------------------------------------- node phase
+        if (st.active && st.tg.y == 0u) {
+            if (st.Reps >= TT_MAX_REPS) {  // :373 loop bound
+                st.active = false;
+                if (sub == 0u) {
+                    if (STATS) C.reps++;
+                    exhaust(st);
+                }
+            } else if (st.cg.y & 0xff000000u) {  // :374-403
+                const uint32_t cio = firstbithigh(st.cg.y);
+                const uint32_t slot = (cio - 24u) ^ (st.oct & 0xffu);
+                const uint32_t rel = __builtin_popcount(st.cg.y & ~(0xffffffffu << slot));
+                const uint32_t child = st.cg.x + rel;
+                st.cg.y &= ~(1u << cio);
+                bool ok = true;
+                if (st.cg.y & 0xff000000u) TT_PUSH(st.cg, ok);
+                if (ok) {
+                    const uint32_t no = node_offset(child);
+                    const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
+                                n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
+                                n4 = buffer_load16(nodes, no + 64u);
+                    const uint32_t hitmask =
+                        group_or<G>(node_intersect_part<G>(n0, n1, n2, n3, n4, st.ray, st.oct, st.max_distance, sub));
+                    st.cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
+                    st.tg.y = hitmask & 0x00ffffffu;
+                    st.cg.x = n1.x + (uint32_t)st.NodeOffset;
+                    st.tg.x = n1.y + (uint32_t)st.TriOffset;
+                    st.Reps++;
+                    if (STATS && sub == 0u) C.nodes++;
+                } else {
+                    st.active = false;
+                    if (sub == 0u) {
+                        if (STATS) C.ovf++;
+                        atomicAdd(&A.ctl->err_overflow, 1u);
+                    }
+                }
+            } else {  // :404-407
+                st.tg = st.cg;
+                st.cg = make_uint2(0u, 0u);
+            }
+            if (st.active && st.tg.y != 0u && st.tlas_ss == -1) {  // :411-435 TLAS leaf -> BLAS
+                const uint32_t mo = firstbithigh(st.tg.y);
+                st.tg.y &= ~(1u << mo);
+                const int32_t mesh_id = A.tlas[st.tg.x + mo];
+                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
+                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                st.NodeOffset = mo4.y;
+                st.TriOffset = mo4.x;
+                bool ok = true;
+                if (st.tg.y != 0u) TT_PUSH(st.tg, ok);
+                if (ok && (st.cg.y & 0xff000000u)) TT_PUSH(st.cg, ok);
+                if (ok) {
+                    st.tlas_ss = stack_size;
+                    st.MatOffset = mo4.z;
+                    const LaneRay& ray = st.ray;
+                    LaneRay nr;
+                    nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
+                    nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
+                    nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
+                    nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
+                    nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
+                    nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
+                    nr.ix = 1.0f / nr.dx;
+                    nr.iy = 1.0f / nr.dy;
+                    nr.iz = 1.0f / nr.dz;
+                    st.ray = nr;
+                    st.oct = octant_inv4(st.ray);
+                    st.cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                    if (STATS && sub == 0u) C.blas++;
+                } else {
+                    st.active = false;
+                    if (sub == 0u) {
+                        if (STATS) C.ovf++;
+                        atomicAdd(&A.ctl->err_overflow, 1u);
+                    }
+                }
+                st.tg.y = 0u;
+            }
+        }
+
+        // --------------------------------------------------------- triangle phase
+        // :436-446: highest bit first until the first occluder; lane `sub` takes the sub-th triangle
+        if (st.active && st.tg.y != 0u) {
+            uint32_t m = st.tg.y;
+#pragma unroll
+            for (uint32_t k = 0; k + 1 < (uint32_t)G; k++)
+                if (k < sub && m) m &= ~(1u << firstbithigh(m));
+            const bool has = m != 0u;
+            bool occ = false;
+            if (has)
+                occ = shadow_triangle<MATCHECK>(tris, A.mat, (int32_t)(st.tg.x + firstbithigh(m)), st.MatOffset, st.ray,
+                                                st.max_distance);
+            // the first occluder in the reference's order (lowest sub), G if none
+            const uint32_t first = (uint32_t)group_min_u64<G>(occ ? (uint64_t)sub : (uint64_t)G);
+            if (STATS && sub == 0u)
+                C.tris += first < (uint32_t)G ? first + 1u : min((uint32_t)__builtin_popcount(st.tg.y), (uint32_t)G);
+            if (first < (uint32_t)G) {  // :449-454
+                st.active = false;
+                if (sub == 0u) {
+                    if (STATS) C.occ++;
+                    occlude(st);
+                }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < (uint32_t)G; k++)
+                    if (st.tg.y) st.tg.y &= ~(1u << firstbithigh(st.tg.y));
+            }
+        }
+
+        // ----------------------------------------- advance: pop / finish (:456-494)
+        if (st.active && st.tg.y == 0u && (st.cg.y & 0xff000000u) == 0u) {
+            if (stack_size != 0) {
+                if (stack_size == st.tlas_ss) {
+                    st.NodeOffset = 0;
+                    st.TriOffset = 0;
+                    st.tlas_ss = -1;
+                    st.ray = st.wray;
+                    st.oct = octant_inv4(st.ray);
+                }
+                TT_POP(st.cg);
+            } else {
+                st.active = false;
+                if (sub == 0u) {
+                    if (STATS) C.vis++;
+                    reach(st);
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 template <bool STATS, bool MATCHECK>
@@ -91,12 +299,52 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
     int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, Reps = 0;
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_occ = 0, c_rays = 0, c_vis = 0, c_reps = 0, c_ovf = 0;
 
+    // a finished ray's outputs: occluded (:449-454), Reps exhausted (:373), reached the light (:457-485)
+    auto do_occlude = [&](uint32_t ri) {
+        A.rays[ri].t = 0.0f;
+        if (A.visibility) A.visibility[ri] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    };
+    auto do_exhaust = [&](uint32_t ri) {
+        if (A.visibility) A.visibility[ri] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+    };
+    auto do_reach = [&](uint32_t ri, const LaneRay& w) {  // TerrainExists false
+        const tt_shadow_ray& R = A.rays[ri];
+        const uint32_t pix = R.PixelIndex;
+        const float t = R.t;
+        if (A.visibility) A.visibility[ri] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        if (A.bounce == 0 && A.nee_pos && pix / A.width < A.height) {
+            const float d = fabsf(t);
+            A.nee_pos[pix] = make_float4(w.ox + w.dx * d, w.oy + w.dy * d, w.oz + w.dz * d, 0.0f);
+        }
+        if (A.bounce == 0 && t >= 0.0f && A.colors) {  // Direct += illumination * throughput (1)
+            tt_col_data& C = A.colors[pix];
+            C.Direct[0] = C.Direct[0] + R.illumination[0] * 1.0f;
+            C.Direct[1] = C.Direct[1] + R.illumination[1] * 1.0f;
+            C.Direct[2] = C.Direct[2] + R.illumination[2] * 1.0f;
+        }
+    };
+
     while (true) {
         // ---------------------------------------------------------------- refill
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
         const bool pool_dry = !more && pool_next >= pool_end;
         if (n_idle == TT_WAVE && pool_dry) break;
+#if TT_WIDE
+        // the queue is dry and the live rays fit in 2-lane groups: cooperative drain (tt_wide.h)
+        if (pool_dry && TT_WAVE - n_idle <= TT_WIDE_ENTER) {
+            ShadowWide st{ray, wray, max_distance, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset,
+                          MatOffset, Reps, ray_index, tid, gtid, active};
+            regroup_shadow<2>(st, __ballot(active), lane);
+            auto occ_w = [&](const ShadowWide& w) { do_occlude(w.ray_index); };
+            auto reach_w = [&](const ShadowWide& w) { do_reach(w.ray_index, w.wray); };
+            auto exh_w = [&](const ShadowWide& w) { do_exhaust(w.ray_index); };
+            shadow_wide_phase<STATS, MATCHECK, 2>(A, st, s_stack, spill, spill_stride, nodes, tris, lane,
+                                                  ShadowCounters{c_nodes, c_tris, c_blas, c_occ, c_vis, c_reps, c_ovf},
+                                                  occ_w, reach_w, exh_w);
+            break;
+        }
+#endif
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
@@ -150,7 +398,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
             if (Reps >= TT_MAX_REPS) {  // :373 loop bound: nothing is written
                 active = false;
                 if (STATS) c_reps++;
-                if (A.visibility) A.visibility[ray_index] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+                do_exhaust(ray_index);
             } else if (cg.y & 0xff000000u) {  // :374-403
                 const uint32_t cio = firstbithigh(cg.y);
                 const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
@@ -226,8 +474,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 shadow_triangle<MATCHECK>(tris, A.mat, (int32_t)(tg.x + ti), MatOffset, ray, max_distance);
             if (STATS) c_tris++;
             if (occ) {  // :449-454
-                A.rays[ray_index].t = 0.0f;
-                if (A.visibility) A.visibility[ray_index] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                do_occlude(ray_index);
                 active = false;
                 if (STATS) c_occ++;
             }
@@ -245,20 +492,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 }
                 TT_POP(cg);
             } else {  // reached the light (TerrainExists false): :457-485
-                const tt_shadow_ray& R = A.rays[ray_index];
-                const uint32_t pix = R.PixelIndex;
-                const float t = R.t;
-                if (A.visibility) A.visibility[ray_index] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-                if (A.bounce == 0 && A.nee_pos && pix / A.width < A.height) {
-                    const float d = fabsf(t);
-                    A.nee_pos[pix] = make_float4(wray.ox + wray.dx * d, wray.oy + wray.dy * d, wray.oz + wray.dz * d, 0.0f);
-                }
-                if (A.bounce == 0 && t >= 0.0f && A.colors) {  // Direct += illumination * throughput (1)
-                    tt_col_data& C = A.colors[pix];
-                    C.Direct[0] = C.Direct[0] + R.illumination[0] * 1.0f;
-                    C.Direct[1] = C.Direct[1] + R.illumination[1] * 1.0f;
-                    C.Direct[2] = C.Direct[2] + R.illumination[2] * 1.0f;
-                }
+                do_reach(ray_index, wray);
                 active = false;
                 if (STATS) c_vis++;
             }
