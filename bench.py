@@ -179,10 +179,18 @@ def main():
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the HIP engine has no CPU fallback)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # RCCL ("nccl") over xGMI, one process per GPU. TT_BENCH_DIST_BACKEND=gloo is a rehearsal mode for
+    # boxes with fewer GPUs than ranks (ranks share devices, host-side reductions); not a bench mode.
+    backend = os.environ.get("TT_BENCH_DIST_BACKEND", "nccl")
+    gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend=backend)
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -195,7 +203,7 @@ def main():
     am.add_parent(blas, None, mats)
     scene = am.build()
     log(f"rank {rank}: scene {len(scene.tris)} tris, {len(scene.nodes)} nodes, build {time.time() - t0:.2f}s")
-    eng = tthip.Engine(local_rank, stream=torch.cuda.current_stream(dev).cuda_stream)
+    eng = tthip.Engine(gpu, stream=torch.cuda.current_stream(dev).cuda_stream)
     eng.upload(scene)
 
     # ------------------------------------------------------------------ resident rays
@@ -239,10 +247,10 @@ def main():
     launch_ms = eng.timing_read()
     total_rays = float(rays_per_step * args.steps)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([total_rays], dtype=torch.float64, device=dev)
+        r = torch.tensor([total_rays], dtype=torch.float64, device=red_dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         total_rays = float(r.item())
 
@@ -282,7 +290,7 @@ def main():
 
     gather_ms = None
     if args.gather and world > 1:
-        hits = rays[: WH * 48].view(WH, 48)[:, 32:48].contiguous()
+        hits = rays[: WH * 48].view(WH, 48)[:, 32:48].contiguous().to(red_dev)
         out = [torch.empty_like(hits) for _ in range(world)] if rank == 0 else None
         torch.cuda.synchronize(dev)
         tg = time.perf_counter()
