@@ -374,6 +374,8 @@ def main():
                    "seed": hex(args.seed), "parallelism": f"sample-sharded x{world} (frames_accumulated=rank)",
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
+                   "trace_ms_primary_median": round(float(np.median(prim_ms)), 4),
+                   "trace_ms_bounce_median": round(float(np.median(bnc_ms)), 4),
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
                    "gather_ms": None if gather_ms is None else round(gather_ms, 3),
                    "aux_shadow_nee": shadow, "aux_configs": aux},
