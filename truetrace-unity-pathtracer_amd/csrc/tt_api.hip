@@ -98,6 +98,7 @@ struct tt_ctx {
     DevBuf<int32_t> tlas;
     DevBuf<tt_mesh_data> mesh_raw;
     DevBuf<MeshGpu> mesh;
+    DevBuf<LeafMesh> leaf;
     DevBuf<uint32_t> mat_tag;
     DevBuf<CutoutMat> mat_cut;
     DevBuf<uint8_t> atlas;      // _AlphaAtlas (R8)
@@ -325,6 +326,19 @@ void derive_mesh(const tt_mesh_data& in, MeshGpu& o) {
     o.root = in.mesh_data_bvh_offsets & 0x7fffffff;
 }
 
+// LeafMesh[i] = the mesh record TLASBVH8Indices[i] names (indices were validated at upload)
+std::vector<LeafMesh> derive_leaves(const std::vector<int32_t>& tlas, const std::vector<tt_mesh_data>& md) {
+    std::vector<LeafMesh> out(std::max<size_t>(1, tlas.size()));
+    for (size_t i = 0; i < tlas.size(); i++) {
+        LeafMesh& l = out[i];
+        std::memset(&l, 0, sizeof(l));
+        const int32_t m = tlas[i];
+        if (m >= 0 && (size_t)m < md.size()) derive_mesh(md[(size_t)m], l.m);
+        l.mesh_id = m;
+    }
+    return out;
+}
+
 void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
     o.p0x = t.pos0[0];
     o.p0y = t.pos0[1];
@@ -462,6 +476,7 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->mesh.release();
     c->mat_tag.release();
     c->mat_cut.release();
+    c->leaf.release();
     c->atlas.release();
     tt_refit_free(c->refit);
     for (auto& kv : c->blas_refit) {
@@ -566,6 +581,13 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     TT_HIP(c, hipMemcpy(c->tlas.p, tlas, sizeof(int32_t) * n_tlas, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->mesh_raw.p, md, sizeof(tt_mesh_data) * n_mesh, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->mesh.p, mg.data(), sizeof(MeshGpu) * n_mesh, hipMemcpyHostToDevice));
+    {
+        const std::vector<LeafMesh> lv = derive_leaves(std::vector<int32_t>(tlas, tlas + n_tlas),
+                                                       std::vector<tt_mesh_data>(md, md + n_mesh));
+        c->leaf.release();
+        if ((e = c->leaf.alloc(lv.size())) != hipSuccess) return hip_fail(c, e, "TLAS leaf records");
+        TT_HIP(c, hipMemcpy(c->leaf.p, lv.data(), sizeof(LeafMesh) * lv.size(), hipMemcpyHostToDevice));
+    }
     TT_HIP(c, hipMemcpy(c->mat_tag.p, tags.data(), sizeof(uint32_t) * tags.size(), hipMemcpyHostToDevice));
     if (h.any_cutout) {
         if ((e = c->mat_cut.alloc(h.cut.size())) != hipSuccess) return hip_fail(c, e, "cutout records");
@@ -769,6 +791,8 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     TT_HIP(c, hipSetDevice(c->device));
     TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, md, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, hipMemcpyAsync(c->mesh.p + first, mg.data(), sizeof(MeshGpu) * count, hipMemcpyHostToDevice, c->stream));
+    const std::vector<LeafMesh> lv = derive_leaves(c->host.tlas, c->host.mesh);
+    TT_HIP(c, hipMemcpyAsync(c->leaf.p, lv.data(), sizeof(LeafMesh) * lv.size(), hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -849,6 +873,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.n_tris = c->host.n_tris;
     a.tlas = c->tlas.p;
     a.mesh = c->mesh.p;
+    a.leaf = c->leaf.p;
     a.mat_tag = c->mat_tag.p;
     a.n_mat = c->host.n_mat;
     a.mat = mat_view(c);
@@ -968,6 +993,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     a.n_tris = c->host.n_tris;
     a.tlas = c->tlas.p;
     a.mesh = c->mesh.p;
+    a.leaf = c->leaf.p;
     a.mat_tag = c->mat_tag.p;
     a.n_mat = c->host.n_mat;
     a.mat = mat_view(c);

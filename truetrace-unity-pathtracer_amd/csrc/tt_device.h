@@ -31,6 +31,17 @@ struct MeshGpu {
 };
 static_assert(sizeof(MeshGpu) == 64, "MeshGpu is 64 bytes");
 
+// The mesh record of TLASBVH8Indices[i], stored at i (80 B): a TLAS leaf reaches its instance's
+// transform and offsets with one round of independent loads instead of the dependent
+// TLASBVH8Indices -> _MeshData pair (IntersectionKernels.compute:197-213). Rebuilt whenever the
+// mesh records or the TLAS indices change.
+struct LeafMesh {
+    MeshGpu m;
+    int32_t mesh_id;  // TLASBVH8Indices[i]
+    int32_t pad[3];
+};
+static_assert(sizeof(LeafMesh) == 80, "LeafMesh is 80 bytes");
+
 // Control block, zeroed by hipMemsetAsync before every trace launch.
 struct TraceControl {
     uint32_t seg_ticket[8 * 32];  // per-segment dequeue tickets, one 128-B line each
@@ -70,6 +81,7 @@ struct TraceArgs {
     uint32_t n_tris;
     const int32_t* tlas;         // TLASBVH8Indices
     const MeshGpu* mesh;         // traversal-layout mesh records
+    const LeafMesh* leaf;        // mesh record per TLAS index position
     const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
     uint32_t n_mat;
     MatView mat;                 // material checks (Invisible, Cutout)
@@ -96,6 +108,7 @@ struct ShadowArgs {
     uint32_t n_tris;
     const int32_t* tlas;
     const MeshGpu* mesh;
+    const LeafMesh* leaf;
     const uint32_t* mat_tag;     // MaterialData.Tag per material (n_mat entries)
     uint32_t n_mat;
     MatView mat;                 // material checks (IsBackground / ShadowCaster, Cutout)

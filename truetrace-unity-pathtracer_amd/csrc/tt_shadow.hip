@@ -179,10 +179,9 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
             if (st.active && st.tg.y != 0u && st.tlas_ss == -1) {  // :411-435 TLAS leaf -> BLAS
                 const uint32_t mo = firstbithigh(st.tg.y);
                 st.tg.y &= ~(1u << mo);
-                const int32_t mesh_id = A.tlas[st.tg.x + mo];
-                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4* mp = reinterpret_cast<const float4*>(A.leaf + (st.tg.x + mo));  // LeafMesh
                 const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
                 st.NodeOffset = mo4.y;
                 st.TriOffset = mo4.x;
                 bool ok = true;
@@ -431,10 +430,9 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
             if (active && tg.y != 0u && tlas_ss == -1) {  // :411-435 TLAS leaf -> BLAS
                 const uint32_t mo = firstbithigh(tg.y);
                 tg.y &= ~(1u << mo);
-                const int32_t mesh_id = A.tlas[tg.x + mo];
-                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
                 const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
                 NodeOffset = mo4.y;
                 TriOffset = mo4.x;
                 bool ok = true;

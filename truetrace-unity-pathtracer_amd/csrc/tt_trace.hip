@@ -333,10 +333,10 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
                 const uint32_t mo = firstbithigh(tg.y);
                 tg.y &= ~(1u << mo);
-                mesh_id = A.tlas[tg.x + mo];
-                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
+                const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
                 const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
+                const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
+                mesh_id = reinterpret_cast<const int4*>(mp)[4].x;
                 NodeOffset = mo4.y;
                 TriOffset = mo4.x;
                 bool ok = true;

@@ -238,10 +238,10 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
             if (st.active && st.tg.y != 0u && st.tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
                 const uint32_t mo = firstbithigh(st.tg.y);
                 st.tg.y &= ~(1u << mo);
-                st.mesh_id = A.tlas[st.tg.x + mo];
-                const float4* mp = reinterpret_cast<const float4*>(A.mesh + st.mesh_id);
+                const float4* mp = reinterpret_cast<const float4*>(A.leaf + (st.tg.x + mo));  // LeafMesh
                 const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + st.mesh_id)[3];
+                const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
+                st.mesh_id = reinterpret_cast<const int4*>(mp)[4].x;
                 st.NodeOffset = mo4.y;
                 st.TriOffset = mo4.x;
                 bool ok = true;
