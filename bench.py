@@ -165,6 +165,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather hit records to rank 0 after timing")
+    ap.add_argument("--shard", choices=["sample", "tiles"], default="sample",
+                    help="sample: every rank traces its own full-frame sample (weak scaling, default); tiles: "
+                         "the frame's 64x64 tiles are dealt round-robin to ranks, each traces its pixels and their "
+                         "bounces, and the primary hit records are RCCL-gathered to rank 0 (strong scaling, "
+                         "SURVEY 8e)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     ap.add_argument("--aux", default="c3,c4,c5",
                     help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,c5; '' = none)")
@@ -213,20 +218,34 @@ def main():
     colors["Data"][:, 3] = 1.0  # shade set Data.w = CurBounce + 1 = 1 at bounce 0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
     c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H, 0.3, far)
-    eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
-    s_prim = eng.trace(rays, WH, 0, far, W, H, info=info, device=True, stats=True)
-    nb = eng.enqueue_bounce(rays, WH, 0, far, W, H, frames=rank, max_bounce=1, device=True)
+    tiles = args.shard == "tiles"
+    frames = 0 if tiles else rank
+    if tiles:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), at the buffer's start
+        import ttdist
+
+        pix = torch.from_numpy(ttdist.tile_pixels(W, H, world, rank)).to(dev)
+        n_prim = int(pix.shape[0])
+        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
+        rays.view(2 * WH, 48)[:n_prim] = full.view(WH, 48)[pix]
+        del full
+    else:
+        n_prim = WH
+        eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
+    s_prim = eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, stats=True)
+    nb = eng.enqueue_bounce(rays, n_prim, 0, far, W, H, frames=frames, max_bounce=1, device=True)
     s_bnc = eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
     torch.cuda.synchronize(dev)
-    rays_per_step = WH + nb
-    B_prim = alg_bytes(s_prim, 0, WH)
+    rays_per_step = n_prim + nb
+    B_prim = alg_bytes(s_prim, 0, n_prim)
     B_bnc = alg_bytes(s_bnc, 1, nb)
-    log(f"rank {rank}: primary {WH} rays nodes/ray {s_prim.node_visits / WH:.2f} tris/ray {s_prim.tri_tests / WH:.2f} "
+    log(f"rank {rank}: primary {n_prim} rays nodes/ray {s_prim.node_visits / max(n_prim, 1):.2f} "
+        f"tris/ray {s_prim.tri_tests / max(n_prim, 1):.2f} "
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(nb, 1):.2f} "
         f"tris/ray {s_bnc.tri_tests / max(nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}")
 
     def step():
-        eng.trace(rays, WH, 0, far, W, H, info=info, device=True, asynchronous=True)
+        eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, asynchronous=True)
         eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
 
     for _ in range(args.warmup):
@@ -264,7 +283,7 @@ def main():
     # rays first (occluded rays get t = 0 in place), only the kernel is timed (HIP events).
     shadow = None
     if not args.no_shadow:
-        sr = nee_rays(torch, rays, WH, far, light=(0.0, 9.0, 0.5))
+        sr = nee_rays(torch, rays, n_prim, far, light=(0.0, 9.0, 0.5))
         ns = int(sr.shape[0]) // 48
         work = torch.empty_like(sr)
         s_sh = None
@@ -288,15 +307,30 @@ def main():
     if world == 1 and args.aux:
         aux = aux_configs(torch, tthip, eng, dev, args, set(args.aux.split(",")))
 
-    gather_ms = None
-    if args.gather and world > 1:
-        hits = rays[: WH * 48].view(WH, 48)[:, 32:48].contiguous().to(red_dev)
-        out = [torch.empty_like(hits) for _ in range(world)] if rank == 0 else None
+    gather_ms, gather_parity = None, None
+    if (args.gather or tiles) and world > 1:
+        # primary hit records (16 B per ray) to rank 0 in one collective; tile shards are padded to
+        # the largest (ttdist.gather_hits) and rank 0 reassembles the frame in screen order
+        hits = rays[: n_prim * 48].view(n_prim, 48)[:, 32:48].contiguous().view(torch.int32).to(red_dev)
         torch.cuda.synchronize(dev)
         tg = time.perf_counter()
-        dist.gather(hits, out, dst=0)
+        if tiles:
+            parts = ttdist.gather_hits(hits, world, rank)
+        else:
+            out = [torch.empty_like(hits) for _ in range(world)] if rank == 0 else None
+            dist.gather(hits, out, dst=0)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - tg) * 1e3
+        if tiles and rank == 0:
+            frame = ttdist.assemble_tiles(parts, W, H, world)
+            # SURVEY 8(e) parity: the gathered frame must equal one GPU tracing the whole frame
+            one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
+            eng.trace(one, WH, 0, far, W, H, device=True)
+            ref = one[: WH * 48].view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+            gather_parity = bool(np.array_equal(frame, ref))
+            log(f"gathered frame: {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels, "
+                f"identical to a single-GPU trace: {gather_parity}")
 
     if rank != 0:
         if world > 1:
@@ -314,7 +348,7 @@ def main():
         nthreads = max(1, args.cpu_threads)
         done, reps, tc0 = 0, 0, time.perf_counter()
         while True:
-            O.trace(scene, host_rays, WH, 0, far, W, H, info=host_info, nthreads=nthreads)
+            O.trace(scene, host_rays, n_prim, 0, far, W, H, info=host_info, nthreads=nthreads)
             O.trace(scene, host_rays, nb, 1, far, W, H, info=host_info, colors=colors, nthreads=nthreads)
             done += rays_per_step
             reps += 1
@@ -329,7 +363,7 @@ def main():
             pass
         cpu = {"value": round(done / tcpu / 1e6, 3), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
                "host_cpu": model, "hardware_threads": os.cpu_count(),
-               "sample": f"full step workload ({WH} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
+               "sample": f"full step workload ({n_prim} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
                          f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {nthreads} threads; "
                          f"C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
                          + ("not run: no .NET runtime (dotnet) on the box" if shutil.which("dotnet") is None
@@ -364,20 +398,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if tiles else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza)",
         "config": {"workload": "sponza_primary_plus_1_bounce_1080p", "scene": "Sponza-shaped CWBVH8 (C2)",
                    "tris": int(len(scene.tris)), "cwbvh_nodes": int(len(scene.nodes)), "width": W, "height": H,
-                   "primary_rays": WH, "bounce_rays": int(nb), "rays_per_step_per_gpu": int(rays_per_step),
-                   "seed": hex(args.seed), "parallelism": f"sample-sharded x{world} (frames_accumulated=rank)",
+                   "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_per_gpu": int(rays_per_step),
+                   "seed": hex(args.seed),
+                   "parallelism": (f"64x64 screen tiles round-robin over {world} ranks + RCCL gather of primary hits"
+                                   if tiles else f"sample-sharded x{world} (frames_accumulated=rank)"),
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
                    "trace_ms_primary_median": round(float(np.median(prim_ms)), 4),
                    "trace_ms_bounce_median": round(float(np.median(bnc_ms)), 4),
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
                    "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                   "gather_identical_to_1gpu": gather_parity,
                    "aux_shadow_nee": shadow, "aux_configs": aux},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
