@@ -112,6 +112,7 @@ struct tt_ctx {
     struct BlasRefit {
         RefitDev dev;
         uint64_t gen = ~0ull;
+        uint32_t node_base = ~0u;  // the mesh's NodeOffset the plan was built for
         DevBuf<float> boxes;
     };
     std::map<uint32_t, BlasRefit> blas_refit;
@@ -674,7 +675,7 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     }
     TT_HIP(c, hipSetDevice(c->device));
     tt_ctx::BlasRefit& R = c->blas_refit[p->mesh_index];
-    if (R.gen != c->scene_gen || R.boxes.n < (size_t)6 * p->n_tris) {
+    if (R.gen != c->scene_gen || R.node_base != node_base || R.boxes.n < (size_t)6 * p->n_tris) {
         RefitPlan plan;
         const tt_cwbvh_node* base = c->host.nodes.data() + node_base;
         if (!tt_refit_build_plan(base, (uint32_t)(c->host.nodes.size() - node_base), plan))
@@ -687,6 +688,7 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
         TT_HIP(c, tt_refit_prepare(plan, base, n_used, R.dev));
         if (R.boxes.n < (size_t)6 * p->n_tris) TT_HIP(c, R.boxes.alloc((size_t)6 * p->n_tris));
         R.gen = c->scene_gen;
+        R.node_base = node_base;
     }
     BlasConstructArgs a{};
     a.vertices = vertices;
