@@ -343,8 +343,15 @@ tt_status tt_timing_read(tt_ctx* ctx, float* ms, uint32_t max, uint32_t* n);
 
 /* SIMD-efficiency diagnostics of the last synchronous TT_TRACE_STATS launch: wave loop
  * iterations, iterations with node-phase work, node-phase lanes, iterations with triangle-phase
- * work, triangle-phase lanes, active lanes (sums over waves); out8[6..7] reserved. */
+ * work, triangle-phase lanes, active lanes (sums over waves), node-phase lanes visiting the
+ * same node as the wave's first node-phase lane, wave-uniform node phases. */
 tt_status tt_trace_diagnostics(const tt_ctx* ctx, uint64_t* out8);
+
+/* Self-test of the fast reciprocal the kernels use for rcp() (numerics contract: correctly
+ * rounded 1.0f/x): evaluates it and the full IEEE division for all 2^32 fp32 bit patterns on the
+ * context's device and returns the number of inputs whose results differ (bitwise, NaN == NaN) in
+ * *mismatches; 0 is required. Synchronous, a few milliseconds. */
+tt_status tt_selftest_rcp(tt_ctx* ctx, uint64_t* mismatches);
 
 /* Wait for all work issued on the context's stream. */
 tt_status tt_sync(tt_ctx* ctx);

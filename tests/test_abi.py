@@ -60,3 +60,20 @@ def test_null_context_is_rejected():
     assert L.tt_trace_closest(None, C.byref(p), None, None, None, None) == tthip.TT_ERR_INVALID_ARG
     assert L.tt_scene_upload(None, None, 0, None, 0, None, 0, None, 0, None, 0) == tthip.TT_ERR_INVALID_ARG
     assert L.tt_last_error(None) == b"null context"
+
+
+def test_every_bound_hip_function_has_a_prototype():
+    """ctypes defaults to int arguments: a bound function without argtypes would truncate the
+    64-bit context pointer. Every declared function that takes arguments must carry argtypes."""
+    L = tthip.hip_lib()
+    src = open(os.path.join(REPO, "include", "truetrace_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    no_args = set(re.findall(r"\b(tt_[a-z0-9_]+)\s*\(\s*(?:void)?\s*\)", src))
+    missing = [n for n in declared("truetrace_hip.h") if n not in no_args and getattr(L, n).argtypes is None]
+    assert not missing, missing
+
+
+def test_null_context_selftest_is_rejected():
+    L = tthip.hip_lib()
+    n = C.c_uint64()
+    assert L.tt_selftest_rcp(None, C.addressof(n)) == tthip.TT_ERR_INVALID_ARG

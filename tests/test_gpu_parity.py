@@ -21,6 +21,13 @@ from parity_util import CPU_THREADS, FAR, assert_same, same_floats, trace_both
 pytestmark = pytest.mark.gpu
 
 
+# ------------------------------------------------------------------ numerics contract
+def test_fast_reciprocal_is_correctly_rounded_for_every_input(engine):
+    """rcp() is pinned to the correctly rounded 1.0f/x; the kernels compute it as v_rcp_f32 + one FMA
+    Newton step for normal inputs with a full-division fallback. Exhaustive over all 2^32 inputs."""
+    assert engine.selftest_rcp() == 0
+
+
 # ------------------------------------------------------------------ known answers
 @pytest.mark.parametrize("case", K.ALL_CASES, ids=lambda c: c.__name__)
 def test_kat_on_gpu(engine, case):

@@ -31,6 +31,8 @@ for b in (0, 1):
     print(f"  active lanes / iteration {d['active_lanes'] / it:.1f} of 64")
     print(f"  node phase: {d['node_iters'] / it:.1%} of iterations run it, {d['node_lanes'] / max(d['node_iters'], 1):.1f} lanes each")
     print(f"  tri phase:  {d['tri_iters'] / it:.1%} of iterations run it, {d['tri_lanes'] / max(d['tri_iters'], 1):.1f} lanes each")
+    print(f"  node uniformity: {d['lead_same_lanes'] / max(d['node_lanes'], 1):.1%} of node visits share the first lane's node, "
+          f"{d['uniform_node_iters'] / max(d['node_iters'], 1):.1%} of node phases are wave-uniform")
     print(f"  node visits per wave-iteration {s.node_visits / it:.1f}, tri tests per wave-iteration {s.tri_tests / it:.1f}")
     print(f"  per ray: nodes {s.node_visits / n:.2f}, tris {s.tri_tests / n:.2f}, BLAS entries {s.blas_entries / n:.2f}, "
           f"kernel (stats build) {s.kernel_ms:.3f} ms")

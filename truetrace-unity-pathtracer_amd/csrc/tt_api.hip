@@ -31,6 +31,7 @@ hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_of
 hipError_t tt_launch_resolve(const tt_ray_data* rays, uint32_t ray_offset, uint32_t n, float far_plane,
                              const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* md, uint32_t n_mesh,
                              float* out, hipStream_t st);
+hipError_t tt_launch_rcp_selftest(unsigned long long* d_bad, hipStream_t st);
 
 namespace {
 
@@ -532,6 +533,24 @@ tt_status tt_timing_read(tt_ctx* c, float* ms, uint32_t max, uint32_t* n) {
 tt_status tt_trace_diagnostics(const tt_ctx* c, uint64_t* out8) {
     if (!c || !out8) return TT_ERR_INVALID_ARG;
     for (int k = 0; k < 8; k++) out8[k] = c->last_diag[k];
+    return TT_OK;
+}
+
+tt_status tt_selftest_rcp(tt_ctx* c, uint64_t* mismatches) {
+    if (!c || !mismatches) return TT_ERR_INVALID_ARG;
+    TT_HIP(c, hipSetDevice(c->device));
+    DevBuf<unsigned long long> bad;
+    struct Release {
+        DevBuf<unsigned long long>& b;
+        ~Release() { b.release(); }
+    } release{bad};
+    TT_HIP(c, bad.alloc(1));
+    TT_HIP(c, hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), c->stream));
+    TT_HIP(c, tt_launch_rcp_selftest(bad.p, c->stream));
+    unsigned long long h = 0;
+    TT_HIP(c, hipMemcpyAsync(&h, bad.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    *mismatches = (uint64_t)h;
     return TT_OK;
 }
 

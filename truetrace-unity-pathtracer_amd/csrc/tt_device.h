@@ -7,6 +7,25 @@
 
 #include "../../include/truetrace_hip.h"
 
+// rcp(x) of the reference (IntersectionKernels.compute:22,145,214), pinned to the correctly rounded
+// IEEE 1.0f / x (numerics contract, include/truetrace_hip.h). v_rcp_f32 plus one FMA Newton step
+// (e = fma(-a, r, 1), r' = fma(e, r, r)) equals the correctly rounded quotient for every input whose
+// biased exponent is 1..252 -- checked exhaustively over all 2^32 inputs on gfx950
+// (tt_selftest_rcp, tests/test_gpu_parity.py) -- so only zeros, denormals, |a| >= 2^126 (denormal
+// result), infinities and NaNs take the compiler's full division sequence (v_div_scale/fmas/fixup).
+#ifndef TT_FAST_RCP
+#define TT_FAST_RCP 1  // 0: always the full division sequence (A/B measurement)
+#endif
+__device__ __forceinline__ float rcp_rn(float a) {
+    if (!TT_FAST_RCP) return 1.0f / a;
+    const uint32_t e = (__float_as_uint(a) >> 23) & 0xffu;
+    if (__builtin_expect(e - 1u < 252u, 1)) {
+        const float r = __builtin_amdgcn_rcpf(a);
+        return __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
+    }
+    return 1.0f / a;
+}
+
 // Traversal-layout triangle, 48 B: the 36 B of positions the Moller-Trumbore test reads
 // (CudaTriangle pos0/posedge1/posedge2, CommonData.cginc:63-66) + MatDat, padded so one
 // triangle is three 16-B loads. Built from AggTris at upload; AggTris itself also stays in
@@ -50,7 +69,8 @@ struct TraceControl {
     uint32_t pad[2];
     unsigned long long stats[8];  // rays, nodes, tris, blas, hits, reps_exhausted, overflow, accepts
     unsigned long long diag[8];   // STATS-build SIMD diagnostics: wave iterations, node-phase iterations,
-                                  // node-phase lanes, tri-phase iterations, tri-phase lanes, active lanes
+                                  // node-phase lanes, tri-phase iterations, tri-phase lanes, active lanes,
+                                  // node lanes sharing the first lane's node, wave-uniform node phases
 };
 
 // Per-material record for the Cutout alpha test (row f3), 32 B; only uploaded when a Cutout

@@ -40,7 +40,7 @@ __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, con
     const float hy = fma_(r.dz, e2x, -(r.dx * e2z));
     const float hz = fma_(r.dx, e2y, -(r.dy * e2x));
     const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
-    const float f = 1.0f / aa;
+    const float f = rcp_rn(aa);
     const float sx = r.ox - p0x, sy = r.oy - p0y, sz = r.oz - p0z;
     const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
     const float qx = fma_(sy, e1z, -(sz * e1y));
@@ -198,9 +198,9 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
                     nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
                     nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
                     nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = 1.0f / nr.dx;
-                    nr.iy = 1.0f / nr.dy;
-                    nr.iz = 1.0f / nr.dz;
+                    nr.ix = rcp_rn(nr.dx);
+                    nr.iy = rcp_rn(nr.dy);
+                    nr.iz = rcp_rn(nr.dz);
                     st.ray = nr;
                     st.oct = octant_inv4(st.ray);
                     st.cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
@@ -374,9 +374,9 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 ray.dy = __uint_as_float(r1.y);
                 ray.dz = __uint_as_float(r1.z);
                 max_distance = fabsf(__uint_as_float(r1.w));
-                ray.ix = 1.0f / ray.dx;
-                ray.iy = 1.0f / ray.dy;
-                ray.iz = 1.0f / ray.dz;
+                ray.ix = rcp_rn(ray.dx);
+                ray.iy = rcp_rn(ray.dy);
+                ray.iz = rcp_rn(ray.dz);
                 wray = ray;
                 oct = octant_inv4(ray);
                 cg = make_uint2(0u, 0x80000000u);
@@ -448,9 +448,9 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                     nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
                     nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
                     nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = 1.0f / nr.dx;
-                    nr.iy = 1.0f / nr.dy;
-                    nr.iz = 1.0f / nr.dz;
+                    nr.ix = rcp_rn(nr.dx);
+                    nr.iy = rcp_rn(nr.dy);
+                    nr.iz = rcp_rn(nr.dz);
                     ray = nr;
                     oct = octant_inv4(ray);
                     cg = make_uint2((uint32_t)mo4.w, 0x80000000u);

@@ -102,6 +102,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
     uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
+    uint32_t d_lead_same = 0, d_uniform = 0;  // node-step uniformity (lanes sharing the first lane's node)
 #ifdef TT_DIAG_TL
     uint32_t d_tl = 0;
 #endif
@@ -121,9 +122,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         w.dx = __uint_as_float(r1.x);
         w.dy = __uint_as_float(r1.y);
         w.dz = __uint_as_float(r1.z);
-        w.ix = 1.0f / w.dx;
-        w.iy = 1.0f / w.dy;
-        w.iz = 1.0f / w.dz;
+        w.ix = rcp_rn(w.dx);
+        w.iy = rcp_rn(w.dy);
+        w.iz = rcp_rn(w.dz);
         return w;
 #else
         return wray;
@@ -220,9 +221,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 ray.dx = __uint_as_float(r1.x);
                 ray.dy = __uint_as_float(r1.y);
                 ray.dz = __uint_as_float(r1.z);
-                ray.ix = 1.0f / ray.dx;
-                ray.iy = 1.0f / ray.dy;
-                ray.iz = 1.0f / ray.dz;
+                ray.ix = rcp_rn(ray.dx);
+                ray.iy = rcp_rn(ray.dy);
+                ray.iz = rcp_rn(ray.dz);
 #if !TT_WRAY_RELOAD
                 wray = ray;
 #endif
@@ -304,11 +305,26 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 bool ok = true;
                 if (cg.y & 0xff000000u) TT_PUSH(cg, ok);
                 if (ok) {
+                    if (STATS) {  // how many node-phase lanes visit the same node as the first one
+                        const uint32_t lead = __builtin_amdgcn_readfirstlane(child);
+                        const uint64_t same = __ballot(child == lead), all = __ballot(true);
+                        d_lead_same += child == lead ? 1u : 0u;
+                        d_uniform += (same == all && lane == (uint32_t)__builtin_ctzll(all)) ? 1u : 0u;
+                    }
                     const uint32_t no = node_offset(child);
                     const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
                                 n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
                                 n4 = buffer_load16(nodes, no + 64u);
                     const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
+#ifdef TT_EXP_LOAD_PAD  // diagnostic: N extra 16-B loads of the same node per step (texture-path headroom)
+                    {
+#pragma unroll
+                        for (int k = 0; k < TT_EXP_LOAD_PAD; k++) {
+                            const uint4 pad = buffer_load16(nodes, no + 16u * (uint32_t)(k % 5));
+                            asm volatile("; pad use %0" ::"v"(pad.x));
+                        }
+                    }
+#endif
 #ifdef TT_DIAG_NODEHIST  // diagnostic: visits per node index -> diag_times (as uint32[n_nodes])
                     if (A.diag_times) atomicAdd(reinterpret_cast<uint32_t*>(A.diag_times) + child, 1u);
 #endif
@@ -352,9 +368,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
                     nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
                     nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = 1.0f / nr.dx;
-                    nr.iy = 1.0f / nr.dy;
-                    nr.iz = 1.0f / nr.dz;
+                    nr.ix = rcp_rn(nr.dx);
+                    nr.iy = rcp_rn(nr.dy);
+                    nr.iz = rcp_rn(nr.dz);
                     ray = nr;
                     oct = octant_inv4(ray);
                     cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
@@ -447,6 +463,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #pragma unroll
             for (int k = 0; k < 6; k++) atomicAdd(&A.ctl->diag[k], (unsigned long long)d[k]);
         }
+        const uint32_t ls = wave_sum(d_lead_same), un = wave_sum(d_uniform);
+        if (lane == 0) {
+            atomicAdd(&A.ctl->diag[6], (unsigned long long)ls);
+            atomicAdd(&A.ctl->diag[7], (unsigned long long)un);
+        }
     }
 }
 
@@ -535,9 +556,9 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
                 ray.dx = __uint_as_float(r1.x);
                 ray.dy = __uint_as_float(r1.y);
                 ray.dz = __uint_as_float(r1.z);
-                ray.ix = 1.0f / ray.dx;
-                ray.iy = 1.0f / ray.dy;
-                ray.iz = 1.0f / ray.dz;
+                ray.ix = rcp_rn(ray.dx);
+                ray.iy = rcp_rn(ray.dy);
+                ray.iz = rcp_rn(ray.dz);
                 wray = ray;
                 oct = octant_inv4(ray);
                 best.t = A.far_plane;
@@ -642,9 +663,9 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
                     nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
                     nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
                     nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = 1.0f / nr.dx;
-                    nr.iy = 1.0f / nr.dy;
-                    nr.iz = 1.0f / nr.dz;
+                    nr.ix = rcp_rn(nr.dx);
+                    nr.iy = rcp_rn(nr.dy);
+                    nr.iz = rcp_rn(nr.dz);
                     ray = nr;
                     oct = octant_inv4(ray);
                     cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
@@ -674,7 +695,7 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
             const float hy = fma_(ray.dz, e2x, -(ray.dx * e2z));
             const float hz = fma_(ray.dx, e2y, -(ray.dy * e2x));
             const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
-            const float f = 1.0f / aa;
+            const float f = rcp_rn(aa);
             const float sx = ray.ox - p0x, sy = ray.oy - p0y, sz = ray.oz - p0z;
             const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
             const float qx = fma_(sy, e1z, -(sz * e1y));

@@ -250,7 +250,7 @@ __device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tri
     const float hy = fma_(r.dz, e2x, -(r.dx * e2z));
     const float hz = fma_(r.dx, e2y, -(r.dy * e2x));
     const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
-    const float f = 1.0f / aa;
+    const float f = rcp_rn(aa);
     const float sx = r.ox - p0x, sy = r.oy - p0y, sz = r.oz - p0z;
     const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
     // q = cross(s, e1)

@@ -258,9 +258,9 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
                     nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
                     nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
                     nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = 1.0f / nr.dx;
-                    nr.iy = 1.0f / nr.dy;
-                    nr.iz = 1.0f / nr.dz;
+                    nr.ix = rcp_rn(nr.dx);
+                    nr.iy = rcp_rn(nr.dy);
+                    nr.iz = rcp_rn(nr.dz);
                     st.ray = nr;
                     st.oct = octant_inv4(st.ray);
                     st.cg = make_uint2((uint32_t)mo4.w, 0x80000000u);

@@ -170,7 +170,8 @@ _HIP = None
 HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_destroy", "tt_last_error",
                "tt_scene_upload", "tt_scene_update_nodes", "tt_scene_update_meshdata", "tt_scene_bytes",
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
-               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics"]
+               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics",
+               "tt_selftest_rcp"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
@@ -266,6 +267,8 @@ def hip_lib():
         L.tt_scene_validate.restype = i32
         L.tt_trace_diagnostics.argtypes = [vp, vp]
         L.tt_trace_diagnostics.restype = i32
+        L.tt_selftest_rcp.argtypes = [vp, vp]
+        L.tt_selftest_rcp.restype = i32
         L.tt_timing_reset.argtypes = [vp]
         L.tt_timing_read.argtypes = [vp, vp, u32, C.POINTER(u32)]
         for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
@@ -618,8 +621,16 @@ class Engine:
     def diagnostics(self) -> dict:
         d = np.zeros(8, np.uint64)
         self._check(self.L.tt_trace_diagnostics(self.h, d.ctypes.data), "tt_trace_diagnostics")
-        keys = ["iterations", "node_iters", "node_lanes", "tri_iters", "tri_lanes", "active_lanes"]
-        return {k: int(v) for k, v in zip(keys, d[:6])}
+        keys = ["iterations", "node_iters", "node_lanes", "tri_iters", "tri_lanes", "active_lanes", "lead_same_lanes",
+                "uniform_node_iters"]
+        return {k: int(v) for k, v in zip(keys, d)}
+
+    def selftest_rcp(self) -> int:
+        """Inputs (of all 2^32 fp32 bit patterns) where the kernels' fast reciprocal differs from the
+        correctly rounded 1.0f/x on this device (tt_selftest_rcp); must be 0."""
+        n = C.c_uint64()
+        self._check(self.L.tt_selftest_rcp(self.h, C.addressof(n)), "tt_selftest_rcp")
+        return n.value
 
     def scene_bytes(self) -> int:
         b = C.c_uint64()
