@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -23,6 +24,7 @@ void tt_shadow_occupancy_table(int* out4);
 uint32_t tt_trace_block_size();
 uint32_t tt_trace_spill_entries();
 uint32_t tt_trace_lds_bytes();
+uint32_t tt_trace_ncache_cap();
 hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uint32_t h, float near_plane, float far_plane,
                               int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays, hipStream_t st);
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
@@ -100,6 +102,8 @@ struct tt_ctx {
     DevBuf<tt_mesh_data> mesh_raw;
     DevBuf<MeshGpu> mesh;
     DevBuf<LeafMesh> leaf;
+    DevBuf<uint32_t> ncache;      // LDS node-cache plan: slot -> node index, then slot -> child code
+    uint32_t n_ncache = 0, ncache_root = 0;
     DevBuf<uint32_t> mat_tag;
     DevBuf<CutoutMat> mat_cut;
     DevBuf<uint8_t> atlas;      // _AlphaAtlas (R8)
@@ -341,6 +345,76 @@ std::vector<LeafMesh> derive_leaves(const std::vector<int32_t>& tlas, const std:
     return out;
 }
 
+// LDS node-cache plan of the closest-hit kernel (tt_trace.hip, TT_NCACHE): up to `cap` nodes
+// taken breadth first from the TLAS root (node 0) through TLAS leaves into the instances' BLAS
+// roots, so the cache holds the scene graph's top levels, which take most node visits
+// (profiles/r01_diag_nodehist.txt: depth <= 3 carries ~50% of primary visits). A node's internal
+// children (base_child + NodeOffset + rank, IntersectionKernels.compute:160-163) are cached as a
+// whole group in consecutive slots or not at all, so the kernel finds child `rank` of a cached
+// group at `first slot + rank`. codes[s] = first child slot + 1 of slot s (0: children not cached);
+// leaves[i].root_code = slot + 1 of leaf i's BLAS root for its NodeOffset. Only the topology is
+// planned here; the kernel copies the cached nodes from the live buffer at every launch.
+void plan_node_cache(const SceneHost& h, std::vector<LeafMesh>& leaves, uint32_t cap, std::vector<uint32_t>& ids,
+                     std::vector<uint32_t>& codes, uint32_t& root_code) {
+    ids.clear();
+    codes.clear();
+    root_code = 0;
+    for (LeafMesh& l : leaves) l.root_code = 0;
+    const uint64_t N = h.nodes.size();
+    if (cap == 0 || N == 0) return;
+    struct Item {
+        uint32_t node, off, slot;
+        bool tlas;
+    };
+    std::deque<Item> q;
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> roots;  // (root, NodeOffset) -> code
+    ids.push_back(0);
+    codes.push_back(0);
+    root_code = 1;
+    q.push_back({0u, 0u, 0u, true});
+    while (!q.empty()) {
+        const Item it = q.front();
+        q.pop_front();
+        const tt_cwbvh_node& n = h.nodes[it.node];
+        const uint32_t k = (uint32_t)__builtin_popcount(n.e_imask >> 24);
+        const uint64_t base = (uint64_t)n.base_child + it.off;
+        if (k && ids.size() + k <= cap && base + k <= N) {
+            codes[it.slot] = (uint32_t)ids.size() + 1u;
+            for (uint32_t r = 0; r < k; r++) {
+                q.push_back({(uint32_t)(base + r), it.off, (uint32_t)ids.size(), it.tlas});
+                ids.push_back((uint32_t)(base + r));
+                codes.push_back(0);
+            }
+        }
+        if (!it.tlas) continue;
+        for (int c = 0; c < 8; c++) {  // TLAS leaf children: instance records base_tri + offset + j
+            const uint32_t m = (n.meta[c >> 2] >> (8 * (c & 3))) & 0xffu;
+            if (m == 0 || (m & 0x1fu) >= 24u) continue;
+            const uint32_t cnt = (uint32_t)__builtin_popcount((m >> 5) & 7u);
+            for (uint32_t j = 0; j < cnt; j++) {
+                const uint64_t li = (uint64_t)n.base_tri + (m & 0x1fu) + j;
+                if (li >= leaves.size() || li >= h.tlas.size()) continue;
+                LeafMesh& L = leaves[li];
+                if (L.mesh_id < 0 || (size_t)L.mesh_id >= h.mesh.size()) continue;
+                const uint32_t root = (uint32_t)L.m.root, off = (uint32_t)L.m.NodeOffset;
+                const auto key = std::make_pair(root, off);
+                auto f = roots.find(key);
+                if (f == roots.end()) {
+                    uint32_t code = 0;
+                    if (ids.size() < cap && root < N) {
+                        code = (uint32_t)ids.size() + 1u;
+                        q.push_back({root, off, (uint32_t)ids.size(), false});
+                        ids.push_back(root);
+                        codes.push_back(0);
+                    }
+                    f = roots.emplace(key, code).first;
+                }
+                L.root_code = f->second;
+            }
+        }
+    }
+}
+
 void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
     o.p0x = t.pos0[0];
     o.p0y = t.pos0[1];
@@ -562,6 +636,10 @@ tt_status tt_sync(tt_ctx* c) {
     return TT_OK;
 }
 
+namespace {
+tt_status refresh_leaves(tt_ctx* c);
+}
+
 tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris,
                           uint32_t n_tris, const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md,
                           uint32_t n_mesh, const tt_material* mats, uint32_t n_mat) {
@@ -601,13 +679,6 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     TT_HIP(c, hipMemcpy(c->tlas.p, tlas, sizeof(int32_t) * n_tlas, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->mesh_raw.p, md, sizeof(tt_mesh_data) * n_mesh, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->mesh.p, mg.data(), sizeof(MeshGpu) * n_mesh, hipMemcpyHostToDevice));
-    {
-        const std::vector<LeafMesh> lv = derive_leaves(std::vector<int32_t>(tlas, tlas + n_tlas),
-                                                       std::vector<tt_mesh_data>(md, md + n_mesh));
-        c->leaf.release();
-        if ((e = c->leaf.alloc(lv.size())) != hipSuccess) return hip_fail(c, e, "TLAS leaf records");
-        TT_HIP(c, hipMemcpy(c->leaf.p, lv.data(), sizeof(LeafMesh) * lv.size(), hipMemcpyHostToDevice));
-    }
     TT_HIP(c, hipMemcpy(c->mat_tag.p, tags.data(), sizeof(uint32_t) * tags.size(), hipMemcpyHostToDevice));
     if (h.any_cutout) {
         if ((e = c->mat_cut.alloc(h.cut.size())) != hipSuccess) return hip_fail(c, e, "cutout records");
@@ -619,6 +690,13 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->any_shadow_skip = c->host.any_shadow_skip;
     c->any_cutout = c->host.any_cutout;
     c->any_atlas_shadow = c->host.any_atlas_shadow;
+    c->leaf.release();
+    c->n_ncache = 0;
+    c->ncache_root = 0;
+    {
+        const tt_status st = refresh_leaves(c);
+        if (st != TT_OK) return st;
+    }
     c->has_scene = true;
     return TT_OK;
 }
@@ -776,6 +854,36 @@ tt_status tt_scene_validate(const tt_cwbvh_node* nodes, uint32_t n_nodes, const 
     return st;
 }
 
+namespace {
+// Rebuilds the TLAS leaf records and the LDS node-cache plan from the host mirror (on upload and
+// after node / mesh-record updates, which may change the topology) and uploads both on the stream.
+tt_status refresh_leaves(tt_ctx* c) {
+    std::vector<LeafMesh> lv = derive_leaves(c->host.tlas, c->host.mesh);
+    std::vector<uint32_t> ids, codes;
+    uint32_t root_code = 0;
+    plan_node_cache(c->host, lv, tt_trace_ncache_cap(), ids, codes, root_code);
+    if (c->leaf.n < lv.size()) {
+        c->leaf.release();
+        const hipError_t e = c->leaf.alloc(lv.size());
+        if (e != hipSuccess) return hip_fail(c, e, "TLAS leaf records");
+    }
+    TT_HIP(c, hipMemcpyAsync(c->leaf.p, lv.data(), sizeof(LeafMesh) * lv.size(), hipMemcpyHostToDevice, c->stream));
+    ids.insert(ids.end(), codes.begin(), codes.end());
+    if (!ids.empty()) {
+        if (c->ncache.n < ids.size()) {
+            c->ncache.release();
+            const hipError_t e = c->ncache.alloc(ids.size());
+            if (e != hipSuccess) return hip_fail(c, e, "node-cache plan");
+        }
+        TT_HIP(c, hipMemcpyAsync(c->ncache.p, ids.data(), sizeof(uint32_t) * ids.size(), hipMemcpyHostToDevice, c->stream));
+    }
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    c->n_ncache = (uint32_t)codes.size();
+    c->ncache_root = root_code;
+    return TT_OK;
+}
+}  // namespace
+
 tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
@@ -792,7 +900,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, nodes, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
-    return TT_OK;
+    return refresh_leaves(c);
 }
 
 tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, const tt_mesh_data* md) {
@@ -812,10 +920,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     TT_HIP(c, hipSetDevice(c->device));
     TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, md, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, hipMemcpyAsync(c->mesh.p + first, mg.data(), sizeof(MeshGpu) * count, hipMemcpyHostToDevice, c->stream));
-    const std::vector<LeafMesh> lv = derive_leaves(c->host.tlas, c->host.mesh);
-    TT_HIP(c, hipMemcpyAsync(c->leaf.p, lv.data(), sizeof(LeafMesh) * lv.size(), hipMemcpyHostToDevice, c->stream));
-    TT_HIP(c, hipStreamSynchronize(c->stream));
-    return TT_OK;
+    return refresh_leaves(c);
 }
 
 tt_status tt_scene_bytes(const tt_ctx* c, uint64_t* bytes) {
@@ -912,6 +1017,9 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.bounce = p->bounce;
     a.flags = p->flags;
     a.tile_swizzle = (p->n_rays == wh && p->screen_width % 8 == 0 && p->screen_height % 8 == 0) ? 1u : 0u;
+    a.ncache = c->ncache.p;
+    a.n_ncache = c->n_ncache;
+    a.root_code = c->ncache_root;
     const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout;
     const uint32_t waves_needed = (p->n_rays + 255u) / 256u;  // one TT_CHUNK per wave at least
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;

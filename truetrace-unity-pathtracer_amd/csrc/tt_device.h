@@ -56,8 +56,9 @@ static_assert(sizeof(MeshGpu) == 64, "MeshGpu is 64 bytes");
 // mesh records or the TLAS indices change.
 struct LeafMesh {
     MeshGpu m;
-    int32_t mesh_id;  // TLASBVH8Indices[i]
-    int32_t pad[3];
+    int32_t mesh_id;     // TLASBVH8Indices[i]
+    uint32_t root_code;  // LDS node-cache code of the instance's BLAS root (0: not cached, else slot + 1)
+    int32_t pad[2];
 };
 static_assert(sizeof(LeafMesh) == 80, "LeafMesh is 80 bytes");
 
@@ -118,6 +119,9 @@ struct TraceArgs {
     int32_t bounce;
     uint32_t flags;              // TT_TRACE_*
     uint32_t tile_swizzle;       // 1: work index -> 8x8 screen tiles (n_rays == W*H, W,H % 8 == 0)
+    const uint32_t* ncache;      // LDS node cache plan: node index per slot [n_ncache], then child codes [n_ncache]
+    uint32_t n_ncache;           // cached nodes (<= tt_trace_ncache_cap())
+    uint32_t root_code;          // cache code of the TLAS root (node 0): 1 when slot 0 holds it
 };
 
 // Any-hit visibility launch (tt_shadow.hip, kernel_shadow replacement).

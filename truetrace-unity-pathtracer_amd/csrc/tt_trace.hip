@@ -70,6 +70,18 @@ template <bool STATS, bool MATCHECK, int INFO>
 __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
+#if TT_NCACHE
+    // LDS node cache: copies of the top levels of the scene graph (planned on the host, breadth
+    // first from the TLAS root, whole sibling groups; tt_api.hip plan_node_cache), loaded from the
+    // live node buffer at every launch so refits are always seen. A node group whose children sit in
+    // the cache carries their first slot + 1 in bits 8-23 of cg.y (bits the reference leaves zero
+    // in a node group: imask is bits 0-7, child hit bits 24-31); the visit order is unchanged.
+    __shared__ uint4 s_nc[TT_NCACHE * 5];
+    __shared__ uint32_t s_ncode[TT_NCACHE];
+    for (uint32_t i = tid; i < A.n_ncache * 5u; i += TT_BLOCK) s_nc[i] = A.nodes[A.ncache[i / 5u] * 5u + i % 5u];
+    for (uint32_t i = tid; i < A.n_ncache; i += TT_BLOCK) s_ncode[i] = A.ncache[A.n_ncache + i];
+    __syncthreads();
+#endif
     const uint32_t gtid = blockIdx.x * TT_BLOCK + tid;
     const uint32_t spill_stride = gridDim.x * TT_BLOCK;
     uint2* __restrict__ spill = A.spill;
@@ -233,7 +245,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 best.v = 0.0f;
                 best.mesh_id = 0;
                 best.tri_id = -1;
-                cg = make_uint2(0u, 0x80000000u);
+                cg = make_uint2(0u, 0x80000000u | (TT_NCACHE ? A.root_code << 8 : 0u));
                 tg = make_uint2(0u, 0u);
                 stack_size = 0;
                 tlas_ss = -1;
@@ -311,10 +323,29 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                         d_lead_same += child == lead ? 1u : 0u;
                         d_uniform += (same == all && lane == (uint32_t)__builtin_ctzll(all)) ? 1u : 0u;
                     }
-                    const uint32_t no = node_offset(child);
-                    const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
-                                n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
-                                n4 = buffer_load16(nodes, no + 64u);
+                    uint4 n0, n1, n2, n3, n4;
+                    uint32_t ncode = 0;
+#if TT_NCACHE
+                    const uint32_t gcode = (cg.y >> 8) & 0xffffu;
+                    if (gcode) {
+                        const uint32_t s = gcode - 1u + rel;
+                        const uint4* np = s_nc + s * 5u;
+                        n0 = np[0];
+                        n1 = np[1];
+                        n2 = np[2];
+                        n3 = np[3];
+                        n4 = np[4];
+                        ncode = s_ncode[s];
+                    } else
+#endif
+                    {
+                        const uint32_t no = node_offset(child);
+                        n0 = buffer_load16(nodes, no);
+                        n1 = buffer_load16(nodes, no + 16u);
+                        n2 = buffer_load16(nodes, no + 32u);
+                        n3 = buffer_load16(nodes, no + 48u);
+                        n4 = buffer_load16(nodes, no + 64u);
+                    }
                     const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
 #ifdef TT_EXP_LOAD_PAD  // diagnostic: N extra 16-B loads of the same node per step (texture-path headroom)
                     {
@@ -328,7 +359,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #ifdef TT_DIAG_NODEHIST  // diagnostic: visits per node index -> diag_times (as uint32[n_nodes])
                     if (A.diag_times) atomicAdd(reinterpret_cast<uint32_t*>(A.diag_times) + child, 1u);
 #endif
-                    cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
+                    cg.y = (hitmask & 0xff000000u) | (n0.w >> 24) | (ncode << 8);
                     tg.y = hitmask & 0x00ffffffu;
                     cg.x = n1.x + (uint32_t)NodeOffset;
                     tg.x = n1.y + (uint32_t)TriOffset;
@@ -352,7 +383,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
                 const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
                 const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
-                mesh_id = reinterpret_cast<const int4*>(mp)[4].x;
+                const int4 mo5 = reinterpret_cast<const int4*>(mp)[4];
+                mesh_id = mo5.x;
                 NodeOffset = mo4.y;
                 TriOffset = mo4.x;
                 bool ok = true;
@@ -373,7 +405,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     nr.iz = rcp_rn(nr.dz);
                     ray = nr;
                     oct = octant_inv4(ray);
-                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u | (TT_NCACHE ? (uint32_t)mo5.y << 8 : 0u));
                     if (STATS) c_blas++;
                 } else {
                     active = false;
@@ -887,7 +919,10 @@ hipError_t tt_trace_occupancy_table(int* out12) {
 }
 
 uint32_t tt_trace_block_size() { return TT_BLOCK; }
-uint32_t tt_trace_lds_bytes() { return (uint32_t)(TT_LDS_ENTRIES * TT_BLOCK * sizeof(uint2)); }
+uint32_t tt_trace_lds_bytes() {
+    return (uint32_t)(TT_LDS_ENTRIES * TT_BLOCK * sizeof(uint2) + (TT_KERNEL_UNIFORM ? 0 : TT_NCACHE * 84));
+}
+uint32_t tt_trace_ncache_cap() { return TT_KERNEL_UNIFORM ? 0u : (uint32_t)TT_NCACHE; }
 uint32_t tt_trace_spill_entries() {
     return (TT_KERNEL_UNIFORM || TT_LDS_STACK >= TT_STACK_SIZE) ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK);
 }

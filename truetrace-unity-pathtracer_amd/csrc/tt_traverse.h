@@ -35,6 +35,9 @@
 #ifndef TT_LDS_STACK
 #define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
 #endif
+#ifndef TT_NCACHE
+#define TT_NCACHE 0       // LDS node-cache slots per block (closest-hit kernel; 0: off)
+#endif
 #ifndef TT_WAVES_PER_EU
 #define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
 #endif
