@@ -125,6 +125,38 @@ def test_golden_device_pointers(engine):
     assert np.array_equal(it.cpu().numpy().view(np.uint32).reshape(-1, 4), g["info0"])
 
 
+def test_back_to_back_async_launches(engine):
+    """Asynchronous launches skip the control-block reset: the previous trace launch's last wave
+    re-zeroes the dequeue tickets. A chain of async traces of different sizes (with a synchronous
+    launch and a stats launch in the chain) must give every ray the record a lone launch gives."""
+    import torch
+
+    sc = tthip.single_object_scene(tthip.Mesh.soup(7, 30000, 1.0, 0.08))
+    W, H = 320, 200
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 2.6), (-0.1, -0.05, -1.0), (0, 1, 0), 60.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    engine.upload(sc)
+    ref = rays.copy()
+    engine.trace(ref, W * H, 0, FAR, W, H)
+    dev = torch.device("cuda:0")
+    sizes = [W * H, 777, W * H, W * H - 5, 64, W * H, 1, W * H]
+    bufs = [torch.from_numpy(rays.view(np.uint8).copy()).to(dev) for _ in sizes]
+    torch.cuda.synchronize()
+    for k, (b, n) in enumerate(zip(bufs, sizes)):
+        if k == 3:
+            engine.trace(b, n, 0, FAR, W, H, device=True)  # synchronous, in the middle of the chain
+        elif k == 5:
+            engine.trace(b, n, 0, FAR, W, H, device=True, stats=True)
+        else:
+            engine.trace(b, n, 0, FAR, W, H, device=True, asynchronous=True)
+    torch.cuda.synchronize()
+    hits = int((ref["hits"][: W * H, 1] != 0xFFFFFFFF).sum())
+    assert hits > W * H // 4
+    for b, n in zip(bufs, sizes):
+        got = b.cpu().numpy().view(tthip.RAY_DTYPE)
+        assert np.array_equal(got["hits"][:n], ref["hits"][:n]), n
+
+
 # ------------------------------------------------------------------ random scenes
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
 def test_random_soup_random_camera(engine, seed):

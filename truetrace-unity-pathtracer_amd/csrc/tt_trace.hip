@@ -501,6 +501,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             atomicAdd(&A.ctl->diag[7], (unsigned long long)un);
         }
     }
+    sched_release(A.ctl, lane);
 }
 
 // ------------------------------------------------------------- uniform-step kernel
@@ -861,6 +862,7 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
             for (int k = 0; k < 6; k++) atomicAdd(&A.ctl->diag[k], (unsigned long long)d[k]);
         }
     }
+    sched_release(A.ctl, lane);
 }
 
 #ifndef TT_KERNEL_UNIFORM
