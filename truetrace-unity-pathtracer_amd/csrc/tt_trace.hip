@@ -118,6 +118,12 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #ifdef TT_DIAG_TL
     uint32_t d_tl = 0;
 #endif
+#ifdef TT_DIAG_BLOCKS  // wave executions of each loop block -> diag_times[k] (uint64)
+    uint32_t db[10] = {};
+#define DB(k) do { if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) db[k]++; } while (0)
+#else
+#define DB(k) do { } while (0)
+#endif
 #ifdef TT_DIAG_RAYS  // per-ray (start, end, iterations, node visits): diag_times -> uint4[n_rays]
     uint32_t r_t0 = 0, r_iter = 0, r_nodes = 0;
 #endif
@@ -159,6 +165,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     uint64_t t_wide = 0;  // when the wave entered the cooperative drain phase (0: never)
 #endif
     while (true) {
+        DB(0);
         // ---------------------------------------------------------------- refill
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
@@ -169,6 +176,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         // finished rays write their records in batches, right before their lanes are refilled
         if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry) || to_wide) {
             if (pending) {
+                DB(9);
                 finish_ray();
                 pending = false;
             }
@@ -194,6 +202,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
 #endif
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
+            DB(1);
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
@@ -305,6 +314,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
         // A lane is at the top of the reference's loop exactly when no leaf triangles are pending.
         if (active && tg.y == 0u) {
+            DB(2);
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
@@ -378,6 +388,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 cg = make_uint2(0u, 0u);
             }
             if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
+                DB(3);
                 const uint32_t mo = firstbithigh(tg.y);
                 tg.y &= ~(1u << mo);
                 const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
@@ -436,6 +447,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         if (tri_pass && active && tg.y != 0u) {
 #else
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
+            DB(4);
 #endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
@@ -451,8 +463,10 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         // One place for every lane whose group is used up, whether it came from a node step or
         // from its last triangle this pass (equivalent order: the reference pops right after).
         if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+            DB(5);
             if (stack_size != 0) {
                 if (stack_size == tlas_ss) {
+                    DB(6);
                     NodeOffset = 0;
                     TriOffset = 0;
                     tlas_ss = -1;
@@ -460,9 +474,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     oct = octant_inv4(ray);
                 }
                 TT_POP(cg);
+                DB(7);
             } else {
 #if TT_DEFER_FINISH
                 pending = true;  // written at the next refill (or when the wave drains)
+                DB(8);
 #else
                 finish_ray();
 #endif
@@ -501,6 +517,13 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             atomicAdd(&A.ctl->diag[7], (unsigned long long)un);
         }
     }
+#ifdef TT_DIAG_BLOCKS
+    if (A.diag_times)
+        for (int k = 0; k < 10; k++) {
+            const uint32_t v = wave_sum(db[k]);
+            if (lane == 0 && v) atomicAdd(A.diag_times + k, (unsigned long long)v);
+        }
+#endif
     sched_release(A.ctl, lane);
 }
 
