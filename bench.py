@@ -87,6 +87,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
       c3  C2 geometry, primary + 3 diffuse bounces (each bounce's compacted rays kept in their own
           buffer so every repetition traces identical rays)
       c4  Bistro-shaped two-level instancing, 1920x1080 primary + bounce 1
+      refit  per-frame GPU TLAS refit (C4 instances) and BLAS refit (C2 mesh as a deforming mesh)
       c5  San-Miguel-shaped 10M tris, 3840x2160 primary (single GPU; 8 GPUs shard it by tiles)"""
     import ttconfigs as T
 
@@ -135,17 +136,69 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             ms = timed_launches(eng, launches, max(1, args.warmup), max(3, args.steps // 2))
             pack(name, counts, ms, dict(extra_fn(sc), width=W, height=H, build_s=round(build_s, 1)))
             del bufs, info, colors_t
+            return sc
         except Exception as e:  # auxiliary: record, never lose the metric line
             out[name] = {"error": f"{type(e).__name__}: {e}"}
             log(f"aux {name} failed: {e}")
+            return None
+
+    def time_calls(fn, warmup, steps):
+        """Per-call GPU time (ms) of `fn` (asynchronous launches on the context stream, which is
+        torch's current stream here) from CUDA/HIP events around each call."""
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize(dev)
+        return np.asarray([a.elapsed_time(b) for a, b in ev], np.float64)
 
     if "c3" in which:
         run("c3_sponza_primary_plus_3_bounces_1080p", T.c2_sponza, T.C2_VIEW, 1920, 1080, 3,
             lambda sc: {"tris": int(len(sc.tris))})
+    sc4 = None
     if "c4" in which:
-        run("c4_bistro_primary_plus_1_bounce_1080p", T.c4_bistro, T.C4_VIEW, 1920, 1080, 1,
+        sc4 = run("c4_bistro_primary_plus_1_bounce_1080p", T.c4_bistro, T.C4_VIEW, 1920, 1080, 1,
             lambda sc: {"unique_tris": int(len(sc.tris)), "instanced_tris": sc.meta["instanced_tris"],
                         "unique_blas": 600, "instances": 2400, "cwbvh_nodes": int(len(sc.nodes))})
+    if "refit" in which:
+        # row f4 per frame: the GPU TLAS refit of the C4 scene (AssetManager.RefitTLAS, 2,400
+        # instance boxes -> TLAS nodes) and the BLAS refit of the C2 mesh as a deforming mesh
+        # (ParentObject.RefitMesh: 262k triangles re-derived + BLAS refit), device-resident inputs.
+        rec = {}
+        try:
+            if sc4 is None:
+                sc4 = T.c4_bistro()
+            eng.upload(sc4)
+            aabbs = torch.from_numpy(np.ascontiguousarray(sc4.meta["mesh_aabbs"], np.float32)).to(dev)
+            ms = time_calls(lambda: eng.tlas_refit(sc4.tlas_nodes, aabbs, device=True, asynchronous=True),
+                            3, max(5, args.steps))
+            rec["tlas_refit_c4"] = {"instances": int(len(sc4.meshdata)), "tlas_nodes": int(sc4.tlas_nodes),
+                                    "ms_median": round(float(np.median(ms)), 4), "ms_mean": round(float(ms.mean()), 4)}
+            mesh = tthip.Mesh.sponza()
+            blas = tthip.Blas(mesh)
+            am = tthip.AssetManager()
+            am.add_parent(blas, None, np.zeros(7, tthip.MAT_DTYPE))
+            eng.upload(am.build())
+            pos, nrm, idx = mesh.arrays()
+            vtx = np.zeros((len(pos), 10), np.float32)  # Unity-like stride: position, normal, tangent
+            vtx[:, 0:3], vtx[:, 3:6] = pos, nrm
+            v_t = torch.from_numpy(vtx).to(dev)
+            i_t = torch.from_numpy(np.ascontiguousarray(idx, np.int32)).to(dev)
+            l_t = torch.from_numpy(blas.leaf_order()).to(dev)
+            ms = time_calls(lambda: eng.blas_refit(0, v_t, i_t, l_t, None, device=True, asynchronous=True),
+                            3, max(5, args.steps))
+            n_tris = int(len(idx) // 3)
+            rec["blas_refit_c2"] = {"tris": n_tris, "ms_median": round(float(np.median(ms)), 4),
+                                    "ms_mean": round(float(ms.mean()), 4),
+                                    "mtris_s": round(n_tris / float(np.median(ms)) / 1e3, 1)}
+        except Exception as e:  # auxiliary: record, never lose the metric line
+            rec["error"] = f"{type(e).__name__}: {e}"
+        out["f4_refit_per_frame"] = rec
+        log(f"aux refit: {rec}")
     if "c5" in which:
         run("c5_san_miguel_primary_4k", T.c5_san_miguel, T.C5_VIEW, 3840, 2160, 0,
             lambda sc: {"tris": int(len(sc.tris)), "cwbvh_nodes": int(len(sc.nodes))})
@@ -171,8 +224,9 @@ def main():
                          "bounces, and the primary hit records are RCCL-gathered to rank 0 (strong scaling, "
                          "SURVEY 8e)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
-    ap.add_argument("--aux", default="c3,c4,c5",
-                    help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,c5; '' = none)")
+    ap.add_argument("--aux", default="c3,c4,refit,c5",
+                    help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,refit,c5;"
+                         " '' = none)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
