@@ -357,6 +357,34 @@ def main():
         log(f"shadow: {ns} NEE rays {shadow['trace_ms']} ms/launch = {shadow['mrays_s']} Mrays/s, "
             f"{shadow['occluded']} occluded")
 
+    # ---- auxiliary: the ray producers around the trace (excluded from the metric):
+    # Generate (1080p primary rays) and the diffuse-bounce enqueue with wave-ballot compaction, on a
+    # scratch copy of the traced rays; HIP events around each call (the enqueue call includes its
+    # survivor-count readback).
+    producers = None
+    if world == 1:
+        scratch = rays.clone()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2 * args.steps)]
+        for k in range(args.steps):
+            a, b = ev[k]
+            a.record()
+            eng.generate(scratch, c2w, ip, W, H, 0.3, far, jitter=1, frames=frames, max_bounce=1, device=True)
+            b.record()
+        torch.cuda.synchronize(dev)
+        gen_ms = [a.elapsed_time(b) for a, b in ev[:args.steps]]
+        for k in range(args.steps):
+            scratch.copy_(rays)
+            a, b = ev[args.steps + k]
+            a.record()
+            eng.enqueue_bounce(scratch, n_prim, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+            b.record()
+        torch.cuda.synchronize(dev)
+        enq_ms = [a.elapsed_time(b) for a, b in ev[args.steps:]]
+        producers = {"generate_ms": round(float(np.median(gen_ms)), 4), "primary_rays": n_prim,
+                     "enqueue_compact_ms": round(float(np.median(enq_ms)), 4), "bounce_rays": nb}
+        del scratch
+        log(f"ray producers: {producers}")
+
     aux = None
     if world == 1 and args.aux:
         aux = aux_configs(torch, tthip, eng, dev, args, set(args.aux.split(",")))
@@ -469,7 +497,7 @@ def main():
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
                    "gather_ms": None if gather_ms is None else round(gather_ms, 3),
                    "gather_identical_to_1gpu": gather_parity,
-                   "aux_shadow_nee": shadow, "aux_configs": aux},
+                   "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),
