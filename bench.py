@@ -205,6 +205,64 @@ def aux_configs(torch, tthip, eng, dev, args, which):
     return out
 
 
+def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
+    """BASELINE configs[4] as the north star lays it out, run after the metric when
+    N > 1: the San-Miguel-shaped scene (10 M tris) replicated on every rank, the 3840x2160 frame's
+    64x64 tiles dealt round-robin, each rank tracing its primary rays (HIP events, median of the
+    timed launches), then one gather of the 16-B hit records to rank 0, which reassembles the frame
+    and compares it with one GPU tracing the whole frame. Strong scaling: frame time = slowest rank.
+    Failures are agreed on collectively before the gather, so one rank's error cannot hang the rest."""
+    import ttconfigs as T
+    import ttdist
+
+    rec, ok, ms = {}, 1, 0.0
+    W, H, far = 3840, 2160, T.FAR
+    WH = W * H
+    try:
+        t0 = time.time()
+        sc = T.c5_san_miguel()
+        build_s = time.time() - t0
+        eng.upload(sc)
+        c2w, ip = T.C5_VIEW.camera(W, H)
+        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=1, device=True)
+        pix = torch.from_numpy(ttdist.tile_pixels(W, H, world, rank)).to(dev)
+        n = int(pix.shape[0])
+        mine = full.view(WH, 48)[pix].contiguous()
+        launch = [lambda: eng.trace(mine, n, 0, far, W, H, device=True, asynchronous=True)]
+        ms = float(np.median(timed_launches(eng, launch, max(1, args.warmup), max(3, args.steps // 2))))
+        rec.update(rays_this_rank=n, build_s=round(build_s, 1))
+    except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
+        ok = 0
+        rec["error"] = f"rank {rank}: {type(e).__name__}: {e}"
+        log(f"c5 tiles failed: {rec['error']}")
+    flags = torch.tensor([float(ok), ms], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(flags[:1], op=dist.ReduceOp.MIN)
+    t_max = torch.tensor([ms], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    if flags[0].item() < 1.0:
+        return rec if rank == 0 else None
+    hits = mine.view(n, 48)[:, 32:48].contiguous().view(torch.int32).to(red_dev)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    tg = time.perf_counter()
+    parts = ttdist.gather_hits(hits, world, rank)
+    torch.cuda.synchronize(dev)
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    if rank != 0:
+        return None
+    frame = ttdist.assemble_tiles(parts, W, H, world)
+    eng.trace(full, WH, 0, far, W, H, device=True)
+    ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+    frame_ms = float(t_max.item())
+    rec.update(config="c5_san_miguel_4k_tiles", ranks=world, tile=64, frame_rays=WH,
+               trace_ms_slowest_rank=round(frame_ms, 4), trace_ms_rank0=round(ms, 4),
+               mrays_s_frame=round(WH / frame_ms / 1e3, 1), gather_ms=round(gather_ms, 3),
+               identical_to_1gpu=bool(np.array_equal(frame, ref)))
+    log(f"c5 tiles: {rec}")
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,6 +282,8 @@ def main():
                          "bounces, and the primary hit records are RCCL-gathered to rank 0 (strong scaling, "
                          "SURVEY 8e)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
+    ap.add_argument("--no-c5-tiles", action="store_true",
+                    help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
     ap.add_argument("--aux", default="c3,c4,refit,c5",
                     help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,refit,c5;"
                          " '' = none)")
@@ -414,6 +474,10 @@ def main():
             log(f"gathered frame: {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels, "
                 f"identical to a single-GPU trace: {gather_parity}")
 
+    c5t = None
+    if world > 1 and not args.no_c5_tiles:
+        c5t = c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world)
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -497,7 +561,8 @@ def main():
                    "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
                    "gather_ms": None if gather_ms is None else round(gather_ms, 3),
                    "gather_identical_to_1gpu": gather_parity,
-                   "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux},
+                   "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
+                   "aux_c5_tiles": c5t},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),
