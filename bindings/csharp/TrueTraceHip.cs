@@ -99,6 +99,9 @@ namespace TrueTrace.Hip
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload_alpha_atlas(IntPtr ctx, byte* texels,
             uint width, uint height);
+        // _TextureAtlas decoded to RGBA half (4 x ushort per texel), for the stained-glass shadow tint.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload_texture_atlas(IntPtr ctx, ushort* rgbaHalf,
+            uint width, uint height);
         // RefitTLAS: MeshAABBs as {BBMax.xyz, BBMin.xyz} per mesh; flags: TT_TRACE_DEVICE_PTRS / ASYNC.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_tlas_refit(IntPtr ctx, uint nTlasNodes, float* meshAabbs,
             uint nMesh, uint flags);
@@ -172,6 +175,15 @@ namespace TrueTrace.Hip
         {
             fixed (byte* t = texels)
                 Check(Native.tt_scene_upload_alpha_atlas(m_ctx, t, (uint)width, (uint)height));
+        }
+
+        /// The _TextureAtlas binding of SetMeshTraceBuffers (AssetManager.cs:82): the BC6H albedo atlas
+        /// decoded to RGBA half texels (e.g. Graphics.Blit into an RGBAHalf RenderTexture, then
+        /// AsyncGPUReadback), once per scene change, before tracing shadows through glass materials.
+        public unsafe void SetTextureAtlas(ushort[] rgbaHalf, int width, int height)
+        {
+            fixed (ushort* t = rgbaHalf)
+                Check(Native.tt_scene_upload_texture_atlas(m_ctx, t, (uint)width, (uint)height));
         }
 
         /// AssetManager.RefitTLAS(Boxes, cmd) (AssetManager.cs:1473-1548): re-quantizes the TLAS

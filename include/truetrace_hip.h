@@ -243,6 +243,16 @@ tt_status tt_scene_update_meshdata(tt_ctx* ctx, uint32_t first, uint32_t count,
  * clamp(floor(uv*size)); linear = taps at floor(uv*size - 0.5) and +1, clamped, weights
  * f = x - floor(x), lerp(a,b,f) = a*(1-f) + b*f in x then y, texel value = byte / 255.0f. */
 tt_status tt_scene_upload_alpha_atlas(tt_ctx* ctx, const uint8_t* texels, uint32_t width, uint32_t height);
+/* _TextureAtlas (AssetManager.cs:82, :275; declared Texture2D<half4>, CommonData.cginc:272): the
+ * albedo atlas, BC6H in the reference, handed over DECODED as RGBA half texels (4 x uint16 IEEE
+ * binary16 per texel, row-major, same row orientation as the alpha atlas). The any-hit kernel reads
+ * it for the stained-glass shadow tint (triangle_intersect_shadow, CommonData.cginc:613-625 with
+ * IgnoreGlassShadow + StainedGlassShadows, GlobalDefines.cginc:3,8): a glass surface (specTrans == 1)
+ * never occludes; it multiplies the ray's throughput by surfaceColor * (texel.xyz + 2) / 3, texel =
+ * point-clamp sample at AlignUV(BaseUv, AlbedoTexScale, AlbedoTex). Copied to HBM; replaces any
+ * previous atlas. Without it, tt_trace_shadow on a scene with glass materials returns
+ * TT_ERR_UNSUPPORTED. */
+tt_status tt_scene_upload_texture_atlas(tt_ctx* ctx, const uint16_t* rgba_half, uint32_t width, uint32_t height);
 
 /* Per-frame TLAS refit on the GPU: AssetManager.RefitTLAS
  * (AssetManager.cs:1473-1548) with BVHRefitter.compute's RefitBVHLayer / NodeUpdate / NodeCompress
@@ -379,8 +389,10 @@ typedef struct tt_shadow_params {
  *   nee_pos        : nullable float4[W*H]; at bounce 0, unoccluded rays write
  *                    (origin + direction * |t|, 0) to NEEPosA[pixel] (:461).
  * The radiance-cache, PrimaryNEERay and bounce > 0 Indirect accumulations (RGBE / log-luminance
- * encodings) stay with the caller, driven by `visibility`. Scenes with Cutout materials or
- * specTrans == 1 (glass tint samples the texture atlas) return TT_ERR_UNSUPPORTED. */
+ * encodings) stay with the caller, driven by `visibility`. Scenes with Cutout materials need the
+ * alpha atlas and scenes with glass (specTrans == 1, stained-glass tint) the texture atlas;
+ * without them the call returns TT_ERR_UNSUPPORTED. throughput = product of the glass tints of the
+ * surfaces crossed, in traversal order (IEEE: t *= (c * (x + 2)) / 3 per component). */
 tt_status tt_trace_shadow(tt_ctx* ctx, const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
                           tt_col_data* global_colors, float* nee_pos, tt_stats* stats);
 

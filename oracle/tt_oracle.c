@@ -161,6 +161,52 @@ static float sample_linear(float u, float v) {
 }
 
 /* BaseUv = tex0 * (1 - u - v) + texedge1 * u + texedge2 * v (raw vertex UVs, ParentObject.cs:1039-1041) */
+/* ------------------------------------------------ texture atlas (f1 stained glass) */
+/* _TextureAtlas decoded to RGBA half texels (Texture2D<half4>, CommonData.cginc:272). */
+static const uint16_t* g_tex = NULL;
+static uint32_t g_tex_w = 0, g_tex_h = 0;
+
+void tt_oracle_set_texture_atlas(const uint16_t* rgba_half, uint32_t width, uint32_t height) {
+    g_tex = rgba_half;
+    g_tex_w = rgba_half ? width : 0;
+    g_tex_h = rgba_half ? height : 0;
+}
+
+/* IEEE binary16 -> binary32, exact (NaNs keep their payload, quieted) */
+static float half_to_float(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    uint32_t bits;
+    if (e == 0x1fu) {
+        bits = sign | 0x7f800000u | (m << 13) | (m ? 0x00400000u : 0u);
+    } else if (e != 0) {
+        bits = sign | ((e + 112u) << 23) | (m << 13);
+    } else if (m == 0) {
+        bits = sign;
+    } else { /* subnormal half: normalise */
+        uint32_t mm = m, ee = 113u;
+        while (!(mm & 0x400u)) {
+            mm <<= 1;
+            ee--;
+        }
+        bits = sign | (ee << 23) | ((mm & 0x3ffu) << 13);
+    }
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+/* StainedGlassShadows tint (CommonData.cginc:621-622): throughput *= surfaceColor *
+ * (_TextureAtlas.SampleLevel(my_point_clamp_sampler, AlignUV(BaseUv, AlbedoTexScale, AlbedoTex), 0).xyz
+ * + 2) / 3, per component in that association, IEEE division (pinned). */
+static void glass_tint(const tt_material* m, float bu, float bv, float throughput[3]) {
+    float tu, tv;
+    align_uv(bu, bv, m->AlbedoTexScale, m->AlbedoTex, &tu, &tv);
+    const int x = atlas_clamp(floorf(tu * (float)g_tex_w), g_tex_w);
+    const int y = atlas_clamp(floorf(tv * (float)g_tex_h), g_tex_h);
+    const uint16_t* t = &g_tex[4 * ((size_t)y * g_tex_w + (size_t)x)];
+    for (int k = 0; k < 3; k++) throughput[k] = throughput[k] * ((m->surfaceColor[k] * (half_to_float(t[k]) + 2.0f)) / 3.0f);
+}
+
 static void base_uv(const tt_cuda_triangle* T, float u, float v, float* bu, float* bv) {
     const float w = 1.0f - u - v;
     *bu = T->tex0[0] * w + T->texedge1[0] * u + T->texedge2[0] * v;
@@ -459,10 +505,11 @@ tt_status tt_oracle_trace(const tt_cwbvh_node* nodes, uint32_t n_nodes,
 /* ------------------------------------------------------ any-hit (kernel_shadow) */
 /* triangle_intersect_shadow — CommonData.cginc:593-634 with AdvancedAlphaMapped,
  * IgnoreGlassShadow and StainedGlassShadows on (GlobalDefines.cginc:1-8). The material checks run
- * BEFORE the t-range test (:611-629). Returns 1 = occluder, 0 = not, 3 = a material that needs
- * the alpha / texture atlases (Cutout, specTrans == 1: unsupported). */
+ * BEFORE the t-range test (:611-629): a glass surface (specTrans == 1) that passes the alpha test
+ * tints `throughput` even outside (0, max_distance) and never occludes. Returns 1 = occluder,
+ * 0 = not, 3 = a material whose atlas was not set (Cutout: alpha atlas, glass: texture atlas). */
 static int intersect_triangle_shadow(const scene* s, int tri_id, const Ray* ray, float max_distance,
-                                     int MatOffset, uint32_t* accepts) {
+                                     int MatOffset, uint32_t* accepts, float throughput[3]) {
     const tt_cuda_triangle* T = &s->tris[tri_id];
     const int MaterialIndex = MatOffset + (int)T->MatDat;
     const v3 pos0 = ld3(T->pos0), posedge1 = ld3(T->posedge1), posedge2 = ld3(T->posedge2);
@@ -481,13 +528,20 @@ static int intersect_triangle_shadow(const scene* s, int tri_id, const Ray* ray,
                 const tt_material* m = &s->mats[MaterialIndex];
                 const int tag = (int)m->Tag;
                 if (((tag >> TT_FLAG_IS_BACKGROUND) & 1) || ((tag >> TT_FLAG_SHADOW_CASTER) & 1)) return 0;
-                if (m->specTrans == 1.0f) return 3; /* glass tint samples the texture atlas */
-                if (m->MatType == TT_MAT_CUTOUT_INDEX) { /* :613-616, point sampler */
-                    if (!g_atlas) return 3;
-                    float bu, bv, au, av;
+                if (m->MatType == TT_MAT_CUTOUT_INDEX || m->specTrans == 1.0f) { /* :613-627 */
+                    float bu, bv;
                     base_uv(T, u, v, &bu, &bv);
-                    align_uv(bu, bv, m->AlbedoTexScale, m->AlphaTex, &au, &av);
-                    if (sample_point(au, av) < m->AlphaCutoff) return 0;
+                    if (m->MatType == TT_MAT_CUTOUT_INDEX) { /* :616, point sampler */
+                        if (!g_atlas) return 3;
+                        float au, av;
+                        align_uv(bu, bv, m->AlbedoTexScale, m->AlphaTex, &au, &av);
+                        if (sample_point(au, av) < m->AlphaCutoff) return 0;
+                    }
+                    if (m->specTrans == 1.0f) { /* IgnoreGlassShadow + StainedGlassShadows: tint, never occlude */
+                        if (!g_tex) return 3;
+                        glass_tint(m, bu, bv, throughput);
+                        return 0;
+                    }
                 }
             }
             if (t > 0.0f && t < max_distance) {
@@ -532,7 +586,7 @@ static int intersect_bvh_shadow(const shadow_job* J, uint32_t i) {
     ray.direction = ld3(SR->direction);
     ray.direction_inv = vrcp(ray.direction);
     ray2 = ray;
-    const float throughput[3] = {1.0f, 1.0f, 1.0f};
+    float throughput[3] = {1.0f, 1.0f, 1.0f}; /* :361, scaled by stained-glass tints */
     TriOffset = 0;
     MatOffset = 0;
     Reps = 0;
@@ -603,7 +657,7 @@ static int intersect_bvh_shadow(const shadow_job* J, uint32_t i) {
                     triangle_group.y &= ~(1u << triangle_index);
                     cnt.tri_tests++;
                     const int r = intersect_triangle_shadow(s, (int)(triangle_group.x + triangle_index), &ray,
-                                                            max_distance, MatOffset, &cnt.accepts);
+                                                            max_distance, MatOffset, &cnt.accepts, throughput);
                     if (r == 3) { status = 3; goto done; }
                     if (r) { hit = 1; break; }
                 }
@@ -691,7 +745,7 @@ tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
     if (p->screen_width == 0 || p->screen_height == 0) return TT_ERR_INVALID_ARG;
     scene s = {nodes, n_nodes, tris, n_tris, tlas_indices, n_tlas, meshdata, n_mesh, materials, n_mat};
     for (uint32_t m = 0; m < n_mat; m++)
-        if ((materials[m].MatType == TT_MAT_CUTOUT_INDEX && !g_atlas) || materials[m].specTrans == 1.0f)
+        if ((materials[m].MatType == TT_MAT_CUTOUT_INDEX && !g_atlas) || (materials[m].specTrans == 1.0f && !g_tex))
             return TT_ERR_UNSUPPORTED;
     shadow_job J = {&s, p, shadow_rays, visibility, global_colors, nee_pos, counts};
     if (nthreads < 1) nthreads = 1;

@@ -94,6 +94,8 @@ tt_status tt_oracle_blas_refit(tt_cwbvh_node* nodes, uint32_t n_nodes, tt_cuda_t
 /* The R8 alpha atlas Cutout materials sample (see tt_scene_upload_alpha_atlas); NULL clears it.
  * Process-global (test infrastructure): set it before tracing a scene with Cutout materials. */
 void tt_oracle_set_alpha_atlas(const uint8_t* texels, uint32_t width, uint32_t height);
+/* _TextureAtlas as RGBA half texels (4 x uint16 per texel, row-major) for the stained-glass tint */
+void tt_oracle_set_texture_atlas(const uint16_t* rgba_half, uint32_t width, uint32_t height);
 
 #ifdef __cplusplus
 }

@@ -248,3 +248,72 @@ def shadow_case_cutout():
 
 ALL_CASES.append(case_cutout)
 SHADOW_CASES.append(shadow_case_cutout)
+
+
+# ------------------------------------------ stained-glass shadow tint (§8 f1, CommonData.cginc:613-625)
+GLASS_COLORS = {1: (0.5, 1.0, 0.25), 2: (1.0, 0.75, 1.0), 3: (0.8, 0.6, 0.4)}
+
+
+def glass_texture_atlas():
+    """4x4 RGBA half atlas with a distinct value per texel and channel."""
+    y, x = np.mgrid[0:4, 0:4]
+    a = np.zeros((4, 4, 4), np.float16)
+    a[..., 0] = 0.1 * x + 0.01 * y
+    a[..., 1] = 0.5 + 0.125 * x - 0.03 * y
+    a[..., 2] = 1.7 - 0.2 * x + 0.07 * y
+    a[..., 3] = 1.0
+    return a
+
+
+def glass_factor(mat, texel_xy, atlas):
+    """surfaceColor * (texel.xyz + 2) / 3 in float32, per component."""
+    c = np.asarray(GLASS_COLORS[mat], np.float32)
+    t = atlas[texel_xy[1], texel_xy[0], :3].astype(np.float32)
+    return (c * (t + np.float32(2.0))) / np.float32(3.0)
+
+
+def shadow_case_glass():
+    """Four unit triangles in two leaves of one node, visited z = -1, -0.5, -0.25, 0 (highest
+    triangle bit first): an
+    opaque one at z = -1 (t = 2), glass + Cutout at z = -0.5 (alpha atlas: columns 0-1
+    transparent), plain glass without an albedo texture at z = -0.25 (AlignUV -> (-1, -1) -> texel
+    (0, 0)), glass at z = 0 with the atlas rectangle = the whole atlas (uv = barycentrics).
+    Glass never occludes and tints even beyond |t| (the material checks precede the t test);
+    a Cutout-rejected glass surface does not tint. Returns (name, scene, rays, status, throughput)."""
+    tris = [hb.tri((0.0, 0.0, z), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), matdat=m)
+            for z, m in ((0.0, 1), (-0.25, 2), (-0.5, 3), (-1.0, 0))]
+    for t in tris:
+        t["tex0"], t["texedge1"], t["texedge2"] = (0.0, 0.0), (1.0, 0.0), (0.0, 1.0)
+    root = hb.make_node((-1.0, -1.0, -1.0), (E6, E6, E6), 0, 0,
+                        [(0, "leaf", (64, 64, 0), (128, 128, 65), (0, 3)),
+                         (1, "leaf", (64, 64, 0), (128, 128, 65), (3, 1))])
+    mats = np.zeros(4, tthip.MAT_DTYPE)
+    whole = (16384 | (16384 << 15), 0)
+    for m, col in GLASS_COLORS.items():
+        mats[m]["specTrans"] = 1.0
+        mats[m]["surfaceColor"] = col
+        mats[m]["AlbedoTexScale"] = (1.0, 1.0, 0.0, 0.0)
+        mats[m]["AlbedoTex"] = whole if m != 2 else (0, 0)
+    mats[3]["MatType"] = tthip.MAT_CUTOUT_INDEX
+    mats[3]["AlphaCutoff"] = 0.5
+    mats[3]["AlphaTex"] = whole
+    sc = hb.scene([root], tris, materials=mats)
+    alpha = np.zeros((4, 4), np.uint8)
+    alpha[:, 2:] = 255
+    sc.alpha_atlas = alpha
+    sc.texture_atlas = glass_texture_atlas()
+    d = (0.0, 0.0, -1.0)
+    a, c = (0.25, 0.25, 1.0), (0.6, 0.2, 1.0)
+    rays = hb.shadow_rays([a, a, c, a, a], [d] * 5, [1.75, 2.5, 1.75, 0.5, 1.1])
+    at = sc.texture_atlas
+    f0a = glass_factor(1, (1, 1), at)   # z = 0 at uv (0.25, 0.25)
+    f1 = glass_factor(2, (0, 0), at)    # no albedo texture: texel (0, 0)
+    f0c = glass_factor(1, (2, 0), at)   # z = 0 at uv (0.6, 0.2)
+    f2c = glass_factor(3, (2, 0), at)   # glass + cutout passes the alpha test at uv (0.6, 0.2)
+    one = np.ones(3, np.float32)
+    thr = [(one * f1) * f0a, None, ((one * f2c) * f1) * f0c, one, (one * f1) * f0a]
+    # 1.75: reaches, tinted by z = -0.25 and z = 0 (z = -0.5 rejected by the alpha test);
+    # 2.5: the opaque triangle at t = 2 occludes; uv (0.6, 0.2): all three glass surfaces tint;
+    # 0.5: the leaf box starts beyond |t| (culled, no tint); 1.1: the glass at t = 1.25 lies beyond
+    # |t| and still tints
+    return "shadow_glass", sc, rays, [0, 4, 0, 0, 0], thr

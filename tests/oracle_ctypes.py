@@ -53,6 +53,8 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_shadow.restype = i32
         L.tt_oracle_set_alpha_atlas.argtypes = [vp, u32, u32]
         L.tt_oracle_set_alpha_atlas.restype = None
+        L.tt_oracle_set_texture_atlas.argtypes = [vp, u32, u32]
+        L.tt_oracle_set_texture_atlas.restype = None
         L.tt_oracle_tlas_refit.argtypes = [vp, u32, vp, u32, vp, u32]
         L.tt_oracle_tlas_refit.restype = i32
         L.tt_oracle_blas_refit.argtypes = [vp, u32, vp, u32, vp, u32, u32, vp, u32, u32, vp, u32, vp, vp]
@@ -63,11 +65,13 @@ def lib(prefer_v3: bool = True):
 
 
 _ATLAS_KEEP = None
+_TEX_KEEP = None
 
 
 def _set_atlas(scene):
-    """The oracle's alpha atlas is process-global: point it at the scene's (or clear it)."""
-    global _ATLAS_KEEP
+    """The oracle's alpha and texture atlases are process-global: point them at the scene's (or
+    clear them)."""
+    global _ATLAS_KEEP, _TEX_KEEP
     a = getattr(scene, "alpha_atlas", None)
     if a is None:
         _ATLAS_KEEP = None
@@ -75,6 +79,13 @@ def _set_atlas(scene):
     else:
         _ATLAS_KEEP = np.ascontiguousarray(a, np.uint8)
         lib().tt_oracle_set_alpha_atlas(_ATLAS_KEEP.ctypes.data, _ATLAS_KEEP.shape[1], _ATLAS_KEEP.shape[0])
+    t = getattr(scene, "texture_atlas", None)
+    if t is None:
+        _TEX_KEEP = None
+        lib().tt_oracle_set_texture_atlas(None, 0, 0)
+    else:
+        _TEX_KEEP = np.ascontiguousarray(t, np.float16)
+        lib().tt_oracle_set_texture_atlas(_TEX_KEEP.ctypes.data, _TEX_KEEP.shape[1], _TEX_KEEP.shape[0])
 
 
 def trace(scene: "tthip.Scene", rays: np.ndarray, n_rays: int, bounce: int, far_plane: float, width: int,

@@ -500,6 +500,74 @@ def test_cutout_random_soup_closest_and_shadow(engine, seed):
     shadow_both(engine, sc, sr, 0, W, H, upload=False)
 
 
+# ------------------------------------------------------------------ stained-glass shadows (§8 f1)
+def test_shadow_glass_kat_on_gpu(engine):
+    name, sc, rays, expected, thr = K.shadow_case_glass()
+    n = len(rays)
+    rg, vg, s, cnt = shadow_both(engine, sc, rays, 0, n, 1)
+    assert cnt["status"].tolist() == expected
+    for i, e in enumerate(expected):
+        if e == 0:
+            assert vg[i, :3].tobytes() == thr[i].astype(np.float32).tobytes(), i
+
+
+def test_shadow_glass_without_texture_atlas_is_refused():
+    _, sc, rays, _, _ = K.shadow_case_glass()
+    sc.texture_atlas = None
+    e = tthip.Engine(0)
+    try:
+        e.upload(sc)
+        with pytest.raises(tthip.TTError) as ex:
+            e.trace_shadow(rays.copy(), len(rays), 0, len(rays), 1)
+        assert ex.value.status == tthip.TT_ERR_UNSUPPORTED
+    finally:
+        e.close()
+
+
+def glass_soup(seed):
+    """Random soup with opaque, glass (textured / untextured), glass + Cutout and Cutout materials,
+    random UVs (wrapping), a noisy alpha atlas and a random RGBA half texture atlas."""
+    rng = np.random.default_rng(seed)
+    sc = cutout_soup(seed)
+    n = len(sc.tris)
+    sc.tris["MatDat"] = rng.integers(0, 5, n)
+    mats = np.zeros(5, tthip.MAT_DTYPE)
+    for m in (1, 2, 3):
+        mats[m]["specTrans"] = 1.0
+        mats[m]["surfaceColor"] = rng.uniform(0.2, 1.0, 3)
+        mats[m]["AlbedoTexScale"] = [rng.uniform(0.5, 2), rng.uniform(0.5, 2), rng.uniform(-1, 1), rng.uniform(-1, 1)]
+        lo = rng.integers(0, 8000, 2)
+        hi = lo + rng.integers(1000, 8000, 2)
+        mats[m]["AlbedoTex"] = [int(hi[0]) | (int(hi[1]) << 15), int(lo[0]) | (int(lo[1]) << 15)] if m != 2 else [0, 0]
+    for m in (3, 4):
+        mats[m]["MatType"] = tthip.MAT_CUTOUT_INDEX
+        mats[m]["AlphaCutoff"] = rng.uniform(0.2, 0.8)
+        lo = rng.integers(0, 8000, 2)
+        hi = lo + rng.integers(1000, 8000, 2)
+        mats[m]["AlphaTex"] = [int(hi[0]) | (int(hi[1]) << 15), int(lo[0]) | (int(lo[1]) << 15)]
+    mats[4]["AlbedoTexScale"] = [1.0, 1.0, 0.0, 0.0]
+    sc.materials = mats
+    sc.texture_atlas = rng.uniform(0.0, 4.0, (24, 40, 4)).astype(np.float16)
+    return sc
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_glass_random_soup_shadow(engine, seed):
+    """Throughput = product of the glass tints in traversal order, bit for bit against the oracle,
+    including the cooperative drain phase (the tints of a group's triangles multiplied in order)."""
+    sc = glass_soup(seed)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    sr = hb.nee_rays_from_hits(rg, W * H, (0.5, 2.0, 2.5), seed)
+    _, vg, _, sc_cnt = shadow_both(engine, sc, sr, 0, W, H, upload=False)
+    reached = sc_cnt["status"] == 0
+    tinted = reached & (vg[:, :3] != 1.0).any(1)
+    assert tinted.sum() > 100, "glass must tint a good share of the unoccluded rays"
+
+
 # ------------------------------------------------------------------ TLAS refit (§8 f4)
 def refit_scene(seed, offsets=None, n_inst=120):
     rng = np.random.default_rng(seed)

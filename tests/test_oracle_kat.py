@@ -276,3 +276,31 @@ def test_degenerate_rays_are_deterministic_on_the_oracle():
     assert st1 == st2 == 0
     assert np.array_equal(a.view(np.uint8), b.view(np.uint8)) and np.array_equal(c1, c2)
     assert set(np.unique(c1["status"]).tolist()) <= {0, 1}
+
+
+def test_shadow_glass_tint_kat():
+    """Stained-glass shadows (CommonData.cginc:613-625): known throughputs, visibility xyz and
+    GlobalColors.Direct = 0.5 + illumination * throughput, bit for bit."""
+    name, sc, rays, expected, thr = K.shadow_case_glass()
+    n = len(rays)
+    rays["illumination"] = (0.75, 1.5, 3.0)
+    rays["PixelIndex"] = np.arange(n)
+    vis = np.full((n, 4), 7.0, np.float32)
+    colors = np.zeros(n, tthip.COL_DTYPE)
+    colors["Direct"] = 0.5
+    st, cnt = O.shadow(sc, rays, n, 0, n, 1, visibility=vis, colors=colors, counts=True)
+    assert st == tthip.TT_OK
+    assert cnt["status"].tolist() == expected
+    for i, e in enumerate(expected):
+        if e == 0:
+            assert vis[i].tobytes() == np.append(thr[i], np.float32(1.0)).astype(np.float32).tobytes(), i
+            want = np.float32(0.5) + np.asarray((0.75, 1.5, 3.0), np.float32) * thr[i]
+            assert colors["Direct"][i].astype(np.float32).tobytes() == want.astype(np.float32).tobytes(), i
+    assert not np.array_equal(thr[0], np.ones(3, np.float32))
+
+
+def test_shadow_glass_needs_texture_atlas():
+    _, sc, rays, _, _ = K.shadow_case_glass()
+    sc.texture_atlas = None
+    st, _ = O.shadow(sc, rays, len(rays), 0, len(rays), 1)
+    assert st == tthip.TT_ERR_UNSUPPORTED

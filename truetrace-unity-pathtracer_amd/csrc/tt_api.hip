@@ -67,9 +67,10 @@ struct SceneHost {
     uint32_t n_mat = 0;
     std::vector<uint32_t> matdat;  // only kept when a material sets the Invisible flag
     bool any_shadow_skip = false;  // IsBackground / ShadowCaster present (shadow material checks)
-    bool any_atlas_shadow = false; // specTrans == 1 present (shadow glass tint: unsupported)
+    bool any_atlas_shadow = false; // specTrans == 1 present (shadow glass tint: needs the texture atlas)
     bool any_cutout = false;       // Cutout materials present (need the alpha atlas)
     std::vector<CutoutMat> cut;    // per material, when any_cutout
+    std::vector<GlassMat> glass;   // per material, when any_atlas_shadow
 };
 
 }  // namespace
@@ -107,6 +108,9 @@ struct tt_ctx {
     uint32_t n_ncache = 0, ncache_root = 0;
     DevBuf<uint32_t> mat_tag;
     DevBuf<CutoutMat> mat_cut;
+    DevBuf<GlassMat> mat_glass;
+    DevBuf<uint2> tex;          // _TextureAtlas, decoded RGBA half texels
+    uint32_t tex_w = 0, tex_h = 0;
     DevBuf<uint8_t> atlas;      // _AlphaAtlas (R8)
     uint32_t atlas_w = 0, atlas_h = 0;
     // TLAS refit (f4): plan valid for (scene generation, n_tlas_nodes)
@@ -293,7 +297,8 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
     any_invisible = false;
     tags.assign(std::max<uint32_t>(n_mat, 1u), 0u);
     for (uint32_t m = 0; m < n_mat; m++) {
-        tags[m] = mats[m].Tag & ~(1u << TT_MATWORD_CUTOUT);
+        tags[m] = mats[m].Tag & ~((1u << TT_MATWORD_CUTOUT) | (1u << TT_MATWORD_GLASS));
+        if (mats[m].specTrans == 1.0f) tags[m] |= 1u << TT_MATWORD_GLASS;  // stained-glass shadow tint
         if (mats[m].MatType == TT_MAT_CUTOUT_INDEX) {  // alpha test, IntersectionKernels.compute:35-40
             tags[m] |= 1u << TT_MATWORD_CUTOUT;
             h.any_cutout = true;
@@ -309,6 +314,16 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
             r.alpha_tex[0] = mats[m].AlphaTex[0];
             r.alpha_tex[1] = mats[m].AlphaTex[1];
             r.cutoff = mats[m].AlphaCutoff;
+            for (int k = 0; k < 4; k++) r.scale[k] = mats[m].AlbedoTexScale[k];
+        }
+    }
+    if (h.any_atlas_shadow) {
+        h.glass.assign(n_mat, GlassMat{});
+        for (uint32_t m = 0; m < n_mat; m++) {
+            GlassMat& r = h.glass[m];
+            r.albedo_tex[0] = mats[m].AlbedoTex[0];
+            r.albedo_tex[1] = mats[m].AlbedoTex[1];
+            for (int k = 0; k < 3; k++) r.color[k] = mats[m].surfaceColor[k];
             for (int k = 0; k < 4; k++) r.scale[k] = mats[m].AlbedoTexScale[k];
         }
     }
@@ -553,8 +568,10 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->mesh.release();
     c->mat_tag.release();
     c->mat_cut.release();
+    c->mat_glass.release();
     c->leaf.release();
     c->atlas.release();
+    c->tex.release();
     tt_refit_free(c->refit);
     for (auto& kv : c->blas_refit) {
         tt_refit_free(kv.second.dev);
@@ -668,6 +685,7 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->mesh.release();
     c->mat_tag.release();
     c->mat_cut.release();
+    c->mat_glass.release();
     hipError_t e;
     if ((e = c->nodes.alloc(n_nodes)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
         (e = c->tris.alloc(n_tris)) != hipSuccess || (e = c->tlas.alloc(n_tlas)) != hipSuccess ||
@@ -684,6 +702,10 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     if (h.any_cutout) {
         if ((e = c->mat_cut.alloc(h.cut.size())) != hipSuccess) return hip_fail(c, e, "cutout records");
         TT_HIP(c, hipMemcpy(c->mat_cut.p, h.cut.data(), sizeof(CutoutMat) * h.cut.size(), hipMemcpyHostToDevice));
+    }
+    if (h.any_atlas_shadow) {
+        if ((e = c->mat_glass.alloc(h.glass.size())) != hipSuccess) return hip_fail(c, e, "glass records");
+        TT_HIP(c, hipMemcpy(c->mat_glass.p, h.glass.data(), sizeof(GlassMat) * h.glass.size(), hipMemcpyHostToDevice));
     }
     c->host = std::move(h);
     c->any_invisible = any_invisible;
@@ -713,6 +735,20 @@ tt_status tt_scene_upload_alpha_atlas(tt_ctx* c, const uint8_t* texels, uint32_t
     TT_HIP(c, hipMemcpy(c->atlas.p, texels, (size_t)width * height, hipMemcpyHostToDevice));
     c->atlas_w = width;
     c->atlas_h = height;
+    return TT_OK;
+}
+
+tt_status tt_scene_upload_texture_atlas(tt_ctx* c, const uint16_t* rgba_half, uint32_t width, uint32_t height) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (!rgba_half || width == 0 || height == 0 || (uint64_t)width * height > 0x7fffffffull / 8u)
+        return fail(c, TT_ERR_INVALID_ARG, "tt_scene_upload_texture_atlas: empty or oversized atlas");
+    TT_HIP(c, hipSetDevice(c->device));
+    c->tex.release();
+    c->tex_w = c->tex_h = 0;
+    TT_HIP(c, c->tex.alloc((size_t)width * height));
+    TT_HIP(c, hipMemcpy(c->tex.p, rgba_half, (size_t)width * height * 8u, hipMemcpyHostToDevice));
+    c->tex_w = width;
+    c->tex_h = height;
     return TT_OK;
 }
 
@@ -941,6 +977,10 @@ MatView mat_view(const tt_ctx* c) {
     m.n_mat = c->host.n_mat;
     m.atlas_w = c->atlas_w;
     m.atlas_h = c->atlas_h;
+    m.glass = c->mat_glass.p;
+    m.tex = c->tex.p;
+    m.tex_w = c->tex_w;
+    m.tex_h = c->tex_h;
     return m;
 }
 }  // namespace
@@ -1078,10 +1118,10 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or shadow rays");
     if (p->screen_width == 0 || p->screen_height == 0) return fail(c, TT_ERR_INVALID_ARG, "zero screen size");
     if (p->bounce < 0) return fail(c, TT_ERR_INVALID_ARG, "negative bounce");
-    if (c->any_atlas_shadow)
+    if (c->any_atlas_shadow && !c->tex.p)
         return fail(c, TT_ERR_UNSUPPORTED,
-                    "scene has glass (specTrans == 1) materials: the shadow tint samples the texture atlas "
-                    "(CommonData.cginc:618-625), not supported");
+                    "scene has glass (specTrans == 1) materials but no texture atlas was uploaded "
+                    "(tt_scene_upload_texture_atlas; the shadow tint samples it, CommonData.cginc:618-625)");
     if (c->any_cutout && !c->atlas.p)
         return fail(c, TT_ERR_UNSUPPORTED,
                     "scene has Cutout materials but no alpha atlas was uploaded (tt_scene_upload_alpha_atlas)");
@@ -1144,7 +1184,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     a.height = p->screen_height;
     a.bounce = p->bounce;
     a.flags = p->flags;
-    const bool matcheck = c->any_shadow_skip || c->any_cutout;
+    const bool matcheck = c->any_shadow_skip || c->any_cutout || c->any_atlas_shadow;
     const uint32_t blocks_needed = ((p->n_rays + 255u) / 256u + 3u) / 4u;
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));

@@ -85,15 +85,30 @@ struct CutoutMat {
 };
 static_assert(sizeof(CutoutMat) == 32, "CutoutMat is 32 bytes");
 #define TT_MATWORD_CUTOUT 31u
+#define TT_MATWORD_GLASS 30u  // specTrans == 1 (stained-glass shadow tint, any-hit kernel)
+
+// Per-material record for the stained-glass shadow tint (row f1), 48 B; only uploaded when a
+// material has specTrans == 1.
+struct GlassMat {
+    int32_t albedo_tex[2];  // MaterialData.AlbedoTex (atlas rectangle, 15-bit fixed point)
+    float color[3];         // MaterialData.surfaceColor
+    float pad0;
+    float scale[4];         // MaterialData.AlbedoTexScale
+    float pad1[2];
+};
+static_assert(sizeof(GlassMat) == 48, "GlassMat is 48 bytes");
 
 // Everything the material checks of the triangle tests read (IntersectionKernels.compute:35-48,
 // CommonData.cginc:611-617).
 struct MatView {
-    const uint32_t* word;         // Tag | Cutout << 31, per material
+    const uint32_t* word;         // Tag | Cutout << 31 | Glass << 30, per material
     const CutoutMat* cut;         // per material (nullptr without Cutout materials)
     const tt_cuda_triangle* raw;  // AggTris (raw UVs for the cutout sample)
     const uint8_t* atlas;         // _AlphaAtlas, R8
     uint32_t n_mat, atlas_w, atlas_h;
+    const GlassMat* glass;        // per material (nullptr without glass materials)
+    const uint2* tex;             // _TextureAtlas, RGBA half texels (8 B)
+    uint32_t tex_w, tex_h;
 };
 
 struct TraceArgs {

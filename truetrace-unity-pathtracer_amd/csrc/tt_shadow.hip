@@ -8,8 +8,8 @@
 //  * the first occluder ends the ray (:441-454): t = 0 is written back to ShadowRaysBuffer;
 //  * triangle_intersect_shadow (CommonData.cginc:593-634) reads the material BEFORE the t-range
 //    test and ignores IsBackground / ShadowCaster surfaces; Cutout runs the point-sampled alpha
-//    test; glass (specTrans == 1) tints through the BC6H texture atlas and is rejected on the host
-//    (TT_ERR_UNSUPPORTED);
+//    test; glass (specTrans == 1) never occludes and tints the throughput through the texture
+//    atlas (stained-glass shadows), in traversal order;
 //  * the same cooperative drain phase as the closest-hit kernel (tt_wide.h): once the queue is dry
 //    the live rays regroup into 2/4/8-lane groups; a triangle pass tests up to G of the leaf's
 //    triangles and the ray is occluded if any of them occludes (what the sequential loop, which
@@ -21,9 +21,11 @@
 namespace {
 
 // triangle_intersect_shadow — CommonData.cginc:593-634. Returns true for an occluder.
+// A glass surface (specTrans == 1) never occludes; it multiplies `thr` by its tint (:617-625).
 template <bool MATCHECK>
 __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, int32_t tri_id,
-                                                int32_t mat_offset, const LaneRay& r, float max_distance) {
+                                                int32_t mat_offset, const LaneRay& r, float max_distance,
+                                                float3& thr) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
     const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u);
     uint2 c;
@@ -55,11 +57,26 @@ __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, con
         // (:613-616); out-of-range material = zeros
         const uint32_t mi = (uint32_t)(mat_offset + (int32_t)c.y);
         const uint32_t w = mi < M.n_mat ? M.word[mi] : 0u;
+        const bool glass = (w >> TT_MATWORD_GLASS) & 1u, cutout = (w >> TT_MATWORD_CUTOUT) & 1u;
         if (((w >> TT_FLAG_IS_BACKGROUND) | (w >> TT_FLAG_SHADOW_CASTER)) & 1u) {
             occ = false;
-        } else if (occ && ((w >> TT_MATWORD_CUTOUT) & 1u)) {
-            const CutoutMat cm = M.cut[mi];
-            if (sample_point(M, align_uv(base_uv(M, tri_id, u, v), cm)) < cm.cutoff) occ = false;
+        } else if (glass || (occ && cutout)) {
+            // the alpha test comes first (:616); a glass surface that passes it tints (:621-622)
+            const float2 buv = base_uv(M, tri_id, u, v);
+            bool rejected = false;
+            if (cutout) {
+                const CutoutMat cm = M.cut[mi];
+                rejected = sample_point(M, align_uv(buv, cm)) < cm.cutoff;
+            }
+            if (rejected) {
+                occ = false;
+            } else if (glass) {
+                const float3 f = glass_tint(M, M.glass[mi], buv);
+                thr.x = thr.x * f.x;
+                thr.y = thr.y * f.y;
+                thr.z = thr.z * f.z;
+                occ = false;
+            }
         }
     }
     return occ;
@@ -68,6 +85,7 @@ __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, con
 struct ShadowWide {
     LaneRay ray, wray;
     float max_distance;
+    float3 thr;
     uint2 cg, tg;
     uint32_t oct;
     int32_t stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset, Reps;
@@ -96,6 +114,9 @@ __device__ __forceinline__ void regroup_shadow(ShadowWide& s, uint64_t lead, uin
     shfl_ray(s.ray, src);
     shfl_ray(s.wray, src);
     s.max_distance = shfl_f(s.max_distance, src);
+    s.thr.x = shfl_f(s.thr.x, src);
+    s.thr.y = shfl_f(s.thr.y, src);
+    s.thr.z = shfl_f(s.thr.z, src);
     s.cg.x = shfl_u(s.cg.x, src);
     s.cg.y = shfl_u(s.cg.y, src);
     s.tg.x = shfl_u(s.tg.x, src);
@@ -225,9 +246,10 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
                 if (k < sub && m) m &= ~(1u << firstbithigh(m));
             const bool has = m != 0u;
             bool occ = false;
+            float3 f = make_float3(1.0f, 1.0f, 1.0f);  // this lane's glass tint (1: none)
             if (has)
                 occ = shadow_triangle<MATCHECK>(tris, A.mat, (int32_t)(st.tg.x + firstbithigh(m)), st.MatOffset, st.ray,
-                                                st.max_distance);
+                                                st.max_distance, f);
             // the first occluder in the reference's order (lowest sub), G if none
             const uint32_t first = (uint32_t)group_min_u64<G>(occ ? (uint64_t)sub : (uint64_t)G);
             if (STATS && sub == 0u)
@@ -239,6 +261,15 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
                     occlude(st);
                 }
             } else {
+                if (MATCHECK) {  // the tints in the reference's order (lane k holds the k-th triangle)
+                    const uint32_t base = lane & ~(uint32_t)(G - 1);
+#pragma unroll
+                    for (uint32_t k = 0; k < (uint32_t)G; k++) {
+                        st.thr.x = st.thr.x * shfl_f(f.x, base + k);
+                        st.thr.y = st.thr.y * shfl_f(f.y, base + k);
+                        st.thr.z = st.thr.z * shfl_f(f.z, base + k);
+                    }
+                }
 #pragma unroll
                 for (uint32_t k = 0; k < (uint32_t)G; k++)
                     if (st.tg.y) st.tg.y &= ~(1u << firstbithigh(st.tg.y));
@@ -292,6 +323,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
     uint32_t ray_index = 0;
     LaneRay ray{}, wray{};
     float max_distance = 0.0f;
+    float3 thr = make_float3(1.0f, 1.0f, 1.0f);  // throughput (:361), scaled by glass tints
     uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
     uint32_t oct = 0;
     int32_t stack_size = 0, tlas_ss = -1;
@@ -306,20 +338,20 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
     auto do_exhaust = [&](uint32_t ri) {
         if (A.visibility) A.visibility[ri] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
     };
-    auto do_reach = [&](uint32_t ri, const LaneRay& w) {  // TerrainExists false
+    auto do_reach = [&](uint32_t ri, const LaneRay& w, const float3& thr) {  // TerrainExists false
         const tt_shadow_ray& R = A.rays[ri];
         const uint32_t pix = R.PixelIndex;
         const float t = R.t;
-        if (A.visibility) A.visibility[ri] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        if (A.visibility) A.visibility[ri] = make_float4(thr.x, thr.y, thr.z, 1.0f);
         if (A.bounce == 0 && A.nee_pos && pix / A.width < A.height) {
             const float d = fabsf(t);
             A.nee_pos[pix] = make_float4(w.ox + w.dx * d, w.oy + w.dy * d, w.oz + w.dz * d, 0.0f);
         }
-        if (A.bounce == 0 && t >= 0.0f && A.colors) {  // Direct += illumination * throughput (1)
+        if (A.bounce == 0 && t >= 0.0f && A.colors) {  // Direct += illumination * throughput (:469)
             tt_col_data& C = A.colors[pix];
-            C.Direct[0] = C.Direct[0] + R.illumination[0] * 1.0f;
-            C.Direct[1] = C.Direct[1] + R.illumination[1] * 1.0f;
-            C.Direct[2] = C.Direct[2] + R.illumination[2] * 1.0f;
+            C.Direct[0] = C.Direct[0] + R.illumination[0] * thr.x;
+            C.Direct[1] = C.Direct[1] + R.illumination[1] * thr.y;
+            C.Direct[2] = C.Direct[2] + R.illumination[2] * thr.z;
         }
     };
 
@@ -332,11 +364,11 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
 #if TT_WIDE
         // the queue is dry and the live rays fit in 2-lane groups: cooperative drain (tt_wide.h)
         if (pool_dry && TT_WAVE - n_idle <= TT_WIDE_ENTER) {
-            ShadowWide st{ray, wray, max_distance, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset,
+            ShadowWide st{ray, wray, max_distance, thr, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset,
                           MatOffset, Reps, ray_index, tid, gtid, active};
             regroup_shadow<2>(st, __ballot(active), lane);
             auto occ_w = [&](const ShadowWide& w) { do_occlude(w.ray_index); };
-            auto reach_w = [&](const ShadowWide& w) { do_reach(w.ray_index, w.wray); };
+            auto reach_w = [&](const ShadowWide& w) { do_reach(w.ray_index, w.wray, w.thr); };
             auto exh_w = [&](const ShadowWide& w) { do_exhaust(w.ray_index); };
             shadow_wide_phase<STATS, MATCHECK, 2>(A, st, s_stack, spill, spill_stride, nodes, tris, lane,
                                                   ShadowCounters{c_nodes, c_tris, c_blas, c_occ, c_vis, c_reps, c_ovf},
@@ -374,6 +406,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 ray.dy = __uint_as_float(r1.y);
                 ray.dz = __uint_as_float(r1.z);
                 max_distance = fabsf(__uint_as_float(r1.w));
+                thr = make_float3(1.0f, 1.0f, 1.0f);
                 ray.ix = rcp_rn(ray.dx);
                 ray.iy = rcp_rn(ray.dy);
                 ray.iz = rcp_rn(ray.dz);
@@ -469,7 +502,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool occ =
-                shadow_triangle<MATCHECK>(tris, A.mat, (int32_t)(tg.x + ti), MatOffset, ray, max_distance);
+                shadow_triangle<MATCHECK>(tris, A.mat, (int32_t)(tg.x + ti), MatOffset, ray, max_distance, thr);
             if (STATS) c_tris++;
             if (occ) {  // :449-454
                 do_occlude(ray_index);
@@ -490,7 +523,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 }
                 TT_POP(cg);
             } else {  // reached the light (TerrainExists false): :457-485
-                do_reach(ray_index, wray);
+                do_reach(ray_index, wray, thr);
                 active = false;
                 if (STATS) c_vis++;
             }

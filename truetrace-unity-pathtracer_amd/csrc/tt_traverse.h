@@ -184,19 +184,19 @@ struct Best {
 // Evaluated branch-free; the accept predicate is exactly the reference's nested conditions.
 // ------------------------------------------------------- alpha atlas (row f3, pinned filtering)
 // AlignUV — CommonData.cginc:569-591 (Rotation 0, IsAlbedo false)
-__device__ __forceinline__ float2 align_uv(float bu, float bv, const CutoutMat& m) {
-    if (m.alpha_tex[0] <= 0) return make_float2(-1.0f, -1.0f);
-    const float dx = (float)(((uint32_t)m.alpha_tex[0]) & 0x7FFFu) / 16384.0f;
-    const float dy = (float)(((uint32_t)m.alpha_tex[0]) >> 15) / 16384.0f;
-    const float dz = (float)(((uint32_t)m.alpha_tex[1]) & 0x7FFFu) / 16384.0f;
-    const float dw = (float)(((uint32_t)m.alpha_tex[1]) >> 15) / 16384.0f;
-    float x = bu * m.scale[0] + m.scale[2];
-    float y = bv * m.scale[1] + m.scale[3];
+__device__ __forceinline__ float2 align_uv(float bu, float bv, const int32_t* tex, const float* scale) {
+    if (tex[0] <= 0) return make_float2(-1.0f, -1.0f);
+    const float dx = (float)(((uint32_t)tex[0]) & 0x7FFFu) / 16384.0f;
+    const float dy = (float)(((uint32_t)tex[0]) >> 15) / 16384.0f;
+    const float dz = (float)(((uint32_t)tex[1]) & 0x7FFFu) / 16384.0f;
+    const float dw = (float)(((uint32_t)tex[1]) >> 15) / 16384.0f;
+    float x = bu * scale[0] + scale[2];
+    float y = bv * scale[1] + scale[3];
     x = x < 0.0f ? 1.0f - fmodf(fabsf(x), 1.0f) : fmodf(fabsf(x), 1.0f);
     y = y < 0.0f ? 1.0f - fmodf(fabsf(y), 1.0f) : fmodf(fabsf(y), 1.0f);
     return make_float2(x * (dx - dz) + dz, y * (dy - dw) + dw);
 }
-__device__ __forceinline__ float2 align_uv(float2 b, const CutoutMat& m) { return align_uv(b.x, b.y, m); }
+__device__ __forceinline__ float2 align_uv(float2 b, const CutoutMat& m) { return align_uv(b.x, b.y, m.alpha_tex, m.scale); }
 __device__ __forceinline__ int atlas_clamp(float c, uint32_t n) { return (int)fminf(fmaxf(c, 0.0f), (float)(n - 1u)); }
 __device__ __forceinline__ float atlas_texel(const MatView& M, int x, int y) {
     return (float)M.atlas[(size_t)y * M.atlas_w + (size_t)x] / 255.0f;
@@ -217,6 +217,26 @@ __device__ __forceinline__ float sample_linear(const MatView& M, float2 uv) {
     const float b = atlas_texel(M, ix0, iy1) * (1.0f - fx) + atlas_texel(M, ix1, iy1) * fx;
     return a * (1.0f - fy) + b * fy;
 }
+// IEEE binary16 -> binary32 (exact; v_cvt_f32_f16)
+__device__ __forceinline__ float half_bits_to_float(uint32_t h) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+}
+// _TextureAtlas.SampleLevel(my_point_clamp_sampler, uv, 0).xyz on the decoded RGBA half atlas
+__device__ __forceinline__ float3 sample_tex_point(const MatView& M, float2 uv) {
+    const int x = atlas_clamp(floorf(uv.x * (float)M.tex_w), M.tex_w);
+    const int y = atlas_clamp(floorf(uv.y * (float)M.tex_h), M.tex_h);
+    const uint2 t = M.tex[(size_t)y * M.tex_w + (size_t)x];
+    return make_float3(half_bits_to_float(t.x & 0xffffu), half_bits_to_float(t.x >> 16),
+                       half_bits_to_float(t.y & 0xffffu));
+}
+// StainedGlassShadows tint factor of a glass surface (CommonData.cginc:621-622):
+// surfaceColor * (texel.xyz + 2) / 3 per component, IEEE division (pinned).
+__device__ __forceinline__ float3 glass_tint(const MatView& M, const GlassMat& g, float2 buv) {
+    const float3 x = sample_tex_point(M, align_uv(buv.x, buv.y, g.albedo_tex, g.scale));
+    return make_float3((g.color[0] * (x.x + 2.0f)) / 3.0f, (g.color[1] * (x.y + 2.0f)) / 3.0f,
+                       (g.color[2] * (x.z + 2.0f)) / 3.0f);
+}
+
 // BaseUv = tex0 * (1 - u - v) + texedge1 * u + texedge2 * v (IntersectionKernels.compute:37)
 __device__ __forceinline__ float2 base_uv(const MatView& M, int32_t tri_id, float u, float v) {
     const float2* t = reinterpret_cast<const float2*>(reinterpret_cast<const char*>(M.raw + tri_id) + 60);

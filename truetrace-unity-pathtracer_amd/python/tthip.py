@@ -253,6 +253,7 @@ def hip_lib():
         L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
         L.tt_trace_shadow.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, C.POINTER(Stats)]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
+        L.tt_scene_upload_texture_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
         L.tt_scene_read_nodes.argtypes = [vp, u32, u32, vp]
         L.tt_scene_read_tris.argtypes = [vp, u32, u32, vp]
@@ -448,6 +449,7 @@ class Scene:
     tlas_nodes: int = 0
     meta: dict = field(default_factory=dict)
     alpha_atlas: Optional[np.ndarray] = None  # _AlphaAtlas, uint8 [height, width] (Cutout materials)
+    texture_atlas: Optional[np.ndarray] = None  # _TextureAtlas decoded, float16 [height, width, 4] (glass)
 
     def save(self, path: str):
         np.savez_compressed(path, nodes=self.nodes.view(np.uint8), tris=self.tris.view(np.uint8),
@@ -593,12 +595,21 @@ class Engine:
         self._check(st, "tt_scene_upload")
         if s.alpha_atlas is not None:
             self.upload_alpha_atlas(s.alpha_atlas)
+        if s.texture_atlas is not None:
+            self.upload_texture_atlas(s.texture_atlas)
 
     def upload_alpha_atlas(self, atlas: np.ndarray):
         """_AlphaAtlas (AssetManager.cs:260-262): R8 texels, row 0 = v in [0, 1/height)."""
         a = np.ascontiguousarray(atlas, np.uint8)
         self._check(self.L.tt_scene_upload_alpha_atlas(self.h, _ptr(a), a.shape[1], a.shape[0]),
                     "tt_scene_upload_alpha_atlas")
+
+    def upload_texture_atlas(self, atlas: np.ndarray):
+        """_TextureAtlas (AssetManager.cs:275) decoded to RGBA half: float16 [height, width, 4]."""
+        a = np.ascontiguousarray(atlas, np.float16)
+        assert a.ndim == 3 and a.shape[2] == 4
+        self._check(self.L.tt_scene_upload_texture_atlas(self.h, _ptr(a), a.shape[1], a.shape[0]),
+                    "tt_scene_upload_texture_atlas")
 
     def update_nodes(self, first: int, nodes: np.ndarray):
         self._check(self.L.tt_scene_update_nodes(self.h, first, len(nodes), _ptr(nodes)), "tt_scene_update_nodes")
