@@ -198,3 +198,19 @@ def test_validator_rejects_malformed():
     meta = int(nodes[2]["meta"][0]) & ~0xFF
     nodes[2]["meta"][0] = meta | (0b111 << 5) | 23
     assert tthip.validate(tthip.Scene(nodes, sc.tris, sc.tlas, sc.meshdata, sc.materials))[0] == tthip.TT_ERR_INVALID_ARG
+
+
+def test_parallel_build_identical_to_serial(monkeypatch):
+    """Large meshes build their top BVH2 subtrees, the three per-axis presorts, the top SAH sweeps
+    (>= 2^20 primitives) and the BVH8 cost pass on several threads; the sequential depth-first node
+    numbering is kept (a subtree of k primitives takes 2(k-1) slots), so nodes, leaf-ordered
+    triangles and the leaf map must equal the single-threaded build (TT_BUILD_SERIAL) byte for byte."""
+    mesh = tthip.Mesh.soup(77, (1 << 20) + 4096, 4.0, 0.02)
+    par = tthip.Blas(mesh)
+    monkeypatch.setenv("TT_BUILD_SERIAL", "1")
+    ser = tthip.Blas(mesh)
+    (pn, pt), (sn, st) = par.arrays(), ser.arrays()
+    assert par.info.n_nodes == ser.info.n_nodes and par.info.bvh2_depth == ser.info.bvh2_depth
+    assert np.array_equal(pn.view(np.uint8), sn.view(np.uint8))
+    assert np.array_equal(pt.view(np.uint8), st.view(np.uint8))
+    assert np.array_equal(par.leaf_order(), ser.leaf_order())

@@ -6,11 +6,15 @@
 
 #include <pthread.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <new>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -189,6 +193,30 @@ struct DotNetSort {
     }
 };
 
+// A thread with a large stack (the builders recurse to BVH2 depth); runs inline if it cannot start.
+struct BigThread {
+    pthread_t th{};
+    bool started = false;
+    std::function<void()> fn;
+    template <class F>
+    void start(F&& f) {
+        fn = std::forward<F>(f);
+        pthread_attr_t attr;
+        pthread_attr_init(&attr);
+        pthread_attr_setstacksize(&attr, (size_t)1 << 28);
+        auto tramp = [](void* p) -> void* {
+            (*static_cast<std::function<void()>*>(p))();
+            return nullptr;
+        };
+        started = pthread_create(&th, &attr, tramp, &fn) == 0;
+        pthread_attr_destroy(&attr);
+    }
+    void join() {
+        if (started) pthread_join(th, nullptr);
+        else fn();
+    }
+};
+
 // ---------------------------------------------------------------- BVH2Builder
 struct BVHNode2Data {
     AABB aabb;
@@ -205,39 +233,75 @@ struct BVH2Builder {
     std::vector<float> SAH;
     const AABB* Primitives = nullptr;
     int PrimCount = 0;
-    uint32_t max_depth = 0;
+    std::atomic<uint32_t> max_depth{0};
 
     struct ObjectSplit {
         int index;
         float cost;
         int dimension;
         AABB aabb_left, aabb_right;
-    } split;
+    };
 
+    // The full SAH sweep of one axis (BVH2Builder.cs:62-96): the split with the lowest cost, ties to
+    // the lowest index (the sweep runs downwards with `cost <= best`). Scratch (SAH, temp) is used at
+    // [first_index, first_index + index_count) of its axis, so disjoint subtrees and the three axes
+    // can run concurrently.
+    struct AxisBest {
+        float cost;
+        int index;
+        AABB right;
+    };
+    AxisBest sweep_axis(int dimension, int first_index, int index_count) {
+        AxisBest b;
+        b.cost = std::numeric_limits<float>::max();
+        b.index = -1;
+        b.right.init();
+        AABB aabb_left, aabb_right;
+        aabb_left.init();
+        aabb_right.init();
+        const int Offset = PrimCount * dimension + first_index;
+        float* sah = &SAH[(size_t)PrimCount * dimension + first_index];
+        for (int i = 1; i < index_count; i++) {
+            aabb_left.Extend(Primitives[DimensionedIndices[Offset + i - 1]]);
+            sah[i] = surface_area(aabb_left) * (float)i;
+        }
+        for (int i = index_count - 1; i > 0; i--) {
+            aabb_right.Extend(Primitives[DimensionedIndices[Offset + i]]);
+            const float cost = sah[i] + surface_area(aabb_right) * (float)(index_count - i);
+            if (cost <= b.cost) {
+                b.cost = cost;
+                b.index = first_index + i;
+                b.right = aabb_right;
+            }
+        }
+        return b;
+    }
+    // partition_sah: the reference sweeps x, y, z in turn with one running `cost <= split.cost`, so
+    // an axis takes over exactly when its own best cost is <= the best so far.
+    static constexpr int kAxisParMin = 1 << 20;
     ObjectSplit partition_sah(int first_index, int index_count) {
+        ObjectSplit split;
         split.cost = std::numeric_limits<float>::max();
         split.index = -1;
         split.dimension = -1;
         split.aabb_left.init();
         split.aabb_right.init();
-        AABB aabb_left, aabb_right;
-        for (int dimension = 0; dimension < 3; dimension++) {
-            aabb_left.init();
-            aabb_right.init();
-            const int Offset = PrimCount * dimension + first_index;
-            for (int i = 1; i < index_count; i++) {
-                aabb_left.Extend(Primitives[DimensionedIndices[Offset + i - 1]]);
-                SAH[i] = surface_area(aabb_left) * (float)i;
-            }
-            for (int i = index_count - 1; i > 0; i--) {
-                aabb_right.Extend(Primitives[DimensionedIndices[Offset + i]]);
-                const float cost = SAH[i] + surface_area(aabb_right) * (float)(index_count - i);
-                if (cost <= split.cost) {
-                    split.cost = cost;
-                    split.index = first_index + i;
-                    split.dimension = dimension;
-                    split.aabb_right = aabb_right;
-                }
+        AxisBest best[3];
+        if (parallel && index_count >= kAxisParMin) {
+            std::thread t1([&] { best[1] = sweep_axis(1, first_index, index_count); });
+            std::thread t2([&] { best[2] = sweep_axis(2, first_index, index_count); });
+            best[0] = sweep_axis(0, first_index, index_count);
+            t1.join();
+            t2.join();
+        } else {
+            for (int d = 0; d < 3; d++) best[d] = sweep_axis(d, first_index, index_count);
+        }
+        for (int d = 0; d < 3; d++) {
+            if (best[d].index != -1 && best[d].cost <= split.cost) {
+                split.cost = best[d].cost;
+                split.index = best[d].index;
+                split.dimension = d;
+                split.aabb_right = best[d].right;
             }
         }
         const int Offset = split.dimension * PrimCount;
@@ -246,8 +310,17 @@ struct BVH2Builder {
         return split;
     }
 
-    void BuildRecursive(int nodesi, int& node_index, int first_index, int index_count, uint32_t depth) {
-        if (depth > max_depth) max_depth = depth;
+    // BuildRecursive (BVH2Builder.cs:166-217). A subtree of k primitives takes 2(k-1) node slots of
+    // the sequential depth-first numbering, so the right subtree's first slot is known before the
+    // left one is built: large subtrees near the root are built on their own threads and the nodes
+    // are exactly the sequential ones.
+    static constexpr int kParMin = 1 << 16;
+    static constexpr uint32_t kParDepth = 4;
+    bool parallel = true;  // TT_BUILD_SERIAL set: one thread (the tests compare both)
+    void BuildRecursive(int nodesi, int node_index, int first_index, int index_count, uint32_t depth) {
+        for (uint32_t m = max_depth.load(std::memory_order_relaxed); depth > m &&
+             !max_depth.compare_exchange_weak(m, depth, std::memory_order_relaxed);) {
+        }
         if (index_count == 1) {
             BVH2Nodes[nodesi].left = first_index;
             BVH2Nodes[nodesi].count = (uint32_t)index_count;
@@ -260,22 +333,31 @@ struct BVH2Builder {
             indices_going_left[DimensionedIndices[Offset + i]] = i < sp.index;
         for (int dim = 0; dim < 3; dim++) {
             if (dim == sp.dimension) continue;
-            int left = 0;
-            int right = sp.index - first_index;
+            int left = first_index;
+            int right = sp.index;
             Offset = dim * PrimCount;
             for (int i = first_index; i < IndexEnd; i++) {
                 const int index = DimensionedIndices[Offset + i];
                 temp[indices_going_left[index] ? (left++) : (right++)] = index;
             }
-            std::memcpy(&DimensionedIndices[Offset + first_index], temp.data(), sizeof(int) * (size_t)index_count);
+            std::memcpy(&DimensionedIndices[Offset + first_index], temp.data() + first_index,
+                        sizeof(int) * (size_t)index_count);
         }
         BVH2Nodes[nodesi].left = node_index;
         BVH2Nodes[BVH2Nodes[nodesi].left].aabb = sp.aabb_left;
         BVH2Nodes[BVH2Nodes[nodesi].left + 1].aabb = sp.aabb_right;
-        node_index += 2;
         const int l = BVH2Nodes[nodesi].left;
-        BuildRecursive(l, node_index, first_index, sp.index - first_index, depth + 1);
-        BuildRecursive(l + 1, node_index, sp.index, first_index + index_count - sp.index, depth + 1);
+        const int n_left = sp.index - first_index, n_right = first_index + index_count - sp.index;
+        const int next_left = node_index + 2, next_right = next_left + 2 * (n_left - 1);
+        if (parallel && index_count >= kParMin && depth < kParDepth) {
+            BigThread t;
+            t.start([=] { BuildRecursive(l, next_left, first_index, n_left, depth + 1); });
+            BuildRecursive(l + 1, next_right, sp.index, n_right, depth + 1);
+            t.join();
+        } else {
+            BuildRecursive(l, next_left, first_index, n_left, depth + 1);
+            BuildRecursive(l + 1, next_right, sp.index, n_right, depth + 1);
+        }
     }
 
     void build(const AABB* prims, int n) {
@@ -283,7 +365,7 @@ struct BVH2Builder {
         Primitives = prims;
         FinalIndices.resize(n);
         temp.assign(n, 0);
-        SAH.assign(n, 0.0f);
+        SAH.assign((size_t)n * 3, 0.0f);
         indices_going_left.assign(n, 0);
         DimensionedIndices.resize((size_t)n * 3);
         std::vector<float> cx(n), cy(n), cz(n);
@@ -302,14 +384,22 @@ struct BVH2Builder {
             BVH2Nodes[0].aabb.Extend(prims[i]);
         }
         const float* centers[3] = {cx.data(), cy.data(), cz.data()};
-        for (int d = 0; d < 3; d++) {
-            for (int i = 0; i < n; i++) FinalIndices[i] = i;
-            DotNetSort s{FinalIndices.data(), KeyCmp{centers[d]}};
+        auto sort_axis = [&](int d) {  // the three per-axis sorts are independent
+            int* seg = &DimensionedIndices[(size_t)n * d];
+            for (int i = 0; i < n; i++) seg[i] = i;
+            DotNetSort s{seg, KeyCmp{centers[d]}};
             s.Sort(n);
-            std::memcpy(&DimensionedIndices[(size_t)n * d], FinalIndices.data(), sizeof(int) * (size_t)n);
+        };
+        parallel = std::getenv("TT_BUILD_SERIAL") == nullptr;
+        if (parallel && n >= kParMin) {
+            std::thread t1(sort_axis, 1), t2(sort_axis, 2);
+            sort_axis(0);
+            t1.join();
+            t2.join();
+        } else {
+            for (int d = 0; d < 3; d++) sort_axis(d);
         }
-        int nodeIndex = 2;
-        BuildRecursive(0, nodeIndex, 0, n, 0);
+        BuildRecursive(0, 2, 0, n, 0);
         std::memcpy(FinalIndices.data(), DimensionedIndices.data(), sizeof(int) * (size_t)n);
     }
 };
@@ -360,7 +450,8 @@ struct BVH8Builder {
     const BVHNode2Data* nodes = nullptr;
     float cost2[8][8];
 
-    int calculate_cost(int node_index) {
+    bool parallel = false;  // the cost pass of large trees runs its top subtrees on their own threads
+    int calculate_cost(int node_index, uint32_t depth = 0) {
         const BVHNode2Data& node = nodes[node_index];
         int num_primitives;
         if (node.count > 0) {
@@ -372,7 +463,17 @@ struct BVH8Builder {
                 decisions[node_index * 7 + i].Type = 0;
             }
         } else {
-            num_primitives = calculate_cost(node.left) + calculate_cost(node.left + 1);
+            const int l = node.left;
+            if (parallel && depth < 4) {  // disjoint subtrees write disjoint cost / decision entries
+                int a = 0;
+                BigThread t;
+                t.start([&] { a = calculate_cost(l, depth + 1); });
+                const int b = calculate_cost(l + 1, depth + 1);
+                t.join();
+                num_primitives = a + b;
+            } else {
+                num_primitives = calculate_cost(l, depth + 1) + calculate_cost(l + 1, depth + 1);
+            }
             {
                 const float cost_leaf = num_primitives <= 3 ? (float)num_primitives * surface_area(node.aabb)
                                                             : std::numeric_limits<float>::max();
@@ -571,6 +672,7 @@ struct BVH8Builder {
         nodes = bvh2.BVH2Nodes.data();
         cwbvhindex_count = 0;
         cwbvhnode_count = 1;
+        parallel = bvh2.parallel && bvh2.PrimCount >= (1 << 16);
         if (calculate_cost(0) < 0) return false;
         if (!collapse(bvh2.FinalIndices.data(), 0, 0)) return false;
         BVH8Nodes.resize((size_t)cwbvhnode_count);
