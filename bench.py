@@ -476,7 +476,11 @@ def main():
 
     c5t = None
     if world > 1 and not args.no_c5_tiles:
-        c5t = c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world)
+        try:  # failures before the gather are agreed on inside; this catches rank 0's reassembly
+            c5t = c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world)
+        except Exception as e:  # noqa: BLE001 — auxiliary, never lose the metric line
+            c5t = {"error": f"{type(e).__name__}: {e}"}
+            log(f"c5 tiles failed: {e}")
 
     if rank != 0:
         if world > 1:
