@@ -126,9 +126,9 @@ def test_golden_device_pointers(engine):
 
 
 def test_back_to_back_async_launches(engine):
-    """Asynchronous launches skip the control-block reset: the previous trace launch's last wave
-    re-zeroes the dequeue tickets. A chain of async traces of different sizes (with a synchronous
-    launch and a stats launch in the chain) must give every ray the record a lone launch gives."""
+    """A chain of asynchronous traces of different sizes on one stream (with a synchronous launch
+    and a stats launch in the chain) must give every ray the record a lone launch gives: each
+    launch starts from a clean control block (dequeue tickets, error counters)."""
     import torch
 
     sc = tthip.single_object_scene(tthip.Mesh.soup(7, 30000, 1.0, 0.08))

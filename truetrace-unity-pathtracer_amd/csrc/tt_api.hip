@@ -85,7 +85,6 @@ struct tt_ctx {
     uint32_t grid_of[12] = {};  // resident persistent grid per kernel instantiation
     uint32_t shadow_grid_of[4] = {};  // the same for the any-hit kernel (stats * 2 + matcheck)
     TraceControl* ctl = nullptr;
-    bool ctl_clean = false;  // dequeue tickets are zero (a trace kernel's last wave re-zeroes them)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
     hipEvent_t ring0[256] = {}, ring1[256] = {};
     uint32_t ring_n = 0, ring_base = 0;
@@ -1066,16 +1065,13 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
     const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],
                                                  blocks_needed));
-    // Back-to-back asynchronous launches skip the control-block memset (a fill kernel plus a
-    // dependency gap, ~5 us per launch): the previous trace launch's last wave re-zeroed the
-    // tickets (sched_release). Synchronous and stats launches still zero everything they read back.
-    static const bool always_reset = std::getenv("TT_CTL_ALWAYS_RESET") != nullptr;  // A/B knob
-    if (!async || want_stats || !c->ctl_clean || always_reset) TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
+    // The control block is zeroed before every launch. (A kernel-side reset by the last wave to
+    // exit would save the ~5 us fill, but its device-scope release fence per exiting wave writes
+    // back L2 under the still-running waves: measured 15% slower, profiles/r01_exp_ctl_reset.txt.)
+    TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
-    c->ctl_clean = false;
     TT_HIP(c, tt_launch_trace(a, want_stats, matcheck, info_mode, grid, c->stream));
-    c->ctl_clean = true;
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     c->ring_n++;
     c->ev0 = c->ring0[slot];
@@ -1191,7 +1187,6 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
-    c->ctl_clean = false;  // the any-hit kernel leaves its tickets behind
     TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     c->ring_n++;

@@ -67,8 +67,7 @@ struct TraceControl {
     uint32_t seg_ticket[8 * 32];  // per-segment dequeue tickets, one 128-B line each
     uint32_t err_overflow;    // rays that overflowed the 16-entry stack
     uint32_t err_unsupported; // cutout material reached (never with a validated scene)
-    uint32_t waves_done;      // trace kernels: waves that left; the last one re-zeroes the tickets
-    uint32_t pad;
+    uint32_t pad[2];
     unsigned long long stats[8];  // rays, nodes, tris, blas, hits, reps_exhausted, overflow, accepts
     unsigned long long diag[8];   // STATS-build SIMD diagnostics: wave iterations, node-phase iterations,
                                   // node-phase lanes, tri-phase iterations, tri-phase lanes, active lanes,

@@ -524,7 +524,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             if (lane == 0 && v) atomicAdd(A.diag_times + k, (unsigned long long)v);
         }
 #endif
-    sched_release(A.ctl, lane);
 }
 
 // ------------------------------------------------------------- uniform-step kernel
@@ -885,7 +884,6 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
             for (int k = 0; k < 6; k++) atomicAdd(&A.ctl->diag[k], (unsigned long long)d[k]);
         }
     }
-    sched_release(A.ctl, lane);
 }
 
 #ifndef TT_KERNEL_UNIFORM

@@ -366,22 +366,6 @@ __device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_
     return 0u;
 }
 
-// Kernel epilogue of the trace kernels: the last wave to leave re-zeroes the dequeue tickets (and
-// the exit count), so the next launch needs no hipMemsetAsync of the control block; every wave's
-// final (exhausted) dequeue precedes its exit count, and the fences order the two.
-__device__ __forceinline__ void sched_release(TraceControl* ctl, uint32_t lane) {
-    if (lane == 0) {
-        __threadfence();
-        const uint32_t waves = gridDim.x * (TT_BLOCK / TT_WAVE);
-        if (atomicAdd(&ctl->waves_done, 1u) == waves - 1u) {
-            __threadfence();
-#pragma unroll
-            for (uint32_t k = 0; k < TT_SEGS; k++) atomicExch(&ctl->seg_ticket[k * 32u], 0u);
-            atomicExch(&ctl->waves_done, 0u);
-        }
-    }
-}
-
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
