@@ -55,11 +55,12 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
                     o.w = miss ? 1u : 0u;
                 }
             }
-            if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+            if (write) io_store16(reinterpret_cast<uint4*>(A.info) + (size_t)ty * A.width + tx, o);
         }
     }
     const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-    reinterpret_cast<uint4*>(R)[2] = make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+    io_store16(reinterpret_cast<uint4*>(R) + 2,
+               make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv));
     return best.t != A.far_plane;
 }
 }  // namespace
@@ -233,9 +234,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 }
                 ray_index = A.ray_offset + local;
                 const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
-                const uint4 r0 = rp[0], r1 = rp[1];
+                const uint4 r0 = io_load16(rp), r1 = io_load16(rp + 1);
                 pix = r0.w;
-                if (INFO == 2) col_w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
+                if (INFO == 2) col_w = (pix < A.width * A.height) ? io_loadf(&A.colors[pix].Data[3]) : 0.0f;
                 ray.ox = __uint_as_float(r0.x);
                 ray.oy = __uint_as_float(r0.y);
                 ray.oz = __uint_as_float(r0.z);

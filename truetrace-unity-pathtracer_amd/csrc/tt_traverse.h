@@ -38,6 +38,9 @@
 #ifndef TT_NCACHE
 #define TT_NCACHE 0       // LDS node-cache slots per block (closest-hit kernel; 0: off)
 #endif
+#ifndef TT_NT_IO
+#define TT_NT_IO 0        // bit 0: ray-record loads, bit 1: hit / info stores with the non-temporal hint
+#endif
 #ifndef TT_WAVES_PER_EU
 #define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
 #endif
@@ -364,6 +367,31 @@ __device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_
         S.est = 0;
     }
     return 0u;
+}
+
+// Streaming accesses of the per-ray records (read or written once per launch): with TT_NT_IO they
+// carry the non-temporal hint so they do not displace BVH nodes / triangles in L2 and MALL.
+__device__ __forceinline__ uint4 io_load16(const uint4* p) {
+#if TT_NT_IO & 1
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void io_store16(uint4* p, uint4 v) {
+#if TT_NT_IO & 2
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ float io_loadf(const float* p) {
+#if TT_NT_IO & 1
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
 }
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
