@@ -84,7 +84,9 @@ struct tt_ctx {
     uint32_t grid = 0;
     uint32_t grid_of[12] = {};  // resident persistent grid per kernel instantiation
     uint32_t shadow_grid_of[4] = {};  // the same for the any-hit kernel (stats * 2 + matcheck)
-    TraceControl* ctl = nullptr;
+    TraceControl* ctl = nullptr;  // two control blocks: a trace launch uses one and zeroes the other
+    uint32_t ctl_cur = 0;          // the block the next launch uses
+    bool ctl_zero[2] = {false, false};  // known zero when the next launch on the stream runs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
     hipEvent_t ring0[256] = {}, ring1[256] = {};
     uint32_t ring_n = 0, ring_base = 0;
@@ -528,7 +530,7 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     for (int k = 0; k < 12; k++) max_grid = std::max(max_grid, c->grid_of[k]);
     for (int k = 0; k < 4; k++) max_grid = std::max(max_grid, c->shadow_grid_of[k]);
     c->spill_threads = max_grid * tt_trace_block_size();
-    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), sizeof(TraceControl)) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), 2 * sizeof(TraceControl)) != hipSuccess) {
         tt_ctx_destroy(c);
         return TT_ERR_OOM;
     }
@@ -1046,7 +1048,9 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.rays = d_rays;
     a.info = d_info;
     a.colors = d_colors;
-    a.ctl = c->ctl;
+    const uint32_t ci = c->ctl_cur;
+    a.ctl = c->ctl + ci;
+    a.ctl_next = c->ctl + (ci ^ 1u);
     a.spill = c->spill.p;
     if (const char* e = std::getenv("TT_DIAG_TIMES_PTR")) a.diag_times = reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0));
     a.n_rays = p->n_rays;
@@ -1065,20 +1069,28 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
     const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],
                                                  blocks_needed));
-    // The control block is zeroed before every launch. (A kernel-side reset by the last wave to
-    // exit would save the ~5 us fill, but its device-scope release fence per exiting wave writes
-    // back L2 under the still-running waves: measured 15% slower, profiles/r01_exp_ctl_reset.txt.)
-    TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
+    // Control blocks: every trace kernel zeroes the OTHER block at its start (block 0, plain stores;
+    // the previous launch on the stream, which used it, has finished), so back-to-back async
+    // launches need no fill kernel in between. Synchronous / stats launches, and the first launch
+    // after an any-hit launch, still zero their block here. (A reset by the last wave to exit instead
+    // needs a device-scope fence per wave, which writes back L2 under the draining waves: measured
+    // 15% slower, profiles/r01_exp_ctl_reset.txt.)
+    static const bool always_reset = std::getenv("TT_CTL_ALWAYS_RESET") != nullptr;  // A/B knob
+    if (!async || want_stats || !c->ctl_zero[ci] || always_reset)
+        TT_HIP(c, hipMemsetAsync(c->ctl + ci, 0, sizeof(TraceControl), c->stream));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
+    c->ctl_zero[0] = c->ctl_zero[1] = false;
     TT_HIP(c, tt_launch_trace(a, want_stats, matcheck, info_mode, grid, c->stream));
+    c->ctl_zero[ci ^ 1u] = true;
+    c->ctl_cur = ci ^ 1u;
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     c->ring_n++;
     c->ev0 = c->ring0[slot];
     c->ev1 = c->ring1[slot];
     if (async) return TT_OK;
     TraceControl ctl;
-    TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl + ci, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
     if (!dev) {
         TT_HIP(c, hipMemcpyAsync(rays + off, d_rays + off, sizeof(tt_ray_data) * p->n_rays, hipMemcpyDeviceToHost, c->stream));
         if (info) TT_HIP(c, hipMemcpyAsync(info, d_info, sizeof(uint32_t) * 4 * wh, hipMemcpyDeviceToHost, c->stream));
@@ -1173,7 +1185,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     a.visibility = d_vis;
     a.colors = d_col;
     a.nee_pos = d_nee;
-    a.ctl = c->ctl;
+    a.ctl = c->ctl + c->ctl_cur;
     a.spill = c->spill.p;
     a.n_rays = p->n_rays;
     a.width = p->screen_width;
@@ -1184,9 +1196,10 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     const uint32_t blocks_needed = ((p->n_rays + 255u) / 256u + 3u) / 4u;
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));
-    TT_HIP(c, hipMemsetAsync(c->ctl, 0, sizeof(TraceControl), c->stream));
+    TT_HIP(c, hipMemsetAsync(c->ctl + c->ctl_cur, 0, sizeof(TraceControl), c->stream));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
+    c->ctl_zero[0] = c->ctl_zero[1] = false;  // the any-hit kernel zeroes nothing
     TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     c->ring_n++;
@@ -1194,7 +1207,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     c->ev1 = c->ring1[slot];
     if (async) return TT_OK;
     TraceControl ctl;
-    TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl + c->ctl_cur, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
     if (!dev) {
         TT_HIP(c, hipMemcpyAsync(rays, d_rays, sizeof(tt_shadow_ray) * p->n_rays, hipMemcpyDeviceToHost, c->stream));
         if (visibility)

@@ -134,6 +134,7 @@ struct TraceArgs {
     int32_t bounce;
     uint32_t flags;              // TT_TRACE_*
     uint32_t tile_swizzle;       // 1: work index -> 8x8 screen tiles (n_rays == W*H, W,H % 8 == 0)
+    TraceControl* ctl_next;      // the other control block: zeroed by this launch for the next one
     const uint32_t* ncache;      // LDS node cache plan: node index per slot [n_ncache], then child codes [n_ncache]
     uint32_t n_ncache;           // cached nodes (<= tt_trace_ncache_cap())
     uint32_t root_code;          // cache code of the TLAS root (node 0): 1 when slot 0 holds it

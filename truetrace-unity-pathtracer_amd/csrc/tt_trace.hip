@@ -71,6 +71,7 @@ template <bool STATS, bool MATCHECK, int INFO>
 __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
+    zero_next_control(A.ctl_next, tid);
 #if TT_NCACHE
     // LDS node cache: copies of the top levels of the scene graph (planned on the host, breadth
     // first from the TLAS root, whole sibling groups; tt_api.hip plan_node_cache), loaded from the
@@ -545,6 +546,7 @@ template <bool STATS, bool MATCHECK, int INFO>
 __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
     __shared__ uint2 s_stack[TT_UNIFORM_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
+    zero_next_control(A.ctl_next, tid);
     const uint32_t lane = tid & (TT_WAVE - 1);
 
     uint32_t pool_next = 0, pool_end = 0, more = 1;

@@ -394,6 +394,15 @@ __device__ __forceinline__ float io_loadf(const float* p) {
 #endif
 }
 
+// Zeroes the next launch's control block (block 0; plain stores, no fence: the kernel boundary
+// orders them before the next launch on the stream).
+__device__ __forceinline__ void zero_next_control(TraceControl* next, uint32_t tid) {
+    if (blockIdx.x == 0 && next) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(next);
+        for (uint32_t i = tid; i < (uint32_t)(sizeof(TraceControl) / 4); i += TT_BLOCK) w[i] = 0u;
+    }
+}
+
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
