@@ -443,7 +443,9 @@ void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
     o.e2y = t.posedge2[1];
     o.e2z = t.posedge2[2];
     o.matdat = t.MatDat;
+#if !TT_TRI40
     o.pad0 = o.pad1 = 0;
+#endif
 }
 
 bool is_device_ptr(const void* p) {

@@ -30,14 +30,19 @@ __device__ __forceinline__ float rcp_rn(float a) {
 // (CudaTriangle pos0/posedge1/posedge2, CommonData.cginc:63-66) + MatDat, padded so one
 // triangle is three 16-B loads. Built from AggTris at upload; AggTris itself also stays in
 // HBM for the attribute resolve.
+#ifndef TT_TRI40
+#define TT_TRI40 0  // 1: 40-B traversal triangles (no padding; 8-B aligned 16-B loads)
+#endif
 struct TriPos {
     float p0x, p0y, p0z, e1x;
     float e1y, e1z, e2x, e2y;
     float e2z;
     uint32_t matdat;
+#if !TT_TRI40
     uint32_t pad0, pad1;
+#endif
 };
-static_assert(sizeof(TriPos) == 48, "TriPos is 48 bytes");
+static_assert(sizeof(TriPos) == (TT_TRI40 ? 40 : 48), "TriPos size");
 
 // Traversal-layout mesh record, 64 B: W2L rows 0-2 (row-major, 12 floats) + the four offsets
 // IntersectBVH reads on a TLAS->BLAS switch (IntersectionKernels.compute:197-213).

@@ -100,7 +100,11 @@ __device__ __forceinline__ uint32_t node_offset(uint32_t i) {
 }
 __device__ __forceinline__ uint32_t tri_offset(uint32_t i) {
     uint32_t r;
+#if TT_TRI40
+    asm("v_lshl_add_u32 %0, %1, 2, %1\n\tv_lshlrev_b32 %0, 3, %0" : "=&v"(r) : "v"(i));
+#else
     asm("v_lshl_add_u32 %0, %1, 1, %1\n\tv_lshlrev_b32 %0, 4, %0" : "=&v"(r) : "v"(i));
+#endif
     return r;
 }
 
