@@ -1063,6 +1063,8 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.bounce = p->bounce;
     a.flags = p->flags;
     a.tile_swizzle = (p->n_rays == wh && p->screen_width % 8 == 0 && p->screen_height % 8 == 0) ? 1u : 0u;
+    a.div_width = fastdiv_make(std::max(1u, p->screen_width));
+    a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
     a.ncache = c->ncache.p;
     a.n_ncache = c->n_ncache;
     a.root_code = c->ncache_root;

@@ -115,6 +115,23 @@ struct MatView {
     uint32_t tex_w, tex_h;
 };
 
+// Exact unsigned division by a launch-constant divisor (round-up multiplier, valid for every
+// 32-bit n and d >= 1): q = (t + ((n - t) >> s1)) >> s2 with t = umulhi(m, n). The host fills it
+// (fastdiv_make); replaces the ~40-instruction VALU udiv in the refill and pixel decode.
+struct FastDiv {
+    uint32_t m, s1, s2;
+};
+__host__ inline FastDiv fastdiv_make(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) l++;
+    const unsigned __int128 m = (((unsigned __int128)1 << 32) * (((unsigned __int128)1 << l) - d)) / d + 1u;
+    return FastDiv{(uint32_t)m, l < 1 ? l : 1u, l > 1 ? l - 1 : 0u};
+}
+__device__ __forceinline__ uint32_t fastdiv(uint32_t n, const FastDiv& d) {
+    const uint32_t t = __umulhi(d.m, n);
+    return (t + ((n - t) >> d.s1)) >> d.s2;
+}
+
 struct TraceArgs {
     const uint4* nodes;          // 80 B nodes as 5 x uint4
     uint32_t n_nodes;
@@ -143,6 +160,8 @@ struct TraceArgs {
     const uint32_t* ncache;      // LDS node cache plan: node index per slot [n_ncache], then child codes [n_ncache]
     uint32_t n_ncache;           // cached nodes (<= tt_trace_ncache_cap())
     uint32_t root_code;          // cache code of the TLAS root (node 0): 1 when slot 0 holds it
+    FastDiv div_width;           // n / width (pixel decode of finished rays)
+    FastDiv div_tiles;           // n / (width / 8) (8x8 tile swizzle in the refill)
 };
 
 // Any-hit visibility launch (tt_shadow.hip, kernel_shadow replacement).

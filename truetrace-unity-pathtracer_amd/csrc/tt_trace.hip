@@ -24,7 +24,7 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
                                              const Best& best, const LaneRay& wr) {
     tt_ray_data* R = A.rays + ray_index;
     if (INFO != 0) {
-        const uint32_t tx = pix % A.width, ty = pix / A.width;
+        const uint32_t ty = fastdiv(pix, A.div_width), tx = pix - ty * A.width;
         if (ty < A.height) {
             uint4 o;
             bool write = false;
@@ -230,7 +230,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 if (A.tile_swizzle) {
                     const uint32_t tw = A.width >> 3;
                     const uint32_t t = widx >> 6, l = widx & 63u;
-                    const uint32_t ty = t / tw, tx = t - ty * tw;
+                    const uint32_t ty = fastdiv(t, A.div_tiles), tx = t - ty * tw;
                     local = (ty * 8u + (l >> 3)) * A.width + tx * 8u + (l & 7u);
                 }
                 ray_index = A.ray_offset + local;
@@ -602,7 +602,7 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
                 if (A.tile_swizzle) {
                     const uint32_t tw = A.width >> 3;
                     const uint32_t t = widx >> 6, l = widx & 63u;
-                    const uint32_t ty = t / tw, tx = t - ty * tw;
+                    const uint32_t ty = fastdiv(t, A.div_tiles), tx = t - ty * tw;
                     local = (ty * 8u + (l >> 3)) * A.width + tx * 8u + (l & 7u);
                 }
                 ray_index = A.ray_offset + local;
@@ -817,7 +817,7 @@ __global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
                 tt_ray_data* R = A.rays + ray_index;
                 if (INFO != 0) {
                     const uint32_t pix = R->PixelIndex;
-                    const uint32_t tx = pix % A.width, ty = pix / A.width;
+                    const uint32_t ty = fastdiv(pix, A.div_width), tx = pix - ty * A.width;
                     if (ty < A.height) {
                         uint4 o = make_uint4(0, 0, 0, 0);
                         bool write = false;
