@@ -10,9 +10,17 @@ resident in HBM in the reference's 2*W*H ping-pong RayData buffer. Ray generatio
 bounce enqueue run once during setup (they are the caller's kernels, not the trace).
 
 Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): one process per GPU, scene
-replicated per GPU, each rank traces its own independent sample (frames_accumulated = rank,
-sub-pixel jitter) of the 1080p view — weak scaling with no data-path collective. An optional
-RCCL gather of the hit records to rank 0 runs after the timed region (--gather).
+replicated per GPU, the 1080p frame's 64x64 screen tiles dealt round-robin to the ranks (SURVEY.md
+§8(e)). Each rank traces its tiles' primary rays and their bounce-1 rays, then the primary hit
+records go to rank 0 in ONE RCCL gather over xGMI -- inside the timed step, so a step is a whole
+frame and ``value`` is frame rays / frame time (strong scaling). ``--shard sample`` instead has
+every rank trace its own full-frame sample (weak scaling, no data-path collective); that layout is
+also reported as ``config.aux_sample_sharded``.
+
+Streams: torch and the engine share ONE stream (a torch.cuda.Stream made current before any
+allocation and passed to tt_ctx_create), so every torch copy / collective and every engine launch
+is ordered, and every per-launch time comes from HIP events on that stream (the engine's own
+timing ring, tt_timing_read).
 """
 from __future__ import annotations
 
@@ -143,18 +151,16 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             return None
 
     def time_calls(fn, warmup, steps):
-        """Per-call GPU time (ms) of `fn` (asynchronous launches on the context stream, which is
-        torch's current stream here) from CUDA/HIP events around each call."""
+        """Per-call GPU time (ms) of `fn` (one asynchronous engine call on the shared stream) from
+        the engine's timing ring: HIP events around the call's device work on that stream."""
         for _ in range(warmup):
             fn()
-        torch.cuda.synchronize(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b in ev:
-            a.record()
+        eng.timing_reset()
+        for _ in range(steps):
             fn()
-            b.record()
-        torch.cuda.synchronize(dev)
-        return np.asarray([a.elapsed_time(b) for a, b in ev], np.float64)
+        ms = np.asarray(eng.timing_read(), np.float64)
+        assert len(ms) == steps, (len(ms), steps)
+        return ms
 
     if "c3" in which:
         run("c3_sponza_primary_plus_3_bounces_1080p", T.c2_sponza, T.C2_VIEW, 1920, 1080, 3,
@@ -263,6 +269,72 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     return rec
 
 
+def cpu_share():
+    """(hardware threads, CPUs this process may run on, cgroup CPU quota or None)."""
+    hw = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = hw
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return hw, aff, quota
+
+
+def cpu_baseline(scene, rays, info_n, n_prim, nb, colors, far, W, H, seconds):
+    """The scalar oracle (oracle/tt_oracle.c, -O3, no intrinsics) on the host cores over the same
+    step workload (primary + bounce-1 rays), repeated for ~`seconds`. Primary figure: every CPU the
+    process may run on (sched_getaffinity); a 16-thread run is kept as a secondary field (the
+    per-GPU CPU share the GPU box grants)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ctypes as O  # the oracle is only the CPU baseline here, never the measured path
+    import tthip
+
+    host_rays = rays.cpu().numpy().view(tthip.RAY_DTYPE).copy()
+    host_info = np.zeros((info_n, 4), np.uint32)
+    hw, aff, quota = cpu_share()
+
+    def run(nthreads, budget):
+        done, reps, tc0 = 0, 0, time.perf_counter()
+        while True:
+            O.trace(scene, host_rays, n_prim, 0, far, W, H, info=host_info, nthreads=nthreads)
+            O.trace(scene, host_rays, nb, 1, far, W, H, info=host_info, colors=colors, nthreads=nthreads)
+            done += n_prim + nb
+            reps += 1
+            if time.perf_counter() - tc0 >= budget:
+                break
+        t = time.perf_counter() - tc0
+        return done / t / 1e6, reps, t
+
+    v_all, reps, tcpu = run(aff, seconds)
+    v16 = None
+    if aff != 16:
+        v16, _, _ = run(16, seconds / 2)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
+    cpu = {"value": round(v_all, 3), "unit": "Mrays/s", "cores": aff, "kind": "port",
+           "host_cpu": model, "hardware_threads": hw, "cgroup_cpu_quota": quota,
+           "value_16_threads": None if v16 is None else round(v16, 3),
+           "sample": f"full step workload ({n_prim} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
+                     f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {aff} threads "
+                     f"(all CPUs of the process' affinity mask; cgroup quota {quota}); "
+                     f"C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
+                     + ("not run: no .NET runtime (dotnet) on the box" if shutil.which("dotnet") is None
+                        else "not run by bench.py: see tools/dump_scene_raw.py")}
+    log(f"cpu baseline {cpu['value']} Mrays/s on {aff} threads ({reps} reps, {tcpu:.1f}s); 16 threads: {v16}")
+    return cpu
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -273,14 +345,12 @@ def main():
     ap.add_argument("--tris", type=int, default=262267)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x53504F4E)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true", help="RCCL-gather hit records to rank 0 after timing")
-    ap.add_argument("--shard", choices=["sample", "tiles"], default="sample",
-                    help="sample: every rank traces its own full-frame sample (weak scaling, default); tiles: "
-                         "the frame's 64x64 tiles are dealt round-robin to ranks, each traces its pixels and their "
-                         "bounces, and the primary hit records are RCCL-gathered to rank 0 (strong scaling, "
-                         "SURVEY 8e)")
+    ap.add_argument("--shard", choices=["tiles", "sample"], default="tiles",
+                    help="N > 1 layout. tiles (default, SURVEY 8e): the frame's 64x64 tiles are dealt round-robin "
+                         "to ranks, each traces its pixels and their bounce-1 rays, and the primary hit records are "
+                         "RCCL-gathered to rank 0 inside every timed step (strong scaling). sample: every rank "
+                         "traces its own full-frame sample, no collective (weak scaling)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     ap.add_argument("--no-c5-tiles", action="store_true",
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
@@ -295,21 +365,26 @@ def main():
     import torch  # first: tthip must bind to torch's HIP runtime (see tthip.hip_lib)
     import torch.distributed as dist
     import tthip
+    import ttdist
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the HIP engine has no CPU fallback)")
     # RCCL ("nccl") over xGMI, one process per GPU. TT_BENCH_DIST_BACKEND=gloo is a rehearsal mode for
-    # boxes with fewer GPUs than ranks (ranks share devices, host-side reductions); not a bench mode.
+    # boxes with fewer GPUs than ranks (ranks share devices, host-side collectives); not a bench mode.
     backend = os.environ.get("TT_BENCH_DIST_BACKEND", "nccl")
     gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    # ONE stream for torch and the engine, current before anything is allocated or launched
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=dev)
         else:
             dist.init_process_group(backend=backend)
+    tiles = world > 1 and args.shard == "tiles"
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -322,7 +397,9 @@ def main():
     am.add_parent(blas, None, mats)
     scene = am.build()
     log(f"rank {rank}: scene {len(scene.tris)} tris, {len(scene.nodes)} nodes, build {time.time() - t0:.2f}s")
-    eng = tthip.Engine(gpu, stream=torch.cuda.current_stream(dev).cuda_stream)
+    eng = tthip.Engine(gpu, stream=stream.cuda_stream)
+    assert eng.stream == stream.cuda_stream == torch.cuda.current_stream(dev).cuda_stream != 0, \
+        "engine and torch must share one (non-NULL) stream"
     eng.upload(scene)
 
     # ------------------------------------------------------------------ resident rays
@@ -332,20 +409,18 @@ def main():
     colors["Data"][:, 3] = 1.0  # shade set Data.w = CurBounce + 1 = 1 at bounce 0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
     c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H, 0.3, far)
-    tiles = args.shard == "tiles"
-    frames = 0 if tiles else rank
+    # C2 primary rays are generated without jitter; the sample layout jitters by rank
+    jitter, frames = (1, rank) if (world > 1 and not tiles) else (0, 0)
     if tiles:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), at the buffer's start
-        import ttdist
-
         pix = torch.from_numpy(ttdist.tile_pixels(W, H, world, rank)).to(dev)
         n_prim = int(pix.shape[0])
         full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
+        eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         rays.view(2 * WH, 48)[:n_prim] = full.view(WH, 48)[pix]
         del full
     else:
         n_prim = WH
-        eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
+        eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
     s_prim = eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, stats=True)
     nb = eng.enqueue_bounce(rays, n_prim, 0, far, W, H, frames=frames, max_bounce=1, device=True)
     s_bnc = eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
@@ -358,17 +433,32 @@ def main():
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(nb, 1):.2f} "
         f"tris/ray {s_bnc.tri_tests / max(nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}")
 
+    # tiles: the frame's primary hit records go to rank 0 in one gather per step (shards padded to
+    # the largest so every rank sends one equal-size message)
+    sizes, hits_buf, gather_list = None, None, None
+    if tiles:
+        n_t = torch.tensor([n_prim], dtype=torch.int64, device=red_dev)
+        sz = [torch.zeros_like(n_t) for _ in range(world)]
+        dist.all_gather(sz, n_t)
+        sizes = [int(x.item()) for x in sz]
+        hits_buf = torch.zeros((max(sizes), 4), dtype=torch.int32, device=red_dev)
+        gather_list = [torch.empty_like(hits_buf) for _ in range(world)] if rank == 0 else None
+    prim_hits = rays[: n_prim * 48].view(n_prim, 48)[:, 32:48].view(torch.int32)
+
     def step():
         eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, asynchronous=True)
         eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+        if tiles:
+            hits_buf[:n_prim].copy_(prim_hits)
+            dist.gather(hits_buf, gather_list, dst=0)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    eng.timing_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.timing_reset()
     t_start = time.perf_counter()
     for i in range(args.steps):
         step()
@@ -378,7 +468,9 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     launch_ms = eng.timing_read()
+    assert len(launch_ms) == 2 * args.steps, (len(launch_ms), args.steps)
     total_rays = float(rays_per_step * args.steps)
+    trace_ms_rank = float(np.sum(launch_ms)) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -386,60 +478,104 @@ def main():
         r = torch.tensor([total_rays], dtype=torch.float64, device=red_dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         total_rays = float(r.item())
+        tr = torch.tensor([trace_ms_rank], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(tr, op=dist.ReduceOp.MAX)
+        trace_ms_slowest = float(tr.item())
+    else:
+        trace_ms_slowest = trace_ms_rank
 
     prim_ms = launch_ms[0::2]
     bnc_ms = launch_ms[1::2]
     avg_ms = float(np.mean(launch_ms))
     achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9  # GB/s per launch, averaged over both launches
 
+    # tiles: SURVEY 8(e) parity -- the gathered frame must equal one GPU tracing the whole frame
+    gather_parity = None
+    if tiles and rank == 0:
+        frame = ttdist.assemble_tiles([g[:n] for g, n in zip(gather_list, sizes)], W, H, world)
+        one = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
+        eng.trace(one, WH, 0, far, W, H, device=True)
+        ref = one.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+        gather_parity = bool(np.array_equal(frame, ref))
+        del one
+        log(f"gathered frame: {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels, "
+            f"identical to a single-GPU trace: {gather_parity}")
+
+    # secondary N > 1 layout: every rank traces its own full-frame jittered sample (weak scaling)
+    sample_sharded = None
+    if tiles:
+        srays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(srays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
+        eng.trace(srays, WH, 0, far, W, H, device=True)
+        snb = eng.enqueue_bounce(srays, WH, 0, far, W, H, frames=rank, max_bounce=1, device=True)
+
+        def sstep():
+            eng.trace(srays, WH, 0, far, W, H, info=info, device=True, asynchronous=True)
+            eng.trace(srays, snb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+
+        for _ in range(args.warmup):
+            sstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            sstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        st = torch.tensor([time.perf_counter() - ts, float((WH + snb) * args.steps)], dtype=torch.float64,
+                          device=red_dev)
+        tmax = st[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        rsum = st[1:].clone()
+        dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
+        sample_sharded = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
+                          "scaling": "weak", "ranks": world,
+                          "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4)}
+        del srays
+        log(f"sample-sharded (weak) layout: {sample_sharded}")
+
     # ---- auxiliary (not the metric): any-hit NEE visibility rays (tt_trace_shadow)
-    # from this rank's primary hit points toward a point light; each launch restores the pristine
-    # rays first (occluded rays get t = 0 in place), only the kernel is timed (HIP events).
+    # from this rank's primary hit points toward a point light. Every launch first restores the
+    # pristine rays (occluded rays get t = 0 in place) on the shared stream; only the kernel is timed.
     shadow = None
     if not args.no_shadow:
         sr = nee_rays(torch, rays, n_prim, far, light=(0.0, 9.0, 0.5))
         ns = int(sr.shape[0]) // 48
         work = torch.empty_like(sr)
-        s_sh = None
+        work.copy_(sr)
+        s_sh = eng.trace_shadow(work, ns, 0, W, H, device=True, stats=True)
         for k in range(args.warmup + args.steps):
             if k == args.warmup:
-                torch.cuda.synchronize(dev)
                 eng.timing_reset()
             work.copy_(sr)
-            if k == 0:
-                s_sh = eng.trace_shadow(work, ns, 0, W, H, device=True, stats=True)
-            else:
-                eng.trace_shadow(work, ns, 0, W, H, device=True, asynchronous=True)
+            eng.trace_shadow(work, ns, 0, W, H, device=True, asynchronous=True)
         sh_ms = eng.timing_read()
+        assert len(sh_ms) == args.steps
         shadow = {"rays": ns, "trace_ms": round(float(np.mean(sh_ms)), 4),
+                  "trace_ms_median": round(float(np.median(sh_ms)), 4),
                   "mrays_s": round(ns / float(np.mean(sh_ms)) / 1e3, 1),
                   "occluded": int(s_sh.hits), "nodes_per_ray": round(s_sh.node_visits / max(ns, 1), 2)}
         log(f"shadow: {ns} NEE rays {shadow['trace_ms']} ms/launch = {shadow['mrays_s']} Mrays/s, "
             f"{shadow['occluded']} occluded")
 
     # ---- auxiliary: the ray producers around the trace (excluded from the metric):
-    # Generate (1080p primary rays) and the diffuse-bounce enqueue with wave-ballot compaction, on a
-    # scratch copy of the traced rays; HIP events around each call (the enqueue call includes its
-    # survivor-count readback).
+    # Generate (1080p primary rays) and the diffuse-bounce enqueue with wave-ballot compaction (counter
+    # reset + kernel), on a scratch copy of the traced rays restored before every call; engine timing ring.
     producers = None
     if world == 1:
         scratch = rays.clone()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2 * args.steps)]
+        eng.timing_reset()
         for k in range(args.steps):
-            a, b = ev[k]
-            a.record()
-            eng.generate(scratch, c2w, ip, W, H, 0.3, far, jitter=1, frames=frames, max_bounce=1, device=True)
-            b.record()
-        torch.cuda.synchronize(dev)
-        gen_ms = [a.elapsed_time(b) for a, b in ev[:args.steps]]
+            eng.generate(scratch, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
+        gen_ms = eng.timing_read()
+        eng.timing_reset()
         for k in range(args.steps):
             scratch.copy_(rays)
-            a, b = ev[args.steps + k]
-            a.record()
             eng.enqueue_bounce(scratch, n_prim, 0, far, W, H, frames=frames, max_bounce=1, device=True)
-            b.record()
-        torch.cuda.synchronize(dev)
-        enq_ms = [a.elapsed_time(b) for a, b in ev[args.steps:]]
+        enq_ms = eng.timing_read()
         producers = {"generate_ms": round(float(np.median(gen_ms)), 4), "primary_rays": n_prim,
                      "enqueue_compact_ms": round(float(np.median(enq_ms)), 4), "bounce_rays": nb}
         del scratch
@@ -448,31 +584,6 @@ def main():
     aux = None
     if world == 1 and args.aux:
         aux = aux_configs(torch, tthip, eng, dev, args, set(args.aux.split(",")))
-
-    gather_ms, gather_parity = None, None
-    if (args.gather or tiles) and world > 1:
-        # primary hit records (16 B per ray) to rank 0 in one collective; tile shards are padded to
-        # the largest (ttdist.gather_hits) and rank 0 reassembles the frame in screen order
-        hits = rays[: n_prim * 48].view(n_prim, 48)[:, 32:48].contiguous().view(torch.int32).to(red_dev)
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        if tiles:
-            parts = ttdist.gather_hits(hits, world, rank)
-        else:
-            out = [torch.empty_like(hits) for _ in range(world)] if rank == 0 else None
-            dist.gather(hits, out, dst=0)
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        if tiles and rank == 0:
-            frame = ttdist.assemble_tiles(parts, W, H, world)
-            # SURVEY 8(e) parity: the gathered frame must equal one GPU tracing the whole frame
-            one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-            eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
-            eng.trace(one, WH, 0, far, W, H, device=True)
-            ref = one[: WH * 48].view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
-            gather_parity = bool(np.array_equal(frame, ref))
-            log(f"gathered frame: {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels, "
-                f"identical to a single-GPU trace: {gather_parity}")
 
     c5t = None
     if world > 1 and not args.no_c5_tiles:
@@ -490,35 +601,7 @@ def main():
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        import oracle_ctypes as O  # the oracle is only the CPU baseline here, never the measured path
-
-        host_rays = rays.cpu().numpy().view(tthip.RAY_DTYPE).copy()
-        host_info = np.zeros((WH, 4), np.uint32)
-        nthreads = max(1, args.cpu_threads)
-        done, reps, tc0 = 0, 0, time.perf_counter()
-        while True:
-            O.trace(scene, host_rays, n_prim, 0, far, W, H, info=host_info, nthreads=nthreads)
-            O.trace(scene, host_rays, nb, 1, far, W, H, info=host_info, colors=colors, nthreads=nthreads)
-            done += rays_per_step
-            reps += 1
-            if time.perf_counter() - tc0 >= args.cpu_seconds:
-                break
-        tcpu = time.perf_counter() - tc0
-        model = "unknown"
-        try:
-            with open("/proc/cpuinfo") as f:
-                model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
-        except OSError:
-            pass
-        cpu = {"value": round(done / tcpu / 1e6, 3), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
-               "host_cpu": model, "hardware_threads": os.cpu_count(),
-               "sample": f"full step workload ({n_prim} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
-                         f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {nthreads} threads; "
-                         f"C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
-                         + ("not run: no .NET runtime (dotnet) on the box" if shutil.which("dotnet") is None
-                            else "not run by bench.py: see tools/dump_scene_raw.py")}
-        log(f"cpu baseline {cpu['value']} Mrays/s ({reps} reps, {tcpu:.1f}s)")
+        cpu = cpu_baseline(scene, rays, WH, n_prim, nb, colors, far, W, H, args.cpu_seconds)
 
     # fabric traffic per launch from the round's separate rocprofv3 --pmc pass of this same command
     # (tools/profile_round.sh -> profiles/traffic_latest.json); null when no such pass was committed
@@ -548,23 +631,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if tiles else "weak",
+        "scaling": "weak" if (world > 1 and not tiles) else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza)",
         "config": {"workload": "sponza_primary_plus_1_bounce_1080p", "scene": "Sponza-shaped CWBVH8 (C2)",
                    "tris": int(len(scene.tris)), "cwbvh_nodes": int(len(scene.nodes)), "width": W, "height": H,
-                   "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_per_gpu": int(rays_per_step),
+                   "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_rank0": int(rays_per_step),
+                   "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "jitter": jitter,
                    "seed": hex(args.seed),
-                   "parallelism": (f"64x64 screen tiles round-robin over {world} ranks + RCCL gather of primary hits"
-                                   if tiles else f"sample-sharded x{world} (frames_accumulated=rank)"),
+                   "parallelism": ("single GPU, full frame" if world == 1 else
+                                   (f"64x64 screen tiles round-robin over {world} ranks + one RCCL gather of the "
+                                    f"primary hit records to rank 0 per step (inside the timed step)" if tiles
+                                    else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
+                   "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it",
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
                    "trace_ms_primary_median": round(float(np.median(prim_ms)), 4),
                    "trace_ms_bounce_median": round(float(np.median(bnc_ms)), 4),
-                   "kernel_mrays_s_trace_only": round(rays_per_step / (float(np.sum(launch_ms)) / args.steps) / 1e3, 2),
-                   "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                   "trace_ms_per_step_slowest_rank": round(trace_ms_slowest, 4),
+                   "kernel_mrays_s_trace_only": round(rays_per_step / trace_ms_rank / 1e3, 2),
                    "gather_identical_to_1gpu": gather_parity,
+                   "aux_sample_sharded": sample_sharded,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -195,7 +195,11 @@ typedef struct tt_config {
     uint32_t flags;        /* reserved, 0                                        */
     uint64_t max_rays;     /* capacity of the staging ray buffer for host-pointer
                               traces (2*W*H for a wavefront ray buffer); 0 = none */
-    void* stream;          /* hipStream_t to issue on; NULL = library-owned stream */
+    void* stream;          /* hipStream_t to issue on; NULL = a library-owned BLOCKING
+                              stream (it orders with the legacy NULL stream in both
+                              directions, so a caller that writes device buffers on the
+                              NULL stream, e.g. PyTorch's default stream, needs no extra
+                              synchronisation before or after a call) */
 } tt_config;
 
 /* Create / destroy a per-GPU context. */
@@ -346,8 +350,12 @@ typedef struct tt_stats {
 tt_status tt_trace_closest(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
                            uint32_t* primary_info, const tt_col_data* global_colors,
                            tt_stats* stats);
-/* Per-launch trace kernel durations (HIP events on the context stream), recorded for every
- * tt_trace_closest since the last tt_timing_reset (ring of 256 launches). Synchronizes. */
+/* Per-call GPU durations (HIP events on the context stream, in issue order) since the last
+ * tt_timing_reset (ring of 256 entries). One entry per call of tt_trace_closest and
+ * tt_trace_shadow (the trace kernel alone), tt_generate_primary (the generate kernel),
+ * tt_enqueue_diffuse_bounce (counter reset + enqueue kernel), tt_tlas_refit and tt_blas_refit
+ * (the whole device-side refit). Host<->device staging copies are never inside an entry.
+ * Synchronizes. */
 tt_status tt_timing_reset(tt_ctx* ctx);
 tt_status tt_timing_read(tt_ctx* ctx, float* ms, uint32_t max, uint32_t* n);
 

@@ -480,9 +480,9 @@ tt_status tt_oracle_trace(const tt_cwbvh_node* nodes, uint32_t n_nodes,
     if (st != TT_OK) return st;
     trace_job J = {&s, p, global_rays, primary_info, global_colors, counts};
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 256) nthreads = 256;
-    worker ws[256];
-    pthread_t th[256];
+    if (nthreads > 1024) nthreads = 1024;
+    worker ws[1024];
+    pthread_t th[1024];
     for (int t = 0; t < nthreads; t++) {
         ws[t].J = &J;
         ws[t].tid = (uint32_t)t;
@@ -749,9 +749,9 @@ tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
             return TT_ERR_UNSUPPORTED;
     shadow_job J = {&s, p, shadow_rays, visibility, global_colors, nee_pos, counts};
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 256) nthreads = 256;
-    shadow_worker ws[256];
-    pthread_t th[256];
+    if (nthreads > 1024) nthreads = 1024;
+    shadow_worker ws[1024];
+    pthread_t th[1024];
     for (int t = 0; t < nthreads; t++) {
         ws[t].J = &J;
         ws[t].tid = (uint32_t)t;

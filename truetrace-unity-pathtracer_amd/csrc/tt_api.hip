@@ -126,6 +126,7 @@ struct tt_ctx {
         uint32_t node_base = ~0u;  // the mesh's NodeOffset the plan was built for
         DevBuf<float> boxes;
     };
+
     std::map<uint32_t, BlasRefit> blas_refit;
     DevBuf<float> st_vtx;
     DevBuf<int32_t> st_idx, st_leaf;
@@ -144,6 +145,19 @@ struct tt_ctx {
     DevBuf<float4> st_nee;
     unsigned long long last_diag[8] = {};
 };
+
+// Per-call timing ring entries (tt_timing_read) around device work issued on the context stream.
+static hipError_t ring_open(tt_ctx* c, uint32_t& slot) {
+    slot = c->ring_n % TT_RING;
+    return hipEventRecord(c->ring0[slot], c->stream);
+}
+static hipError_t ring_close(tt_ctx* c, uint32_t slot) {
+    const hipError_t e = hipEventRecord(c->ring1[slot], c->stream);
+    c->ring_n++;
+    c->ev0 = c->ring0[slot];
+    c->ev1 = c->ring1[slot];
+    return e;
+}
 
 namespace {
 
@@ -493,7 +507,9 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     if (cfg->stream) {
         c->stream = static_cast<hipStream_t>(cfg->stream);
     } else {
-        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        // blocking (default-flag) stream: ordered with the legacy NULL stream, so callers that
+        // fill device buffers on it (torch's default stream) cannot race the engine
+        if (hipStreamCreate(&c->stream) != hipSuccess) {
             delete c;
             return TT_ERR_HIP;
         }
@@ -780,7 +796,10 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
         TT_HIP(c, hipMemcpyAsync(c->st_boxes.p, mesh_aabbs, sizeof(float) * 6 * n_mesh, hipMemcpyHostToDevice, c->stream));
         d_boxes = c->st_boxes.p;
     }
+    uint32_t slot;
+    TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
+    TT_HIP(c, ring_close(c, slot));
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -850,8 +869,11 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     a.boxes = R.boxes.p;
     a.tris88 = c->tris_raw.p + tri_base;
     a.tripos = c->tris.p + tri_base;
+    uint32_t slot;
+    TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_blas_construct(a, c->stream));
     TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
+    TT_HIP(c, ring_close(c, slot));
     if (!(p->flags & TT_TRACE_ASYNC) || !dev) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1287,8 +1309,11 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
     } else if (!is_device_ptr(rays)) {
         return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but rays is not device memory");
     }
+    uint32_t slot;
+    TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_launch_generate(c->cam.p, c->cam.p + 16, cam->width, cam->height, cam->near_plane, cam->far_plane,
                                  cam->jitter, cam->frames_accumulated, cam->max_bounce, d, c->stream));
+    TT_HIP(c, ring_close(c, slot));
     if (!dev) TT_HIP(c, hipMemcpyAsync(rays, d, sizeof(tt_ray_data) * wh, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
@@ -1314,9 +1339,12 @@ tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_
         d = c->st_rays.p;
         TT_HIP(c, hipMemcpyAsync(d + src, rays + src, sizeof(tt_ray_data) * p->n_rays, hipMemcpyHostToDevice, c->stream));
     }
+    uint32_t slot;
+    TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 16, c->stream));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
                                c->mesh_raw.p, c->counter.p, c->stream));
+    TT_HIP(c, ring_close(c, slot));
     uint32_t cnt = 0;
     TT_HIP(c, hipMemcpyAsync(&cnt, c->counter.p, 4, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));

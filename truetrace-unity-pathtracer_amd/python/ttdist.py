@@ -20,15 +20,20 @@ from typing import List
 import numpy as np
 
 
-def tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64) -> np.ndarray:
-    """Pixel indices owned by ``rank`` under round-robin tile sharding, in tile order."""
+def tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64, block: int = 8) -> np.ndarray:
+    """Pixel indices owned by ``rank`` under round-robin tile sharding, in tile order. Inside a
+    tile the pixels run in ``block``x``block`` sub-blocks (row-major blocks, row-major pixels in a
+    block), so the 64 rays a wave dequeues together are an 8x8 screen patch, as the trace
+    kernel's own swizzle makes them for full-frame batches."""
     tx, ty = (width + tile - 1) // tile, (height + tile - 1) // tile
     out = []
     for t in range(rank, tx * ty, world):
         x0, y0 = (t % tx) * tile, (t // tx) * tile
         ys, xs = np.meshgrid(np.arange(y0, min(y0 + tile, height)), np.arange(x0, min(x0 + tile, width)),
                              indexing="ij")
-        out.append((ys * width + xs).reshape(-1))
+        ys, xs = ys.reshape(-1), xs.reshape(-1)
+        order = np.lexsort((xs, ys, (xs - x0) // block, (ys - y0) // block))
+        out.append((ys * width + xs)[order])
     return np.concatenate(out).astype(np.int64) if out else np.zeros(0, np.int64)
 
 
