@@ -409,8 +409,12 @@ def main():
     colors["Data"][:, 3] = 1.0  # shade set Data.w = CurBounce + 1 = 1 at bounce 0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
     c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H, 0.3, far)
-    # C2 primary rays are generated without jitter; the sample layout jitters by rank
-    jitter, frames = (1, rank) if (world > 1 and not tiles) else (0, 0)
+    # Primary rays come from the reference's default Generate (RayGenKernels.compute:46-47 with
+    # UseReCur = false, RayTracingMaster.cs:189): sub-pixel jitter random(0, pixel_index) - 0.5. The
+    # UseReCur variant (no jitter, SURVEY 8(d)'s determinism choice) is measured as aux_recur_unjittered:
+    # its screen column x = W/2 has direction.z == -0.0 exactly, whose NaN z slabs make ~1,000 rays
+    # walk ~900 nodes each (tools/long_rays.py). The sample layout jitters with frames = rank.
+    jitter, frames = 1, (rank if (world > 1 and not tiles) else 0)
     if tiles:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), at the buffer's start
         pix = torch.from_numpy(ttdist.tile_pixels(W, H, world, rank)).to(dev)
         n_prim = int(pix.shape[0])
@@ -537,6 +541,25 @@ def main():
         del srays
         log(f"sample-sharded (weak) layout: {sample_sharded}")
 
+    # ---- auxiliary: the UseReCur ray generation (no jitter), primary + bounce 1, N=1
+    recur = None
+    if world == 1:
+        rr = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(rr, c2w, ip, W, H, 0.3, far, jitter=0, frames=0, max_bounce=1, device=True)
+        rs = eng.trace(rr, WH, 0, far, W, H, info=info, device=True, stats=True)
+        rnb = eng.enqueue_bounce(rr, WH, 0, far, W, H, frames=0, max_bounce=1, device=True)
+        launches = [lambda: eng.trace(rr, WH, 0, far, W, H, info=info, device=True, asynchronous=True),
+                    lambda: eng.trace(rr, rnb, 1, far, W, H, info=info, colors=colors_t, device=True,
+                                      asynchronous=True)]
+        rms = timed_launches(eng, launches, args.warmup, args.steps)
+        rmean = rms.mean(0)
+        recur = {"primary_rays": WH, "bounce_rays": rnb, "trace_ms": [round(float(m), 4) for m in rmean],
+                 "mrays_s": round((WH + rnb) / float(rmean.sum()) / 1e3, 1),
+                 "primary_nodes_per_ray": round(rs.node_visits / WH, 2), "reps_exhausted": int(rs.reps_exhausted),
+                 "note": "RayGenKernels.compute:47 with UseReCur: column x=W/2 has direction.z == -0.0 (NaN z slabs)"}
+        del rr
+        log(f"recur (unjittered) primary + bounce: {recur}")
+
     # ---- auxiliary (not the metric): any-hit NEE visibility rays (tt_trace_shadow)
     # from this rank's primary hit points toward a point light. Every launch first restores the
     # pristine rays (occluded rays get t = 0 in place) on the shared stream; only the kernel is timed.
@@ -634,7 +657,8 @@ def main():
         "scaling": "weak" if (world > 1 and not tiles) else "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza)",
+        "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza); primary rays from the reference's "
+                "default Generate (jittered, UseReCur=false)",
         "config": {"workload": "sponza_primary_plus_1_bounce_1080p", "scene": "Sponza-shaped CWBVH8 (C2)",
                    "tris": int(len(scene.tris)), "cwbvh_nodes": int(len(scene.nodes)), "width": W, "height": H,
                    "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_rank0": int(rays_per_step),
@@ -652,7 +676,7 @@ def main():
                    "trace_ms_per_step_slowest_rank": round(trace_ms_slowest, 4),
                    "kernel_mrays_s_trace_only": round(rays_per_step / trace_ms_rank / 1e3, 2),
                    "gather_identical_to_1gpu": gather_parity,
-                   "aux_sample_sharded": sample_sharded,
+                   "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -9,7 +9,7 @@ launches each rank of an N-GPU run would issue (rank 0's tiles = the largest sha
     t_frame(N) = t_primary(shard_N) + t_bounce(shard_N) [+ gather, reported separately]
     eff(N)     = t_frame(1) / (N * t_frame(N))
 
-C2 (Sponza-shaped 1080p, primary + bounce 1) and C5 (San-Miguel-shaped 4K primary). Every time is
+C2 (Sponza-shaped 1080p, primary + bounce 1, the reference's default jittered Generate) and C5 (San-Miguel-shaped 4K primary). Every time is
 a HIP-event launch time on the shared torch/engine stream (tt_timing_read), median of --steps.
 Output: one JSON document on stdout (commit under profiles/).
 """
@@ -57,7 +57,7 @@ def main():
         WH = W * H
         c2w, ip = view.camera(W, H)
         full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(full, c2w, ip, W, H, T.NEAR, T.FAR, jitter=0, frames=0, max_bounce=1, device=True)
+        eng.generate(full, c2w, ip, W, H, T.NEAR, T.FAR, jitter=1, frames=0, max_bounce=1, device=True)
         rows = []
         for n_gpus in (1, 2, 4, 8):
             pix = torch.from_numpy(ttdist.tile_pixels(W, H, n_gpus, 0)).to(dev)

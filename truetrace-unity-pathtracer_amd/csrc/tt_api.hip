@@ -1076,7 +1076,11 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.ctl = c->ctl + ci;
     a.ctl_next = c->ctl + (ci ^ 1u);
     a.spill = c->spill.p;
+#if defined(TT_DIAG_TIMES) || defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST) || \
+    defined(TT_DIAG_BLOCKS) || defined(TT_DIAG_SOLO)
+    // diagnostic builds only: a device buffer for the kernel's timing records
     if (const char* e = std::getenv("TT_DIAG_TIMES_PTR")) a.diag_times = reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0));
+#endif
     a.n_rays = p->n_rays;
     a.ray_offset = off;
     a.width = p->screen_width;

@@ -22,13 +22,12 @@ struct RefitPlan {
     std::vector<std::vector<int32_t>> layers;  // NodePair indices per depth
 };
 
-// Device state of a prepared refit.
+// Device state of a prepared refit (one launch per refit: tt_refit.hip refit_tree).
 struct RefitDev {
-    int32_t *pair_bvh = nullptr, *pair_slot = nullptr, *to_bvh = nullptr, *fwd = nullptr, *layers = nullptr;
-    float *bb = nullptr, *P = nullptr, *boxes = nullptr;
-    uint32_t *E = nullptr, *Q = nullptr;
-    uint32_t n_pairs = 0, n_nodes = 0, n_boxes = 0;
-    std::vector<uint32_t> layer_off, layer_n;  // into `layers`
+    int32_t *starts = nullptr, *fwd = nullptr, *parent = nullptr, *node_of = nullptr;
+    uint32_t* arrive = nullptr;
+    float* bb = nullptr;
+    uint32_t n_pairs = 0, n_nodes = 0, n_starts = 0;
 };
 
 bool tt_refit_build_plan(const tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, RefitPlan& R);

@@ -8,9 +8,17 @@
 //    current vertex buffer, then the same NodeInitializer / RefitLayer (:177-212) / NodeUpdate /
 //    NodeCompress over the plan ParentObject.Construct builds (:679-730).
 //
-// MI355X shape: the refit is a few thousand tiny records per frame, latency- not bandwidth-bound;
-// it runs as one short launch per BVH depth level on the context stream (no host sync), so a
-// trace enqueued after it on the same stream sees the new TLAS nodes.
+// MI355X shape: the refit is a few thousand tiny records per frame, latency- not bandwidth-bound,
+// so it is ONE launch (not the reference's one dispatch per depth level, AssetManager.cs:1531-1567):
+// a thread per leaf NodePair computes its box, then climbs. Each NodePair has an arrival counter;
+// the thread whose arrival completes a parent's 8 slots computes that parent's box (the same union
+// loop over the same 8 entries as RefitBVHLayer), then NodeUpdate of the parent's 8 child slots and
+// NodeCompress of the BVH node the parent documents -- in registers, straight into the 80-B node --
+// and climbs on. Boxes are handed between threads (and XCDs) with write-through sc1 stores, a
+// vmcnt(0) drain and an agent-scope atomic; the completing thread reads them with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility). The counters are reset by the thread that
+// completed them, so consecutive refits need no memset. On the context stream, so a trace
+// enqueued after it sees the new nodes.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -40,36 +48,34 @@ __device__ __forceinline__ uint32_t ftou_d3d(float f) {
     return (uint32_t)f;
 }
 
-__global__ void refit_init(float* __restrict__ bb, uint32_t n) {  // NodeInitializer
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    for (int a = 0; a < 3; a++) {
-        bb[6 * i + a] = -9999999999.0f;     // BBMax
-        bb[6 * i + 3 + a] = 9999999999.0f;  // BBMin
-    }
+// Write-through box stores / L1-bypassing box loads for the cross-thread hand-off.
+__device__ __forceinline__ void st_box(float* bb, int32_t id, const float v[6]) {
+    float* o = bb + 6 * (size_t)id;
+#pragma unroll
+    for (int k = 0; k < 6; k++) __hip_atomic_store(o + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_box(const float* bb, size_t i) {
+    return __hip_atomic_load(bb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // RefitBVHLayer (TLAS: leaf ranges index the boxes through TLASCWBVHIndices) / RefitLayer (BLAS:
-// leaf ranges are triangle boxes in leaf order, box_idx == nullptr): one NodePair per thread
-__global__ void refit_layer(const int32_t* __restrict__ layer, uint32_t n, const int32_t* __restrict__ fwd,
-                            const int32_t* __restrict__ box_idx, const float* __restrict__ boxes,
-                            float* __restrict__ bb) {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= n) return;
-    const int32_t id = layer[t];
+// leaf ranges are triangle boxes in leaf order, box_idx == nullptr) for NodePair `id`: union of
+// its row's 8 entries, in slot order, from the accumulators the reference starts with.
+__device__ __forceinline__ void pair_union(int32_t id, const int32_t* __restrict__ fwd, const int32_t* __restrict__ box_idx,
+                                           const float* __restrict__ boxes, const float* bb, float o[6]) {
     float mx0 = -99999999.0f, mx1 = -99999999.0f, mx2 = -99999999.0f;
     float mn0 = 99999999.0f, mn1 = 99999999.0f, mn2 = 99999999.0f;
     for (int k = 0; k < 8; k++) {
         const int32_t leaf = fwd[8 * id + k];
         if (leaf == 0) continue;
         if (leaf < 0) {
-            const float* c = bb + 6 * (size_t)(-leaf - 1);
-            mx0 = fmaxf(mx0, c[0]);
-            mx1 = fmaxf(mx1, c[1]);
-            mx2 = fmaxf(mx2, c[2]);
-            mn0 = fminf(mn0, c[3]);
-            mn1 = fminf(mn1, c[4]);
-            mn2 = fminf(mn2, c[5]);
+            const size_t c = 6 * (size_t)(-leaf - 1);
+            mx0 = fmaxf(mx0, ld_box(bb, c + 0));
+            mx1 = fmaxf(mx1, ld_box(bb, c + 1));
+            mx2 = fmaxf(mx2, ld_box(bb, c + 2));
+            mn0 = fminf(mn0, ld_box(bb, c + 3));
+            mn1 = fminf(mn1, ld_box(bb, c + 4));
+            mn2 = fminf(mn2, ld_box(bb, c + 5));
         } else {
             const int32_t v = leaf - 1;
             const int32_t start = v / 24, end = start + v % 24;
@@ -84,7 +90,6 @@ __global__ void refit_layer(const int32_t* __restrict__ layer, uint32_t n, const
             }
         }
     }
-    float* o = bb + 6 * (size_t)id;
     o[0] = mx0;
     o[1] = mx1;
     o[2] = mx2;
@@ -93,45 +98,75 @@ __global__ void refit_layer(const int32_t* __restrict__ layer, uint32_t n, const
     o[5] = mn2;
 }
 
-// NodeUpdate: NodePair id (>= 1) re-quantizes its slot of its BVH8 node against the node's bounds
-__global__ void refit_update(uint32_t n_pairs, const int32_t* __restrict__ pair_bvh, const int32_t* __restrict__ pair_slot,
-                             const int32_t* __restrict__ to_bvh, const float* __restrict__ bb, float* __restrict__ P,
-                             uint32_t* __restrict__ E, uint32_t* __restrict__ Q) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n_pairs || i == 0) return;
-    const int32_t node = pair_bvh[i], slot = pair_slot[i];
-    const float* par = bb + 6 * (size_t)to_bvh[node];
-    const float* me = bb + 6 * (size_t)i;
-    float tmx[3] = {me[0], me[1], me[2]}, tmn[3] = {me[3], me[4], me[5]};
-    if (tmx[0] < -10000.0f)
-        for (int a = 0; a < 3; a++) tmx[a] = tmn[a] = par[3 + a];
+// NodeUpdate of the 8 child slots of internal NodePair `p` (whose box is `par`) against the BVH
+// node `node` it documents, then NodeCompress of that node: full uints shifted and OR-ed, as the
+// reference packs them (out-of-range quantized values spill into the neighbouring bytes there too).
+__device__ __forceinline__ void update_compress(int32_t p, const float par[6], const int32_t* __restrict__ fwd,
+                                                const float* bb, tt_cwbvh_node* __restrict__ node) {
+    float P[3], e[3];
+    uint32_t E[3];
     for (int a = 0; a < 3; a++) {
-        const float e = pow2_ceil_log2((par[a] - par[3 + a]) * 0.003921569f);
-        const float p = par[3 + a];
-        P[3 * node + a] = p;
-        E[3 * node + a] = __float_as_uint(e) >> 23;
-        Q[48 * node + 8 * (2 * a + 1) + slot] = ftou_d3d(ceilf((tmx[a] - p) / e));
-        Q[48 * node + 8 * (2 * a) + slot] = ftou_d3d(floorf((tmn[a] - p) / e));
+        e[a] = pow2_ceil_log2((par[a] - par[3 + a]) * 0.003921569f);
+        P[a] = par[3 + a];
+        E[a] = __float_as_uint(e[a]) >> 23;
+    }
+    uint32_t words[6][2] = {};
+    for (int k = 0; k < 8; k++) {
+        const size_t c = 6 * (size_t)(-fwd[8 * p + k] - 1);
+        float tmx[3] = {ld_box(bb, c + 0), ld_box(bb, c + 1), ld_box(bb, c + 2)};
+        float tmn[3] = {ld_box(bb, c + 3), ld_box(bb, c + 4), ld_box(bb, c + 5)};
+        if (tmx[0] < -10000.0f)
+            for (int a = 0; a < 3; a++) tmx[a] = tmn[a] = par[3 + a];
+        for (int a = 0; a < 3; a++) {
+            const uint32_t hi = ftou_d3d(ceilf((tmx[a] - P[a]) / e[a]));
+            const uint32_t lo = ftou_d3d(floorf((tmn[a] - P[a]) / e[a]));
+            words[2 * a][k >> 2] |= lo << (8 * (k & 3));
+            words[2 * a + 1][k >> 2] |= hi << (8 * (k & 3));
+        }
+    }
+    const uint32_t imask = node->e_imask >> 24;
+    node->p[0] = P[0];
+    node->p[1] = P[1];
+    node->p[2] = P[2];
+    node->e_imask = E[0] | (E[1] << 8) | (E[2] << 16) | (imask << 24);
+    uint32_t* dst[6] = {node->qlo_x, node->qhi_x, node->qlo_y, node->qhi_y, node->qlo_z, node->qhi_z};
+    for (int w = 0; w < 6; w++) {
+        dst[w][0] = words[w][0];
+        dst[w][1] = words[w][1];
     }
 }
 
-// NodeCompress: pack the fixed layout into 80-B nodes (full uints shifted and OR-ed, as the reference)
-__global__ void refit_compress(uint32_t n_nodes, const float* __restrict__ P, const uint32_t* __restrict__ E,
-                               const uint32_t* __restrict__ Q, tt_cwbvh_node* __restrict__ nodes) {
-    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
-    if (n >= n_nodes) return;
-    tt_cwbvh_node& o = nodes[n];
-    const uint32_t imask = o.e_imask >> 24;
-    o.p[0] = P[3 * n];
-    o.p[1] = P[3 * n + 1];
-    o.p[2] = P[3 * n + 2];
-    o.e_imask = E[3 * n] | (E[3 * n + 1] << 8) | (E[3 * n + 2] << 16) | (imask << 24);
-    uint32_t* words[6] = {o.qlo_x, o.qhi_x, o.qlo_y, o.qhi_y, o.qlo_z, o.qhi_z};
-    for (int w = 0; w < 6; w++)
-        for (int h = 0; h < 2; h++) {
-            const uint32_t* q = Q + 48 * n + 8 * w + 4 * h;
-            words[w][h] = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
-        }
+struct RefitTreeArgs {
+    const int32_t* starts;  // leaf NodePairs (rows without NodePair entries)
+    uint32_t n_starts;
+    const int32_t* fwd;     // ForwardStack rows, 8 per NodePair
+    const int32_t* parent;  // parent NodePair
+    const int32_t* node_of; // BVH node an internal NodePair documents (-1: leaf NodePair)
+    uint32_t* arrive;       // arrival counters (0 between refits)
+    float* bb;              // NodePair boxes {BBMax, BBMin}
+    const float* boxes;     // primitive boxes (instances or triangles)
+    const int32_t* box_idx; // TLASCWBVHIndices (TLAS) or nullptr (BLAS)
+    tt_cwbvh_node* nodes;
+};
+
+__global__ void refit_tree(RefitTreeArgs t) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= t.n_starts) return;
+    int32_t id = t.starts[s];
+    while (true) {
+        float box[6];
+        pair_union(id, t.fwd, t.box_idx, t.boxes, t.bb, box);
+        const int32_t n = t.node_of[id];
+        if (n >= 0) update_compress(id, box, t.fwd, t.bb, t.nodes + n);
+        if (id == 0) break;  // the root pair: the whole tree is done
+        st_box(t.bb, id, box);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the box has left this CU before the arrival
+        const int32_t p = t.parent[id];
+        const uint32_t prev = __hip_atomic_fetch_add(t.arrive + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev != 7u) break;  // not the last of the parent's 8 slots
+        __hip_atomic_store(t.arrive + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        id = p;
+    }
 }
 
 // ------------------------------------------------------------------ Construct (BLAS refit)
@@ -294,8 +329,7 @@ bool tt_refit_build_plan(const tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, Refi
 }
 
 void tt_refit_free(RefitDev& d) {
-    for (void* p : {(void*)d.pair_bvh, (void*)d.pair_slot, (void*)d.to_bvh, (void*)d.fwd, (void*)d.layers, (void*)d.bb,
-                    (void*)d.P, (void*)d.boxes, (void*)d.E, (void*)d.Q})
+    for (void* p : {(void*)d.starts, (void*)d.fwd, (void*)d.parent, (void*)d.node_of, (void*)d.arrive, (void*)d.bb})
         if (p) (void)hipFree(p);
     d = RefitDev();
 }
@@ -308,48 +342,31 @@ static hipError_t up(T** dst, const std::vector<T>& v) {
 }
 
 hipError_t tt_refit_prepare(const RefitPlan& R, const tt_cwbvh_node* host_nodes, uint32_t n_tlas_nodes, RefitDev& d) {
+    (void)host_nodes;
     tt_refit_free(d);
-    d.n_pairs = (uint32_t)R.pair_bvh.size();
+    const size_t N = R.pair_bvh.size();
+    d.n_pairs = (uint32_t)N;
     d.n_nodes = n_tlas_nodes;
-    std::vector<int32_t> flat;
-    for (const auto& l : R.layers) {
-        d.layer_off.push_back((uint32_t)flat.size());
-        d.layer_n.push_back((uint32_t)l.size());
-        flat.insert(flat.end(), l.begin(), l.end());
-    }
-    // fixed-layout node state, seeded from the current node bytes (NodeUpdate rewrites all of it)
-    std::vector<float> P(3 * (size_t)n_tlas_nodes);
-    std::vector<uint32_t> E(3 * (size_t)n_tlas_nodes), Q(48 * (size_t)n_tlas_nodes);
-    for (uint32_t n = 0; n < n_tlas_nodes; n++) {
-        const tt_cwbvh_node& s = host_nodes[n];
-        for (int a = 0; a < 3; a++) {
-            P[3 * n + a] = s.p[a];
-            E[3 * n + a] = (s.e_imask >> (8 * a)) & 0xffu;
-        }
-        const uint32_t* words[6] = {s.qlo_x, s.qhi_x, s.qlo_y, s.qhi_y, s.qlo_z, s.qhi_z};
-        for (int w = 0; w < 6; w++)
-            for (int k = 0; k < 8; k++) Q[48 * n + 8 * w + k] = (words[w][k >> 2] >> (8 * (k & 3))) & 0xffu;
-    }
+    std::vector<int32_t> starts, node_of(N, -1);
+    for (size_t i = 0; i < N; i++)
+        if (R.leaf[i]) starts.push_back((int32_t)i);
+    for (uint32_t n = 0; n < n_tlas_nodes; n++)
+        if (n == 0 || R.to_bvh[n] != 0) node_of[(size_t)R.to_bvh[n]] = (int32_t)n;
+    d.n_starts = (uint32_t)starts.size();
     hipError_t e;
-    if ((e = up(&d.pair_bvh, R.pair_bvh)) != hipSuccess || (e = up(&d.pair_slot, R.pair_slot)) != hipSuccess ||
-        (e = up(&d.to_bvh, R.to_bvh)) != hipSuccess || (e = up(&d.fwd, R.fwd)) != hipSuccess ||
-        (e = up(&d.layers, flat)) != hipSuccess || (e = up(&d.P, P)) != hipSuccess || (e = up(&d.E, E)) != hipSuccess ||
-        (e = up(&d.Q, Q)) != hipSuccess)
+    if ((e = up(&d.starts, starts)) != hipSuccess || (e = up(&d.fwd, R.fwd)) != hipSuccess ||
+        (e = up(&d.parent, R.parent)) != hipSuccess || (e = up(&d.node_of, node_of)) != hipSuccess)
         return e;
-    return hipMalloc(reinterpret_cast<void**>(&d.bb), 6 * sizeof(float) * d.n_pairs);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&d.arrive), sizeof(uint32_t) * N)) != hipSuccess) return e;
+    if ((e = hipMemset(d.arrive, 0, sizeof(uint32_t) * N)) != hipSuccess) return e;
+    return hipMalloc(reinterpret_cast<void**>(&d.bb), 6 * sizeof(float) * N);
 }
 
-// One frame: boxes (device, n_mesh x 6 floats) -> TLAS nodes [0, n_nodes) of `nodes`.
+// One frame: primitive boxes (device) -> the nodes of `nodes` the plan covers. One launch.
 hipError_t tt_refit_run(RefitDev& d, const float* boxes, const int32_t* box_index, tt_cwbvh_node* nodes, hipStream_t st) {
-    hipLaunchKernelGGL(refit_init, dim3(grid_of(d.n_pairs)), dim3(kBlock), 0, st, d.bb, d.n_pairs);
-    for (int l = (int)d.layer_n.size() - 1; l >= 0; l--) {
-        if (!d.layer_n[l]) continue;
-        hipLaunchKernelGGL(refit_layer, dim3(grid_of(d.layer_n[l])), dim3(kBlock), 0, st, d.layers + d.layer_off[l],
-                           d.layer_n[l], d.fwd, box_index, boxes, d.bb);
-    }
-    hipLaunchKernelGGL(refit_update, dim3(grid_of(d.n_pairs)), dim3(kBlock), 0, st, d.n_pairs, d.pair_bvh, d.pair_slot,
-                       d.to_bvh, d.bb, d.P, d.E, d.Q);
-    hipLaunchKernelGGL(refit_compress, dim3(grid_of(d.n_nodes)), dim3(kBlock), 0, st, d.n_nodes, d.P, d.E, d.Q, nodes);
+    if (!d.n_starts) return hipSuccess;
+    RefitTreeArgs t{d.starts, d.n_starts, d.fwd, d.parent, d.node_of, d.arrive, d.bb, boxes, box_index, nodes};
+    hipLaunchKernelGGL(refit_tree, dim3(grid_of(d.n_starts)), dim3(kBlock), 0, st, t);
     return hipGetLastError();
 }
 

@@ -258,20 +258,31 @@ struct TriCand {
     float t, u, v;
     bool cand, accept;
 };
-template <bool MATCHECK>
-__device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
-                                                      int32_t tri_id, int32_t mat_offset, const LaneRay& r,
-                                                      float best_t) {
-    const uint32_t to = tri_offset((uint32_t)tri_id);
-    // 36 B of positions (+ MatDat when materials are checked): two 16-B loads and a 4- or 8-B one
-    const uint4 a = buffer_load16(tris, to), b = buffer_load16(tris, to + 16u);
+// The 36 B of positions (+ MatDat when materials are checked) of one triangle: two 16-B loads and
+// a 4- or 8-B one.
+struct TriData {
+    uint4 a, b;
     uint2 c;
+};
+template <bool MATCHECK>
+__device__ __forceinline__ TriData triangle_load(__amdgpu_buffer_rsrc_t tris, int32_t tri_id) {
+    const uint32_t to = tri_offset((uint32_t)tri_id);
+    TriData d;
+    d.a = buffer_load16(tris, to);
+    d.b = buffer_load16(tris, to + 16u);
     if (MATCHECK) {
-        c = buffer_load8(tris, to + 32u);
+        d.c = buffer_load8(tris, to + 32u);
     } else {
-        c.x = buffer_load4(tris, to + 32u);
-        c.y = 0u;
+        d.c.x = buffer_load4(tris, to + 32u);
+        d.c.y = 0u;
     }
+    return d;
+}
+template <bool MATCHECK>
+__device__ __forceinline__ TriCand triangle_test(const TriData& d, const MatView& M, bool bounce0, int32_t tri_id,
+                                                 int32_t mat_offset, const LaneRay& r, float best_t) {
+    const uint4 a = d.a, b = d.b;
+    const uint2 c = d.c;
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
     const float e1x = __uint_as_float(a.w), e1y = __uint_as_float(b.x), e1z = __uint_as_float(b.y);
     const float e2x = __uint_as_float(b.z), e2y = __uint_as_float(b.w), e2z = __uint_as_float(c.x);
@@ -307,6 +318,12 @@ __device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tri
         if (bounce0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) R.accept = false;
     }
     return R;
+}
+template <bool MATCHECK>
+__device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
+                                                      int32_t tri_id, int32_t mat_offset, const LaneRay& r,
+                                                      float best_t) {
+    return triangle_test<MATCHECK>(triangle_load<MATCHECK>(tris, tri_id), M, bounce0, tri_id, mat_offset, r, best_t);
 }
 
 template <bool MATCHECK>
