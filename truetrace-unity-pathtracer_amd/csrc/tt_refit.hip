@@ -48,46 +48,46 @@ __device__ __forceinline__ uint32_t ftou_d3d(float f) {
     return (uint32_t)f;
 }
 
-// Write-through box stores / L1-bypassing box loads for the cross-thread hand-off.
-__device__ __forceinline__ void st_box(float* bb, int32_t id, const float v[6]) {
-    float* o = bb + 6 * (size_t)id;
-#pragma unroll
-    for (int k = 0; k < 6; k++) __hip_atomic_store(o + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// NodePair boxes for the cross-thread hand-off: 32 B {BBMax, BBMin.x | BBMin.yz, pad}, written
+// through (sc1, aux 16) and read L1-bypassing (sc1) as two 16-B buffer accesses.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_box(__amdgpu_buffer_rsrc_t bb, int32_t id, const float v[6]) {
+    const uint32_t off = (uint32_t)id * 32u;
+    __builtin_amdgcn_raw_buffer_store_b128(f32x4{v[0], v[1], v[2], v[3]}, bb, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(f32x4{v[4], v[5], 0.0f, 0.0f}, bb, off + 16u, 0, 16);
 }
-__device__ __forceinline__ float ld_box(const float* bb, size_t i) {
-    return __hip_atomic_load(bb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void ld_box(__amdgpu_buffer_rsrc_t bb, int32_t id, float v[6]) {
+    const uint32_t off = (uint32_t)id * 32u;
+    const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bb, off, 0, 16));
+    const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bb, off + 16u, 0, 16));
+    v[0] = a.x;
+    v[1] = a.y;
+    v[2] = a.z;
+    v[3] = a.w;
+    v[4] = b.x;
+    v[5] = b.y;
 }
 
-// RefitBVHLayer (TLAS: leaf ranges index the boxes through TLASCWBVHIndices) / RefitLayer (BLAS:
-// leaf ranges are triangle boxes in leaf order, box_idx == nullptr) for NodePair `id`: union of
-// its row's 8 entries, in slot order, from the accumulators the reference starts with.
-__device__ __forceinline__ void pair_union(int32_t id, const int32_t* __restrict__ fwd, const int32_t* __restrict__ box_idx,
-                                           const float* __restrict__ boxes, const float* bb, float o[6]) {
+// RefitLayer (BLAS: leaf ranges are triangle boxes in leaf order, box_idx == nullptr) /
+// RefitBVHLayer (TLAS: leaf ranges index the boxes through TLASCWBVHIndices) for a leaf NodePair:
+// the union of its row's entries, in slot order, from the accumulators the reference starts with.
+__device__ __forceinline__ void leaf_union(int32_t id, const int32_t* __restrict__ fwd, const int32_t* __restrict__ box_idx,
+                                           const float* __restrict__ boxes, float o[6]) {
     float mx0 = -99999999.0f, mx1 = -99999999.0f, mx2 = -99999999.0f;
     float mn0 = 99999999.0f, mn1 = 99999999.0f, mn2 = 99999999.0f;
     for (int k = 0; k < 8; k++) {
         const int32_t leaf = fwd[8 * id + k];
-        if (leaf == 0) continue;
-        if (leaf < 0) {
-            const size_t c = 6 * (size_t)(-leaf - 1);
-            mx0 = fmaxf(mx0, ld_box(bb, c + 0));
-            mx1 = fmaxf(mx1, ld_box(bb, c + 1));
-            mx2 = fmaxf(mx2, ld_box(bb, c + 2));
-            mn0 = fminf(mn0, ld_box(bb, c + 3));
-            mn1 = fminf(mn1, ld_box(bb, c + 4));
-            mn2 = fminf(mn2, ld_box(bb, c + 5));
-        } else {
-            const int32_t v = leaf - 1;
-            const int32_t start = v / 24, end = start + v % 24;
-            for (int32_t i4 = start; i4 < end; i4++) {
-                const float* b = boxes + 6 * (size_t)(box_idx ? box_idx[i4] : i4);  // AABB {BBMax, BBMin}
-                mx0 = fmaxf(mx0, b[0]);
-                mx1 = fmaxf(mx1, b[1]);
-                mx2 = fmaxf(mx2, b[2]);
-                mn0 = fminf(mn0, b[3]);
-                mn1 = fminf(mn1, b[4]);
-                mn2 = fminf(mn2, b[5]);
-            }
+        if (leaf <= 0) continue;  // a leaf NodePair's row holds no NodePair entries
+        const int32_t v = leaf - 1;
+        const int32_t start = v / 24, end = start + v % 24;
+        for (int32_t i4 = start; i4 < end; i4++) {
+            const float* b = boxes + 6 * (size_t)(box_idx ? box_idx[i4] : i4);  // AABB {BBMax, BBMin}
+            mx0 = fmaxf(mx0, b[0]);
+            mx1 = fmaxf(mx1, b[1]);
+            mx2 = fmaxf(mx2, b[2]);
+            mn0 = fminf(mn0, b[3]);
+            mn1 = fminf(mn1, b[4]);
+            mn2 = fminf(mn2, b[5]);
         }
     }
     o[0] = mx0;
@@ -98,25 +98,49 @@ __device__ __forceinline__ void pair_union(int32_t id, const int32_t* __restrict
     o[5] = mn2;
 }
 
-// NodeUpdate of the 8 child slots of internal NodePair `p` (whose box is `par`) against the BVH
-// node `node` it documents, then NodeCompress of that node: full uints shifted and OR-ed, as the
-// reference packs them (out-of-range quantized values spill into the neighbouring bytes there too).
-__device__ __forceinline__ void update_compress(int32_t p, const float par[6], const int32_t* __restrict__ fwd,
-                                                const float* bb, tt_cwbvh_node* __restrict__ node) {
+// An internal NodePair `p` (all 8 children NodePairs complete): its box is the union of the
+// children's boxes in slot order (RefitBVHLayer / RefitLayer), then NodeUpdate of the 8 child
+// slots against it and NodeCompress of the BVH node it documents: full uints shifted and OR-ed, as
+// the reference packs them (out-of-range quantized values spill into the neighbouring bytes there
+// too). The 8 children boxes are loaded once, all in flight together.
+__device__ __forceinline__ void internal_pair(int32_t p, const int32_t* __restrict__ fwd, __amdgpu_buffer_rsrc_t bb,
+                                              tt_cwbvh_node* __restrict__ node, float par[6]) {
+    float cb[8][6];
+#pragma unroll
+    for (int k = 0; k < 8; k++) ld_box(bb, -fwd[8 * p + k] - 1, cb[k]);
+    float mx0 = -99999999.0f, mx1 = -99999999.0f, mx2 = -99999999.0f;
+    float mn0 = 99999999.0f, mn1 = 99999999.0f, mn2 = 99999999.0f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        mx0 = fmaxf(mx0, cb[k][0]);
+        mx1 = fmaxf(mx1, cb[k][1]);
+        mx2 = fmaxf(mx2, cb[k][2]);
+        mn0 = fminf(mn0, cb[k][3]);
+        mn1 = fminf(mn1, cb[k][4]);
+        mn2 = fminf(mn2, cb[k][5]);
+    }
+    par[0] = mx0;
+    par[1] = mx1;
+    par[2] = mx2;
+    par[3] = mn0;
+    par[4] = mn1;
+    par[5] = mn2;
     float P[3], e[3];
     uint32_t E[3];
+#pragma unroll
     for (int a = 0; a < 3; a++) {
         e[a] = pow2_ceil_log2((par[a] - par[3 + a]) * 0.003921569f);
         P[a] = par[3 + a];
         E[a] = __float_as_uint(e[a]) >> 23;
     }
     uint32_t words[6][2] = {};
+#pragma unroll
     for (int k = 0; k < 8; k++) {
-        const size_t c = 6 * (size_t)(-fwd[8 * p + k] - 1);
-        float tmx[3] = {ld_box(bb, c + 0), ld_box(bb, c + 1), ld_box(bb, c + 2)};
-        float tmn[3] = {ld_box(bb, c + 3), ld_box(bb, c + 4), ld_box(bb, c + 5)};
+        float tmx[3] = {cb[k][0], cb[k][1], cb[k][2]};
+        float tmn[3] = {cb[k][3], cb[k][4], cb[k][5]};
         if (tmx[0] < -10000.0f)
             for (int a = 0; a < 3; a++) tmx[a] = tmn[a] = par[3 + a];
+#pragma unroll
         for (int a = 0; a < 3; a++) {
             const uint32_t hi = ftou_d3d(ceilf((tmx[a] - P[a]) / e[a]));
             const uint32_t lo = ftou_d3d(floorf((tmn[a] - P[a]) / e[a]));
@@ -130,6 +154,7 @@ __device__ __forceinline__ void update_compress(int32_t p, const float par[6], c
     node->p[2] = P[2];
     node->e_imask = E[0] | (E[1] << 8) | (E[2] << 16) | (imask << 24);
     uint32_t* dst[6] = {node->qlo_x, node->qhi_x, node->qlo_y, node->qhi_y, node->qlo_z, node->qhi_z};
+#pragma unroll
     for (int w = 0; w < 6; w++) {
         dst[w][0] = words[w][0];
         dst[w][1] = words[w][1];
@@ -143,7 +168,8 @@ struct RefitTreeArgs {
     const int32_t* parent;  // parent NodePair
     const int32_t* node_of; // BVH node an internal NodePair documents (-1: leaf NodePair)
     uint32_t* arrive;       // arrival counters (0 between refits)
-    float* bb;              // NodePair boxes {BBMax, BBMin}
+    float* bb;              // NodePair boxes, 32 B each (st_box / ld_box)
+    uint32_t n_pairs;
     const float* boxes;     // primitive boxes (instances or triangles)
     const int32_t* box_idx; // TLASCWBVHIndices (TLAS) or nullptr (BLAS)
     tt_cwbvh_node* nodes;
@@ -152,20 +178,19 @@ struct RefitTreeArgs {
 __global__ void refit_tree(RefitTreeArgs t) {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= t.n_starts) return;
+    const __amdgpu_buffer_rsrc_t bb = __builtin_amdgcn_make_buffer_rsrc(t.bb, 0, (int)(t.n_pairs * 32u), 0x00020000);
     int32_t id = t.starts[s];
-    while (true) {
-        float box[6];
-        pair_union(id, t.fwd, t.box_idx, t.boxes, t.bb, box);
-        const int32_t n = t.node_of[id];
-        if (n >= 0) update_compress(id, box, t.fwd, t.bb, t.nodes + n);
-        if (id == 0) break;  // the root pair: the whole tree is done
-        st_box(t.bb, id, box);
+    float box[6];
+    leaf_union(id, t.fwd, t.box_idx, t.boxes, box);
+    while (id != 0) {  // the root pair completes the tree
+        st_box(bb, id, box);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the box has left this CU before the arrival
         const int32_t p = t.parent[id];
         const uint32_t prev = __hip_atomic_fetch_add(t.arrive + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev != 7u) break;  // not the last of the parent's 8 slots
+        if (prev != 7u) return;  // not the last of the parent's 8 slots
         __hip_atomic_store(t.arrive + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         id = p;
+        internal_pair(id, t.fwd, bb, t.nodes + t.node_of[id], box);
     }
 }
 
@@ -359,13 +384,13 @@ hipError_t tt_refit_prepare(const RefitPlan& R, const tt_cwbvh_node* host_nodes,
         return e;
     if ((e = hipMalloc(reinterpret_cast<void**>(&d.arrive), sizeof(uint32_t) * N)) != hipSuccess) return e;
     if ((e = hipMemset(d.arrive, 0, sizeof(uint32_t) * N)) != hipSuccess) return e;
-    return hipMalloc(reinterpret_cast<void**>(&d.bb), 6 * sizeof(float) * N);
+    return hipMalloc(reinterpret_cast<void**>(&d.bb), 8 * sizeof(float) * N);
 }
 
 // One frame: primitive boxes (device) -> the nodes of `nodes` the plan covers. One launch.
 hipError_t tt_refit_run(RefitDev& d, const float* boxes, const int32_t* box_index, tt_cwbvh_node* nodes, hipStream_t st) {
     if (!d.n_starts) return hipSuccess;
-    RefitTreeArgs t{d.starts, d.n_starts, d.fwd, d.parent, d.node_of, d.arrive, d.bb, boxes, box_index, nodes};
+    RefitTreeArgs t{d.starts, d.n_starts, d.fwd, d.parent, d.node_of, d.arrive, d.bb, d.n_pairs, boxes, box_index, nodes};
     hipLaunchKernelGGL(refit_tree, dim3(grid_of(d.n_starts)), dim3(kBlock), 0, st, t);
     return hipGetLastError();
 }
