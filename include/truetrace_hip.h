@@ -316,7 +316,18 @@ enum {
     TT_TRACE_USE_RESTIRGI = 1u << 1, /* uniform UseReSTIRGI (RayTracingMaster.cs:558)   */
     TT_TRACE_USE_ASVGF = 1u << 2,    /* uniform UseASVGF    (RayTracingMaster.cs:562)   */
     TT_TRACE_STATS = 1u << 3,        /* count node visits / tri tests into tt_stats     */
-    TT_TRACE_ASYNC = 1u << 4         /* device pointers only: return without syncing    */
+    TT_TRACE_ASYNC = 1u << 4,        /* device pointers only: return without syncing    */
+    /* The reference's compile-time trace variants (GlobalDefines.cginc:4,11; both off there by
+     * default), tested in IntersectTriangle after the Cutout alpha test:
+     *   IgnoreGlassMain  (IntersectionKernels.compute:42-44): a candidate whose material has
+     *                    specTrans == 1 is skipped;
+     *   IgnoreBackfacing (:45-47): at bounce 0, a candidate whose material has specTrans != 1
+     *                    (out-of-range materials read as zeros, so they count) is skipped when
+     *                    dot(normalize(cross(normalize(posedge1), normalize(posedge2))), dir) <= 0,
+     *                    dir = the ray in the space the triangle is tested in; normalize(v) pinned
+     *                    as v * (1 / sqrt(dot(v, v))), cross / dot as in the numerics contract. */
+    TT_TRACE_IGNORE_GLASS = 1u << 5,
+    TT_TRACE_IGNORE_BACKFACING = 1u << 6
 };
 
 typedef struct tt_trace_params {

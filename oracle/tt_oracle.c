@@ -213,11 +213,21 @@ static void base_uv(const tt_cuda_triangle* T, float u, float v, float* bu, floa
     *bv = T->tex0[1] * w + T->texedge1[1] * u + T->texedge2[1] * v;
 }
 
-/* IntersectTriangle — IntersectionKernels.compute:14-57 (AdvancedAlphaMapped on,
- * IgnoreGlassMain off, IgnoreBackfacing off; GlobalDefines.cginc:1-11). Returns 0, or 3
- * when a Cutout material is reached without an alpha atlas (unsupported). */
+static v3 vnormalize(v3 v);
+
+/* IgnoreBackfacing (IntersectionKernels.compute:46): dot(normalize(cross(normalize(posedge1),
+ * normalize(posedge2))), ray.direction) <= 0 rejects, ray.direction being the ray in the space the
+ * triangle is tested in (object space inside a BLAS). normalize pinned as v * (1 / sqrt(dot(v, v))). */
+static int backfacing(const v3 e1, const v3 e2, const v3 d) {
+    return vdot(vnormalize(vcross(vnormalize(e1), vnormalize(e2))), d) <= 0.0f;
+}
+
+/* IntersectTriangle — IntersectionKernels.compute:14-57 (AdvancedAlphaMapped on; GlobalDefines.cginc
+ * :1-11). IgnoreGlassMain (:42-44) and IgnoreBackfacing (:45-47) are compile-time defines there, off
+ * by default; here they are the TT_TRACE_IGNORE_GLASS / TT_TRACE_IGNORE_BACKFACING launch flags.
+ * Returns 0, or 3 when a Cutout material is reached without an alpha atlas (unsupported). */
 static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray* ray,
-                              RayHit* ray_hit, int MatOffset, int CurBounce, uint32_t* accepts) {
+                              RayHit* ray_hit, int MatOffset, int CurBounce, uint32_t flags, uint32_t* accepts) {
     const tt_cuda_triangle* T = &s->tris[tri_id];
     const v3 pos0 = ld3(T->pos0), posedge1 = ld3(T->posedge1), posedge2 = ld3(T->posedge2);
     const v3 h = vcross(ray->direction, posedge2);
@@ -235,8 +245,10 @@ static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray
                 /* _Materials[MatOffset + MatDat]; an out-of-range StructuredBuffer read returns zeros
                  * in D3D, i.e. a material with no flags (MatType 0, Tag 0) */
                 const int MaterialIndex = MatOffset + (int)T->MatDat;
+                float specTrans = 0.0f;
                 if (MaterialIndex >= 0 && (uint32_t)MaterialIndex < s->n_mat) {
                     const tt_material* m = &s->mats[MaterialIndex];
+                    specTrans = m->specTrans;
                     if (m->MatType == TT_MAT_CUTOUT_INDEX) { /* :35-40 */
                         if (!g_atlas) return 3;
                         float bu, bv, au, av;
@@ -244,8 +256,14 @@ static int intersect_triangle(const scene* s, int mesh_id, int tri_id, const Ray
                         align_uv(bu, bv, m->AlbedoTexScale, m->AlphaTex, &au, &av);
                         if (sample_linear(au, av) < m->AlphaCutoff) return 0;
                     }
-                    if (CurBounce == 0 && ((((int)m->Tag) >> TT_FLAG_INVISIBLE) & 1) == 1) return 0;
                 }
+                if ((flags & TT_TRACE_IGNORE_GLASS) && specTrans == 1.0f) return 0; /* :42-44 */
+                if ((flags & TT_TRACE_IGNORE_BACKFACING) && CurBounce == 0 && specTrans != 1.0f && /* :45-47 */
+                    backfacing(posedge1, posedge2, ray->direction))
+                    return 0;
+                if (MaterialIndex >= 0 && (uint32_t)MaterialIndex < s->n_mat &&
+                    CurBounce == 0 && ((((int)s->mats[MaterialIndex].Tag) >> TT_FLAG_INVISIBLE) & 1) == 1)
+                    return 0;
                 ray_hit->t = t;
                 ray_hit->u = u;
                 ray_hit->v = v;
@@ -374,7 +392,7 @@ static int intersect_bvh(const trace_job* J, uint32_t i) {
                     triangle_group.y &= ~(1u << triangle_index);
                     cnt.tri_tests++;
                     if (intersect_triangle(s, mesh_id, (int)(triangle_group.x + triangle_index), &ray,
-                                           &bestHit, MatOffset, CurBounce, &cnt.accepts)) {
+                                           &bestHit, MatOffset, CurBounce, P->flags, &cnt.accepts)) {
                         status = 3;
                         goto done;
                     }

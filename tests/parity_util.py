@@ -42,3 +42,34 @@ def same_floats(a, b) -> bool:
     same_bits = a.view(np.uint32) == b.view(np.uint32)
     both_nan = np.isnan(a) & np.isnan(b)
     return bool(np.all(same_bits | both_nan))
+
+
+def bounce_rays(scene, rays, W, H, seed):
+    """Seeded bounce-1 rays from the primary hits in rays[:W*H] (second half of the ping-pong
+    buffer): origin = hit point + 1e-3 * geometric normal (world space, facing the incoming ray),
+    direction = a random unit vector in that hemisphere. Returns (rays, count)."""
+    import tthip  # noqa: F401  (dtype only)
+
+    n = W * H
+    rng = np.random.default_rng(seed)
+    h = rays["hits"][:n]
+    idx = np.nonzero(h[:, 1] != 0xFFFFFFFF)[0]
+    t = h[idx, 2].view(np.float32)
+    o = rays["origin"][idx] + rays["direction"][idx] * t[:, None]
+    tri = scene.tris[h[idx, 1].astype(np.int64)]
+    ng = np.cross(tri["posedge1"], tri["posedge2"]).astype(np.float64)
+    md = scene.meshdata[h[idx, 0].astype(np.int64)]
+    w2l = md["W2L"].reshape(-1, 4, 4).transpose(0, 2, 1)[:, :3, :3]
+    ng = np.einsum("nji,nj->ni", w2l, ng)
+    ng /= np.linalg.norm(ng, axis=1, keepdims=True) + 1e-30
+    ng *= np.where((ng * rays["direction"][idx]).sum(1, keepdims=True) > 0, -1.0, 1.0)
+    d = rng.normal(size=(len(idx), 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d = np.where((d * ng).sum(1, keepdims=True) < 0, -d, d)
+    out = rays.copy()
+    m = len(idx)
+    out["origin"][n:n + m] = (o + 1e-3 * ng).astype(np.float32)
+    out["direction"][n:n + m] = d.astype(np.float32)
+    out["PixelIndex"][n:n + m] = rays["PixelIndex"][idx]
+    out["hits"][n:n + m] = h[idx]
+    return out, m

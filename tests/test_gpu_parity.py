@@ -16,7 +16,7 @@ import kat_cases as K
 import oracle_ctypes as O
 import tthip
 
-from parity_util import CPU_THREADS, FAR, assert_same, same_floats, trace_both
+from parity_util import CPU_THREADS, FAR, assert_same, bounce_rays, same_floats, trace_both
 
 pytestmark = pytest.mark.gpu
 
@@ -772,3 +772,31 @@ def test_coincident_triangles_tie_break(engine, seed):
     rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H)
     assert_same(rg, rc, ig, ic, 0, W * H)
     assert s.accepts == int(cnt["accepts"].sum())
+
+
+# ------------------------------------------------ trace variants IgnoreGlassMain / IgnoreBackfacing
+@pytest.mark.parametrize("seed", [61, 62])
+@pytest.mark.parametrize("flags", [tthip.TT_TRACE_IGNORE_GLASS, tthip.TT_TRACE_IGNORE_BACKFACING,
+                                   tthip.TT_TRACE_IGNORE_GLASS | tthip.TT_TRACE_IGNORE_BACKFACING])
+def test_trace_variant_flags_random_soup(engine, seed, flags):
+    """IntersectionKernels.compute:42-47 as launch flags, bit for bit against the oracle on a soup
+    with glass, glass + Cutout, Cutout and opaque materials (some MatDat out of range), primary
+    rays with _PrimaryTriangleInfo and bounce-1 rays (IgnoreBackfacing applies at bounce 0 only)."""
+    sc = glass_soup(seed)
+    rng = np.random.default_rng(seed)
+    sc.tris["MatDat"] = np.where(rng.random(len(sc.tris)) < 0.05, 9, sc.tris["MatDat"])  # out of range
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    rg, rc, ig, ic, s, cnt = trace_both(engine, sc, rays, W * H, 0, W, H, flags=flags)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    plain = rays.copy()
+    O.trace(sc, plain, W * H, 0, FAR, W, H)
+    changed = int((plain["hits"][: W * H] != rc["hits"][: W * H]).any(1).sum())
+    assert changed > 50, "the variant must change a good share of the primary hits"
+    r1, n1 = bounce_rays(sc, rc, W, H, seed)
+    if n1:
+        colors = np.zeros(W * H, tthip.COL_DTYPE)
+        colors["Data"][:, 3] = 1.0
+        rg1, rc1, ig1, ic1, _, _ = trace_both(engine, sc, r1, n1, 1, W, H, colors=colors, flags=flags, upload=False)
+        assert_same(rg1, rc1, ig1, ic1, W * H, n1)

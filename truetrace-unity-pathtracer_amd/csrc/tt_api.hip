@@ -1094,7 +1094,9 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.ncache = c->ncache.p;
     a.n_ncache = c->n_ncache;
     a.root_code = c->ncache_root;
-    const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout;
+    const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout ||
+                          ((p->flags & TT_TRACE_IGNORE_GLASS) && c->host.any_atlas_shadow) ||
+                          ((p->flags & TT_TRACE_IGNORE_BACKFACING) && p->bounce == 0);
     const uint32_t waves_needed = (p->n_rays + 255u) / 256u;  // one TT_CHUNK per wave at least
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
     const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],

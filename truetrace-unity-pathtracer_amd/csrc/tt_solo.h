@@ -240,7 +240,7 @@ __device__ void solo_run(const TraceArgs& A, WideState st, uint2 stk, __amdgpu_b
             dg_twait += TT_SOLO_T() - t1;
 #endif
             if (has && !tri_pf) td = triangle_load<MATCHECK>(tris, tri_id);
-            if (has) c = triangle_test<MATCHECK>(td, A.mat, A.bounce == 0, tri_id, st.MatOffset, st.ray, st.best.t);
+            if (has) c = triangle_test<MATCHECK>(td, A.mat, A.bounce == 0, A.flags, tri_id, st.MatOffset, st.ray, st.best.t);
             if (STATS) {  // the reference's sequential count of t-test passes, highest bit first
                 const uint32_t f = (c.cand ? 1u : 0u) | (c.accept ? 2u : 0u);
                 float run = st.best.t;

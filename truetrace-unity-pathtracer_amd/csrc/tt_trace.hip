@@ -453,8 +453,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
-            const bool acc = intersect_triangle<MATCHECK>(tris, A.mat, A.bounce == 0, (int32_t)(tg.x + ti), mesh_id,
-                                                          MatOffset, ray, best);
+            const bool acc = intersect_triangle<MATCHECK>(tris, A.mat, A.bounce == 0, A.flags, (int32_t)(tg.x + ti),
+                                                          mesh_id, MatOffset, ray, best);
             if (STATS) {
                 c_tris++;
                 c_acc += acc ? 1u : 0u;

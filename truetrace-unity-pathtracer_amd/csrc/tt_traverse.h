@@ -278,9 +278,23 @@ __device__ __forceinline__ TriData triangle_load(__amdgpu_buffer_rsrc_t tris, in
     }
     return d;
 }
+// IgnoreBackfacing (IntersectionKernels.compute:46): dot(normalize(cross(normalize(e1), normalize(e2))),
+// dir) <= 0, normalize(v) = v * (1 / sqrt(dot(v, v))) with the pinned dot / cross.
+__device__ __forceinline__ float3 normalize_pinned(float x, float y, float z) {
+    const float inv = 1.0f / sqrtf(fma_(z, z, fma_(y, y, x * x)));
+    return make_float3(x * inv, y * inv, z * inv);
+}
+__device__ __forceinline__ bool backfacing(float e1x, float e1y, float e1z, float e2x, float e2y, float e2z,
+                                           const LaneRay& r) {
+    const float3 a = normalize_pinned(e1x, e1y, e1z), b = normalize_pinned(e2x, e2y, e2z);
+    const float3 n = normalize_pinned(fma_(a.y, b.z, -(a.z * b.y)), fma_(a.z, b.x, -(a.x * b.z)),
+                                      fma_(a.x, b.y, -(a.y * b.x)));
+    return fma_(n.z, r.dz, fma_(n.y, r.dy, n.x * r.dx)) <= 0.0f;
+}
+
 template <bool MATCHECK>
-__device__ __forceinline__ TriCand triangle_test(const TriData& d, const MatView& M, bool bounce0, int32_t tri_id,
-                                                 int32_t mat_offset, const LaneRay& r, float best_t) {
+__device__ __forceinline__ TriCand triangle_test(const TriData& d, const MatView& M, bool bounce0, uint32_t tflags,
+                                                 int32_t tri_id, int32_t mat_offset, const LaneRay& r, float best_t) {
     const uint4 a = d.a, b = d.b;
     const uint2 c = d.c;
     const float p0x = __uint_as_float(a.x), p0y = __uint_as_float(a.y), p0z = __uint_as_float(a.z);
@@ -315,22 +329,28 @@ __device__ __forceinline__ TriCand triangle_test(const TriData& d, const MatView
             const CutoutMat cm = M.cut[mi];
             if (sample_linear(M, align_uv(base_uv(M, tri_id, u, v), cm)) < cm.cutoff) R.accept = false;
         }
+        const bool glass = (w >> TT_MATWORD_GLASS) & 1u;  // specTrans == 1
+        if ((tflags & TT_TRACE_IGNORE_GLASS) && glass) R.accept = false;  // :42-44
+        if ((tflags & TT_TRACE_IGNORE_BACKFACING) && bounce0 && !glass && R.accept &&  // :45-47
+            backfacing(e1x, e1y, e1z, e2x, e2y, e2z, r))
+            R.accept = false;
         if (bounce0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) R.accept = false;
     }
     return R;
 }
 template <bool MATCHECK>
 __device__ __forceinline__ TriCand triangle_candidate(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
-                                                      int32_t tri_id, int32_t mat_offset, const LaneRay& r,
-                                                      float best_t) {
-    return triangle_test<MATCHECK>(triangle_load<MATCHECK>(tris, tri_id), M, bounce0, tri_id, mat_offset, r, best_t);
+                                                      uint32_t tflags, int32_t tri_id, int32_t mat_offset,
+                                                      const LaneRay& r, float best_t) {
+    return triangle_test<MATCHECK>(triangle_load<MATCHECK>(tris, tri_id), M, bounce0, tflags, tri_id, mat_offset, r,
+                                   best_t);
 }
 
 template <bool MATCHECK>
-__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0,
+__device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, const MatView& M, bool bounce0, uint32_t tflags,
                                                    int32_t tri_id, int32_t mesh_id, int32_t mat_offset,
                                                    const LaneRay& r, Best& best) {
-    const TriCand c = triangle_candidate<MATCHECK>(tris, M, bounce0, tri_id, mat_offset, r, best.t);
+    const TriCand c = triangle_candidate<MATCHECK>(tris, M, bounce0, tflags, tri_id, mat_offset, r, best.t);
     if (c.accept) {
         best.t = c.t;
         best.u = c.u;

@@ -305,7 +305,8 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
             const bool has = m != 0u;
             const int32_t tri_id = (int32_t)(st.tg.x + (has ? firstbithigh(m) : 0u));
             TriCand c{0.0f, 0.0f, 0.0f, false, false};
-            if (has) c = triangle_candidate<MATCHECK>(tris, A.mat, A.bounce == 0, tri_id, st.MatOffset, st.ray, st.best.t);
+            if (has) c = triangle_candidate<MATCHECK>(tris, A.mat, A.bounce == 0, A.flags, tri_id, st.MatOffset, st.ray,
+                                                     st.best.t);
             if (STATS) {  // replay the reference's sequential counting of t-test passes ("accepts")
                 float run = st.best.t;
                 uint32_t acc = 0;

@@ -39,6 +39,8 @@ TT_TRACE_USE_RESTIRGI = 1 << 1
 TT_TRACE_USE_ASVGF = 1 << 2
 TT_TRACE_STATS = 1 << 3
 TT_TRACE_ASYNC = 1 << 4
+TT_TRACE_IGNORE_GLASS = 1 << 5       # IgnoreGlassMain (IntersectionKernels.compute:42-44)
+TT_TRACE_IGNORE_BACKFACING = 1 << 6  # IgnoreBackfacing (IntersectionKernels.compute:45-47)
 TT_STACK_SIZE = 16
 TT_MAX_REPS = 1000
 
