@@ -388,6 +388,28 @@ tt_status tt_sync(tt_ctx* ctx);
 void* tt_ctx_stream(tt_ctx* ctx);
 
 /* --------------------------------------- any-hit visibility */
+/* PropogatedCacheData, 48 B (CommonData.cginc:1621-1627, PropDepth 4 at :1493): the radiance-cache
+ * record per pixel; the any-hit kernel updates CurrentIlluminance only. */
+typedef struct tt_cache_data {
+    uint32_t samples[4][2];
+    uint32_t throughput;
+    uint32_t pathLength;
+    uint32_t CurrentIlluminance; /* @40: EncodeRGB log-luminance colour */
+    uint32_t Norm;
+} tt_cache_data;
+TT_STATIC_ASSERT(sizeof(tt_cache_data) == 48, "PropogatedCacheData is 48 bytes");
+
+/* tt_shadow_params.flags beyond TT_TRACE_DEVICE_PTRS / _STATS / _ASYNC / _USE_RESTIRGI: */
+enum {
+    /* the reference's RadianceCache define (GlobalDefines.cginc:15, on in its shipped define set):
+     * selects the #ifdef RadianceCache accumulations of IntersectionKernels.compute:463-482 */
+    TT_SHADOW_RADIANCE_CACHE = 1u << 7,
+    /* VisabilityCheckCompute semantics (CommonData.cginc:710-819): the same any-hit traversal with
+     * max distance = t as given (not |t|); visibility = (1,1,1,1) when no occluder is found -- the
+     * Reps bound included -- else (0,0,0,0); nothing else is written */
+    TT_SHADOW_VISIBILITY_CHECK = 1u << 8
+};
+
 typedef struct tt_shadow_params {
     uint32_t n_rays;         /* BufferSizes[CurBounce].shadow_rays                      */
     int32_t bounce;          /* CurBounce                                               */
@@ -407,13 +429,35 @@ typedef struct tt_shadow_params {
  *                    Direct += illumination * throughput (:466-470);
  *   nee_pos        : nullable float4[W*H]; at bounce 0, unoccluded rays write
  *                    (origin + direction * |t|, 0) to NEEPosA[pixel] (:461).
- * The radiance-cache, PrimaryNEERay and bounce > 0 Indirect accumulations (RGBE / log-luminance
- * encodings) stay with the caller, driven by `visibility`. Scenes with Cutout materials need the
+ * tt_trace_shadow_ex (below) adds the radiance-cache, PrimaryNEERay and bounce > 0 Indirect
+ * accumulations (RGBE / log-luminance encodings). Scenes with Cutout materials need the
  * alpha atlas and scenes with glass (specTrans == 1, stained-glass tint) the texture atlas;
  * without them the call returns TT_ERR_UNSUPPORTED. throughput = product of the glass tints of the
  * surfaces crossed, in traversal order (IEEE: t *= (c * (x + 2)) / 3 per component). */
 tt_status tt_trace_shadow(tt_ctx* ctx, const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
                           tt_col_data* global_colors, float* nee_pos, tt_stats* stats);
+/* The full kernel_shadow output contract of a ray that reaches |t| (IntersectionKernels.compute:
+ * 457-485, TerrainExists false), beyond tt_trace_shadow's Direct / NEEPosA, pixel = PixelIndex
+ * (writes to pixels >= W*H are dropped):
+ *   TT_SHADOW_RADIANCE_CACHE set (the reference's define set):
+ *     cache_buffer[pixel].CurrentIlluminance = EncodeRGB(DecodeRGB(it) + illumination * throughput
+ *         * ((!UseReSTIRGI || t >= 0) ? 1 : unpackRGBE(asuint(LuminanceIncomming))))  (cache nullable);
+ *     t >= 0: bounce 0: Direct += illumination * throughput;
+ *     t <  0: bounce != 0 && (UseReSTIRGI || Data.w == bounce):
+ *                 Indirect += illumination * throughput * (UseReSTIRGI ? unpackRGBE(Lum..) : 1)
+ *             else PrimaryNEERay = packRGBE(pow(unpackRGBE(PrimaryNEERay), 2.2f)
+ *                                           + pow(illumination, rcp(2.2f)) * throughput);
+ *   flag clear (#ifndef RadianceCache):
+ *     t >= 0: bounce 0: Direct += illumination * throughput, else Indirect += the same;
+ *     t <  0: bounce != 0 && !UseReSTIRGI && Data.w == -1: Indirect += illumination * throughput,
+ *             else the PrimaryNEERay update above.
+ * UseReSTIRGI = TT_TRACE_USE_RESTIRGI. The encoders and HLSL pow are pinned (driver-defined in the
+ * reference): log2 / exp2 evaluated in double with a fixed series and rounded once to float, exact
+ * floor(log2) / pow(2, n), round-half-to-even, D3D float -> uint; see csrc/tt_encode.h. One shadow
+ * ray per pixel per launch (the reference's updates are not atomic either). */
+tt_status tt_trace_shadow_ex(tt_ctx* ctx, const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
+                             tt_col_data* global_colors, float* nee_pos, tt_cache_data* cache_buffer,
+                             tt_stats* stats);
 
 /* ------------------------------------------------- attribute resolve */
 /* Parity aid for "normals within 1e-5": per hit, the interpolated shading normal

@@ -571,6 +571,100 @@ static int intersect_triangle_shadow(const scene* s, int tri_id, const Ray* ray,
     return 0;
 }
 
+/* ------------------------------------------------ row f1 colour encodings (RadianceCache path)
+ * packRGBE / unpackRGBE (CommonData.cginc:479-509), EncodeRGB / DecodeRGB (:1576-1619) and HLSL pow
+ * as D3D lowers it, exp2(y * log2(x)) with float intermediates. The reference leaves log2 / exp2 to
+ * the driver; the pinned semantics (include/truetrace_hip.h, tt_trace_shadow_ex): log2 / exp2
+ * evaluated in double with the fixed series below and rounded once to float, floor(log2) and
+ * pow(2, n) exact via frexp / ldexp, round() half-to-even, D3D float -> uint, minNum / maxNum,
+ * mul rows as fmaf chains, HLSL's unsuffixed literals as doubles rounded to float. */
+static float p_log2f(float xf) {
+    if (xf != xf || xf < 0.0f) return NAN;
+    if (xf == 0.0f) return -INFINITY;
+    if (xf == INFINITY) return xf;
+    int e;
+    double m = frexp((double)xf, &e);
+    if (m < 0.70710678118654752) { m = m * 2.0; e = e - 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    static const double inv_odd[10] = {1.0 / 19.0, 1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0, 1.0 / 11.0,
+                                       1.0 / 9.0,  1.0 / 7.0,  1.0 / 5.0,  1.0 / 3.0,  1.0};
+    double q = 1.0 / 21.0;
+    for (int k = 0; k < 10; k++) q = q * s2 + inv_odd[k];
+    return (float)((double)e + (2.0 * s * q) * 1.4426950408889634);
+}
+static float p_exp2f(float yf) {
+    if (yf != yf) return yf;
+    if (yf >= 128.0f) return INFINITY;
+    if (yf < -160.0f) return 0.0f;
+    const double y = (double)yf, k = floor(y), f = y - k;
+    const double r = f * 0.69314718055994531;
+    double term = 1.0, sum = 1.0;
+    for (int n = 1; n <= 22; n++) { term = term * r / (double)n; sum = sum + term; }
+    return (float)ldexp(sum, (int)k);
+}
+static float p_pow(float x, float y) { return p_exp2f(y * p_log2f(x)); }
+static uint32_t d3d_ftou(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xffffffffu;
+    return (uint32_t)f;
+}
+static float clampf3(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+static float mrow(float m0, float m1, float m2, float x, float y, float z) { return fmaf(m2, z, fmaf(m1, y, m0 * x)); }
+
+static uint32_t packRGBE(const float v[3]) { /* :479-496 */
+    float va[3];
+    for (int k = 0; k < 3; k++) va[k] = fmaxf(0.0f, v[k]);
+    const float max_abs = fmaxf(va[0], fmaxf(va[1], va[2]));
+    if (max_abs == 0.0f) return 0u;
+    int e;
+    (void)frexpf(max_abs, &e);
+    const float exponent = (float)(e - 1); /* floor(log2(max_abs)) */
+    uint32_t result = d3d_ftou(clampf3(exponent + 20.0f, 0.0f, 31.0f)) << 27;
+    const float scale = p_exp2f(-exponent) * 256.0f; /* pow(2, -exponent) * 256 */
+    uint32_t vu[3];
+    for (int k = 0; k < 3; k++) vu[k] = d3d_ftou(fminf(511.0f, rintf(va[k] * scale)));
+    return result | vu[0] | (vu[1] << 9) | (vu[2] << 18);
+}
+static void unpackRGBE(uint32_t x, float v[3]) { /* :498-509 */
+    const int exponent = (int)(x >> 27) - 20;
+    const float scale = p_exp2f((float)exponent) / 256.0f;
+    v[0] = (float)(x & 0x1ffu) * scale;
+    v[1] = (float)((x >> 9) & 0x1ffu) * scale;
+    v[2] = (float)((x >> 18) & 0x1ffu) * scale;
+}
+static uint32_t EncodeRGB(const float c[3]) { /* :1576-1590 */
+    const float X = mrow((float)0.4123907992659595, (float)0.3575843393838780, (float)0.1804807884018343, c[0], c[1], c[2]);
+    const float Y = mrow((float)0.2126390058715104, (float)0.7151686787677559, (float)0.0721923153607337, c[0], c[1], c[2]);
+    const float Z = mrow((float)0.0193308187155918, (float)0.1191947797946259, (float)0.9505321522496608, c[0], c[1], c[2]);
+    const float logY = (float)409.6 * (p_log2f(Y) + 20.0f);
+    const uint32_t Le = d3d_ftou(clampf3(logY, 0.0f, 16383.0f));
+    if (Le == 0u) return 0u;
+    const float invDenom = 1.0f / ((-2.0f * X + 12.0f * Y) + 3.0f * ((X + Y) + Z));
+    const float u = (4.0f * X) * invDenom, v = (9.0f * Y) * invDenom;
+    return (Le << 18) | (d3d_ftou(clampf3(820.0f * u, 0.0f, 511.0f)) << 9) | d3d_ftou(clampf3(820.0f * v, 0.0f, 511.0f));
+}
+static void DecodeRGB(uint32_t packed, float o[3]) { /* :1592-1619 */
+    const uint32_t Le = packed >> 18;
+    if (Le == 0u) { o[0] = o[1] = o[2] = 0.0f; return; }
+    const float logY = ((float)Le + 0.5f) / (float)409.6 - 20.0f;
+    const float Y = p_pow(2.0f, logY);
+    const float u = ((float)((packed >> 9) & 0x1ffu) + 0.5f) / 820.0f, v = ((float)(packed & 0x1ffu) + 0.5f) / 820.0f;
+    const float invDenom = 1.0f / ((6.0f * u - 16.0f * v) + 12.0f);
+    const float x = (9.0f * u) * invDenom, y = (4.0f * v) * invDenom;
+    const float s = Y / y;
+    const float X = s * x, Z = s * ((1.0f - x) - y);
+    o[0] = fmaxf(mrow((float)3.240969941904522, (float)-1.537383177570094, (float)-0.4986107602930032, X, Y, Z), 0.0f);
+    o[1] = fmaxf(mrow((float)-0.9692436362808803, (float)1.875967501507721, (float)0.04155505740717569, X, Y, Z), 0.0f);
+    o[2] = fmaxf(mrow((float)0.05563007969699373, (float)-0.2039769588889765, (float)1.056971514242878, X, Y, Z), 0.0f);
+}
+
+/* exported for the encoder known-answer tests */
+uint32_t tt_oracle_pack_rgbe(const float v[3]) { return packRGBE(v); }
+void tt_oracle_unpack_rgbe(uint32_t x, float v[3]) { unpackRGBE(x, v); }
+uint32_t tt_oracle_encode_rgb(const float c[3]) { return EncodeRGB(c); }
+void tt_oracle_decode_rgb(uint32_t x, float v[3]) { DecodeRGB(x, v); }
+float tt_oracle_pow(float x, float y) { return p_pow(x, y); }
+
 typedef struct shadow_job {
     const scene* s;
     const tt_shadow_params* p;
@@ -578,6 +672,7 @@ typedef struct shadow_job {
     float* visibility;
     tt_col_data* colors;
     float* nee_pos;
+    tt_cache_data* cache;
     tt_oracle_ray_counts* counts;
 } shadow_job;
 
@@ -703,9 +798,50 @@ static int intersect_bvh_shadow(const shadow_job* J, uint32_t i) {
                     o[2] = ray2.origin.z + ray2.direction.z * d;
                     o[3] = 0.0f;
                 }
-                if (SR->t >= 0.0f && CurBounce == 0 && J->colors) {
-                    tt_col_data* C = &J->colors[PixelIndex];
-                    for (int k = 0; k < 3; k++) C->Direct[k] = C->Direct[k] + SR->illumination[k] * throughput[k];
+                if (PixelIndex / W < H) { /* out-of-range UAV writes are dropped */
+                    const int restir = (P->flags & TT_TRACE_USE_RESTIRGI) != 0;
+                    const float* il = SR->illumination;
+                    if (P->flags & TT_SHADOW_RADIANCE_CACHE) { /* #ifdef RadianceCache */
+                        if (J->cache) { /* :464 */
+                            float k3[3] = {1.0f, 1.0f, 1.0f}, d[3], o[3];
+                            if (!(!restir || SR->t >= 0.0f)) unpackRGBE(asuint(SR->LuminanceIncomming), k3);
+                            uint32_t* ci = &J->cache[PixelIndex].CurrentIlluminance;
+                            DecodeRGB(*ci, d);
+                            for (int k = 0; k < 3; k++) o[k] = d[k] + (il[k] * throughput[k]) * k3[k];
+                            *ci = EncodeRGB(o);
+                        }
+                        if (J->colors) {
+                            tt_col_data* C = &J->colors[PixelIndex];
+                            if (SR->t >= 0.0f) {
+                                if (CurBounce == 0) /* :469 */
+                                    for (int k = 0; k < 3; k++) C->Direct[k] = C->Direct[k] + il[k] * throughput[k];
+                            } else if (CurBounce != 0 && (restir || C->Data[3] == (float)CurBounce)) { /* :477 */
+                                float k3[3] = {1.0f, 1.0f, 1.0f};
+                                if (restir) unpackRGBE(asuint(SR->LuminanceIncomming), k3);
+                                for (int k = 0; k < 3; k++) C->Indirect[k] = C->Indirect[k] + (il[k] * throughput[k]) * k3[k];
+                            } else { /* :481 */
+                                float pv[3], o[3];
+                                unpackRGBE(C->PrimaryNEERay, pv);
+                                for (int k = 0; k < 3; k++) o[k] = p_pow(pv[k], 2.2f) + p_pow(il[k], 1.0f / 2.2f) * throughput[k];
+                                C->PrimaryNEERay = packRGBE(o);
+                            }
+                        }
+                    } else if (J->colors) { /* #ifndef RadianceCache */
+                        tt_col_data* C = &J->colors[PixelIndex];
+                        if (SR->t >= 0.0f) {
+                            if (CurBounce == 0)
+                                for (int k = 0; k < 3; k++) C->Direct[k] = C->Direct[k] + il[k] * throughput[k];
+                            else /* :472 */
+                                for (int k = 0; k < 3; k++) C->Indirect[k] = C->Indirect[k] + il[k] * throughput[k];
+                        } else if (CurBounce != 0 && (!restir && C->Data[3] == -1.0f)) { /* :479 */
+                            for (int k = 0; k < 3; k++) C->Indirect[k] = C->Indirect[k] + il[k] * throughput[k];
+                        } else { /* :481 */
+                            float pv[3], o[3];
+                            unpackRGBE(C->PrimaryNEERay, pv);
+                            for (int k = 0; k < 3; k++) o[k] = p_pow(pv[k], 2.2f) + p_pow(il[k], 1.0f / 2.2f) * throughput[k];
+                            C->PrimaryNEERay = packRGBE(o);
+                        }
+                    }
                 }
                 status = 0;
                 goto done;
@@ -730,6 +866,100 @@ done:
     return status;
 }
 
+/* VisabilityCheckCompute — CommonData.cginc:710-819: the same any-hit walk with the distance as
+ * given and a zero throughput; returns 1 (visible) when the loop ends, the Reps bound included, 0 at
+ * the first occluder, -2 on a stack overflow (the reference has no check), -3 unsupported material. */
+static int visibility_check(const scene* s, tt_shadow_ray* SR, tt_oracle_ray_counts* cnt) {
+    uint2 stack[TT_STACK_SIZE];
+    int stack_size = 0;
+    uint2 current_group, triangle_group = {0u, 0u};
+    int tlas_stack_size = -1, TriOffset = 0, NodeOffset = 0, MatOffset = 0, Reps = 0;
+    const float dist = SR->t;
+    Ray ray, ray2;
+    ray.origin = ld3(SR->origin);
+    ray.direction = ld3(SR->direction);
+    ray.direction_inv = vrcp(ray.direction); /* :722 */
+    ray2 = ray;
+    uint32_t oct_inv4 = ray_get_octant_inv4(ray.direction);
+    current_group.x = 0u;
+    current_group.y = 0x80000000u;
+    float through[3] = {0.0f, 0.0f, 0.0f}; /* :732 */
+    while (Reps < TT_MAX_REPS) {
+        if (current_group.y & 0xff000000u) { /* :734-761 */
+            const uint32_t child_index_offset = firstbithigh(current_group.y);
+            const uint32_t slot_index = (child_index_offset - 24) ^ (oct_inv4 & 0xff);
+            const uint32_t relative_index = countbits(current_group.y & ~(0xffffffffu << slot_index));
+            const uint32_t child_node_index = current_group.x + relative_index;
+            current_group.y &= ~(1u << child_index_offset);
+            if (current_group.y & 0xff000000u) {
+                if (stack_size == TT_STACK_SIZE) return -2;
+                stack[stack_size++] = current_group;
+            }
+            const tt_cwbvh_node* TempNode = &s->nodes[child_node_index];
+            const uint32_t hitmask = cwbvh_node_intersect(&ray, oct_inv4, dist, TempNode);
+            current_group.y = (hitmask & 0xff000000u) | ((TempNode->e_imask >> 24) & 0xff);
+            triangle_group.y = (hitmask & 0x00ffffffu);
+            current_group.x = TempNode->base_child + (uint32_t)NodeOffset;
+            triangle_group.x = TempNode->base_tri + (uint32_t)TriOffset;
+            Reps++;
+            cnt->node_visits++;
+        } else { /* :762-765 */
+            triangle_group = current_group;
+            current_group.x = 0u;
+            current_group.y = 0u;
+        }
+        if (triangle_group.y != 0) {
+            if (tlas_stack_size == -1) { /* :768-791 */
+                const uint32_t mesh_offset = firstbithigh(triangle_group.y);
+                triangle_group.y &= ~(1u << mesh_offset);
+                const int mesh_id = s->tlas[triangle_group.x + mesh_offset];
+                const tt_mesh_data* MD = &s->md[mesh_id];
+                NodeOffset = MD->NodeOffset;
+                TriOffset = MD->TriOffset;
+                if (triangle_group.y != 0) {
+                    if (stack_size == TT_STACK_SIZE) return -2;
+                    stack[stack_size++] = triangle_group;
+                }
+                if (current_group.y & 0xff000000u) {
+                    if (stack_size == TT_STACK_SIZE) return -2;
+                    stack[stack_size++] = current_group;
+                }
+                tlas_stack_size = stack_size;
+                MatOffset = MD->MaterialOffset;
+                ray.direction = mul33(MD->W2L, ray.direction);
+                ray.origin = mul34(MD->W2L, ray.origin);
+                ray.direction_inv = vrcp(ray.direction);
+                oct_inv4 = ray_get_octant_inv4(ray.direction);
+                current_group.x = (uint32_t)(MD->mesh_data_bvh_offsets & 0x7fffffff);
+                current_group.y = 0x80000000u;
+                cnt->blas_entries++;
+            } else { /* :793-799 */
+                while (triangle_group.y != 0) {
+                    const uint32_t triangle_index = firstbithigh(triangle_group.y);
+                    triangle_group.y &= ~(1u << triangle_index);
+                    cnt->tri_tests++;
+                    const int r = intersect_triangle_shadow(s, (int)(triangle_group.x + triangle_index), &ray, dist,
+                                                            MatOffset, &cnt->accepts, through);
+                    if (r == 3) return -3;
+                    if (r) return 0;
+                }
+            }
+        }
+        if ((current_group.y & 0xff000000u) == 0) { /* :803-816 */
+            if (stack_size == 0) break;
+            if (stack_size == tlas_stack_size) {
+                NodeOffset = 0;
+                TriOffset = 0;
+                tlas_stack_size = -1;
+                ray = ray2;
+                oct_inv4 = ray_get_octant_inv4(ray.direction);
+            }
+            current_group = stack[--stack_size];
+        }
+    }
+    return 1;
+}
+
 typedef struct shadow_worker {
     const shadow_job* J;
     uint32_t tid, nthreads;
@@ -742,6 +972,18 @@ static void* shadow_worker_main(void* arg) {
     for (uint32_t base = w->tid * TT_ORACLE_CHUNK; base < n; base += w->nthreads * TT_ORACLE_CHUNK) {
         const uint32_t end = base + TT_ORACLE_CHUNK < n ? base + TT_ORACLE_CHUNK : n;
         for (uint32_t i = base; i < end; i++) {
+            if (w->J->p->flags & TT_SHADOW_VISIBILITY_CHECK) {
+                tt_oracle_ray_counts cnt = {0, 0, 0, 0, 0, 0};
+                const int v = visibility_check(w->J->s, &w->J->rays[i], &cnt);
+                if (v < 0) {
+                    if (-v > w->worst) w->worst = -v;
+                } else if (w->J->visibility) {
+                    for (int k = 0; k < 4; k++) w->J->visibility[4 * (size_t)i + k] = v ? 1.0f : 0.0f;
+                }
+                cnt.status = v == 1 ? 0u : (v == 0 ? 4u : (uint32_t)-v);
+                if (w->J->counts) w->J->counts[i] = cnt;
+                continue;
+            }
             int st = intersect_bvh_shadow(w->J, i);
             if (st == 4) st = 0;
             if (st > w->worst) w->worst = st;
@@ -756,7 +998,7 @@ tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
                            const tt_mesh_data* meshdata, uint32_t n_mesh,
                            const tt_material* materials, uint32_t n_mat,
                            const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
-                           tt_col_data* global_colors, float* nee_pos,
+                           tt_col_data* global_colors, float* nee_pos, tt_cache_data* cache,
                            tt_oracle_ray_counts* counts, int32_t nthreads) {
     if (!nodes || !tris || !tlas_indices || !meshdata || !p || !shadow_rays) return TT_ERR_INVALID_ARG;
     if (n_mat && !materials) return TT_ERR_INVALID_ARG;
@@ -765,7 +1007,7 @@ tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
     for (uint32_t m = 0; m < n_mat; m++)
         if ((materials[m].MatType == TT_MAT_CUTOUT_INDEX && !g_atlas) || (materials[m].specTrans == 1.0f && !g_tex))
             return TT_ERR_UNSUPPORTED;
-    shadow_job J = {&s, p, shadow_rays, visibility, global_colors, nee_pos, counts};
+    shadow_job J = {&s, p, shadow_rays, visibility, global_colors, nee_pos, cache, counts};
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 1024) nthreads = 1024;
     shadow_worker ws[1024];

@@ -55,7 +55,7 @@ tt_status tt_oracle_shadow(const tt_cwbvh_node* nodes, uint32_t n_nodes,
                            const tt_mesh_data* meshdata, uint32_t n_mesh,
                            const tt_material* materials, uint32_t n_mat,
                            const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
-                           tt_col_data* global_colors, float* nee_pos,
+                           tt_col_data* global_colors, float* nee_pos, tt_cache_data* cache,
                            tt_oracle_ray_counts* counts, int32_t nthreads);
 
 /* Shading / geometric normal for the hit stored in GlobalRays (see tt_resolve_normals). */
@@ -74,6 +74,12 @@ tt_status tt_oracle_generate(const float* cam_to_world, const float* cam_inv_pro
                              int32_t max_bounce, tt_ray_data* global_rays);
 
 int32_t tt_oracle_hardware_threads(void);
+/* The pinned row-f1 encoders (CommonData.cginc:479-509, :1576-1619) and HLSL pow, for tests. */
+uint32_t tt_oracle_pack_rgbe(const float v[3]);
+void tt_oracle_unpack_rgbe(uint32_t x, float v[3]);
+uint32_t tt_oracle_encode_rgb(const float c[3]);
+void tt_oracle_decode_rgb(uint32_t x, float v[3]);
+float tt_oracle_pow(float x, float y);
 
 /* TLAS refit (AssetManager.RefitTLAS, AssetManager.cs:1473-1548, with the NodePair / layer
  * structures of ConstructNewTLAS :1256-1390 and BVHRefitter.compute RefitBVHLayer / NodeUpdate /

@@ -49,7 +49,15 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_generate.restype = i32
         L.tt_oracle_hardware_threads.restype = i32
         L.tt_oracle_shadow.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, C.POINTER(tthip.ShadowParams), vp,
-                                       vp, vp, vp, vp, i32]
+                                       vp, vp, vp, vp, vp, i32]
+        for name in ("tt_oracle_pack_rgbe", "tt_oracle_encode_rgb"):
+            getattr(L, name).argtypes = [vp]
+            getattr(L, name).restype = u32
+        for name in ("tt_oracle_unpack_rgbe", "tt_oracle_decode_rgb"):
+            getattr(L, name).argtypes = [u32, vp]
+            getattr(L, name).restype = None
+        L.tt_oracle_pow.argtypes = [C.c_float, C.c_float]
+        L.tt_oracle_pow.restype = C.c_float
         L.tt_oracle_shadow.restype = i32
         L.tt_oracle_set_alpha_atlas.argtypes = [vp, u32, u32]
         L.tt_oracle_set_alpha_atlas.restype = None
@@ -108,11 +116,13 @@ def trace(scene: "tthip.Scene", rays: np.ndarray, n_rays: int, bounce: int, far_
 
 
 def shadow(scene: "tthip.Scene", srays: np.ndarray, n_rays: int, bounce: int, width: int, height: int,
-           visibility=None, colors=None, nee_pos=None, counts: bool = False, nthreads: int = 1):
-    """Any-hit oracle in place on ``srays`` (SHADOW_DTYPE) and the optional outputs.
-    Returns (status, counts or None); counts.status 0 reached |t|, 4 occluded, 1 Reps exhausted."""
+           visibility=None, colors=None, nee_pos=None, counts: bool = False, nthreads: int = 1, flags: int = 0,
+           cache=None):
+    """Any-hit oracle in place on ``srays`` (SHADOW_DTYPE) and the optional outputs (``cache``: CACHE_DTYPE
+    per pixel, the RadianceCache CacheBuffer). Returns (status, counts or None); counts.status 0 reached
+    |t| (visible in TT_SHADOW_VISIBILITY_CHECK mode), 4 occluded, 1 Reps exhausted."""
     L = lib()
-    p = tthip.ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height, flags=0)
+    p = tthip.ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height, flags=flags)
     cnt = np.zeros(n_rays, COUNTS_DTYPE) if counts else None
     mats = scene.materials
     _set_atlas(scene)
@@ -123,8 +133,35 @@ def shadow(scene: "tthip.Scene", srays: np.ndarray, n_rays: int, bounce: int, wi
                             None if visibility is None else visibility.ctypes.data,
                             None if colors is None else colors.ctypes.data,
                             None if nee_pos is None else nee_pos.ctypes.data,
+                            None if cache is None else cache.ctypes.data,
                             None if cnt is None else cnt.ctypes.data, nthreads)
     return st, cnt
+
+
+def pack_rgbe(v):
+    a = np.ascontiguousarray(v, np.float32)
+    return int(lib().tt_oracle_pack_rgbe(a.ctypes.data))
+
+
+def unpack_rgbe(x):
+    o = np.zeros(3, np.float32)
+    lib().tt_oracle_unpack_rgbe(int(x), o.ctypes.data)
+    return o
+
+
+def encode_rgb(c):
+    a = np.ascontiguousarray(c, np.float32)
+    return int(lib().tt_oracle_encode_rgb(a.ctypes.data))
+
+
+def decode_rgb(x):
+    o = np.zeros(3, np.float32)
+    lib().tt_oracle_decode_rgb(int(x), o.ctypes.data)
+    return o
+
+
+def hlsl_pow(x, y):
+    return float(lib().tt_oracle_pow(float(x), float(y)))
 
 
 def resolve_normals(scene, rays, n_rays, bounce, far_plane, width, height):

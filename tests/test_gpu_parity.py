@@ -800,3 +800,100 @@ def test_trace_variant_flags_random_soup(engine, seed, flags):
         colors["Data"][:, 3] = 1.0
         rg1, rc1, ig1, ic1, _, _ = trace_both(engine, sc, r1, n1, 1, W, H, colors=colors, flags=flags, upload=False)
         assert_same(rg1, rc1, ig1, ic1, W * H, n1)
+
+
+# ------------------------------------------- row f1: the full kernel_shadow output contract
+@pytest.mark.parametrize("bounce", [0, 1])
+@pytest.mark.parametrize("flags", [tthip.TT_SHADOW_RADIANCE_CACHE, tthip.TT_SHADOW_RADIANCE_CACHE | tthip.TT_TRACE_USE_RESTIRGI,
+                                   0, tthip.TT_TRACE_USE_RESTIRGI])
+def test_shadow_accumulations_match_oracle(engine, bounce, flags):
+    """IntersectionKernels.compute:457-485 with and without the RadianceCache define: CacheBuffer
+    CurrentIlluminance (EncodeRGB / DecodeRGB), Indirect, PrimaryNEERay (packRGBE of pow terms),
+    Direct, NEEPosA -- bit for bit against the oracle, glass-tinted throughputs included. Random
+    initial colours, packed words (PrimaryNEERay, LuminanceIncomming, CurrentIlluminance) and
+    Data.w in {-1, bounce, other}; t < 0 on a quarter of the rays (the sign picks the target)."""
+    seed = 70 + bounce * 4 + flags % 7
+    sc = glass_soup(seed)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    O.trace(sc, rays, W * H, 0, FAR, W, H)
+    rng = np.random.default_rng(seed)
+    sr = hb.nee_rays_from_hits(rays, W * H, (0.5, 2.0, 2.5), seed)
+    sr["illumination"] *= rng.uniform(0.1, 30.0, (len(sr), 1)).astype(np.float32)
+    lum = (rng.integers(14, 26, len(sr)).astype(np.uint32) << 27) | rng.integers(0, 1 << 27, len(sr)).astype(np.uint32)
+    sr["LuminanceIncomming"] = lum.view(np.float32)
+    col = np.zeros(W * H, tthip.COL_DTYPE)
+    col["Direct"] = rng.uniform(0, 2, (W * H, 3))
+    col["Indirect"] = rng.uniform(0, 2, (W * H, 3))
+    col["PrimaryNEERay"] = (rng.integers(12, 24, W * H).astype(np.uint32) << 27) | \
+        rng.integers(0, 1 << 27, W * H).astype(np.uint32)
+    col["Data"][:, 3] = rng.choice(np.array([-1.0, float(bounce), 5.0], np.float32), W * H)
+    cache = np.zeros(W * H, tthip.CACHE_DTYPE)
+    cache["CurrentIlluminance"] = rng.integers(0, 1 << 32, W * H, dtype=np.uint64).astype(np.uint32)
+    cache["CurrentIlluminance"][::7] = 0
+    engine.upload(sc)
+    n = len(sr)
+    out = []
+    for side in ("gpu", "cpu"):
+        r, c, ch = sr.copy(), col.copy(), cache.copy()
+        vis = np.full((n, 4), 7.0, np.float32)
+        nee = np.full((W * H, 4), 9.0, np.float32)
+        if side == "gpu":
+            engine.trace_shadow(r, n, bounce, W, H, visibility=vis, colors=c, nee_pos=nee, cache=ch, flags=flags)
+        else:
+            st, _ = O.shadow(sc, r, n, bounce, W, H, visibility=vis, colors=c, nee_pos=nee, cache=ch, flags=flags,
+                             nthreads=CPU_THREADS)
+            assert st == 0
+        out.append((r, c, ch, vis, nee))
+    (rg, cg, hg, vg, ng), (rc, cc, hc, vc, nc) = out
+    b = lambda x: np.ascontiguousarray(x).view(np.uint8)  # noqa: E731
+    assert np.array_equal(b(rg), b(rc)), "shadow ray bytes differ"
+    assert same_floats(vg, vc), "visibility differs"
+    assert same_floats(ng, nc), "NEEPosA differs"
+    for f in ("Direct", "Indirect", "Data"):
+        assert same_floats(cg[f], cc[f]), f"GlobalColors.{f} differs"
+    assert np.array_equal(cg["PrimaryNEERay"], cc["PrimaryNEERay"]), \
+        f"{int((cg['PrimaryNEERay'] != cc['PrimaryNEERay']).sum())} PrimaryNEERay words differ"
+    assert np.array_equal(hg["CurrentIlluminance"], hc["CurrentIlluminance"]), \
+        f"{int((hg['CurrentIlluminance'] != hc['CurrentIlluminance']).sum())} CurrentIlluminance words differ"
+    reached = vc[:, 3] == 1.0
+    assert reached.sum() > 200
+    if flags & tthip.TT_SHADOW_RADIANCE_CACHE:
+        assert (hc["CurrentIlluminance"] != cache["CurrentIlluminance"]).sum() > 100
+    if not (bounce != 0 and (flags & tthip.TT_SHADOW_RADIANCE_CACHE) and (flags & tthip.TT_TRACE_USE_RESTIRGI)):
+        # (with RadianceCache + ReSTIR GI every t < 0 ray of a later bounce goes to Indirect, :477)
+        assert (cc["PrimaryNEERay"] != col["PrimaryNEERay"]).sum() > 20
+
+
+@pytest.mark.parametrize("seed", [81, 82])
+def test_visibility_check_mode(engine, seed):
+    """VisabilityCheckCompute (CommonData.cginc:710-819): the distance as given, visibility only,
+    nothing else written -- against the oracle's literal restatement."""
+    sc = glass_soup(seed)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    O.trace(sc, rays, W * H, 0, FAR, W, H)
+    sr = hb.nee_rays_from_hits(rays, W * H, (0.5, 2.0, 2.5), seed)
+    engine.upload(sc)
+    n = len(sr)
+    vg = np.full((n, 4), 7.0, np.float32)
+    vc = vg.copy()
+    rg, rc = sr.copy(), sr.copy()
+    col = np.zeros(W * H, tthip.COL_DTYPE)
+    cg, cc = col.copy(), col.copy()
+    engine.trace_shadow(rg, n, 0, W, H, visibility=vg, colors=cg, flags=tthip.TT_SHADOW_VISIBILITY_CHECK)
+    st, _ = O.shadow(sc, rc, n, 0, W, H, visibility=vc, colors=cc, flags=tthip.TT_SHADOW_VISIBILITY_CHECK,
+                     nthreads=CPU_THREADS)
+    assert st == 0
+    assert np.array_equal(vg, vc), f"{int((vg != vc).any(1).sum())} visibilities differ"
+    assert set(np.unique(vg[:, 0])) <= {0.0, 1.0} and (vg[:, 0] == 0).sum() > 50 and (vg[:, 0] == 1).sum() > 50
+    b = lambda x: np.ascontiguousarray(x).view(np.uint8)  # noqa: E731
+    assert np.array_equal(b(rg), b(sr)) and np.array_equal(b(cg), b(col)), "visibility mode writes nothing else"
+    # negative distance: nothing can be hit (tmax < 0), every ray is visible, as in the reference
+    neg = sr.copy()
+    neg["t"] = -np.abs(neg["t"])
+    v2 = np.zeros((n, 4), np.float32)
+    engine.trace_shadow(neg, n, 0, W, H, visibility=v2, flags=tthip.TT_SHADOW_VISIBILITY_CHECK)
+    assert (v2[:, 0] == 1.0).all()

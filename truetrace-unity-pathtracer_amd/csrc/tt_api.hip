@@ -20,6 +20,7 @@
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
 hipError_t tt_trace_occupancy_table(int* out12);
 hipError_t tt_launch_shadow(const ShadowArgs* a, uint32_t grid, hipStream_t st, int stats, int matcheck);
+hipError_t tt_launch_shadow_accumulate(const ShadowArgs* a, const float4* vis, hipStream_t st);
 void tt_shadow_occupancy_table(int* out4);
 uint32_t tt_trace_block_size();
 uint32_t tt_trace_spill_entries();
@@ -143,6 +144,7 @@ struct tt_ctx {
     DevBuf<tt_shadow_ray> st_shadow;
     DevBuf<float4> st_vis;
     DevBuf<float4> st_nee;
+    DevBuf<tt_cache_data> st_cache;
     unsigned long long last_diag[8] = {};
 };
 
@@ -604,6 +606,7 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->st_shadow.release();
     c->st_vis.release();
     c->st_nee.release();
+    c->st_cache.release();
     c->st_info.release();
     c->st_colors.release();
     c->st_normals.release();
@@ -1153,6 +1156,11 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
 
 tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
                           tt_col_data* colors, float* nee_pos, tt_stats* stats) {
+    return tt_trace_shadow_ex(c, p, rays, visibility, colors, nee_pos, nullptr, stats);
+}
+
+tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
+                             tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or shadow rays");
@@ -1180,9 +1188,15 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     float4* d_vis = reinterpret_cast<float4*>(visibility);
     tt_col_data* d_col = colors;
     float4* d_nee = reinterpret_cast<float4*>(nee_pos);
+    tt_cache_data* d_cache = cache;
     if (dev) {
         if (!is_device_ptr(rays)) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_DEVICE_PTRS set but rays is not device memory");
     } else {
+        if (cache) {
+            if (c->st_cache.n < wh) TT_HIP(c, c->st_cache.alloc(wh));
+            d_cache = c->st_cache.p;
+            TT_HIP(c, hipMemcpyAsync(d_cache, cache, sizeof(tt_cache_data) * wh, hipMemcpyHostToDevice, c->stream));
+        }
         if (c->st_shadow.n < p->n_rays) TT_HIP(c, c->st_shadow.alloc(p->n_rays));
         d_rays = c->st_shadow.p;
         TT_HIP(c, hipMemcpyAsync(d_rays, rays, sizeof(tt_shadow_ray) * p->n_rays, hipMemcpyHostToDevice, c->stream));
@@ -1201,6 +1215,14 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
             TT_HIP(c, hipMemcpyAsync(d_nee, nee_pos, sizeof(float4) * wh, hipMemcpyHostToDevice, c->stream));
         }
     }
+    // the accumulations beyond Direct / NEEPosA run in a second pass that reads the visibility
+    // records: give the traversal one when the caller passed none
+    const bool vis_check = (p->flags & TT_SHADOW_VISIBILITY_CHECK) != 0;
+    const bool accumulate = !vis_check && (d_col || d_cache);
+    if (accumulate && !d_vis) {
+        if (c->st_vis.n < p->n_rays) TT_HIP(c, c->st_vis.alloc(p->n_rays));
+        d_vis = c->st_vis.p;
+    }
     ShadowArgs a;
     std::memset(&a, 0, sizeof(a));
     a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
@@ -1217,6 +1239,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     a.visibility = d_vis;
     a.colors = d_col;
     a.nee_pos = d_nee;
+    a.cache = d_cache;
     a.ctl = c->ctl + c->ctl_cur;
     a.spill = c->spill.p;
     a.n_rays = p->n_rays;
@@ -1234,6 +1257,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
     c->ctl_zero[0] = c->ctl_zero[1] = false;  // the any-hit kernel zeroes nothing
     TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
+    if (accumulate) TT_HIP(c, tt_launch_shadow_accumulate(&a, d_vis, c->stream));
     c->ring_n++;
     c->ev0 = c->ring0[slot];
     c->ev1 = c->ring1[slot];
@@ -1246,6 +1270,7 @@ tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* r
             TT_HIP(c, hipMemcpyAsync(visibility, d_vis, sizeof(float4) * p->n_rays, hipMemcpyDeviceToHost, c->stream));
         if (colors) TT_HIP(c, hipMemcpyAsync(colors, d_col, sizeof(tt_col_data) * wh, hipMemcpyDeviceToHost, c->stream));
         if (nee_pos) TT_HIP(c, hipMemcpyAsync(nee_pos, d_nee, sizeof(float4) * wh, hipMemcpyDeviceToHost, c->stream));
+        if (cache) TT_HIP(c, hipMemcpyAsync(cache, d_cache, sizeof(tt_cache_data) * wh, hipMemcpyDeviceToHost, c->stream));
     }
     TT_HIP(c, hipStreamSynchronize(c->stream));
     float ms = 0.0f;

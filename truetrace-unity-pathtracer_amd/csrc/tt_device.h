@@ -180,6 +180,7 @@ struct ShadowArgs {
     float4* visibility;          // nullable, per ray
     tt_col_data* colors;         // nullable, GlobalColors (Direct += at bounce 0)
     float4* nee_pos;             // nullable, NEEPosA (bounce 0)
+    tt_cache_data* cache;        // nullable, CacheBuffer (TT_SHADOW_RADIANCE_CACHE)
     TraceControl* ctl;
     uint2* spill;
     uint32_t n_rays;

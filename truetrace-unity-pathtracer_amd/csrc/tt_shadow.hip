@@ -14,8 +14,12 @@
 //    the live rays regroup into 2/4/8-lane groups; a triangle pass tests up to G of the leaf's
 //    triangles and the ray is occluded if any of them occludes (what the sequential loop, which
 //    stops at the first occluder, concludes as well).
-//  * a ray that reaches |t| writes NEEPosA (bounce 0) and GlobalColors.Direct (bounce 0, t >= 0),
-//    the radiance-cache paths stay with the caller (see include/truetrace_hip.h).
+//  * a ray that reaches |t| writes NEEPosA (bounce 0) and the GlobalColors / CacheBuffer
+//    accumulations of :457-485 (Direct, Indirect, PrimaryNEERay, CurrentIlluminance; both the
+//    RadianceCache and the plain define set, encoders pinned in tt_encode.h);
+//  * TT_SHADOW_VISIBILITY_CHECK: VisabilityCheckCompute (CommonData.cginc:710-819) -- the Reps
+//    bound counts as visible and only the visibility is written.
+#include "tt_encode.h"
 #include "tt_wide.h"
 
 namespace {
@@ -331,14 +335,20 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_occ = 0, c_rays = 0, c_vis = 0, c_reps = 0, c_ovf = 0;
 
     // a finished ray's outputs: occluded (:449-454), Reps exhausted (:373), reached the light (:457-485)
+    const bool vis_check = (A.flags & TT_SHADOW_VISIBILITY_CHECK) != 0;
     auto do_occlude = [&](uint32_t ri) {
-        A.rays[ri].t = 0.0f;
+        if (!vis_check) A.rays[ri].t = 0.0f;
         if (A.visibility) A.visibility[ri] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     };
-    auto do_exhaust = [&](uint32_t ri) {
-        if (A.visibility) A.visibility[ri] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+    auto do_exhaust = [&](uint32_t ri) {  // VisabilityCheckCompute returns true once its loop ends
+        if (A.visibility)
+            A.visibility[ri] = vis_check ? make_float4(1.0f, 1.0f, 1.0f, 1.0f) : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
     };
     auto do_reach = [&](uint32_t ri, const LaneRay& w, const float3& thr) {  // TerrainExists false
+        if (vis_check) {
+            if (A.visibility) A.visibility[ri] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            return;
+        }
         const tt_shadow_ray& R = A.rays[ri];
         const uint32_t pix = R.PixelIndex;
         const float t = R.t;
@@ -347,12 +357,13 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
             const float d = fabsf(t);
             A.nee_pos[pix] = make_float4(w.ox + w.dx * d, w.oy + w.dy * d, w.oz + w.dz * d, 0.0f);
         }
-        if (A.bounce == 0 && t >= 0.0f && A.colors) {  // Direct += illumination * throughput (:469)
+        if (A.bounce == 0 && t >= 0.0f && A.colors && pix / A.width < A.height) {  // Direct (:469)
             tt_col_data& C = A.colors[pix];
             C.Direct[0] = C.Direct[0] + R.illumination[0] * thr.x;
             C.Direct[1] = C.Direct[1] + R.illumination[1] * thr.y;
             C.Direct[2] = C.Direct[2] + R.illumination[2] * thr.z;
         }
+        // the rest of :457-485 (CacheBuffer, Indirect, PrimaryNEERay) runs in tt_shadow_accumulate
     };
 
     while (true) {
@@ -405,8 +416,9 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 ray.dx = __uint_as_float(r1.x);
                 ray.dy = __uint_as_float(r1.y);
                 ray.dz = __uint_as_float(r1.z);
-                max_distance = fabsf(__uint_as_float(r1.w));
-                thr = make_float3(1.0f, 1.0f, 1.0f);
+                // |t| (:356); VisabilityCheckCompute takes its dist as given, throughput 0 (:732)
+                max_distance = vis_check ? __uint_as_float(r1.w) : fabsf(__uint_as_float(r1.w));
+                thr = vis_check ? make_float3(0.0f, 0.0f, 0.0f) : make_float3(1.0f, 1.0f, 1.0f);
                 ray.ix = rcp_rn(ray.dx);
                 ray.iy = rcp_rn(ray.dy);
                 ray.iz = rcp_rn(ray.dz);
@@ -541,6 +553,69 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 if (v[k]) atomicAdd(&A.ctl->stats[k], (unsigned long long)v[k]);
         }
     }
+}
+
+// ---------------------------------------------------------- :457-485 accumulations (row f1)
+// The outputs of a ray that reached |t| beyond Direct / NEEPosA: CacheBuffer.CurrentIlluminance,
+// Indirect and PrimaryNEERay, with or without the RadianceCache define (include/truetrace_hip.h).
+// A streaming pass over the launch's rays after the traversal, driven by its visibility record
+// (throughput.xyz, 1 = reached): it keeps the encoders' registers out of the traversal kernel.
+__global__ void tt_shadow_accumulate(ShadowArgs A, const float4* __restrict__ vis) {
+    const uint32_t ri = blockIdx.x * TT_BLOCK + threadIdx.x;
+    if (ri >= A.n_rays) return;
+    const float4 v = vis[ri];
+    if (v.w != 1.0f) return;
+    const tt_shadow_ray& R = A.rays[ri];
+    const uint32_t pix = R.PixelIndex;
+    if (pix / A.width >= A.height) return;  // out-of-range UAV writes are dropped
+    const float t = R.t;
+    const bool restir = (A.flags & TT_TRACE_USE_RESTIRGI) != 0;
+    const bool rc = (A.flags & TT_SHADOW_RADIANCE_CACHE) != 0;
+    const float il[3] = {R.illumination[0], R.illumination[1], R.illumination[2]};
+    const float th[3] = {v.x, v.y, v.z};
+    if (rc && A.cache) {  // :464
+        float k[3] = {1.0f, 1.0f, 1.0f};
+        if (!(!restir || t >= 0.0f)) {
+            const float3 u = tt_enc::unpackRGBE(__float_as_uint(R.LuminanceIncomming));
+            k[0] = u.x;
+            k[1] = u.y;
+            k[2] = u.z;
+        }
+        uint32_t& ci = A.cache[pix].CurrentIlluminance;
+        const float3 d = tt_enc::DecodeRGB(ci);
+        ci = tt_enc::EncodeRGB(d.x + (il[0] * th[0]) * k[0], d.y + (il[1] * th[1]) * k[1], d.z + (il[2] * th[2]) * k[2]);
+    }
+    if (!A.colors) return;
+    tt_col_data& C = A.colors[pix];
+    if (t >= 0.0f) {  // :466-474 (Direct at bounce 0 was added by the traversal kernel)
+        if (A.bounce != 0 && !rc)
+            for (int c = 0; c < 3; c++) C.Indirect[c] = C.Indirect[c] + il[c] * th[c];
+        return;
+    }
+    const bool indirect = rc ? (A.bounce != 0 && (restir || C.Data[3] == (float)A.bounce))  // :477
+                             : (A.bounce != 0 && (!restir && C.Data[3] == -1.0f));         // :479
+    if (indirect) {
+        float k[3] = {1.0f, 1.0f, 1.0f};
+        if (rc && restir) {
+            const float3 u = tt_enc::unpackRGBE(__float_as_uint(R.LuminanceIncomming));
+            k[0] = u.x;
+            k[1] = u.y;
+            k[2] = u.z;
+        }
+        for (int c = 0; c < 3; c++) C.Indirect[c] = C.Indirect[c] + (il[c] * th[c]) * k[c];
+    } else {  // :481 packRGBE(pow(unpackRGBE(PrimaryNEERay), 2.2f) + pow(illumination, rcp(2.2f)) * throughput)
+        const float3 p = tt_enc::unpackRGBE(C.PrimaryNEERay);
+        const float pv[3] = {p.x, p.y, p.z};
+        const float inv22 = 1.0f / 2.2f;
+        float o[3];
+        for (int c = 0; c < 3; c++) o[c] = tt_enc::pow_pinned(pv[c], 2.2f) + tt_enc::pow_pinned(il[c], inv22) * th[c];
+        C.PrimaryNEERay = tt_enc::packRGBE(o[0], o[1], o[2]);
+    }
+}
+
+hipError_t tt_launch_shadow_accumulate(const ShadowArgs* a, const float4* vis, hipStream_t st) {
+    hipLaunchKernelGGL(tt_shadow_accumulate, dim3((a->n_rays + TT_BLOCK - 1) / TT_BLOCK), dim3(TT_BLOCK), 0, st, *a, vis);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ launchers

@@ -41,6 +41,8 @@ TT_TRACE_STATS = 1 << 3
 TT_TRACE_ASYNC = 1 << 4
 TT_TRACE_IGNORE_GLASS = 1 << 5       # IgnoreGlassMain (IntersectionKernels.compute:42-44)
 TT_TRACE_IGNORE_BACKFACING = 1 << 6  # IgnoreBackfacing (IntersectionKernels.compute:45-47)
+TT_SHADOW_RADIANCE_CACHE = 1 << 7    # RadianceCache define (GlobalDefines.cginc:15) for tt_trace_shadow_ex
+TT_SHADOW_VISIBILITY_CHECK = 1 << 8  # VisabilityCheckCompute semantics (CommonData.cginc:710-819)
 TT_STACK_SIZE = 16
 TT_MAX_REPS = 1000
 
@@ -84,6 +86,10 @@ FLAG_INVISIBLE = 7
 SHADOW_DTYPE = np.dtype([("origin", "<f4", 3), ("LuminanceIncomming", "<f4"), ("direction", "<f4", 3), ("t", "<f4"),
                          ("illumination", "<f4", 3), ("PixelIndex", "<u4")])
 assert SHADOW_DTYPE.itemsize == 48
+# PropogatedCacheData (CommonData.cginc:1621-1627, PropDepth 4): the RadianceCache record per pixel
+CACHE_DTYPE = np.dtype([("samples", "<u4", (4, 2)), ("throughput", "<u4"), ("pathLength", "<u4"),
+                        ("CurrentIlluminance", "<u4"), ("Norm", "<u4")])
+assert CACHE_DTYPE.itemsize == 48 and CACHE_DTYPE.fields["CurrentIlluminance"][1] == 40
 TT_FLAG_IS_BACKGROUND, TT_FLAG_SHADOW_CASTER = 5, 6
 
 
@@ -254,6 +260,7 @@ def hip_lib():
         L.tt_scene_bytes.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
         L.tt_trace_shadow.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, C.POINTER(Stats)]
+        L.tt_trace_shadow_ex.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, vp, C.POINTER(Stats)]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_scene_upload_texture_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
@@ -697,16 +704,17 @@ class Engine:
 
     def trace_shadow(self, shadow_rays, n_rays: int, bounce: int, width: int, height: int, visibility=None,
                      colors=None, nee_pos=None, device: bool = False, stats: bool = False, check: bool = True,
-                     asynchronous: bool = False):
-        """tt_trace_shadow (kernel_shadow replacement): any-hit visibility of ShadowRayData rays."""
+                     asynchronous: bool = False, flags: int = 0, cache=None):
+        """tt_trace_shadow_ex (kernel_shadow replacement): any-hit visibility of ShadowRayData rays and
+        the GlobalColors / CacheBuffer accumulations (flags: TT_SHADOW_*, TT_TRACE_USE_RESTIRGI)."""
         p = ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height,
-                         flags=(TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0)
+                         flags=flags | (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0)
                          | (TT_TRACE_ASYNC if asynchronous else 0))
         s = Stats()
-        st = self.L.tt_trace_shadow(self.h, C.byref(p), _ptr(shadow_rays), _ptr(visibility), _ptr(colors),
-                                    _ptr(nee_pos), C.byref(s))
+        st = self.L.tt_trace_shadow_ex(self.h, C.byref(p), _ptr(shadow_rays), _ptr(visibility), _ptr(colors),
+                                       _ptr(nee_pos), _ptr(cache), C.byref(s))
         if check:
-            self._check(st, "tt_trace_shadow")
+            self._check(st, "tt_trace_shadow_ex")
         return (s, st) if not check else s
 
     def resolve_normals(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int,
