@@ -7,7 +7,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -25,7 +24,6 @@ void tt_shadow_occupancy_table(int* out4);
 uint32_t tt_trace_block_size();
 uint32_t tt_trace_spill_entries();
 uint32_t tt_trace_lds_bytes();
-uint32_t tt_trace_ncache_cap();
 hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uint32_t h, float near_plane, float far_plane,
                               int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays, hipStream_t st);
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
@@ -106,8 +104,6 @@ struct tt_ctx {
     DevBuf<tt_mesh_data> mesh_raw;
     DevBuf<MeshGpu> mesh;
     DevBuf<LeafMesh> leaf;
-    DevBuf<uint32_t> ncache;      // LDS node-cache plan: slot -> node index, then slot -> child code
-    uint32_t n_ncache = 0, ncache_root = 0;
     DevBuf<uint32_t> mat_tag;
     DevBuf<CutoutMat> mat_cut;
     DevBuf<GlassMat> mat_glass;
@@ -378,76 +374,6 @@ std::vector<LeafMesh> derive_leaves(const std::vector<int32_t>& tlas, const std:
     return out;
 }
 
-// LDS node-cache plan of the closest-hit kernel (tt_trace.hip, TT_NCACHE): up to `cap` nodes
-// taken breadth first from the TLAS root (node 0) through TLAS leaves into the instances' BLAS
-// roots, so the cache holds the scene graph's top levels, which take most node visits
-// (profiles/r01_diag_nodehist.txt: depth <= 3 carries ~50% of primary visits). A node's internal
-// children (base_child + NodeOffset + rank, IntersectionKernels.compute:160-163) are cached as a
-// whole group in consecutive slots or not at all, so the kernel finds child `rank` of a cached
-// group at `first slot + rank`. codes[s] = first child slot + 1 of slot s (0: children not cached);
-// leaves[i].root_code = slot + 1 of leaf i's BLAS root for its NodeOffset. Only the topology is
-// planned here; the kernel copies the cached nodes from the live buffer at every launch.
-void plan_node_cache(const SceneHost& h, std::vector<LeafMesh>& leaves, uint32_t cap, std::vector<uint32_t>& ids,
-                     std::vector<uint32_t>& codes, uint32_t& root_code) {
-    ids.clear();
-    codes.clear();
-    root_code = 0;
-    for (LeafMesh& l : leaves) l.root_code = 0;
-    const uint64_t N = h.nodes.size();
-    if (cap == 0 || N == 0) return;
-    struct Item {
-        uint32_t node, off, slot;
-        bool tlas;
-    };
-    std::deque<Item> q;
-    std::map<std::pair<uint32_t, uint32_t>, uint32_t> roots;  // (root, NodeOffset) -> code
-    ids.push_back(0);
-    codes.push_back(0);
-    root_code = 1;
-    q.push_back({0u, 0u, 0u, true});
-    while (!q.empty()) {
-        const Item it = q.front();
-        q.pop_front();
-        const tt_cwbvh_node& n = h.nodes[it.node];
-        const uint32_t k = (uint32_t)__builtin_popcount(n.e_imask >> 24);
-        const uint64_t base = (uint64_t)n.base_child + it.off;
-        if (k && ids.size() + k <= cap && base + k <= N) {
-            codes[it.slot] = (uint32_t)ids.size() + 1u;
-            for (uint32_t r = 0; r < k; r++) {
-                q.push_back({(uint32_t)(base + r), it.off, (uint32_t)ids.size(), it.tlas});
-                ids.push_back((uint32_t)(base + r));
-                codes.push_back(0);
-            }
-        }
-        if (!it.tlas) continue;
-        for (int c = 0; c < 8; c++) {  // TLAS leaf children: instance records base_tri + offset + j
-            const uint32_t m = (n.meta[c >> 2] >> (8 * (c & 3))) & 0xffu;
-            if (m == 0 || (m & 0x1fu) >= 24u) continue;
-            const uint32_t cnt = (uint32_t)__builtin_popcount((m >> 5) & 7u);
-            for (uint32_t j = 0; j < cnt; j++) {
-                const uint64_t li = (uint64_t)n.base_tri + (m & 0x1fu) + j;
-                if (li >= leaves.size() || li >= h.tlas.size()) continue;
-                LeafMesh& L = leaves[li];
-                if (L.mesh_id < 0 || (size_t)L.mesh_id >= h.mesh.size()) continue;
-                const uint32_t root = (uint32_t)L.m.root, off = (uint32_t)L.m.NodeOffset;
-                const auto key = std::make_pair(root, off);
-                auto f = roots.find(key);
-                if (f == roots.end()) {
-                    uint32_t code = 0;
-                    if (ids.size() < cap && root < N) {
-                        code = (uint32_t)ids.size() + 1u;
-                        q.push_back({root, off, (uint32_t)ids.size(), false});
-                        ids.push_back(root);
-                        codes.push_back(0);
-                    }
-                    f = roots.emplace(key, code).first;
-                }
-                L.root_code = f->second;
-            }
-        }
-    }
-}
-
 void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
     o.p0x = t.pos0[0];
     o.p0y = t.pos0[1];
@@ -459,9 +385,7 @@ void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
     o.e2y = t.posedge2[1];
     o.e2z = t.posedge2[2];
     o.matdat = t.MatDat;
-#if !TT_TRI40
     o.pad0 = o.pad1 = 0;
-#endif
 }
 
 bool is_device_ptr(const void* p) {
@@ -736,8 +660,6 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->any_cutout = c->host.any_cutout;
     c->any_atlas_shadow = c->host.any_atlas_shadow;
     c->leaf.release();
-    c->n_ncache = 0;
-    c->ncache_root = 0;
     {
         const tt_status st = refresh_leaves(c);
         if (st != TT_OK) return st;
@@ -920,31 +842,17 @@ tt_status tt_scene_validate(const tt_cwbvh_node* nodes, uint32_t n_nodes, const 
 }
 
 namespace {
-// Rebuilds the TLAS leaf records and the LDS node-cache plan from the host mirror (on upload and
-// after node / mesh-record updates, which may change the topology) and uploads both on the stream.
+// Rebuilds the TLAS leaf records from the host mirror (on upload and after node / mesh-record
+// updates, which may change the topology) and uploads them on the stream.
 tt_status refresh_leaves(tt_ctx* c) {
     std::vector<LeafMesh> lv = derive_leaves(c->host.tlas, c->host.mesh);
-    std::vector<uint32_t> ids, codes;
-    uint32_t root_code = 0;
-    plan_node_cache(c->host, lv, tt_trace_ncache_cap(), ids, codes, root_code);
     if (c->leaf.n < lv.size()) {
         c->leaf.release();
         const hipError_t e = c->leaf.alloc(lv.size());
         if (e != hipSuccess) return hip_fail(c, e, "TLAS leaf records");
     }
     TT_HIP(c, hipMemcpyAsync(c->leaf.p, lv.data(), sizeof(LeafMesh) * lv.size(), hipMemcpyHostToDevice, c->stream));
-    ids.insert(ids.end(), codes.begin(), codes.end());
-    if (!ids.empty()) {
-        if (c->ncache.n < ids.size()) {
-            c->ncache.release();
-            const hipError_t e = c->ncache.alloc(ids.size());
-            if (e != hipSuccess) return hip_fail(c, e, "node-cache plan");
-        }
-        TT_HIP(c, hipMemcpyAsync(c->ncache.p, ids.data(), sizeof(uint32_t) * ids.size(), hipMemcpyHostToDevice, c->stream));
-    }
     TT_HIP(c, hipStreamSynchronize(c->stream));
-    c->n_ncache = (uint32_t)codes.size();
-    c->ncache_root = root_code;
     return TT_OK;
 }
 }  // namespace
@@ -1094,9 +1002,6 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.tile_swizzle = (p->n_rays == wh && p->screen_width % 8 == 0 && p->screen_height % 8 == 0) ? 1u : 0u;
     a.div_width = fastdiv_make(std::max(1u, p->screen_width));
     a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
-    a.ncache = c->ncache.p;
-    a.n_ncache = c->n_ncache;
-    a.root_code = c->ncache_root;
     const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout ||
                           ((p->flags & TT_TRACE_IGNORE_GLASS) && c->host.any_atlas_shadow) ||
                           ((p->flags & TT_TRACE_IGNORE_BACKFACING) && p->bounce == 0);

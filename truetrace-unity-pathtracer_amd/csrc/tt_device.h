@@ -30,19 +30,14 @@ __device__ __forceinline__ float rcp_rn(float a) {
 // (CudaTriangle pos0/posedge1/posedge2, CommonData.cginc:63-66) + MatDat, padded so one
 // triangle is three 16-B loads. Built from AggTris at upload; AggTris itself also stays in
 // HBM for the attribute resolve.
-#ifndef TT_TRI40
-#define TT_TRI40 0  // 1: 40-B traversal triangles (no padding; 8-B aligned 16-B loads)
-#endif
 struct TriPos {
     float p0x, p0y, p0z, e1x;
     float e1y, e1z, e2x, e2y;
     float e2z;
     uint32_t matdat;
-#if !TT_TRI40
     uint32_t pad0, pad1;
-#endif
 };
-static_assert(sizeof(TriPos) == (TT_TRI40 ? 40 : 48), "TriPos size");
+static_assert(sizeof(TriPos) == 48, "TriPos size");
 
 // Traversal-layout mesh record, 64 B: W2L rows 0-2 (row-major, 12 floats) + the four offsets
 // IntersectBVH reads on a TLAS->BLAS switch (IntersectionKernels.compute:197-213).
@@ -62,8 +57,7 @@ static_assert(sizeof(MeshGpu) == 64, "MeshGpu is 64 bytes");
 struct LeafMesh {
     MeshGpu m;
     int32_t mesh_id;     // TLASBVH8Indices[i]
-    uint32_t root_code;  // LDS node-cache code of the instance's BLAS root (0: not cached, else slot + 1)
-    int32_t pad[2];
+    int32_t pad[3];
 };
 static_assert(sizeof(LeafMesh) == 80, "LeafMesh is 80 bytes");
 
@@ -157,9 +151,6 @@ struct TraceArgs {
     uint32_t flags;              // TT_TRACE_*
     uint32_t tile_swizzle;       // 1: work index -> 8x8 screen tiles (n_rays == W*H, W,H % 8 == 0)
     TraceControl* ctl_next;      // the other control block: zeroed by this launch for the next one
-    const uint32_t* ncache;      // LDS node cache plan: node index per slot [n_ncache], then child codes [n_ncache]
-    uint32_t n_ncache;           // cached nodes (<= tt_trace_ncache_cap())
-    uint32_t root_code;          // cache code of the TLAS root (node 0): 1 when slot 0 holds it
     FastDiv div_width;           // n / width (pixel decode of finished rays)
     FastDiv div_tiles;           // n / (width / 8) (8x8 tile swizzle in the refill)
 };

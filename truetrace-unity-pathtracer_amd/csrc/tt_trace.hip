@@ -55,12 +55,11 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
                     o.w = miss ? 1u : 0u;
                 }
             }
-            if (write) io_store16(reinterpret_cast<uint4*>(A.info) + (size_t)ty * A.width + tx, o);
+            if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
         }
     }
     const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-    io_store16(reinterpret_cast<uint4*>(R) + 2,
-               make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv));
+    reinterpret_cast<uint4*>(R)[2] = make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
     return best.t != A.far_plane;
 }
 }  // namespace
@@ -72,18 +71,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
     zero_next_control(A.ctl_next, tid);
-#if TT_NCACHE
-    // LDS node cache: copies of the top levels of the scene graph (planned on the host, breadth
-    // first from the TLAS root, whole sibling groups; tt_api.hip plan_node_cache), loaded from the
-    // live node buffer at every launch so refits are always seen. A node group whose children sit in
-    // the cache carries their first slot + 1 in bits 8-23 of cg.y (bits the reference leaves zero
-    // in a node group: imask is bits 0-7, child hit bits 24-31); the visit order is unchanged.
-    __shared__ uint4 s_nc[TT_NCACHE * 5];
-    __shared__ uint32_t s_ncode[TT_NCACHE];
-    for (uint32_t i = tid; i < A.n_ncache * 5u; i += TT_BLOCK) s_nc[i] = A.nodes[A.ncache[i / 5u] * 5u + i % 5u];
-    for (uint32_t i = tid; i < A.n_ncache; i += TT_BLOCK) s_ncode[i] = A.ncache[A.n_ncache + i];
-    __syncthreads();
-#endif
     const uint32_t gtid = blockIdx.x * TT_BLOCK + tid;
     const uint32_t spill_stride = gridDim.x * TT_BLOCK;
     uint2* __restrict__ spill = A.spill;
@@ -129,27 +116,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #ifdef TT_DIAG_RAYS  // per-ray (start, end, iterations, node visits): diag_times -> uint4[n_rays]
     uint32_t r_t0 = 0, r_iter = 0, r_nodes = 0;
 #endif
-    // world-space ray (ray2, IntersectionKernels.compute:151): kept in registers, or re-read from
-    // GlobalRays with the same correctly rounded reciprocals (bit-identical either way)
-    auto world_ray = [&]() -> LaneRay {
-#if TT_WRAY_RELOAD
-        const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
-        const uint4 r0 = rp[0], r1 = rp[1];
-        LaneRay w;
-        w.ox = __uint_as_float(r0.x);
-        w.oy = __uint_as_float(r0.y);
-        w.oz = __uint_as_float(r0.z);
-        w.dx = __uint_as_float(r1.x);
-        w.dy = __uint_as_float(r1.y);
-        w.dz = __uint_as_float(r1.z);
-        w.ix = rcp_rn(w.dx);
-        w.iy = rcp_rn(w.dy);
-        w.iz = rcp_rn(w.dz);
-        return w;
-#else
-        return wray;
-#endif
-    };
+    // the world-space ray (ray2, IntersectionKernels.compute:151), kept in registers
+    auto world_ray = [&]() -> LaneRay { return wray; };
 
     // :229-241: the finished ray's hit record and _PrimaryTriangleInfo
     auto finish_ray = [&]() {
@@ -174,7 +142,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         const bool pool_dry = !more && pool_next >= pool_end;
         // the queue is dry and the live rays fit in 2-lane groups: cooperative drain (tt_wide.h)
         const bool to_wide = TT_WIDE && pool_dry && n_idle < TT_WAVE && TT_WAVE - n_idle <= TT_WIDE_ENTER;
-#if TT_DEFER_FINISH
         // finished rays write their records in batches, right before their lanes are refilled
         if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry) || to_wide) {
             if (pending) {
@@ -183,7 +150,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 pending = false;
             }
         }
-#endif
         if (n_idle == TT_WAVE && pool_dry) break;
 #if TT_WIDE
         if (to_wide) {
@@ -235,9 +201,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 }
                 ray_index = A.ray_offset + local;
                 const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
-                const uint4 r0 = io_load16(rp), r1 = io_load16(rp + 1);
+                const uint4 r0 = rp[0], r1 = rp[1];
                 pix = r0.w;
-                if (INFO == 2) col_w = (pix < A.width * A.height) ? io_loadf(&A.colors[pix].Data[3]) : 0.0f;
+                if (INFO == 2) col_w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
                 ray.ox = __uint_as_float(r0.x);
                 ray.oy = __uint_as_float(r0.y);
                 ray.oz = __uint_as_float(r0.z);
@@ -247,16 +213,14 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 ray.ix = rcp_rn(ray.dx);
                 ray.iy = rcp_rn(ray.dy);
                 ray.iz = rcp_rn(ray.dz);
-#if !TT_WRAY_RELOAD
                 wray = ray;
-#endif
                 oct = octant_inv4(ray);
                 best.t = A.far_plane;
                 best.u = 0.0f;
                 best.v = 0.0f;
                 best.mesh_id = 0;
                 best.tri_id = -1;
-                cg = make_uint2(0u, 0x80000000u | (TT_NCACHE ? A.root_code << 8 : 0u));
+                cg = make_uint2(0u, 0x80000000u);
                 tg = make_uint2(0u, 0u);
                 stack_size = 0;
                 tlas_ss = -1;
@@ -288,17 +252,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     make_uint2((uint32_t)__builtin_amdgcn_s_memrealtime(), na | (more << 8) | ((uint32_t)__builtin_amdgcn_s_memtime() << 12));
             }
             d_tl++;
-        }
-#endif
-#ifdef TT_EXP_VALU_PAD  // diagnostic: N extra independent VALU ops per iteration (is the loop VALU-bound?)
-        {
-            float pad0 = __uint_as_float(lane), pad1 = pad0;
-#pragma unroll
-            for (int k = 0; k < TT_EXP_VALU_PAD / 2; k++) {
-                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pad0) : "v"(pad1));
-                asm volatile("v_add_f32 %0, %0, %1" : "+v"(pad1) : "v"(pad0));
-            }
-            if (pad0 == 1234.5f) best.u = pad1;
         }
 #endif
         // ------------------------------------------------------------- node phase
@@ -335,43 +288,15 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                         d_lead_same += child == lead ? 1u : 0u;
                         d_uniform += (same == all && lane == (uint32_t)__builtin_ctzll(all)) ? 1u : 0u;
                     }
-                    uint4 n0, n1, n2, n3, n4;
-                    uint32_t ncode = 0;
-#if TT_NCACHE
-                    const uint32_t gcode = (cg.y >> 8) & 0xffffu;
-                    if (gcode) {
-                        const uint32_t s = gcode - 1u + rel;
-                        const uint4* np = s_nc + s * 5u;
-                        n0 = np[0];
-                        n1 = np[1];
-                        n2 = np[2];
-                        n3 = np[3];
-                        n4 = np[4];
-                        ncode = s_ncode[s];
-                    } else
-#endif
-                    {
-                        const uint32_t no = node_offset(child);
-                        n0 = buffer_load16(nodes, no);
-                        n1 = buffer_load16(nodes, no + 16u);
-                        n2 = buffer_load16(nodes, no + 32u);
-                        n3 = buffer_load16(nodes, no + 48u);
-                        n4 = buffer_load16(nodes, no + 64u);
-                    }
+                    const uint32_t no = node_offset(child);
+                    const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
+                                n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
+                                n4 = buffer_load16(nodes, no + 64u);
                     const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
-#ifdef TT_EXP_LOAD_PAD  // diagnostic: N extra 16-B loads of the same node per step (texture-path headroom)
-                    {
-#pragma unroll
-                        for (int k = 0; k < TT_EXP_LOAD_PAD; k++) {
-                            const uint4 pad = buffer_load16(nodes, no + 16u * (uint32_t)(k % 5));
-                            asm volatile("; pad use %0" ::"v"(pad.x));
-                        }
-                    }
-#endif
 #ifdef TT_DIAG_NODEHIST  // diagnostic: visits per node index -> diag_times (as uint32[n_nodes])
                     if (A.diag_times) atomicAdd(reinterpret_cast<uint32_t*>(A.diag_times) + child, 1u);
 #endif
-                    cg.y = (hitmask & 0xff000000u) | (n0.w >> 24) | (ncode << 8);
+                    cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
                     tg.y = hitmask & 0x00ffffffu;
                     cg.x = n1.x + (uint32_t)NodeOffset;
                     tg.x = n1.y + (uint32_t)TriOffset;
@@ -418,7 +343,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     nr.iz = rcp_rn(nr.dz);
                     ray = nr;
                     oct = octant_inv4(ray);
-                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u | (TT_NCACHE ? (uint32_t)mo5.y << 8 : 0u));
+                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
                     if (STATS) c_blas++;
                 } else {
                     active = false;
@@ -437,20 +362,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             }
         }
         // --------------------------------------------------------- triangle phase
-#if TT_TRI_MIN > 1
-        // postpone the pass while few lanes have a triangle pending and others still traverse
-        // (per-ray order is unchanged: a lane with pending triangles takes no node step)
-        bool tri_pass = true;
-        {
-            const uint32_t n_tri = (uint32_t)__popcll(__ballot(active && tg.y != 0u));
-            const uint32_t n_act = (uint32_t)__popcll(__ballot(active));
-            tri_pass = n_tri >= TT_TRI_MIN || n_tri == n_act;
-        }
-        if (tri_pass && active && tg.y != 0u) {
-#else
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
             DB(4);
-#endif
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool acc = intersect_triangle<MATCHECK>(tris, A.mat, A.bounce == 0, A.flags, (int32_t)(tg.x + ti),
@@ -478,12 +391,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 TT_POP(cg);
                 DB(7);
             } else {
-#if TT_DEFER_FINISH
                 pending = true;  // written at the next refill (or when the wave drains)
                 DB(8);
-#else
-                finish_ray();
-#endif
                 active = false;
             }
         }
@@ -528,382 +437,10 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
 }
 
-// ------------------------------------------------------------- uniform-step kernel
-// Same traversal semantics as tt_trace_kernel, restructured so that a wave executes ONE
-// straight-line step per iteration: every lane runs the node test and the triangle test, and
-// what each lane commits is chosen with selects (v_cndmask) instead of divergent branches.
-// Hypothesis tested with it: the branchy form was stalled on control flow (~25 branches and
-// exec-mask updates per step). Measured on C2: branches 9.6 vs 25 per iteration and SALU -30%,
-// but VALU +10% and 4-5% slower overall (the loop is VALU-issue-bound at the margin: +100 VALU
-// per iteration cost +15%), so it stays an option (TT_KERNEL_UNIFORM=1), not the default.
-// Lanes that have nothing to do fetch node 0 / triangle 0 (one shared line) and discard the
-// result. Rare transitions (TLAS->BLAS entry, BLAS->TLAS return, ray completion, stack
-// overflow) stay as wave-uniform `if (__any(...))` blocks.
-#ifndef TT_UNIFORM_STACK
-#define TT_UNIFORM_STACK (TT_STACK_SIZE + 1)  // entry 16 is scratch for the unconditional push
-#endif
-template <bool STATS, bool MATCHECK, int INFO>
-__global__ TT_BOUNDS void tt_trace_kernel_u(TraceArgs A) {
-    __shared__ uint2 s_stack[TT_UNIFORM_STACK][TT_BLOCK];
-    const uint32_t tid = threadIdx.x;
-    zero_next_control(A.ctl_next, tid);
-    const uint32_t lane = tid & (TT_WAVE - 1);
-
-    uint32_t pool_next = 0, pool_end = 0, more = 1;
-    const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
-    SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
-    const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
-    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
-    const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
-
-    bool active = false;
-    uint32_t ray_index = 0;
-    LaneRay ray{}, wray{};
-    Best best{};
-    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
-    uint32_t oct = 0;
-    int32_t stack_size = 0, tlas_ss = -1;
-    int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
-    uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
-    uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
-#ifdef TT_DIAG_TIMES
-    const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
-    const uint64_t c_begin = __builtin_amdgcn_s_memtime();
-#endif
-
-    while (true) {
-        // ---------------------------------------------------------------- refill
-        const uint64_t idle = __ballot(!active);
-        const uint32_t n_idle = (uint32_t)__popcll(idle);
-        const bool pool_dry = !more && pool_next >= pool_end;
-        if (n_idle == TT_WAVE && pool_dry) break;
-        if (n_idle >= TT_REFILL_MIN && !pool_dry) {
-            // wave-uniform: take from the wave's pool first, then one dequeue for the rest
-            const uint32_t avail = pool_end - pool_next;
-            uint32_t new_base = 0, new_count = 0;
-            if (avail < n_idle && more) {
-                new_count = sched_reserve(A.ctl, A.n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
-                more = new_count > 0 ? 1u : 0u;
-            }
-            const uint32_t take_old = min(avail, n_idle);
-            const uint32_t take_new = min(n_idle - take_old, new_count);
-            const uint32_t rank = lane_prefix(idle);
-            uint32_t widx = 0xffffffffu;
-            if (rank < take_old) widx = pool_next + rank;
-            else if (rank - take_old < take_new) widx = new_base + (rank - take_old);
-            if (new_count > 0) {  // the old pool was fully consumed (avail < n_idle)
-                pool_next = new_base + take_new;
-                pool_end = new_base + new_count;
-            } else {
-                pool_next += take_old;
-            }
-            if (!active && widx != 0xffffffffu) {
-                uint32_t local = widx;
-                if (A.tile_swizzle) {
-                    const uint32_t tw = A.width >> 3;
-                    const uint32_t t = widx >> 6, l = widx & 63u;
-                    const uint32_t ty = fastdiv(t, A.div_tiles), tx = t - ty * tw;
-                    local = (ty * 8u + (l >> 3)) * A.width + tx * 8u + (l & 7u);
-                }
-                ray_index = A.ray_offset + local;
-                const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
-                const uint4 r0 = rp[0], r1 = rp[1];
-                ray.ox = __uint_as_float(r0.x);
-                ray.oy = __uint_as_float(r0.y);
-                ray.oz = __uint_as_float(r0.z);
-                ray.dx = __uint_as_float(r1.x);
-                ray.dy = __uint_as_float(r1.y);
-                ray.dz = __uint_as_float(r1.z);
-                ray.ix = rcp_rn(ray.dx);
-                ray.iy = rcp_rn(ray.dy);
-                ray.iz = rcp_rn(ray.dz);
-                wray = ray;
-                oct = octant_inv4(ray);
-                best.t = A.far_plane;
-                best.u = 0.0f;
-                best.v = 0.0f;
-                best.mesh_id = 0;
-                best.tri_id = -1;
-                cg = make_uint2(0u, 0x80000000u);
-                tg = make_uint2(0u, 0u);
-                stack_size = 0;
-                tlas_ss = -1;
-                NodeOffset = 0;
-                TriOffset = 0;
-                MatOffset = 0;
-                mesh_id = -1;
-                Reps = 0;
-                active = true;
-                c_rays++;
-            }
-        }
-
-        // ------------------------------------------------------- node step (all lanes)
-        // IntersectionKernels.compute:155-191
-        const bool nodeable = active && tg.y == 0u;
-        const bool exhaust = nodeable && Reps >= TT_MAX_REPS;  // :155 loop bound: no write
-        const bool has_inner = (cg.y & 0xff000000u) != 0u;
-        const bool do_node = nodeable && !exhaust && has_inner;
-        const bool pop_tri = nodeable && !exhaust && !has_inner;  // :188-191
-        const uint32_t cio = firstbithigh(cg.y | 0x01000000u);
-        const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
-        const uint32_t rel = __builtin_popcount(cg.y & ~(0xffffffffu << slot));
-        const uint32_t rem = cg.y & ~(1u << cio);
-        const bool push = do_node && (rem & 0xff000000u) != 0u;
-        const bool overflow = push && stack_size == TT_STACK_SIZE;
-        s_stack[stack_size][tid] = make_uint2(cg.x, rem);  // above the top unless pushed
-        const uint32_t child = do_node ? cg.x + rel : 0u;
-        const uint32_t no = node_offset(child);
-        const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u), n2 = buffer_load16(nodes, no + 32u),
-                    n3 = buffer_load16(nodes, no + 48u), n4 = buffer_load16(nodes, no + 64u);
-        const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
-        const bool commit = do_node && !overflow;
-        {
-            const uint2 ncg = make_uint2(n1.x + (uint32_t)NodeOffset, (hitmask & 0xff000000u) | (n0.w >> 24));
-            const uint2 ntg = make_uint2(n1.y + (uint32_t)TriOffset, hitmask & 0x00ffffffu);
-            const uint2 ocg = cg;
-            cg.x = commit ? ncg.x : (pop_tri ? 0u : ocg.x);
-            cg.y = commit ? ncg.y : (pop_tri ? 0u : ocg.y);
-            tg.x = commit ? ntg.x : (pop_tri ? ocg.x : tg.x);
-            tg.y = commit ? ntg.y : (pop_tri ? ocg.y : tg.y);
-        }
-        stack_size += (push && !overflow) ? 1 : 0;
-        Reps += commit ? 1 : 0;
-        if (STATS) {
-            c_nodes += commit ? 1u : 0u;
-            c_reps += exhaust ? 1u : 0u;
-            c_ovf += overflow ? 1u : 0u;
-            const uint64_t nm = __ballot(commit);
-            if (lane == 0) {
-                d_iter++;
-                d_node_lanes += (uint32_t)__popcll(nm);
-                d_node_iters += nm ? 1u : 0u;
-            }
-        }
-        if (__builtin_expect(__any(overflow), 0)) {
-            if (overflow) atomicAdd(&A.ctl->err_overflow, 1u);
-        }
-        if (exhaust || overflow) {
-            active = false;
-            stack_size = 0;
-            tg.y = 0u;
-            cg.y = 0u;
-        }
-
-        // ----------------------------------------------- TLAS leaf -> BLAS (:194-219)
-        const bool enter = active && tg.y != 0u && tlas_ss == -1;
-        if (__any(enter)) {
-            if (enter) {
-                const uint32_t mo = firstbithigh(tg.y);
-                tg.y &= ~(1u << mo);
-                mesh_id = A.tlas[tg.x + mo];
-                const float4* mp = reinterpret_cast<const float4*>(A.mesh + mesh_id);
-                const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                const int4 mo4 = reinterpret_cast<const int4*>(A.mesh + mesh_id)[3];
-                NodeOffset = mo4.y;
-                TriOffset = mo4.x;
-                bool ok = true;
-                if (tg.y != 0u) {
-                    if (stack_size == TT_STACK_SIZE) ok = false;
-                    else s_stack[stack_size++][tid] = tg;
-                }
-                if (ok && (cg.y & 0xff000000u)) {
-                    if (stack_size == TT_STACK_SIZE) ok = false;
-                    else s_stack[stack_size++][tid] = cg;
-                }
-                if (ok) {
-                    tlas_ss = stack_size;
-                    MatOffset = mo4.z;
-                    LaneRay nr;
-                    nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
-                    nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
-                    nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
-                    nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
-                    nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
-                    nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = rcp_rn(nr.dx);
-                    nr.iy = rcp_rn(nr.dy);
-                    nr.iz = rcp_rn(nr.dz);
-                    ray = nr;
-                    oct = octant_inv4(ray);
-                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
-                    if (STATS) c_blas++;
-                } else {
-                    active = false;
-                    stack_size = 0;
-                    cg.y = 0u;
-                    if (STATS) c_ovf++;
-                    atomicAdd(&A.ctl->err_overflow, 1u);
-                }
-                tg.y = 0u;
-            }
-        }
-
-        // --------------------------------------------- triangle test (all lanes, :220-226)
-        {
-            const bool do_tri = active && tg.y != 0u;
-            const uint32_t ti = firstbithigh(tg.y | 1u);
-            const int32_t tri_id = do_tri ? (int32_t)(tg.x + ti) : 0;
-            const uint32_t to = tri_offset((uint32_t)tri_id);
-            const uint4 ta = buffer_load16(tris, to), tb = buffer_load16(tris, to + 16u), tc = buffer_load16(tris, to + 32u);
-            const float p0x = __uint_as_float(ta.x), p0y = __uint_as_float(ta.y), p0z = __uint_as_float(ta.z);
-            const float e1x = __uint_as_float(ta.w), e1y = __uint_as_float(tb.x), e1z = __uint_as_float(tb.y);
-            const float e2x = __uint_as_float(tb.z), e2y = __uint_as_float(tb.w), e2z = __uint_as_float(tc.x);
-            const float hx = fma_(ray.dy, e2z, -(ray.dz * e2y));
-            const float hy = fma_(ray.dz, e2x, -(ray.dx * e2z));
-            const float hz = fma_(ray.dx, e2y, -(ray.dy * e2x));
-            const float aa = fma_(e1z, hz, fma_(e1y, hy, e1x * hx));
-            const float f = rcp_rn(aa);
-            const float sx = ray.ox - p0x, sy = ray.oy - p0y, sz = ray.oz - p0z;
-            const float u = f * fma_(sz, hz, fma_(sy, hy, sx * hx));
-            const float qx = fma_(sy, e1z, -(sz * e1y));
-            const float qy = fma_(sz, e1x, -(sx * e1z));
-            const float qz = fma_(sx, e1y, -(sy * e1x));
-            const float v = f * fma_(ray.dz, qz, fma_(ray.dy, qy, ray.dx * qx));
-            const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
-            const bool cand = do_tri && (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) &&
-                              (t > 0.0f && t < best.t);
-            bool accept = cand;
-            if (MATCHECK && __any(cand)) {
-                if (cand) {  // :35-48 Cutout, Invisible at CurBounce == 0; out-of-range material = zeros
-                    const uint32_t mi = (uint32_t)(MatOffset + (int32_t)tc.y);
-                    const uint32_t w = mi < A.mat.n_mat ? A.mat.word[mi] : 0u;
-                    if ((w >> TT_MATWORD_CUTOUT) & 1u) {
-                        const CutoutMat cm = A.mat.cut[mi];
-                        if (sample_linear(A.mat, align_uv(base_uv(A.mat, tri_id, u, v), cm)) < cm.cutoff) accept = false;
-                    }
-                    if (A.bounce == 0 && ((w >> TT_FLAG_INVISIBLE) & 1u)) accept = false;
-                }
-            }
-            best.t = accept ? t : best.t;
-            best.u = accept ? u : best.u;
-            best.v = accept ? v : best.v;
-            best.mesh_id = accept ? mesh_id : best.mesh_id;
-            best.tri_id = accept ? tri_id : best.tri_id;
-            tg.y = do_tri ? (tg.y & ~(1u << ti)) : tg.y;
-            if (STATS) {
-                c_tris += do_tri ? 1u : 0u;
-                c_acc += cand ? 1u : 0u;
-                const uint64_t tm = __ballot(do_tri);
-                if (lane == 0) {
-                    d_tri_lanes += (uint32_t)__popcll(tm);
-                    d_tri_iters += tm ? 1u : 0u;
-                }
-            }
-        }
-
-        // ------------------------------------------------------ pop / finish (:228-251)
-        const bool adv = active && tg.y == 0u && (cg.y & 0xff000000u) == 0u;
-        const bool fin = adv && stack_size == 0;
-        const bool pop = adv && stack_size > 0;
-        const bool restore = pop && stack_size == tlas_ss;
-        if (__any(restore)) {
-            if (restore) {  // :243-249 BLAS -> TLAS
-                NodeOffset = 0;
-                TriOffset = 0;
-                tlas_ss = -1;
-                ray = wray;
-                oct = octant_inv4(ray);
-            }
-        }
-        {
-            const uint2 top = s_stack[stack_size > 0 ? stack_size - 1 : 0][tid];
-            cg.x = pop ? top.x : cg.x;
-            cg.y = pop ? top.y : cg.y;
-            stack_size -= pop ? 1 : 0;
-        }
-        if (__any(fin)) {
-            if (fin) {  // :229-241 + set() CommonData.cginc:430-434
-                tt_ray_data* R = A.rays + ray_index;
-                if (INFO != 0) {
-                    const uint32_t pix = R->PixelIndex;
-                    const uint32_t ty = fastdiv(pix, A.div_width), tx = pix - ty * A.width;
-                    if (ty < A.height) {
-                        uint4 o = make_uint4(0, 0, 0, 0);
-                        bool write = false;
-                        if (INFO == 1) {
-                            const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                            o = make_uint4((uint32_t)best.mesh_id, (uint32_t)(best.tri_id - to), __float_as_uint(best.u),
-                                           __float_as_uint(best.v));
-                            write = true;
-                        } else {
-                            const float w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
-                            if (w == -1.0f || (float)A.bounce == w) {
-                                write = true;
-                                const bool miss = best.t == A.far_plane;
-                                if ((A.flags & TT_TRACE_USE_RESTIRGI) && !miss) {
-                                    const int32_t to = A.mesh[best.mesh_id].TriOffset;
-                                    o.x = (uint32_t)best.mesh_id;
-                                    o.y = (uint32_t)(best.tri_id - to);
-                                    o.z = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-                                } else if ((A.flags & TT_TRACE_USE_ASVGF) || !miss) {
-                                    o.x = __float_as_uint(wray.dx);
-                                    o.y = __float_as_uint(wray.dy);
-                                    o.z = __float_as_uint(wray.dz);
-                                } else {
-                                    o.x = __float_as_uint(wray.dx * best.t + wray.ox);
-                                    o.y = __float_as_uint(wray.dy * best.t + wray.oy);
-                                    o.z = __float_as_uint(wray.dz * best.t + wray.oz);
-                                }
-                                o.w = miss ? 1u : 0u;
-                            }
-                        }
-                        if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
-                    }
-                }
-                const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-                reinterpret_cast<uint4*>(R)[2] =
-                    make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
-                if (STATS) c_hits += (best.t != A.far_plane) ? 1u : 0u;
-                active = false;
-                stack_size = 0;
-            }
-        }
-    }
-
-#ifdef TT_DIAG_TIMES
-    {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        const uint32_t rays_done = wave_sum(c_rays);
-        if (lane == 0 && A.diag_times) {
-            const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
-            A.diag_times[4 * w + 0] = t_begin;
-            A.diag_times[4 * w + 1] = t_end;
-            A.diag_times[4 * w + 2] = rays_done;
-            A.diag_times[4 * w + 3] = __builtin_amdgcn_s_memtime() - c_begin;  // shader clock ticks
-        }
-    }
-#endif
-    if (STATS) {
-        const uint32_t vals[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
-                                  wave_sum(c_hits), wave_sum(c_reps), wave_sum(c_ovf), wave_sum(c_acc)};
-        (void)d_active_lanes;
-        if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (vals[k]) atomicAdd(&A.ctl->stats[k], (unsigned long long)vals[k]);
-            const uint32_t d[6] = {d_iter, d_node_iters, d_node_lanes, d_tri_iters, d_tri_lanes, 0u};
-#pragma unroll
-            for (int k = 0; k < 6; k++) atomicAdd(&A.ctl->diag[k], (unsigned long long)d[k]);
-        }
-    }
-}
-
-#ifndef TT_KERNEL_UNIFORM
-#define TT_KERNEL_UNIFORM 0
-#endif
-#if TT_KERNEL_UNIFORM
-#define TT_KERNEL tt_trace_kernel_u
-#define TT_LDS_ENTRIES TT_UNIFORM_STACK
-#else
-#define TT_KERNEL tt_trace_kernel
-#define TT_LDS_ENTRIES TT_LDS_STACK
-#endif
-
 // ------------------------------------------------------------------ launchers
 template <bool S, bool M, int I>
 static hipError_t launch_one(const TraceArgs& a, uint32_t grid, hipStream_t st) {
-    hipLaunchKernelGGL((TT_KERNEL<S, M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+    hipLaunchKernelGGL((tt_trace_kernel<S, M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
     return hipGetLastError();
 }
 
@@ -925,7 +462,7 @@ hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int in
 template <bool S, bool M, int I>
 static int occ_one() {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, TT_KERNEL<S, M, I>, TT_BLOCK, 0) != hipSuccess) b = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_trace_kernel<S, M, I>, TT_BLOCK, 0) != hipSuccess) b = 1;
     return b;
 }
 hipError_t tt_trace_occupancy_table(int* out12) {
@@ -945,10 +482,7 @@ hipError_t tt_trace_occupancy_table(int* out12) {
 }
 
 uint32_t tt_trace_block_size() { return TT_BLOCK; }
-uint32_t tt_trace_lds_bytes() {
-    return (uint32_t)(TT_LDS_ENTRIES * TT_BLOCK * sizeof(uint2) + (TT_KERNEL_UNIFORM ? 0 : TT_NCACHE * 84));
-}
-uint32_t tt_trace_ncache_cap() { return TT_KERNEL_UNIFORM ? 0u : (uint32_t)TT_NCACHE; }
+uint32_t tt_trace_lds_bytes() { return (uint32_t)(TT_LDS_STACK * TT_BLOCK * sizeof(uint2)); }
 uint32_t tt_trace_spill_entries() {
-    return (TT_KERNEL_UNIFORM || TT_LDS_STACK >= TT_STACK_SIZE) ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK);
+    return TT_LDS_STACK >= TT_STACK_SIZE ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK);
 }

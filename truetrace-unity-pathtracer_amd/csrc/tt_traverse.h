@@ -11,23 +11,8 @@
 #ifndef TT_SEGS
 #define TT_SEGS 8         // ray-range segments, one per XCD group (blockIdx % 8), with stealing
 #endif
-#ifndef TT_SDWA_BITS
-#define TT_SDWA_BITS 1    // 1: per-child hit bits with one byte-selecting SDWA shift
-#endif
-#ifndef TT_DEFER_FINISH
-#define TT_DEFER_FINISH 1 // 1: write finished rays' records in batches at refill time
-#endif
-#ifndef TT_TRI_MIN
-#define TT_TRI_MIN 1      // >1: run the triangle pass only when at least this many lanes need it
-#endif
-#ifndef TT_NODE_PK
-#define TT_NODE_PK 0      // 1: node slab fmas as v_pk_fma_f32 pairs (measured ~2% slower on C2)
-#endif
-#ifndef TT_EXACT_TAIL
-#define TT_EXACT_TAIL 0   // 1: exact-size dequeues over the last quarter of each segment (measured: no gain on C2)
-#endif
 #ifndef TT_CHUNK_BIG
-#define TT_CHUNK_BIG 64   // rays per dequeue over the first 3/4 of a segment (then exact)
+#define TT_CHUNK_BIG 64   // rays per dequeue (the surplus waits in the wave's pool)
 #endif
 #ifndef TT_REFILL_MIN
 #define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
@@ -35,17 +20,8 @@
 #ifndef TT_LDS_STACK
 #define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
 #endif
-#ifndef TT_NCACHE
-#define TT_NCACHE 0       // LDS node-cache slots per block (closest-hit kernel; 0: off)
-#endif
-#ifndef TT_NT_IO
-#define TT_NT_IO 0        // bit 0: ray-record loads, bit 1: hit / info stores with the non-temporal hint
-#endif
 #ifndef TT_WAVES_PER_EU
 #define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
-#endif
-#ifndef TT_WRAY_RELOAD
-#define TT_WRAY_RELOAD 0  // 1: re-read the world-space ray from GlobalRays on BLAS exit
 #endif
 #if TT_WAVES_PER_EU > 0
 #define TT_BOUNDS __launch_bounds__(TT_BLOCK, TT_WAVES_PER_EU)
@@ -68,8 +44,6 @@ __device__ __forceinline__ uint32_t octant_inv4(const LaneRay& r) {
            (r.dz < 0.0f ? 0u : 0x01010101u);
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-[[maybe_unused]] __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Node / triangle fetches are raw buffer loads: a 32-bit byte offset per lane (two full-rate
 // shift-adds) instead of a 64-bit address (v_mad_u64_u32), and a bounded descriptor, so an
@@ -100,11 +74,7 @@ __device__ __forceinline__ uint32_t node_offset(uint32_t i) {
 }
 __device__ __forceinline__ uint32_t tri_offset(uint32_t i) {
     uint32_t r;
-#if TT_TRI40
-    asm("v_lshl_add_u32 %0, %1, 2, %1\n\tv_lshlrev_b32 %0, 3, %0" : "=&v"(r) : "v"(i));
-#else
     asm("v_lshl_add_u32 %0, %1, 1, %1\n\tv_lshlrev_b32 %0, 4, %0" : "=&v"(r) : "v"(i));
-#endif
     return r;
 }
 
@@ -138,17 +108,6 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
         const uint32_t z_min = nz ? qhz : qlz, z_max = nz ? qlz : qhz;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-#if TT_NODE_PK
-            // (tmin, tmax) per axis as one v_pk_fma_f32: two IEEE fmas, bitwise the same as fmaf.
-            const f32x2 tx = pk_fma(f32x2{(float)((x_min >> (j * 8)) & 0xffu), (float)((x_max >> (j * 8)) & 0xffu)},
-                                    f32x2{adjx, adjx}, f32x2{orgx, orgx});
-            const f32x2 ty = pk_fma(f32x2{(float)((y_min >> (j * 8)) & 0xffu), (float)((y_max >> (j * 8)) & 0xffu)},
-                                    f32x2{adjy, adjy}, f32x2{orgy, orgy});
-            const f32x2 tz = pk_fma(f32x2{(float)((z_min >> (j * 8)) & 0xffu), (float)((z_max >> (j * 8)) & 0xffu)},
-                                    f32x2{adjz, adjz}, f32x2{orgz, orgz});
-            const float tmin = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 1e-8f));
-            const float tmax = fminf(fminf(tx.y, ty.y), fminf(tz.y, max_distance));
-#else
             const float tminx = fma_((float)((x_min >> (j * 8)) & 0xffu), adjx, orgx);
             const float tminy = fma_((float)((y_min >> (j * 8)) & 0xffu), adjy, orgy);
             const float tminz = fma_((float)((z_min >> (j * 8)) & 0xffu), adjz, orgz);
@@ -157,8 +116,6 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
             const float tmaxz = fma_((float)((z_max >> (j * 8)) & 0xffu), adjz, orgz);
             const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
             const float tmax = fminf(fminf(tmaxx, tmaxy), fminf(tmaxz, max_distance));
-#endif
-#if TT_SDWA_BITS
             // child_bits byte j << bit_index byte j in ONE v_lshlrev_b32_sdwa (both operands byte-selected)
             uint32_t bits;
             if (j == 0)
@@ -173,9 +130,6 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
             else
                 asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3"
                     : "=v"(bits) : "v"(bit_index4), "v"(child_bits4));
-#else
-            const uint32_t bits = ((child_bits4 >> (j * 8)) & 0xffu) << ((bit_index4 >> (j * 8)) & 0xffu);
-#endif
             hit_mask |= (tmin < tmax) ? bits : 0u;
         }
     }
@@ -364,10 +318,8 @@ __device__ __forceinline__ bool intersect_triangle(__amdgpu_buffer_rsrc_t tris, 
 // ------------------------------------------------------------------ ray scheduler
 // The work range is cut into TT_SEGS segments of whole 64-ray tiles; blocks start on segment
 // blockIdx % TT_SEGS (one per XCD under round-robin placement, for L2 locality). A dequeue is ONE
-// returning atomicAdd on the segment's counter (counted in rays). Over the first 3/4 of a
-// segment a wave reserves TT_CHUNK_BIG rays (fewer atomics; the surplus waits in the wave's pool);
-// over the last quarter exactly the lanes it can fill, so no ray waits in a busy wave's pool when
-// the launch drains. A wave whose segment is exhausted probes the others starting at an offset
+// returning atomicAdd on the segment's counter (counted in rays): a wave reserves TT_CHUNK_BIG rays
+// (fewer atomics; the surplus waits in the wave's pool). A wave whose segment is exhausted probes the others starting at an offset
 // derived from its wave id, so thieves spread over all counters instead of converging on one
 // (measured, tools/diag_tl.py: convergent stealing serialised thousands of atomics on one word).
 __device__ __forceinline__ uint32_t seg_lo(uint32_t n_tiles, uint32_t seg) {
@@ -385,7 +337,7 @@ __device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_
         const uint32_t lo = seg_lo(n_tiles, S.seg);
         const uint32_t hi = min(seg_lo(n_tiles, S.seg + 1), n_rays);
         const uint32_t len = hi > lo ? hi - lo : 0u;
-        const uint32_t want = (!TT_EXACT_TAIL || S.est < len - len / 4u) ? max(need, (uint32_t)TT_CHUNK_BIG) : need;
+        const uint32_t want = max(need, (uint32_t)TT_CHUNK_BIG);
         uint32_t off = 0;
         if (lane == 0) off = atomicAdd(&ctl->seg_ticket[S.seg * 32u], want);
         off = __builtin_amdgcn_readfirstlane(off);
@@ -408,31 +360,6 @@ __device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_
         S.est = 0;
     }
     return 0u;
-}
-
-// Streaming accesses of the per-ray records (read or written once per launch): with TT_NT_IO they
-// carry the non-temporal hint so they do not displace BVH nodes / triangles in L2 and MALL.
-__device__ __forceinline__ uint4 io_load16(const uint4* p) {
-#if TT_NT_IO & 1
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ void io_store16(uint4* p, uint4 v) {
-#if TT_NT_IO & 2
-    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
-#else
-    *p = v;
-#endif
-}
-__device__ __forceinline__ float io_loadf(const float* p) {
-#if TT_NT_IO & 1
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
 }
 
 // Zeroes the next launch's control block (block 0; plain stores, no fence: the kernel boundary

@@ -22,7 +22,7 @@
 #endif
 // G = 2 lanes per ray: more than 32 live rays do not fit a wave (measured: 48 gives wrong hits)
 static_assert(TT_WIDE_ENTER >= 1 && TT_WIDE_ENTER <= 32, "TT_WIDE_ENTER must be in [1, 32]");
-#if defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST) || TT_WRAY_RELOAD
+#if defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST)
 #undef TT_WIDE
 #define TT_WIDE 0
 #endif
