@@ -384,6 +384,10 @@ tt_status tt_selftest_rcp(tt_ctx* ctx, uint64_t* mismatches);
 
 /* Wait for all work issued on the context's stream. */
 tt_status tt_sync(tt_ctx* ctx);
+/* Stack overflows (rays that would have pushed a 17th entry and were dropped) of every trace and
+ * any-hit launch since the previous call, TT_TRACE_ASYNC launches included: synchronizes, writes
+ * the count (nullable) and resets it. Returns TT_ERR_STACK_OVERFLOW when it is non-zero. */
+tt_status tt_async_overflows(tt_ctx* ctx, uint64_t* count);
 /* The hipStream_t the context issues on. */
 void* tt_ctx_stream(tt_ctx* ctx);
 

@@ -34,6 +34,8 @@ def lib(prefer_v3: bool = True):
     if _LIB is None:
         d = os.path.join(REPO, "oracle")
         path = os.path.join(d, "libtt_oracle_v3.so") if prefer_v3 and _cpu_has_v3() else os.path.join(d, "libtt_oracle.so")
+        if os.environ.get("TT_ORACLE_LIB"):  # e.g. the AddressSanitizer build (tests/test_native.py)
+            path = os.environ["TT_ORACLE_LIB"]
         if not os.path.exists(path):
             path = os.path.join(d, "libtt_oracle.so")
         if not os.path.exists(path):

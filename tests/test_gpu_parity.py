@@ -897,3 +897,19 @@ def test_visibility_check_mode(engine, seed):
     v2 = np.zeros((n, 4), np.float32)
     engine.trace_shadow(neg, n, 0, W, H, visibility=v2, flags=tthip.TT_SHADOW_VISIBILITY_CHECK)
     assert (v2[:, 0] == 1.0).all()
+
+
+def test_async_chain_stack_overflow_is_reported(engine):
+    """an overflow inside a TT_TRACE_ASYNC chain must not be lost when a later launch
+    zeroes the control block it was counted in: tt_async_overflows reports every launch's."""
+    import torch
+
+    sc, rays = K.stack_overflow_scene(17)
+    engine.upload(sc)
+    engine.async_overflows()  # clear what earlier tests on the shared context left
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(rays.view(np.uint8).copy()).to(dev)
+    for _ in range(3):  # three async launches: each overflows one ray; later launches zero the blocks
+        engine.trace(buf, 1, 0, FAR, 1, 1, device=True, asynchronous=True)
+    assert engine.async_overflows() == 3
+    assert engine.async_overflows() == 0  # reset by the read

@@ -84,6 +84,7 @@ struct tt_ctx {
     uint32_t grid_of[12] = {};  // resident persistent grid per kernel instantiation
     uint32_t shadow_grid_of[4] = {};  // the same for the any-hit kernel (stats * 2 + matcheck)
     TraceControl* ctl = nullptr;  // two control blocks: a trace launch uses one and zeroes the other
+    uint32_t* sticky = nullptr;   // stack overflows of every launch since the last tt_async_overflows
     uint32_t ctl_cur = 0;          // the block the next launch uses
     bool ctl_zero[2] = {false, false};  // known zero when the next launch on the stream runs
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
@@ -474,9 +475,15 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     for (int k = 0; k < 12; k++) max_grid = std::max(max_grid, c->grid_of[k]);
     for (int k = 0; k < 4; k++) max_grid = std::max(max_grid, c->shadow_grid_of[k]);
     c->spill_threads = max_grid * tt_trace_block_size();
-    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), 2 * sizeof(TraceControl)) != hipSuccess) {
+    // two control blocks + the sticky overflow counter behind them
+    if (hipMalloc(reinterpret_cast<void**>(&c->ctl), 2 * sizeof(TraceControl) + 256) != hipSuccess) {
         tt_ctx_destroy(c);
         return TT_ERR_OOM;
+    }
+    c->sticky = reinterpret_cast<uint32_t*>(c->ctl + 2);
+    if (hipMemset(c->ctl, 0, 2 * sizeof(TraceControl) + 256) != hipSuccess) {
+        tt_ctx_destroy(c);
+        return TT_ERR_HIP;
     }
     for (uint32_t i = 0; i < TT_RING; i++) {
         if (hipEventCreate(&c->ring0[i]) != hipSuccess || hipEventCreate(&c->ring1[i]) != hipSuccess) {
@@ -593,6 +600,17 @@ tt_status tt_selftest_rcp(tt_ctx* c, uint64_t* mismatches) {
 }
 
 void* tt_ctx_stream(tt_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+tt_status tt_async_overflows(tt_ctx* c, uint64_t* count) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    uint32_t n = 0;
+    TT_HIP(c, hipMemcpy(&n, c->sticky, sizeof(n), hipMemcpyDeviceToHost));
+    TT_HIP(c, hipMemset(c->sticky, 0, sizeof(n)));
+    if (count) *count = n;
+    if (n) return fail(c, TT_ERR_STACK_OVERFLOW, "%u rays needed more than %d traversal stack entries", n, TT_STACK_SIZE);
+    return TT_OK;
+}
 
 tt_status tt_sync(tt_ctx* c) {
     if (!c) return TT_ERR_INVALID_ARG;
@@ -986,6 +1004,7 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const uint32_t ci = c->ctl_cur;
     a.ctl = c->ctl + ci;
     a.ctl_next = c->ctl + (ci ^ 1u);
+    a.sticky_overflow = c->sticky;
     a.spill = c->spill.p;
 #if defined(TT_DIAG_TIMES) || defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST) || \
     defined(TT_DIAG_BLOCKS) || defined(TT_DIAG_SOLO)
@@ -1146,6 +1165,7 @@ tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     a.nee_pos = d_nee;
     a.cache = d_cache;
     a.ctl = c->ctl + c->ctl_cur;
+    a.sticky_overflow = c->sticky;
     a.spill = c->spill.p;
     a.n_rays = p->n_rays;
     a.width = p->screen_width;

@@ -109,22 +109,16 @@ struct MatView {
     uint32_t tex_w, tex_h;
 };
 
-// Exact unsigned division by a launch-constant divisor (round-up multiplier, valid for every
-// 32-bit n and d >= 1): q = (t + ((n - t) >> s1)) >> s2 with t = umulhi(m, n). The host fills it
-// (fastdiv_make); replaces the ~40-instruction VALU udiv in the refill and pixel decode.
-struct FastDiv {
-    uint32_t m, s1, s2;
-};
-__host__ inline FastDiv fastdiv_make(uint32_t d) {
-    uint32_t l = 0;
-    while (l < 32 && (1ull << l) < d) l++;
-    const unsigned __int128 m = (((unsigned __int128)1 << 32) * (((unsigned __int128)1 << l) - d)) / d + 1u;
-    return FastDiv{(uint32_t)m, l < 1 ? l : 1u, l > 1 ? l - 1 : 0u};
-}
-__device__ __forceinline__ uint32_t fastdiv(uint32_t n, const FastDiv& d) {
-    const uint32_t t = __umulhi(d.m, n);
-    return (t + ((n - t) >> d.s1)) >> d.s2;
-}
+#include "tt_fastdiv.h"
+
+// A ray that overflows the 16-entry stack: counted in the launch's control block (reported by
+// synchronous calls) and in the context's sticky counter (tt_async_overflows), which launches never
+// reset, so overflows inside TT_TRACE_ASYNC chains are not lost when a later launch zeroes the block.
+#define TT_REPORT_OVERFLOW(A)                          \
+    do {                                               \
+        atomicAdd(&(A).ctl->err_overflow, 1u);         \
+        if ((A).sticky_overflow) atomicAdd((A).sticky_overflow, 1u); \
+    } while (0)
 
 struct TraceArgs {
     const uint4* nodes;          // 80 B nodes as 5 x uint4
@@ -141,6 +135,7 @@ struct TraceArgs {
     uint32_t* info;              // _PrimaryTriangleInfo (uint4 per pixel), nullable
     const tt_col_data* colors;   // GlobalColors (bounce > 0 with info)
     TraceControl* ctl;
+    uint32_t* sticky_overflow;   // stack overflows since the last tt_async_overflows (never reset by launches)
     uint2* spill;                // traversal-stack entries beyond TT_LDS_STACK, [entry][thread]
     unsigned long long* diag_times;  // TT_DIAG_TIMES builds: per wave (start, end, rays)
     uint32_t n_rays;
@@ -173,6 +168,7 @@ struct ShadowArgs {
     float4* nee_pos;             // nullable, NEEPosA (bounce 0)
     tt_cache_data* cache;        // nullable, CacheBuffer (TT_SHADOW_RADIANCE_CACHE)
     TraceControl* ctl;
+    uint32_t* sticky_overflow;
     uint2* spill;
     uint32_t n_rays;
     uint32_t width, height;

@@ -194,7 +194,7 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
                     st.active = false;
                     if (sub == 0u) {
                         if (STATS) C.ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
+                        TT_REPORT_OVERFLOW(A);
                     }
                 }
             } else {  // :404-407
@@ -234,7 +234,7 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
                     st.active = false;
                     if (sub == 0u) {
                         if (STATS) C.ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
+                        TT_REPORT_OVERFLOW(A);
                     }
                 }
                 st.tg.y = 0u;
@@ -466,7 +466,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 } else {
                     active = false;
                     if (STATS) c_ovf++;
-                    atomicAdd(&A.ctl->err_overflow, 1u);
+                    TT_REPORT_OVERFLOW(A);
                 }
             } else {  // :404-407
                 tg = cg;
@@ -503,7 +503,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 } else {
                     active = false;
                     if (STATS) c_ovf++;
-                    atomicAdd(&A.ctl->err_overflow, 1u);
+                    TT_REPORT_OVERFLOW(A);
                 }
                 tg.y = 0u;
             }

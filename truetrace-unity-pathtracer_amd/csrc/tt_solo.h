@@ -145,7 +145,7 @@ __device__ void solo_run(const TraceArgs& A, WideState st, uint2 stk, __amdgpu_b
                     if (st.stack_size == TT_STACK_SIZE) {
                         if (lead) {
                             if (STATS) C.ovf++;
-                            atomicAdd(&A.ctl->err_overflow, 1u);
+                            TT_REPORT_OVERFLOW(A);
                         }
                         break;
                     }
@@ -193,7 +193,7 @@ __device__ void solo_run(const TraceArgs& A, WideState st, uint2 stk, __amdgpu_b
                 if (st.stack_size + need > TT_STACK_SIZE) {
                     if (lead) {
                         if (STATS) C.ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
+                        TT_REPORT_OVERFLOW(A);
                     }
                     break;
                 }

@@ -308,7 +308,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 } else {
                     active = false;
                     if (STATS) c_ovf++;
-                    atomicAdd(&A.ctl->err_overflow, 1u);
+                    TT_REPORT_OVERFLOW(A);
                 }
             } else {  // :188-191
                 tg = cg;
@@ -348,7 +348,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 } else {
                     active = false;
                     if (STATS) c_ovf++;
-                    atomicAdd(&A.ctl->err_overflow, 1u);
+                    TT_REPORT_OVERFLOW(A);
                 }
                 tg.y = 0u;
             }

@@ -247,7 +247,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
                     st.active = false;
                     if (sub == 0u) {
                         if (STATS) C.ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
+                        TT_REPORT_OVERFLOW(A);
                     }
                 }
             } else {  // :188-191
@@ -288,7 +288,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
                     st.active = false;
                     if (sub == 0u) {
                         if (STATS) C.ovf++;
-                        atomicAdd(&A.ctl->err_overflow, 1u);
+                        TT_REPORT_OVERFLOW(A);
                     }
                 }
                 st.tg.y = 0u;

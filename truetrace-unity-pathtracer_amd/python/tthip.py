@@ -268,6 +268,7 @@ def hip_lib():
         L.tt_scene_read_tris.argtypes = [vp, u32, u32, vp]
         L.tt_blas_refit.argtypes = [vp, C.POINTER(BlasRefitParams), vp, vp, vp]
         L.tt_sync.argtypes = [vp]
+        L.tt_async_overflows.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
         L.tt_resolve_normals.argtypes = [vp, C.POINTER(TraceParams), vp, vp]
@@ -628,6 +629,14 @@ class Engine:
 
     def sync(self):
         self._check(self.L.tt_sync(self.h), "tt_sync")
+
+    def async_overflows(self) -> int:
+        """tt_async_overflows: stack overflows of all launches since the last call (then reset)."""
+        n = C.c_uint64()
+        st = self.L.tt_async_overflows(self.h, C.byref(n))
+        if st not in (TT_OK, TT_ERR_STACK_OVERFLOW):
+            self._check(st, "tt_async_overflows")
+        return int(n.value)
 
     def timing_reset(self):
         self._check(self.L.tt_timing_reset(self.h), "tt_timing_reset")
