@@ -19,7 +19,11 @@ namespace TrueTrace.Hip
     [Flags]
     public enum TTTraceFlags : uint
     {
-        None = 0, DevicePtrs = 1u << 0, UseReSTIRGI = 1u << 1, UseASVGF = 1u << 2, Stats = 1u << 3, Async = 1u << 4
+        None = 0, DevicePtrs = 1u << 0, UseReSTIRGI = 1u << 1, UseASVGF = 1u << 2, Stats = 1u << 3, Async = 1u << 4,
+        IgnoreGlass = 1u << 5,       // IgnoreGlassMain  (IntersectionKernels.compute:42-44)
+        IgnoreBackfacing = 1u << 6,  // IgnoreBackfacing (IntersectionKernels.compute:45-47)
+        RadianceCache = 1u << 7,     // tt_trace_shadow_ex: the RadianceCache define (GlobalDefines.cginc:15)
+        VisibilityCheck = 1u << 8    // tt_trace_shadow_ex: VisabilityCheckCompute (CommonData.cginc:710-819)
     }
 
     [StructLayout(LayoutKind.Sequential)]
@@ -96,6 +100,17 @@ namespace TrueTrace.Hip
         // GlobalColors (ColData, 64 B), NEEPosA (float4 per pixel); the last three nullable.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_shadow(IntPtr ctx, ref TTShadowParams p,
             void* shadowRays, float* visibility, void* globalColors, float* neePos, out TTStats stats);
+        // + CacheBuffer (PropogatedCacheData, 48 B per pixel, nullable): the full :457-485 output contract.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_shadow_ex(IntPtr ctx, ref TTShadowParams p,
+            void* shadowRays, float* visibility, void* globalColors, float* neePos, void* cacheBuffer, out TTStats stats);
+        // Device-pointer forms: the same entry points, the buffers passed as HIP device addresses.
+        [DllImport(Lib, EntryPoint = "tt_trace_closest")] public static extern TTStatus tt_trace_closest_dev(IntPtr ctx,
+            ref TTTraceParams p, IntPtr globalRays, IntPtr primaryInfo, IntPtr globalColors, out TTStats stats);
+        [DllImport(Lib, EntryPoint = "tt_trace_shadow_ex")] public static extern TTStatus tt_trace_shadow_dev(IntPtr ctx,
+            ref TTShadowParams p, IntPtr shadowRays, IntPtr visibility, IntPtr globalColors, IntPtr neePos,
+            IntPtr cacheBuffer, out TTStats stats);
+        [DllImport(Lib)] public static extern TTStatus tt_async_overflows(IntPtr ctx, out ulong count);
+        [DllImport(Lib)] public static extern IntPtr tt_ctx_stream(IntPtr ctx);
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload_alpha_atlas(IntPtr ctx, byte* texels,
             uint width, uint height);
@@ -119,11 +134,15 @@ namespace TrueTrace.Hip
     {
         IntPtr m_ctx;
 
-        public TrueTraceHipTracer(int device, ulong maxRays)
+        /// `hipStream`: the hipStream_t to issue on (IntPtr.Zero: a library-owned stream).
+        public TrueTraceHipTracer(int device, ulong maxRays, IntPtr hipStream = default)
         {
-            var cfg = new TTConfig { device = device, flags = 0, maxRays = maxRays, stream = IntPtr.Zero };
+            var cfg = new TTConfig { device = device, flags = 0, maxRays = maxRays, stream = hipStream };
             Check(Native.tt_ctx_create(ref cfg, out m_ctx));
         }
+
+        /// The hipStream_t the engine issues on (for ordering the caller's own HIP work around it).
+        public IntPtr Stream => Native.tt_ctx_stream(m_ctx);
 
         /// AssetManager.SetMeshTraceBuffers: the same arrays the AssetManager uploads with
         /// ComputeBuffer.SetData (AssetManager.cs:1760, :1762; ParentObject.cs:270-271).
@@ -154,19 +173,61 @@ namespace TrueTrace.Hip
             return s;
         }
 
-        /// One kernel_shadow dispatch (IntersectionKernels.compute:264-505) for bounce `curBounce`.
-        public unsafe TTStats TraceShadow<TShadow, TCol>(TShadow[] shadowRays, uint nRays, int curBounce, int width,
-                                                         int height, float[] visibility = null,
-                                                         TCol[] globalColors = null, float[] neePos = null)
-            where TShadow : unmanaged where TCol : unmanaged
+        /// One kernel_trace dispatch on buffers that already live in HIP device memory (a HIP-resident
+        /// wavefront): no PCIe round trip of the 2*W*H RayData buffer. `async` returns without waiting
+        /// (stack overflows of async launches: AsyncOverflows()).
+        public TTStats TraceDevice(IntPtr globalRays, uint nRays, int curBounce, float farPlane, int width, int height,
+                                   IntPtr primaryInfo = default, IntPtr globalColors = default,
+                                   TTTraceFlags extra = TTTraceFlags.None, bool async = false)
+        {
+            var p = new TTTraceParams
+            {
+                nRays = nRays, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width, screenHeight = (uint)height,
+                flags = extra | TTTraceFlags.DevicePtrs | (async ? TTTraceFlags.Async : 0)
+            };
+            Check(Native.tt_trace_closest_dev(m_ctx, ref p, globalRays, primaryInfo, globalColors, out TTStats s));
+            return s;
+        }
+
+        /// One kernel_shadow dispatch (IntersectionKernels.compute:264-505) for bounce `curBounce`;
+        /// `cacheBuffer` (PropogatedCacheData per pixel) and `flags` (RadianceCache, VisibilityCheck,
+        /// UseReSTIRGI) select the :457-485 accumulations of the reference's define set.
+        public unsafe TTStats TraceShadow<TShadow, TCol, TCache>(TShadow[] shadowRays, uint nRays, int curBounce, int width,
+                                                                 int height, float[] visibility = null,
+                                                                 TCol[] globalColors = null, float[] neePos = null,
+                                                                 TCache[] cacheBuffer = null,
+                                                                 TTTraceFlags flags = TTTraceFlags.RadianceCache)
+            where TShadow : unmanaged where TCol : unmanaged where TCache : unmanaged
         {
             var p = new TTShadowParams { nRays = nRays, bounce = curBounce, screenWidth = (uint)width,
-                                         screenHeight = (uint)height, flags = 0 };
+                                         screenHeight = (uint)height, flags = flags };
             TTStats s;
             fixed (TShadow* r = shadowRays) fixed (float* vis = visibility) fixed (TCol* col = globalColors)
-            fixed (float* nee = neePos)
-                Check(Native.tt_trace_shadow(m_ctx, ref p, r, vis, col, nee, out s));
+            fixed (float* nee = neePos) fixed (TCache* cache = cacheBuffer)
+                Check(Native.tt_trace_shadow_ex(m_ctx, ref p, r, vis, col, nee, cache, out s));
             return s;
+        }
+
+        /// TraceShadow on HIP device buffers (no host round trip).
+        public TTStats TraceShadowDevice(IntPtr shadowRays, uint nRays, int curBounce, int width, int height,
+                                         IntPtr visibility = default, IntPtr globalColors = default, IntPtr neePos = default,
+                                         IntPtr cacheBuffer = default, TTTraceFlags flags = TTTraceFlags.RadianceCache,
+                                         bool async = false)
+        {
+            var p = new TTShadowParams { nRays = nRays, bounce = curBounce, screenWidth = (uint)width,
+                                         screenHeight = (uint)height,
+                                         flags = flags | TTTraceFlags.DevicePtrs | (async ? TTTraceFlags.Async : 0) };
+            Check(Native.tt_trace_shadow_dev(m_ctx, ref p, shadowRays, visibility, globalColors, neePos, cacheBuffer,
+                                             out TTStats s));
+            return s;
+        }
+
+        /// Stack overflows of every launch since the last call (TT_TRACE_ASYNC chains included).
+        public ulong AsyncOverflows()
+        {
+            var st = Native.tt_async_overflows(m_ctx, out ulong n);
+            if (st != TTStatus.StackOverflow) Check(st);
+            return n;
         }
 
         /// The _AlphaAtlas binding of SetMeshTraceBuffers (AssetManager.cs:75-88): R8 texels, once

@@ -1,0 +1,33 @@
+"""The C# P/Invoke binding (bindings/csharp/TrueTraceHip.cs) is shipped but cannot be compiled
+here (no .NET runtime in the image or on the GPU box). What can be checked without it: every
+[DllImport] entry point is exported by the built library, and the binding's flag values equal the
+header's."""
+import os
+import re
+
+import tthip
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CS = open(os.path.join(REPO, "bindings", "csharp", "TrueTraceHip.cs")).read()
+HDR = open(os.path.join(REPO, "include", "truetrace_hip.h")).read()
+
+
+def test_every_dllimport_is_exported():
+    L = tthip.hip_lib()
+    names = set()
+    for m in re.finditer(r'\[DllImport\(Lib(?:,\s*EntryPoint\s*=\s*"(\w+)")?\)\][^;]*?\bextern\b[^(]*?\b(\w+)\s*\(', CS, re.S):
+        names.add(m.group(1) or m.group(2))
+    assert len(names) >= 18, names
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_flag_values_match_header():
+    cs = {k: int(v) for k, v in re.findall(r"(\w+)\s*=\s*1u\s*<<\s*(\d+)", CS)}
+    hdr = {k: int(v) for k, v in re.findall(r"(TT_(?:TRACE|SHADOW)_\w+)\s*=\s*1u\s*<<\s*(\d+)", HDR)}
+    pairs = {"DevicePtrs": "TT_TRACE_DEVICE_PTRS", "UseReSTIRGI": "TT_TRACE_USE_RESTIRGI",
+             "UseASVGF": "TT_TRACE_USE_ASVGF", "Stats": "TT_TRACE_STATS", "Async": "TT_TRACE_ASYNC",
+             "IgnoreGlass": "TT_TRACE_IGNORE_GLASS", "IgnoreBackfacing": "TT_TRACE_IGNORE_BACKFACING",
+             "RadianceCache": "TT_SHADOW_RADIANCE_CACHE", "VisibilityCheck": "TT_SHADOW_VISIBILITY_CHECK"}
+    for c, h in pairs.items():
+        assert cs[c] == hdr[h], (c, h)
