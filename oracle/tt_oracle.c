@@ -1158,6 +1158,124 @@ tt_status tt_oracle_generate(const float* c2w, const float* ip, uint32_t width, 
     return TT_OK;
 }
 
+/* ------------------------------------------------------------ diffuse bounce enqueue (f2) */
+/* kernel_shade's diffuse path and next-ray append (RayTracingShader.compute:52-84 sample_disc /
+ * sample_cosine_weighted_direction / sample, :99-122 normals, :284 direction, :293 origin offset,
+ * :498-506 append). The reference appends with InterlockedAdd, so its order is the atomics'
+ * order; the library appends in source order (stable compaction) and so does this restatement.
+ * sincos is pinned (HLSL leaves its precision to the driver): cephes minimax polynomials on
+ * [-pi/4, pi/4] with explicit fmaf, |phi| > pi/4 reduced by pi/2 (two-constant Cody-Waite). */
+void tt_oracle_sincos_pinned(float phi, float* s, float* c) {
+    const int big = fabsf(phi) > 0.785398185253143310546875f;
+    const float q = phi > 0.0f ? 1.0f : -1.0f;
+    const float r = big ? fmaf(-q, -4.37113882867379e-8f, fmaf(-q, 1.57079637050628662109375f, phi)) : phi;
+    const float z = r * r;
+    const float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
+    const float cp = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f),
+                               z, -0.5f), z, 1.0f);
+    *s = big ? q * cp : sp;
+    *c = big ? -q * sp : cp;
+}
+/* octahedral_32 — CommonData.cginc:840-846 (the shading-side encoder; round = round-half-even) */
+static uint32_t octahedral_32_cd(v3 nor) {
+    const float sx = nor.x >= 0.0f ? 1.0f : -1.0f, sy = nor.y >= 0.0f ? 1.0f : -1.0f;
+    const float den = nor.x * sx + nor.y * sy + fabsf(nor.z);
+    float x = nor.x / den, y = nor.y / den;
+    if (!(nor.z >= 0.0f)) {
+        const float ox = x;
+        x = (1.0f - (y * sy)) * sx;
+        y = (1.0f - (ox * sx)) * sy;
+    }
+    const uint32_t dx = (uint32_t)rintf(32767.5f + x * 32767.5f), dy = (uint32_t)rintf(32767.5f + y * 32767.5f);
+    return dx | (dy << 16u);
+}
+
+tt_status tt_oracle_enqueue_diffuse_bounce(const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* meshdata,
+                                           uint32_t n_mesh, const tt_trace_params* p, tt_ray_data* global_rays,
+                                           int32_t frames, int32_t max_bounce, uint32_t* n_next) {
+    if (!tris || !meshdata || !p || !global_rays || !n_next) return TT_ERR_INVALID_ARG;
+    const uint32_t wh = p->screen_width * p->screen_height;
+    if (!wh || p->n_rays > wh) return TT_ERR_INVALID_ARG;
+    const uint32_t src = (p->bounce % 2 == 1) ? wh : 0u, dst = (p->bounce % 2 == 1) ? 0u : wh;
+    uint32_t out = 0;
+    for (uint32_t i = 0; i < p->n_rays; i++) {
+        const tt_ray_data* R = &global_rays[src + i];
+        const float t = asfloat(R->hits[2]);
+        if (!(t < p->far_plane) || (int32_t)R->hits[1] < 0) continue;
+        const int32_t mesh_id = (int32_t)R->hits[0], tri = (int32_t)R->hits[1];
+        if ((uint32_t)tri >= n_tris || (uint32_t)mesh_id >= n_mesh) return TT_ERR_INVALID_ARG;
+        /* sample(pdf, pixel_index): random(1, pixel_index), sample_disc, cosine lobe */
+        float rx, ry;
+        random2(1, R->PixelIndex, frames, max_bounce, p->bounce, &rx, &ry);
+        float a = 2.0f * rx - 1.0f, b = 2.0f * ry - 1.0f;
+        if (a == 0.0f) a = 0.00001f;
+        if (b == 0.0f) b = 0.00001f;
+        float phi, rr;
+        if (a * a > b * b) {
+            rr = a;
+            phi = (0.25f * 3.14159265f) * (b / a);
+        } else {
+            rr = b;
+            phi = (0.25f * 3.14159265f) * (a / b) + (0.5f * 3.14159265f);
+        }
+        float sp, cp;
+        tt_oracle_sincos_pinned(phi, &sp, &cp);
+        const float dx = rr * cp, dz = rr * sp;
+        const v3 om = mk(dx, sqrtf(fabsf(1.0f - (dx * dx + dz * dz))), dz);
+        const float pdf = om.y * 0.318309886548f;
+        if (!(pdf > 0.0f)) continue; /* validBSDFSample */
+        /* get() and the hit point */
+        const float u = (float)(R->hits[3] & 0xffffu) / 65535.0f, v = (float)(R->hits[3] >> 16) / 65535.0f;
+        const float* W = meshdata[mesh_id].W2L;
+        const tt_cuda_triangle* T = &tris[tri];
+        const v3 dir = ld3(R->direction), org = ld3(R->origin);
+        const v3 pos = mk(dir.x * t + org.x, dir.y * t + org.y, dir.z * t + org.z);
+        /* Geomnorm = GetTriangleNormal(..., Inverse) (CommonData.cginc:904-911), normalize pinned */
+        const v3 n0 = i_octahedral_32(T->norms[0]), n1 = i_octahedral_32(T->norms[1]),
+                 n2 = i_octahedral_32(T->norms[2]);
+        const float w0 = 1.0f - u - v;
+        const v3 ni = mk(n0.x * w0 + u * n1.x + v * n2.x, n0.y * w0 + u * n1.y + v * n2.y,
+                         n0.z * w0 + u * n1.z + v * n2.z);
+        v3 g = vnormalize(mk(fmaf(M(W, 2, 0), ni.z, fmaf(M(W, 1, 0), ni.y, M(W, 0, 0) * ni.x)),
+                             fmaf(M(W, 2, 1), ni.z, fmaf(M(W, 1, 1), ni.y, M(W, 0, 1) * ni.x)),
+                             fmaf(M(W, 2, 2), ni.z, fmaf(M(W, 1, 2), ni.y, M(W, 0, 2) * ni.x))));
+        /* USGNorm = -normalize(mul(Inverse, cross(normalize(e1), normalize(e2)))) (:112-115) */
+        const v3 c = vcross(vnormalize(ld3(T->posedge1)), vnormalize(ld3(T->posedge2)));
+        v3 us = vnormalize(mk(fmaf(M(W, 2, 0), c.z, fmaf(M(W, 1, 0), c.y, M(W, 0, 0) * c.x)),
+                              fmaf(M(W, 2, 1), c.z, fmaf(M(W, 1, 1), c.y, M(W, 0, 1) * c.x)),
+                              fmaf(M(W, 2, 2), c.z, fmaf(M(W, 1, 2), c.y, M(W, 0, 2) * c.x))));
+        us = mk(-us.x, -us.y, -us.z);
+        if (vdot(us, g) < 0) us = mk(-us.x, -us.y, -us.z);
+        if (vdot(dir, us) > 0.0f) { /* GotFlipped (:120-121) */
+            us = mk(-us.x, -us.y, -us.z);
+            g = mk(-g.x, -g.y, -g.z);
+        }
+        const v3 norm = i_octahedral_32(octahedral_32_cd(g)); /* :123-124 */
+        /* ray.direction = normalize(mul(omega_o, GetTangentSpace(norm))) (CommonData.cginc:332-343) */
+        const v3 helper = fabsf(norm.x) > 0.99f ? mk(0, 0, 1) : mk(1, 0, 0);
+        const v3 tangent = vnormalize(vcross(norm, helper));
+        const v3 binormal = vcross(norm, tangent);
+        const v3 nd = vnormalize(mk(om.x * tangent.x + om.y * norm.x + om.z * binormal.x,
+                                    om.x * tangent.y + om.y * norm.y + om.z * binormal.y,
+                                    om.x * tangent.z + om.y * norm.z + om.z * binormal.z));
+        /* append (:502-504): origin = USGNorm * NormalOffset + pos, pdf, set2(hit) */
+        tt_ray_data* o = &global_rays[dst + out];
+        const tt_ray_data src_ray = *R; /* dst never overlaps src (the other half) */
+        o->origin[0] = us.x * 0.0001f + pos.x;
+        o->origin[1] = us.y * 0.0001f + pos.y;
+        o->origin[2] = us.z * 0.0001f + pos.z;
+        o->PixelIndex = src_ray.PixelIndex;
+        o->direction[0] = nd.x;
+        o->direction[1] = nd.y;
+        o->direction[2] = nd.z;
+        o->last_pdf = pdf;
+        for (int k = 0; k < 4; k++) o->hits[k] = src_ray.hits[k];
+        out++;
+    }
+    *n_next = out;
+    return TT_OK;
+}
+
 int32_t tt_oracle_hardware_threads(void) {
     const long n = sysconf(_SC_NPROCESSORS_ONLN);
     return n > 0 ? (int32_t)n : 1;

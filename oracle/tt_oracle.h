@@ -73,6 +73,13 @@ tt_status tt_oracle_generate(const float* cam_to_world, const float* cam_inv_pro
                              float far_plane, int32_t jitter, int32_t frames_accumulated,
                              int32_t max_bounce, tt_ray_data* global_rays);
 
+/* Diffuse-bounce enqueue (RayTracingShader.compute:52-84, 99-124, 284, 293, 498-506): the survivors
+ * of rays [0, n_rays) of the bounce's half, appended in source order to the other half. */
+tt_status tt_oracle_enqueue_diffuse_bounce(const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* meshdata,
+                                           uint32_t n_mesh, const tt_trace_params* p, tt_ray_data* global_rays,
+                                           int32_t frames, int32_t max_bounce, uint32_t* n_next);
+/* The pinned sincos of the cosine-lobe sample (both sides evaluate exactly this). */
+void tt_oracle_sincos_pinned(float phi, float* s, float* c);
 int32_t tt_oracle_hardware_threads(void);
 /* The pinned row-f1 encoders (CommonData.cginc:479-509, :1576-1619) and HLSL pow, for tests. */
 uint32_t tt_oracle_pack_rgbe(const float v[3]);

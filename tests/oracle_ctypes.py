@@ -50,6 +50,11 @@ def lib(prefer_v3: bool = True):
         L.tt_oracle_generate.argtypes = [vp, vp, u32, u32, C.c_float, C.c_float, i32, i32, i32, vp]
         L.tt_oracle_generate.restype = i32
         L.tt_oracle_hardware_threads.restype = i32
+        L.tt_oracle_enqueue_diffuse_bounce.argtypes = [vp, u32, vp, u32, C.POINTER(tthip.TraceParams), vp, i32, i32,
+                                                       C.POINTER(u32)]
+        L.tt_oracle_enqueue_diffuse_bounce.restype = i32
+        L.tt_oracle_sincos_pinned.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.tt_oracle_sincos_pinned.restype = None
         L.tt_oracle_shadow.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, C.POINTER(tthip.ShadowParams), vp,
                                        vp, vp, vp, vp, vp, i32]
         for name in ("tt_oracle_pack_rgbe", "tt_oracle_encode_rgb"):
@@ -186,6 +191,26 @@ def generate(cam_to_world, cam_inv_proj, width, height, near, far, jitter=0, fra
                               max_bounce, rays.ctypes.data)
     assert st == 0
     return rays
+
+
+def enqueue_bounce(scene, rays, n_rays, bounce, far_plane, width, height, frames=0, max_bounce=3):
+    """Oracle diffuse-bounce enqueue in place on `rays` (2*W*H RayData); returns the survivor count."""
+    L = lib()
+    p = tthip.TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width,
+                          screen_height=height, flags=0)
+    n = C.c_uint32()
+    st = L.tt_oracle_enqueue_diffuse_bounce(scene.tris.ctypes.data, len(scene.tris), scene.meshdata.ctypes.data,
+                                            len(scene.meshdata), C.byref(p), rays.ctypes.data, frames, max_bounce,
+                                            C.byref(n))
+    assert st == 0, st
+    return n.value
+
+
+def sincos_pinned(phi):
+    L = lib()
+    s, c = C.c_float(), C.c_float()
+    L.tt_oracle_sincos_pinned(float(phi), C.byref(s), C.byref(c))
+    return s.value, c.value
 
 
 def tlas_refit(scene: "tthip.Scene", mesh_aabbs: np.ndarray, n_tlas_nodes=None):

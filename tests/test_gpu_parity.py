@@ -285,15 +285,39 @@ def test_bounce_enqueue_compaction(engine):
     engine.upload(sc)
     r = g["rays0"].copy()
     engine.trace(r, W * H, 0, FAR, W, H)
+    ref = r.copy()
     nb = engine.enqueue_bounce(r, W * H, 0, FAR, W, H)
     hit = r["hits"][: W * H, 1] != 0xFFFFFFFF
     assert nb == hit.sum()
     out = r[W * H:W * H + nb]
-    assert sorted(out["PixelIndex"].tolist()) == sorted(r["PixelIndex"][: W * H][hit].tolist())
+    # stable compaction: bit-identical to the oracle's source-order restatement
+    assert O.enqueue_bounce(sc, ref, W * H, 0, FAR, W, H) == nb
+    assert np.array_equal(out.view(np.uint32), ref[W * H:W * H + nb].view(np.uint32))
     assert np.allclose(np.linalg.norm(out["direction"], axis=1), 1.0, atol=1e-5)
     # the compacted bounce rays trace identically on both sides
     rg, rc, ig, ic, _, _ = trace_both(engine, sc, r, nb, 1, W, H, info=False)
     assert_same(rg, rc, ig, ic, W * H, nb)
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 1023, 4095, 4096, 4097, 70001])
+def test_bounce_enqueue_ragged_and_odd_bounce(engine, n):
+    """Tile edges of the look-back scan (4096 rays per tile, 64-tile look-back window) and the odd-bounce
+    direction (second half -> first half), bit-exact against the oracle."""
+    W, H = 400, 300
+    sc = tthip.single_object_scene(tthip.Mesh.soup(7, 3000))
+    engine.upload(sc)
+    c2w, ip = tthip.unity_camera((0.2, 0.1, 3.0), (0, 0, -1), (0, 1, 0), 50, W, H, 0.3, FAR)
+    r = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+    engine.generate(r, c2w, ip, W, H, 0.3, FAR, jitter=1, frames=5, max_bounce=4)
+    engine.trace(r, W * H, 0, FAR, W, H)
+    nb = engine.enqueue_bounce(r, W * H, 0, FAR, W, H, frames=5, max_bounce=4)
+    engine.trace(r, nb, 1, FAR, W, H)
+    m = min(n, nb)
+    ref = r.copy()
+    n2 = engine.enqueue_bounce(r, m, 1, FAR, W, H, frames=5, max_bounce=4)
+    assert O.enqueue_bounce(sc, ref, m, 1, FAR, W, H, frames=5, max_bounce=4) == n2
+    assert np.array_equal(r[:n2].view(np.uint32), ref[:n2].view(np.uint32))
+    assert np.array_equal(r[W * H:].view(np.uint32), ref[W * H:].view(np.uint32))
 
 
 # ------------------------------------------------------------------ BASELINE.json C2 at full size
@@ -314,8 +338,13 @@ def test_sponza_1080p_primary_and_bounce_full_parity(engine, sponza):
     rg, rc, ig, ic, s, cnt = trace_both(engine, sponza, rays, W * H, 0, W, H, upload=False)
     assert_same(rg, rc, ig, ic, 0, W * H)
     assert s.reps_exhausted == int((cnt["status"] == 1).sum())
+    ro = rg.copy()
     nb = engine.enqueue_bounce(rg, W * H, 0, FAR, W, H)
     assert nb > 0.9 * W * H
+    # 2,025 look-back tiles: the compacted bounce rays are bit-identical to the oracle's
+    assert O.enqueue_bounce(sponza, ro, W * H, 0, FAR, W, H) == nb
+    assert np.array_equal(rg[W * H:W * H + nb].view(np.uint32), ro[W * H:W * H + nb].view(np.uint32))
+    del ro
     colors = np.zeros(W * H, tthip.COL_DTYPE)
     colors["Data"][:, 3] = 1.0
     rg2, rc2, ig2, ic2, s2, cnt2 = trace_both(engine, sponza, rg, nb, 1, W, H, colors=colors, upload=False)

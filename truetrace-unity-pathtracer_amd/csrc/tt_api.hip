@@ -29,6 +29,7 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
                             const tt_mesh_data* md, uint32_t* counter, hipStream_t st);
+uint32_t tt_bounce_tiles(uint32_t n);
 hipError_t tt_launch_resolve(const tt_ray_data* rays, uint32_t ray_offset, uint32_t n, float far_plane,
                              const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* md, uint32_t n_mesh,
                              float* out, hipStream_t st);
@@ -1284,7 +1285,9 @@ tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_
     if (!wh || wh > 0x7fffffffull || p->n_rays > wh) return fail(c, TT_ERR_INVALID_ARG, "bad ray count / screen");
     const uint32_t src = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u, dst = (p->bounce % 2 == 1) ? 0u : (uint32_t)wh;
     TT_HIP(c, hipSetDevice(c->device));
-    if (c->counter.n < 4) TT_HIP(c, c->counter.alloc(4));
+    // [0] survivor count, [1] tile ticket, [2..3] pad, then one 64-bit look-back word per tile
+    const size_t ctl_words = 4 + 2 * (size_t)tt_bounce_tiles(p->n_rays);
+    if (c->counter.n < ctl_words) TT_HIP(c, c->counter.alloc(ctl_words));
     const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
     tt_ray_data* d = rays;
     if (!dev) {
@@ -1297,7 +1300,7 @@ tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_
     }
     uint32_t slot;
     TT_HIP(c, ring_open(c, slot));
-    TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 16, c->stream));
+    TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 4 * ctl_words, c->stream));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
                                c->mesh_raw.p, c->counter.p, c->stream));
     TT_HIP(c, ring_close(c, slot));

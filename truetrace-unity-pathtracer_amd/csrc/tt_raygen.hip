@@ -5,8 +5,15 @@
 //    (RayTracingShader.compute:52-84, 99-122, 293, 498-506): hit point, unsmoothed normal
 //    offset, cosine-hemisphere direction in GetTangentSpace(norm), then compaction of the
 //    survivors into the other half of the ping-pong buffer. The reference appends with one
-//    InterlockedAdd per ray; here a wave ballots its survivors, one lane reserves popcount
-//    slots and every survivor writes at base + mbcnt prefix (one atomic per wave).
+//    InterlockedAdd per ray on one counter (RayTracingShader.compute:500), so its order is
+//    whatever the atomics serialise to; one atomic per wave on one word still serialised at
+//    ~88 per microsecond (375 us for a 1080p frame, profiles/r02/r02a_kernel_stats.csv). Here
+//    the compaction is a STABLE single-pass scan: 4096-ray tiles taken in ticket order, a block
+//    ballot/LDS prefix inside the tile and a decoupled look-back over the preceding tiles'
+//    published counts (one 64-bit status word per tile, flag and value together), so the
+//    survivors land in source order -- deterministic, and the oracle restates the same order.
+//  * sincos in the cosine-lobe sample is pinned (sincos_pinned): HLSL leaves its precision to
+//    the driver, so both sides evaluate the same float polynomials with explicit FMAs.
 #include "tt_device.h"
 
 namespace {
@@ -103,99 +110,201 @@ __global__ __launch_bounds__(256) void tt_generate_kernel(const float* __restric
     o[2] = make_uint4(0u, 0u, __float_as_uint(far_plane), 0u);
 }
 
-__global__ __launch_bounds__(256) void tt_bounce_kernel(tt_ray_data* __restrict__ rays, uint32_t src_off, uint32_t dst_off,
+// sin/cos of the disc-sample angle phi in [-3pi/4, 3pi/4] (sample_disc's two branches give
+// [-pi/4, pi/4] and [pi/4, 3pi/4]): cephes single-precision minimax polynomials on
+// [-pi/4, pi/4] evaluated with explicit FMAs; |phi| > pi/4 is reduced by pi/2 (two-constant
+// Cody-Waite). Pinned: oracle/tt_oracle.c sincos_pinned is the same sequence of operations.
+__device__ __forceinline__ void sincos_pinned(float phi, float* s, float* c) {
+    const bool big = fabsf(phi) > 0.785398185253143310546875f;
+    const float q = phi > 0.0f ? 1.0f : -1.0f;
+    const float r = big ? fma_(-q, -4.37113882867379e-8f, fma_(-q, 1.57079637050628662109375f, phi)) : phi;
+    const float z = r * r;
+    const float sp = fma_(fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
+    const float cp = fma_(fma_(fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f), z,
+                               -0.5f), z, 1.0f);
+    // phi = q pi/2 + r: sin(phi) = q cos(r), cos(phi) = -q sin(r)
+    *s = big ? q * cp : sp;
+    *c = big ? -q * sp : cp;
+}
+
+// pdf > 0 decision and omega_o of sample(): cosine-weighted hemisphere from random(1, pixel)
+// (RayTracingShader.compute:52-84)
+__device__ __forceinline__ float3 cosine_sample(uint32_t pixel, int32_t frames, int32_t max_bounce, int32_t cur_bounce,
+                                                float* pdf) {
+    const float2 rnd = random2(1, pixel, frames, max_bounce, cur_bounce);
+    float a = 2.0f * rnd.x - 1.0f, b = 2.0f * rnd.y - 1.0f;
+    if (a == 0.0f) a = 0.00001f;
+    if (b == 0.0f) b = 0.00001f;
+    float phi, rr;
+    if (a * a > b * b) {
+        rr = a;
+        phi = (0.25f * 3.14159265f) * (b / a);
+    } else {
+        rr = b;
+        phi = (0.25f * 3.14159265f) * (a / b) + (0.5f * 3.14159265f);
+    }
+    float sp, cp;
+    sincos_pinned(phi, &sp, &cp);
+    const float dx = rr * cp, dz = rr * sp;
+    const float3 om = make_float3(dx, sqrtf(fabsf(1.0f - (dx * dx + dz * dz))), dz);
+    *pdf = om.y * 0.318309886548f;
+    return om;
+}
+
+// The new ray of a surviving hit (kernel_shade's diffuse path, RayTracingShader.compute:99-122,
+// 284, 293, 503).
+// RayData as three 16-B words: (origin, PixelIndex), (direction, last_pdf), hits
+struct Ray3 {
+    uint4 a, b, h;
+};
+__device__ __forceinline__ void bounce_ray(const Ray3& R, float3 om, float pdf, const tt_cuda_triangle* tris,
+                                           const tt_mesh_data* md, uint4* o) {
+    const float t = __uint_as_float(R.h.z);
+    const int32_t mesh_id = (int32_t)R.h.x, tri = (int32_t)R.h.y;
+    const float u = (float)(R.h.w & 0xffffu) / 65535.0f, v = (float)(R.h.w >> 16) / 65535.0f;
+    const float* W = md[mesh_id].W2L;
+    const tt_cuda_triangle& T = tris[tri];
+    const float3 dir = make_float3(__uint_as_float(R.b.x), __uint_as_float(R.b.y), __uint_as_float(R.b.z));
+    const float3 org = make_float3(__uint_as_float(R.a.x), __uint_as_float(R.a.y), __uint_as_float(R.a.z));
+    const float3 pos = make_float3(dir.x * t + org.x, dir.y * t + org.y, dir.z * t + org.z);
+    // Geomnorm (GetTriangleNormal) and USGNorm (RayTracingShader.compute:111-118)
+    const float3 n0 = i_octahedral_32(T.norms[0]), n1 = i_octahedral_32(T.norms[1]), n2 = i_octahedral_32(T.norms[2]);
+    const float w0 = 1.0f - u - v;
+    float3 g = mul_inv(W, make_float3(n0.x * w0 + u * n1.x + v * n2.x, n0.y * w0 + u * n1.y + v * n2.y,
+                                      n0.z * w0 + u * n1.z + v * n2.z));
+    g = normalize3(g);
+    float3 us = mul_inv(W, cross3(normalize3(make_float3(T.posedge1[0], T.posedge1[1], T.posedge1[2])),
+                                  normalize3(make_float3(T.posedge2[0], T.posedge2[1], T.posedge2[2]))));
+    us = normalize3(us);
+    us = make_float3(-us.x, -us.y, -us.z);
+    if (dot3(us, g) < 0) us = make_float3(-us.x, -us.y, -us.z);
+    if (dot3(dir, us) > 0.0f) {  // GotFlipped: backfacing
+        us = make_float3(-us.x, -us.y, -us.z);
+        g = make_float3(-g.x, -g.y, -g.z);
+    }
+    const float3 norm = i_octahedral_32(octahedral_32(g));
+    // GetTangentSpace(norm) — CommonData.cginc:332-343 (helper (1,0,0), or (0,0,1) if |n.x| > 0.99)
+    const float3 helper = fabsf(norm.x) > 0.99f ? make_float3(0, 0, 1) : make_float3(1, 0, 0);
+    const float3 tangent = normalize3(cross3(norm, helper));
+    const float3 binormal = cross3(norm, tangent);
+    float3 nd = make_float3(om.x * tangent.x + om.y * norm.x + om.z * binormal.x,
+                            om.x * tangent.y + om.y * norm.y + om.z * binormal.y,
+                            om.x * tangent.z + om.y * norm.z + om.z * binormal.z);
+    nd = normalize3(nd);
+    o[0] = make_uint4(__float_as_uint(us.x * 0.0001f + pos.x), __float_as_uint(us.y * 0.0001f + pos.y),
+                      __float_as_uint(us.z * 0.0001f + pos.z), R.a.w);
+    o[1] = make_uint4(__float_as_uint(nd.x), __float_as_uint(nd.y), __float_as_uint(nd.z), __float_as_uint(pdf));
+    o[2] = R.h;
+}
+
+// Decoupled look-back status word of a tile: bits 0-31 the count, bit 32 "aggregate" (this
+// tile's own survivors), bit 33 "inclusive" (survivors of tiles [0, tile]); 0 = not yet published.
+// Flag and value travel in one 64-bit word, so relaxed device-scope atomics suffice (no fences).
+constexpr uint64_t TT_LB_AGG = 1ull << 32, TT_LB_INC = 2ull << 32;
+__device__ __forceinline__ void lb_publish(unsigned long long* st, uint32_t tile, uint64_t flag, uint32_t v) {
+    __hip_atomic_store(st + tile, (unsigned long long)(flag | v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Exclusive prefix of tile `tile` (> 0): one wave reads the 64 preceding status words at once
+// (lane k reads tile - 1 - k), waits until all are published, sums up to and including the
+// nearest inclusive one, and slides the window back when there is none.
+__device__ __forceinline__ uint32_t lb_lookback(unsigned long long* st, uint32_t tile, uint32_t lane) {
+    uint32_t prefix = 0;
+    int32_t j = (int32_t)tile - 1;
+    while (true) {
+        const int32_t idx = j - (int32_t)lane;
+        uint64_t w = TT_LB_INC;  // before tile 0: an inclusive zero
+        if (idx >= 0) {
+            do {
+                w = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((w >> 32) == 0u);
+        }
+        const uint64_t inc = __ballot((w & TT_LB_INC) != 0u);
+        // lanes [0, first inclusive lane] contribute; none inclusive -> all 64, then slide
+        const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;
+        uint32_t v = lane <= stop ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        prefix += v;
+        if (inc) return prefix;
+        j -= 64;
+    }
+}
+
+constexpr uint32_t TT_BOUNCE_K = 4;                          // rays per thread
+constexpr uint32_t TT_BOUNCE_BLOCK = 1024;                   // threads per tile (16 waves)
+constexpr uint32_t TT_BOUNCE_WAVES = TT_BOUNCE_BLOCK / 64;
+constexpr uint32_t TT_BOUNCE_TILE = TT_BOUNCE_BLOCK * TT_BOUNCE_K;  // 4096 rays per tile: few tickets, short look-backs
+
+__global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data* __restrict__ rays, uint32_t src_off, uint32_t dst_off,
                                                         uint32_t n, float far_plane, int32_t cur_bounce, int32_t frames,
                                                         int32_t max_bounce, const tt_cuda_triangle* __restrict__ tris,
-                                                        const tt_mesh_data* __restrict__ md, uint32_t* __restrict__ counter) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool live = false;
-    tt_ray_data nr;
-    if (i < n) {
-        const tt_ray_data R = rays[src_off + i];
-        const float t = __uint_as_float(R.hits[2]);
-        if (t < far_plane && (int32_t)R.hits[1] >= 0) {
-            const int32_t mesh_id = (int32_t)R.hits[0], tri = (int32_t)R.hits[1];
-            const float u = (float)(R.hits[3] & 0xffffu) / 65535.0f, v = (float)(R.hits[3] >> 16) / 65535.0f;
-            const float* W = md[mesh_id].W2L;
-            const tt_cuda_triangle& T = tris[tri];
-            const float3 dir = make_float3(R.direction[0], R.direction[1], R.direction[2]);
-            const float3 org = make_float3(R.origin[0], R.origin[1], R.origin[2]);
-            const float3 pos = make_float3(dir.x * t + org.x, dir.y * t + org.y, dir.z * t + org.z);
-            // Geomnorm (GetTriangleNormal) and USGNorm (RayTracingShader.compute:111-118)
-            const float3 n0 = i_octahedral_32(T.norms[0]), n1 = i_octahedral_32(T.norms[1]), n2 = i_octahedral_32(T.norms[2]);
-            const float w0 = 1.0f - u - v;
-            float3 g = mul_inv(W, make_float3(n0.x * w0 + u * n1.x + v * n2.x, n0.y * w0 + u * n1.y + v * n2.y,
-                                              n0.z * w0 + u * n1.z + v * n2.z));
-            g = normalize3(g);
-            float3 us = mul_inv(W, cross3(normalize3(make_float3(T.posedge1[0], T.posedge1[1], T.posedge1[2])),
-                                          normalize3(make_float3(T.posedge2[0], T.posedge2[1], T.posedge2[2]))));
-            us = normalize3(us);
-            us = make_float3(-us.x, -us.y, -us.z);
-            if (dot3(us, g) < 0) us = make_float3(-us.x, -us.y, -us.z);
-            if (dot3(dir, us) > 0.0f) {  // GotFlipped: backfacing
-                us = make_float3(-us.x, -us.y, -us.z);
-                g = make_float3(-g.x, -g.y, -g.z);
-            }
-            const float3 norm = i_octahedral_32(octahedral_32(g));
-            // sample(): cosine-weighted hemisphere, random(1, pixel) — RayTracingShader.compute:52-84
-            const float2 rnd = random2(1, R.PixelIndex, frames, max_bounce, cur_bounce);
-            float a = 2.0f * rnd.x - 1.0f, b = 2.0f * rnd.y - 1.0f;
-            if (a == 0.0f) a = 0.00001f;
-            if (b == 0.0f) b = 0.00001f;
-            float phi, rr;
-            if (a * a > b * b) {
-                rr = a;
-                phi = (0.25f * 3.14159265f) * (b / a);
-            } else {
-                rr = b;
-                phi = (0.25f * 3.14159265f) * (a / b) + (0.5f * 3.14159265f);
-            }
-            float sp, cp;
-            sincosf(phi, &sp, &cp);
-            const float dx = rr * cp, dz = rr * sp;
-            const float3 om = make_float3(dx, sqrtf(fabsf(1.0f - (dx * dx + dz * dz))), dz);
-            const float pdf = om.y * 0.318309886548f;
-            // GetTangentSpace(norm) — CommonData.cginc (helper (1,0,0), or (0,0,1) if |n.x| > 0.99)
-            const float3 helper = fabsf(norm.x) > 0.99f ? make_float3(0, 0, 1) : make_float3(1, 0, 0);
-            const float3 tangent = normalize3(cross3(norm, helper));
-            const float3 binormal = cross3(norm, tangent);
-            float3 nd = make_float3(om.x * tangent.x + om.y * norm.x + om.z * binormal.x,
-                                    om.x * tangent.y + om.y * norm.y + om.z * binormal.y,
-                                    om.x * tangent.z + om.y * norm.z + om.z * binormal.z);
-            nd = normalize3(nd);
-            if (pdf > 0.0f) {
-                live = true;
-                nr.origin[0] = us.x * 0.0001f + pos.x;
-                nr.origin[1] = us.y * 0.0001f + pos.y;
-                nr.origin[2] = us.z * 0.0001f + pos.z;
-                nr.PixelIndex = R.PixelIndex;
-                nr.direction[0] = nd.x;
-                nr.direction[1] = nd.y;
-                nr.direction[2] = nd.z;
-                nr.last_pdf = pdf;
-                nr.hits[0] = R.hits[0];
-                nr.hits[1] = R.hits[1];
-                nr.hits[2] = R.hits[2];
-                nr.hits[3] = R.hits[3];
+                                                        const tt_mesh_data* __restrict__ md, uint32_t* __restrict__ ctl,
+                                                        unsigned long long* __restrict__ lb, uint32_t n_tiles) {
+    __shared__ uint32_t s_tile, s_prefix;
+    __shared__ uint32_t s_cnt[TT_BOUNCE_K][TT_BOUNCE_WAVES];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(&ctl[1], 1u);  // tiles in ticket order: look-back never waits on an unstarted block
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t base = tile * TT_BOUNCE_TILE;
+    // pass 1: which rays survive (hit, and the cosine sample's pdf > 0); keep the ray and omega_o
+    Ray3 R[TT_BOUNCE_K];
+    float3 om[TT_BOUNCE_K];
+    float pdf[TT_BOUNCE_K];
+    uint64_t live[TT_BOUNCE_K];
+#pragma unroll
+    for (uint32_t k = 0; k < TT_BOUNCE_K; k++) {
+        const uint32_t i = base + k * TT_BOUNCE_BLOCK + tid;
+        bool ok = false;
+        if (i < n) {
+            const uint4* rp = reinterpret_cast<const uint4*>(rays + src_off + i);
+            R[k].a = rp[0];
+            R[k].b = rp[1];
+            R[k].h = rp[2];
+            const float t = __uint_as_float(R[k].h.z);
+            if (t < far_plane && (int32_t)R[k].h.y >= 0) {
+                om[k] = cosine_sample(R[k].a.w, frames, max_bounce, cur_bounce, &pdf[k]);
+                ok = pdf[k] > 0.0f;
             }
         }
+        live[k] = __ballot(ok);
+        if (lane == 0) s_cnt[k][wave] = (uint32_t)__popcll(live[k]);
     }
-    // wave-ballot compaction: one atomic per wave (vs one InterlockedAdd per ray, :500)
-    const uint64_t m = __ballot(live);
-    if (m == 0) return;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader, 64);
-    if (live) {
-        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        uint4* o = reinterpret_cast<uint4*>(rays + dst_off + base + pre);
-        o[0] = make_uint4(__float_as_uint(nr.origin[0]), __float_as_uint(nr.origin[1]), __float_as_uint(nr.origin[2]),
-                          nr.PixelIndex);
-        o[1] = make_uint4(__float_as_uint(nr.direction[0]), __float_as_uint(nr.direction[1]),
-                          __float_as_uint(nr.direction[2]), __float_as_uint(nr.last_pdf));
-        o[2] = make_uint4(nr.hits[0], nr.hits[1], nr.hits[2], nr.hits[3]);
+    __syncthreads();
+    // tile count, published before the look-back so successors can sum past this tile
+    if (wave == 0) {
+        uint32_t total = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < TT_BOUNCE_K; k++)
+            for (uint32_t w = 0; w < TT_BOUNCE_WAVES; w++) total += s_cnt[k][w];
+        uint32_t prefix = 0;
+        if (tile == 0) {
+            if (lane == 0) lb_publish(lb, 0, TT_LB_INC, total);
+        } else {
+            if (lane == 0) lb_publish(lb, tile, TT_LB_AGG, total);
+            prefix = lb_lookback(lb, tile, lane);
+            if (lane == 0) lb_publish(lb, tile, TT_LB_INC, prefix + total);
+        }
+        if (lane == 0) {
+            s_prefix = prefix;
+            if (tile == n_tiles - 1u) ctl[0] = prefix + total;  // the survivor count tt_enqueue returns
+        }
+    }
+    __syncthreads();
+    // pass 2: survivors in source order (k-major, then thread) at prefix + rank
+    uint32_t slot = s_prefix;
+#pragma unroll
+    for (uint32_t k = 0; k < TT_BOUNCE_K; k++) {
+        uint32_t before = 0, all = 0;
+        for (uint32_t w = 0; w < TT_BOUNCE_WAVES; w++) {
+            before += w < wave ? s_cnt[k][w] : 0u;
+            all += s_cnt[k][w];
+        }
+        if ((live[k] >> lane) & 1ull) {
+            const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(live[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live[k], 0u));
+            bounce_ray(R[k], om[k], pdf[k], tris, md, reinterpret_cast<uint4*>(rays + dst_off + slot + before + pre));
+        }
+        slot += all;
     }
 }
 
@@ -208,11 +317,17 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
     return hipGetLastError();
 }
 
+uint32_t tt_bounce_tiles(uint32_t n) { return (n + TT_BOUNCE_TILE - 1u) / TT_BOUNCE_TILE; }
+
+// counter: [0] survivor count, [1] tile ticket, then tt_bounce_tiles(n) 64-bit status words; all
+// zeroed by the caller before the launch.
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
                             const tt_mesh_data* md, uint32_t* counter, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(tt_bounce_kernel, dim3((n + 255u) / 256u), dim3(256), 0, st, rays, src_off, dst_off, n, far_plane,
-                       cur_bounce, frames, max_bounce, tris, md, counter);
+    const uint32_t tiles = tt_bounce_tiles(n);
+    hipLaunchKernelGGL(tt_bounce_kernel, dim3(tiles), dim3(TT_BOUNCE_BLOCK), 0, st, rays, src_off, dst_off, n, far_plane,
+                       cur_bounce, frames, max_bounce, tris, md, counter,
+                       reinterpret_cast<unsigned long long*>(counter + 4), tiles);
     return hipGetLastError();
 }
