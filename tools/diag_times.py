@@ -1,7 +1,9 @@
 """Per-wave start/end timestamps (TT_DIAG_TIMES build) for the C2 primary trace: shows the
-load-balance tail of the persistent kernel."""
+load-balance tail of the persistent kernel. --ranks N traces rank 0's 64x64 tiles of an N-GPU
+tile-sharded frame instead (the per-rank launch under strong scaling)."""
 import os, sys
 import numpy as np
+RANKS = int(sys.argv[sys.argv.index("--ranks") + 1]) if "--ranks" in sys.argv else 1
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"))
 import torch
@@ -15,11 +17,19 @@ eng = tthip.Engine(0, stream=torch.cuda.current_stream(dev).cuda_stream); eng.up
 rays = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
 c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H, 0.3, far)
 eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
+n0 = W * H
+if RANKS > 1:
+    import ttdist
+    pix = torch.from_numpy(ttdist.tile_pixels(W, H, RANKS, 0)).to(dev)
+    full = rays[: W * H * 48].clone()
+    n0 = int(pix.shape[0])
+    rays.view(2 * W * H, 48)[:n0] = full.view(W * H, 48)[pix]
+    del full
 for b in (0, 1):
     if b == 1:
-        nb = eng.enqueue_bounce(rays, W * H, 0, far, W, H, device=True)
+        nb = eng.enqueue_bounce(rays, n0, 0, far, W, H, device=True)
     for _ in range(3):
-        s = eng.trace(rays, W * H if b == 0 else nb, b, far, W, H, device=True)
+        s = eng.trace(rays, n0 if b == 0 else nb, b, far, W, H, device=True)
     t = buf.cpu().numpy().reshape(-1, 4)
     used = t[:, 1] > 0
     t = t[used]
@@ -38,3 +48,8 @@ for b in (0, 1):
               "us; time in drain p50/p90/max", [round(float(np.percentile(dur, q))) for q in (50, 90, 100)], "us")
     end_rel = (en - t0) / 100.0
     print("   end-time percentiles", [round(float(np.percentile(end_rel, q))) for q in (1, 10, 25, 50, 75, 90, 99, 100)])
+    # waves alive / in the drain phase over time (10 buckets of the span)
+    grid = np.linspace(0, span, 11)[1:]
+    alive = [int(((st - t0) / 100.0 <= g).sum() - ((en - t0) / 100.0 <= g).sum()) for g in grid]
+    draining = [int((wide & ((cyc - t0) / 100.0 <= g) & ((en - t0) / 100.0 > g)).sum()) for g in grid]
+    print("   waves alive at 10%..100% of span", alive, "of which in the drain phase", draining)

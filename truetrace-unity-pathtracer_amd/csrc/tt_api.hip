@@ -17,6 +17,7 @@
 #define TT_RING 256u
 
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
+uint32_t tt_trace_chunk_rays();
 hipError_t tt_trace_occupancy_table(int* out12);
 hipError_t tt_launch_shadow(const ShadowArgs* a, uint32_t grid, hipStream_t st, int stats, int matcheck);
 hipError_t tt_launch_shadow_accumulate(const ShadowArgs* a, const float4* vis, hipStream_t st);
@@ -1025,7 +1026,10 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout ||
                           ((p->flags & TT_TRACE_IGNORE_GLASS) && c->host.any_atlas_shadow) ||
                           ((p->flags & TT_TRACE_IGNORE_BACKFACING) && p->bounce == 0);
-    const uint32_t waves_needed = (p->n_rays + 255u) / 256u;  // one TT_CHUNK per wave at least
+    // one dequeue chunk per wave: a launch smaller than the resident grid spreads over as many
+    // waves as it has chunks (r02: sizing this for 256-ray chunks left a 260k-ray launch -- one
+    // rank's shard at 8 GPUs -- on ~1 wave per SIMD, 4 chunks each)
+    const uint32_t waves_needed = (p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays();
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
     const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],
                                                  blocks_needed));
@@ -1174,7 +1178,7 @@ tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     a.bounce = p->bounce;
     a.flags = p->flags;
     const bool matcheck = c->any_shadow_skip || c->any_cutout || c->any_atlas_shadow;
-    const uint32_t blocks_needed = ((p->n_rays + 255u) / 256u + 3u) / 4u;
+    const uint32_t blocks_needed = ((p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays() + 3u) / 4u;
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));
     TT_HIP(c, hipMemsetAsync(c->ctl + c->ctl_cur, 0, sizeof(TraceControl), c->stream));

@@ -260,11 +260,12 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
 #endif
         if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)
             const uint64_t nm = __ballot(active && tg.y == 0u && Reps < TT_MAX_REPS && (cg.y & 0xff000000u));
+            const uint64_t am = __ballot(active);  // outside the lane-0 branch: a ballot there sees lane 0 only
             if (lane == 0) {
                 d_iter++;
                 d_node_lanes += (uint32_t)__popcll(nm);
                 d_node_iters += nm ? 1u : 0u;
-                d_active_lanes += (uint32_t)__popcll(__ballot(active));
+                d_active_lanes += (uint32_t)__popcll(am);
             }
         }
         // A lane is at the top of the reference's loop exactly when no leaf triangles are pending.
@@ -482,6 +483,7 @@ hipError_t tt_trace_occupancy_table(int* out12) {
 }
 
 uint32_t tt_trace_block_size() { return TT_BLOCK; }
+uint32_t tt_trace_chunk_rays() { return TT_CHUNK_BIG; }
 uint32_t tt_trace_lds_bytes() { return (uint32_t)(TT_LDS_STACK * TT_BLOCK * sizeof(uint2)); }
 uint32_t tt_trace_spill_entries() {
     return TT_LDS_STACK >= TT_STACK_SIZE ? 0u : (uint32_t)(TT_STACK_SIZE - TT_LDS_STACK);
