@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Experiment: how much of a launch is load-balance tail? Traces the C2 primary (and bounce-1) rays
+in three chunk orders -- the natural tile order, longest-chunk-first (LPT, per-ray step counts from
+the oracle) and shortest-first -- as compacted batches (n_rays = W*H - 1 disables the tile swizzle, so
+chunk c = records [64c, 64c+64)). Results are order-independent (each ray's traversal is its own);
+only the kernel time changes. --ranks N uses rank 0's tile shard of an N-GPU frame.
+Prints one JSON document."""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+
+def main():
+    ranks = int(sys.argv[sys.argv.index("--ranks") + 1]) if "--ranks" in sys.argv else 1
+    import torch
+    import tthip
+    import ttconfigs as T
+    import ttdist
+    import oracle_ctypes as O
+
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    eng = tthip.Engine(0, stream=stream.cuda_stream)
+    sc = T.c2_sponza()
+    eng.upload(sc)
+    W, H = 1920, 1080
+    WH = W * H
+    c2w, ip = T.C2_VIEW.camera()
+    r = O.generate(c2w, ip, W, H, T.NEAR, T.FAR, jitter=1, frames=0, max_bounce=1)
+    # tile order (8x8 tiles row-major), or rank 0's 64x64 tiles of an N-rank frame
+    if ranks > 1:
+        pix = ttdist.tile_pixels(W, H, ranks, 0)
+    else:
+        pix = np.arange(WH).reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1)
+    base = np.zeros(2 * WH, tthip.RAY_DTYPE)
+    n0 = len(pix)
+    base[:n0] = r[pix]
+    st, cnt = O.trace(sc, base.copy(), n0, 0, T.FAR, W, H, counts=True, nthreads=os.cpu_count() or 8)
+    steps0 = cnt["node_visits"].astype(np.int64) + cnt["tri_tests"].astype(np.int64)
+    out = {"tool": "tools/exp_lpt.py", "ranks": ranks, "launches": {}}
+
+    def run(name, recs, n, bounce, steps):
+        nch = (n + 63) // 64
+        pad = np.zeros(nch * 64, np.int64)
+        pad[:n] = steps
+        cmax = pad.reshape(nch, 64).max(1)
+        orders = {"natural": np.arange(nch), "lpt": np.argsort(-cmax, kind="stable"),
+                  "spt": np.argsort(cmax, kind="stable")}
+        res = {}
+        for oname, o in orders.items():
+            idx = (o[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)
+            idx = idx[idx < n]
+            buf = np.zeros(2 * WH, tthip.RAY_DTYPE)
+            off = WH if bounce == 1 else 0
+            buf[off: off + n] = recs[idx]
+            t = torch.from_numpy(buf.view(np.uint8)).to(dev)
+            nn = n - 1 if n == WH else n  # never the full-frame swizzle
+            eng.trace(t, nn, bounce, T.FAR, W, H, device=True)
+            eng.timing_reset()
+            for _ in range(9):
+                eng.trace(t, nn, bounce, T.FAR, W, H, device=True)
+            ms = eng.timing_read()
+            res[oname] = round(float(np.median(ms)), 4)
+        res["rays"] = n
+        res["steps_mean"] = round(float(steps.mean()), 2)
+        res["steps_max"] = int(steps.max())
+        out["launches"][name] = res
+        print(name, res, file=sys.stderr, flush=True)
+
+    run("primary", base[:n0], n0, 0, steps0)
+    # bounce-1 rays from the oracle's own enqueue of the traced primaries
+    traced = base.copy()
+    O.trace(sc, traced, n0, 0, T.FAR, W, H, nthreads=os.cpu_count() or 8)
+    nb = O.enqueue_bounce(sc, traced, n0, 0, T.FAR, W, H)
+    brec = traced[WH: WH + nb].copy()
+    st, cb = O.trace(sc, traced, nb, 1, T.FAR, W, H, counts=True, nthreads=os.cpu_count() or 8)
+    steps1 = cb["node_visits"].astype(np.int64) + cb["tri_tests"].astype(np.int64)
+    run("bounce1", brec, nb, 1, steps1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
