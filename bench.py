@@ -12,8 +12,9 @@ bounce enqueue run once during setup (they are the caller's kernels, not the tra
 Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): one process per GPU, scene
 replicated per GPU, the 1080p frame's 64x64 screen tiles dealt round-robin to the ranks (SURVEY.md
 §8(e)). Each rank traces its tiles' primary rays and their bounce-1 rays, then the primary hit
-records go to rank 0 in ONE RCCL gather over xGMI -- inside the timed step, so a step is a whole
-frame and ``value`` is frame rays / frame time (strong scaling). ``--shard sample`` instead has
+records go to rank 0 in ONE RCCL gather over xGMI -- inside the timed step (on a second stream,
+overlapped with the bounce-1 trace), so a step is a whole frame and ``value`` is frame rays / frame
+time (strong scaling). ``--shard sample`` instead has
 every rank trace its own full-frame sample (weak scaling, no data-path collective); that layout is
 also reported as ``config.aux_sample_sharded``.
 
@@ -438,8 +439,10 @@ def main():
         f"tris/ray {s_bnc.tri_tests / max(nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}")
 
     # tiles: the frame's primary hit records go to rank 0 in one gather per step (shards padded to
-    # the largest so every rank sends one equal-size message)
-    sizes, hits_buf, gather_list = None, None, None
+    # the largest so every rank sends one equal-size message). The gather runs on its own stream,
+    # overlapped with the bounce-1 trace (which reads and writes only the other half of the
+    # ping-pong buffer); the step ends when both are done, so the timed step includes the collective.
+    sizes, hits_buf, gather_list, comm = None, None, None, None
     if tiles:
         n_t = torch.tensor([n_prim], dtype=torch.int64, device=red_dev)
         sz = [torch.zeros_like(n_t) for _ in range(world)]
@@ -447,14 +450,21 @@ def main():
         sizes = [int(x.item()) for x in sz]
         hits_buf = torch.zeros((max(sizes), 4), dtype=torch.int32, device=red_dev)
         gather_list = [torch.empty_like(hits_buf) for _ in range(world)] if rank == 0 else None
+        comm = torch.cuda.Stream(dev)
     prim_hits = rays[: n_prim * 48].view(n_prim, 48)[:, 32:48].view(torch.int32)
+    # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
+    gather_overlapped = tiles and red_dev.type == "cuda"
 
     def step():
         eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, asynchronous=True)
+        if tiles:
+            comm.wait_stream(stream)  # the primary hit records are final
+            with torch.cuda.stream(comm):
+                hits_buf[:n_prim].copy_(prim_hits)
+                dist.gather(hits_buf, gather_list, dst=0)
         eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
         if tiles:
-            hits_buf[:n_prim].copy_(prim_hits)
-            dist.gather(hits_buf, gather_list, dst=0)
+            stream.wait_stream(comm)  # the next step's primary trace rewrites the gathered half
 
     for _ in range(args.warmup):
         step()
@@ -666,7 +676,9 @@ def main():
                    "seed": hex(args.seed),
                    "parallelism": ("single GPU, full frame" if world == 1 else
                                    (f"64x64 screen tiles round-robin over {world} ranks + one RCCL gather of the "
-                                    f"primary hit records to rank 0 per step (inside the timed step)" if tiles
+                                    f"primary hit records to rank 0 per step (inside the timed step"
+                                    + (", overlapped with the bounce-1 trace on a second stream)" if gather_overlapped
+                                       else ")") if tiles
                                     else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
                    "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it",
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
