@@ -353,6 +353,9 @@ def main():
                          "RCCL-gathered to rank 0 inside every timed step (strong scaling). sample: every rank "
                          "traces its own full-frame sample, no collective (weak scaling)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
+    ap.add_argument("--no-recur", action="store_true",
+                    help="skip the auxiliary unjittered (UseReCur) primary + bounce launches (profiling runs: they "
+                         "use the metric's kernel instantiation and would mix into its rocprof average)")
     ap.add_argument("--no-c5-tiles", action="store_true",
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
     ap.add_argument("--aux", default="c3,c4,refit,c5",
@@ -553,7 +556,7 @@ def main():
 
     # ---- auxiliary: the UseReCur ray generation (no jitter), primary + bounce 1, N=1
     recur = None
-    if world == 1:
+    if world == 1 and not args.no_recur:
         rr = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(rr, c2w, ip, W, H, 0.3, far, jitter=0, frames=0, max_bounce=1, device=True)
         rs = eng.trace(rr, WH, 0, far, W, H, info=info, device=True, stats=True)

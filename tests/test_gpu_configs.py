@@ -1,9 +1,10 @@
 """GPU parity on the BASELINE.json configurations beyond C2's primary + bounce-1 case
 ("Synthetic inputs"; scenes from ``ttconfigs``):
 
-  C3  C2 geometry, primary + 3 diffuse bounces: every bounce's compacted rays (wave-ballot
-      enqueue on the GPU) traced bit-exact against the oracle, with the GlobalColors-gated
-      _PrimaryTriangleInfo forms at bounces 1-3.
+  C3  C2 geometry at 1920x1080, primary + 3 diffuse bounces: every bounce's compacted rays (the
+      GPU's stable look-back enqueue, itself bit-exact against the oracle's enqueue) traced
+      bit-exact against the oracle, with the GlobalColors-gated _PrimaryTriangleInfo forms at
+      bounces 1-3.
   C4  Bistro-shaped two-level instancing (600 unique BLAS, 2,400 instances, 4.8M unique tris) at
       1920x1080: full-frame primary and bounce-1 parity, BLAS-entry counts equal.
   C5  San-Miguel-shaped 10M tris at 3840x2160: determinism, a strided 1/8 oracle sample, and
@@ -28,7 +29,7 @@ def c2():
 
 
 def test_c3_primary_plus_three_bounces(engine, c2):
-    W, H = 960, 540
+    W, H = 1920, 1080  # the bench's C3 frame
     WH = W * H
     c2w, ip = T.C2_VIEW.camera(W, H)
     engine.upload(c2)
@@ -40,9 +41,13 @@ def test_c3_primary_plus_three_bounces(engine, c2):
     assert_same(rg, rc, ig, ic, 0, WH)
     n = WH
     for bounce in (1, 2, 3):
+        ref = rg.copy()
         nb = engine.enqueue_bounce(rg, n, bounce - 1, FAR, W, H, frames=3, max_bounce=3)
         assert 0 < nb <= n
         off = (bounce % 2) * WH
+        assert O.enqueue_bounce(c2, ref, n, bounce - 1, FAR, W, H, frames=3, max_bounce=3) == nb
+        assert np.array_equal(rg[off:off + nb].view(np.uint32), ref[off:off + nb].view(np.uint32))
+        del ref
         assert np.allclose(np.linalg.norm(rg["direction"][off:off + nb], axis=1), 1.0, atol=1e-5)
         rg, rc, ig, ic, s, cnt = trace_both(engine, c2, rg, nb, bounce, W, H, colors=colors, upload=False)
         assert_same(rg, rc, ig, ic, off, nb)
