@@ -1,4 +1,4 @@
-"""Times every kernel variant in lib/variants/ on the C2 workload (each in a fresh process) and
+"""Times every kernel variant in lib/variants/ on the C2 workload (RV_CFG=c4 / c5: that config) (each in a fresh process) and
 checks a strided sample of its hits against the oracle."""
 import glob
 import json
@@ -12,13 +12,22 @@ import os, sys, json, numpy as np
 sys.path.insert(0, os.path.join(os.environ["REPO"], "truetrace-unity-pathtracer_amd", "python"))
 sys.path.insert(0, os.path.join(os.environ["REPO"], "tests"))
 import torch, tthip, oracle_ctypes as O
-W, H, far = 1920, 1080, 1000.0
-blas = tthip.Blas(tthip.Mesh.sponza()); am = tthip.AssetManager(); am.add_parent(blas, None, np.zeros(7, tthip.MAT_DTYPE)); sc = am.build()
+cfg = os.environ.get("RV_CFG", "c2")
+if cfg == "c2":
+    W, H, far = 1920, 1080, 1000.0
+    blas = tthip.Blas(tthip.Mesh.sponza()); am = tthip.AssetManager(); am.add_parent(blas, None, np.zeros(7, tthip.MAT_DTYPE)); sc = am.build()
+    cam = ((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), 60.0)
+else:  # another BASELINE config from ttconfigs (c4: Bistro-shaped two-level, c5: San-Miguel-shaped)
+    import ttconfigs as T
+    sc = {"c4": T.c4_bistro, "c5": T.c5_san_miguel}[cfg]()
+    v = {"c4": T.C4_VIEW, "c5": T.C5_VIEW}[cfg]
+    W, H, far = v.width, v.height, T.FAR
+    cam = (v.position, v.forward, v.vfov)
 dev = torch.device("cuda:0")
 eng = tthip.Engine(0, stream=torch.cuda.current_stream(dev).cuda_stream); eng.upload(sc)
 rays = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
 info = torch.zeros(W * H * 16, dtype=torch.uint8, device=dev)
-c2w, ip = tthip.unity_camera((-10.0, 2.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, W, H, 0.3, far)
+c2w, ip = tthip.unity_camera(cam[0], cam[1], (0.0, 1.0, 0.0), cam[2], W, H, 0.3, far)
 eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=1, frames=0, max_bounce=1, device=True)
 eng.trace(rays, W * H, 0, far, W, H, info=info, device=True)
 nb = eng.enqueue_bounce(rays, W * H, 0, far, W, H, frames=0, max_bounce=1, device=True)
