@@ -7,7 +7,7 @@
       bounces 1-3.
   C4  Bistro-shaped two-level instancing (600 unique BLAS, 2,400 instances, 4.8M unique tris) at
       1920x1080: full-frame primary and bounce-1 parity, BLAS-entry counts equal.
-  C5  San-Miguel-shaped 10M tris at 3840x2160: determinism, a strided 1/8 oracle sample, and
+  C5  San-Miguel-shaped 10M tris at 3840x2160: determinism, full-frame oracle parity, and
       the 8-GPU 64x64 round-robin tile sharding reassembled byte-identical to
       the single-launch frame (hit records and _PrimaryTriangleInfo).
 """
@@ -80,7 +80,7 @@ def test_c4_bistro_1080p_full_parity(engine, c4):
     assert s2.node_visits == int(cnt2["node_visits"].sum())
 
 
-def test_c5_san_miguel_4k_sampled_and_tile_sharded(engine):
+def test_c5_san_miguel_4k_full_parity_and_tile_sharded(engine):
     sc = T.c5_san_miguel()
     assert len(sc.tris) == T.C5_TRIS
     W, H = T.C5_VIEW.width, T.C5_VIEW.height
@@ -95,13 +95,13 @@ def test_c5_san_miguel_4k_sampled_and_tile_sharded(engine):
     b = rays.copy()
     engine.trace(b, WH, 0, FAR, W, H)
     assert np.array_equal(a, b), "two launches must give identical bytes"
-    # strided 1/8 sample against the oracle
-    idx = np.arange(0, WH, 8)
-    sample = np.zeros(2 * len(idx), tthip.RAY_DTYPE)
-    sample[: len(idx)] = rays[idx]
-    st, _ = O.trace(sc, sample, len(idx), 0, FAR, len(idx), 1, nthreads=CPU_THREADS)
+    # the full 4K frame against the oracle (hit records and _PrimaryTriangleInfo)
+    ref = rays.copy()
+    info_ref = np.zeros((WH, 4), np.uint32)
+    st, _ = O.trace(sc, ref, WH, 0, FAR, W, H, info=info_ref, nthreads=CPU_THREADS)
     assert st == 0
-    assert np.array_equal(sample["hits"][: len(idx)], a["hits"][idx])
+    assert np.array_equal(ref["hits"][:WH], a["hits"][:WH])
+    assert np.array_equal(info_ref, info_a)
     # 8-GPU tile sharding, replayed rank by rank on this GPU: compact per-rank ray lists, traced
     # independently, reassembled on "rank 0" -> byte-identical to the single launch
     world = 8
