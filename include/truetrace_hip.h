@@ -299,6 +299,21 @@ typedef struct tt_blas_refit_params {
 tt_status tt_blas_refit(tt_ctx* ctx, const tt_blas_refit_params* p, const float* vertices, const int32_t* indices,
                         const int32_t* leaf_of_triangle);
 
+/* BLAS builder, BVH2 stage, on the GPU (row f4's builder half): BVH2Builder (BVH2Builder.cs:9-217)
+ * restated level by level -- segmented AABB.Extend scans, the full-sweep SAH with the reference's
+ * tie rules, stable partitions -- with outputs identical to the sequential C# recursion and to
+ * tt_bvh2_build (include/truetrace_scene.h), which takes the same arguments minus the presort.
+ *   aabbs:      n x {BBMax[3], BBMin[3]} primitive boxes (host),
+ *   presorted:  3 x n primitive indices, axis x, y, z, each sorted by centroid with .NET's
+ *               Array.Sort (tt_bvh2_presort in truetrace_scene.h: the introsort's tie order decides
+ *               trees, so the sort stays on the host),
+ *   final_indices (n), node_aabbs (2n x 6), node_left (2n), node_count (2n): BVH2Nodes and
+ *               FinalIndices as BVH2Builder leaves them; max_depth: BuildRecursive's deepest level.
+ * Synchronous on the context stream. TT_ERR_UNSUPPORTED if some node has no finite SAH split. */
+tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
+                               int32_t* final_indices, float* node_aabbs, int32_t* node_left, uint32_t* node_count,
+                               uint32_t* max_depth);
+
 /* Copies AggTris [first, first+count) back from HBM (e.g. after tt_blas_refit). */
 tt_status tt_scene_read_tris(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cuda_triangle* out);
 

@@ -51,6 +51,16 @@ typedef struct tt_blas_info {
 } tt_blas_info;
 
 tt_status tt_blas_build(const tt_mesh_input* mesh, tt_blas** out);
+/* The same build in three steps, so the BVH2 stage can run on the GPU (tt_bvh2_build_device in
+ * truetrace_hip.h) with byte-identical results:
+ *   tt_blas_prepare_aabbs   BuildTotal's triangle AABBs (n_indices / 3 x {BBMax[3], BBMin[3]}),
+ *   tt_bvh2_presort         BVH2Builder's three centroid presorts (.NET Array.Sort), 3 x n indices,
+ *   tt_blas_build_from_bvh2 Construct's BVH8 stage + Aggregate over a BVH2 as tt_bvh2_build writes it. */
+tt_status tt_blas_prepare_aabbs(const tt_mesh_input* mesh, float* aabbs_maxmin);
+tt_status tt_bvh2_presort(const float* aabbs_maxmin, uint32_t n, int32_t* presorted);
+tt_status tt_blas_build_from_bvh2(const tt_mesh_input* mesh, const int32_t* final_indices, const float* node_aabbs,
+                                  const int32_t* node_left, const uint32_t* node_count, uint32_t bvh2_depth,
+                                  tt_blas** out);
 tt_status tt_blas_get_info(const tt_blas* b, tt_blas_info* info);
 /* Copies the packed nodes (80 B) and the leaf-ordered triangles (88 B). */
 tt_status tt_blas_copy(const tt_blas* b, tt_cwbvh_node* nodes, tt_cuda_triangle* tris);

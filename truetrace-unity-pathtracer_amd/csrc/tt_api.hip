@@ -941,6 +941,8 @@ MatView mat_view(const tt_ctx* c) {
 }
 }  // namespace
 
+hipStream_t tt_ctx_stream_of(tt_ctx* c) { return c->stream; }  // tt_build.hip
+
 tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
                            const tt_col_data* colors, tt_stats* stats) {
     if (!c) return TT_ERR_INVALID_ARG;

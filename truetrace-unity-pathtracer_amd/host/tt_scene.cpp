@@ -9,6 +9,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -391,6 +392,7 @@ struct BVH2Builder {
             s.Sort(n);
         };
         parallel = std::getenv("TT_BUILD_SERIAL") == nullptr;
+        const auto ts = std::chrono::steady_clock::now();
         if (parallel && n >= kParMin) {
             std::thread t1(sort_axis, 1), t2(sort_axis, 2);
             sort_axis(0);
@@ -399,8 +401,13 @@ struct BVH2Builder {
         } else {
             for (int d = 0; d < 3; d++) sort_axis(d);
         }
+        const auto tr = std::chrono::steady_clock::now();
         BuildRecursive(0, 2, 0, n, 0);
         std::memcpy(FinalIndices.data(), DimensionedIndices.data(), sizeof(int) * (size_t)n);
+        if (std::getenv("TT_BUILD_TIMES"))
+            std::fprintf(stderr, "[build] bvh2 n=%d presort %.3f s, recursive SAH %.3f s\n", n,
+                         std::chrono::duration<double>(tr - ts).count(),
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count());
     }
 };
 
@@ -813,72 +820,218 @@ tt_status tt_bvh2_build(const float* aabbs, uint32_t n, int32_t* final_indices, 
 }
 
 // ParentObject.BuildTotal (ParentObject.cs:973-1111) for one merged child with identity
-// child->parent transform (TransMat = I, Ofst = Ofst2 = 0), then Construct (:679-742),
-// the cwbvh_indices permutation (:1084-1090) and Aggregate (:1091-1092).
-tt_status tt_blas_build(const tt_mesh_input* m, tt_blas** out) {
-    if (!m || !out || !m->positions || !m->indices || m->n_indices < 3 || m->n_indices % 3) return TT_ERR_INVALID_ARG;
+// child->parent transform (TransMat = I, Ofst = Ofst2 = 0): the AggTriangles and the triangle AABBs
+// the builders consume. Triangles are independent: large meshes are prepared on several threads.
+namespace {
+struct BlasPrep {
+    std::vector<tt_cuda_triangle> agg;
+    std::vector<AABB> Triangles;
+    AABB aabb_untransformed;
+};
+tt_status blas_prepare(const tt_mesh_input* m, BlasPrep& P) {
+    if (!m || !m->positions || !m->indices || m->n_indices < 3 || m->n_indices % 3) return TT_ERR_INVALID_ARG;
     for (uint32_t i = 0; i < m->n_indices; i++)
         if (m->indices[i] < 0 || (uint32_t)m->indices[i] >= m->n_vertices) return TT_ERR_INVALID_ARG;
-    const auto t0 = std::chrono::steady_clock::now();
-    tt_blas* b = new (std::nothrow) tt_blas();
-    if (!b) return TT_ERR_OOM;
     const uint32_t ntri = m->n_indices / 3;
     const V3 ParentScale = v3(0.001f / m->lossy_scale[0], 0.001f / m->lossy_scale[1], 0.001f / m->lossy_scale[2]);
-    std::vector<tt_cuda_triangle> agg(ntri);
-    std::vector<AABB> Triangles(ntri);
-    auto P = [&](int i) { return v3(m->positions[3 * i], m->positions[3 * i + 1], m->positions[3 * i + 2]); };
+    P.agg.assign(ntri, tt_cuda_triangle{});
+    P.Triangles.resize(ntri);
+    auto P3 = [&](int i) { return v3(m->positions[3 * i], m->positions[3 * i + 1], m->positions[3 * i + 2]); };
     auto N = [&](int i) { return m->normals ? v3(m->normals[3 * i], m->normals[3 * i + 1], m->normals[3 * i + 2]) : v3(0, 1, 0); };
     auto T = [&](int i) { return m->tangents ? v3(m->tangents[4 * i], m->tangents[4 * i + 1], m->tangents[4 * i + 2]) : v3(1, 0, 0); };
-    for (uint32_t t = 0; t < ntri; t++) {
-        const int Index1 = m->indices[3 * t], Index2 = m->indices[3 * t + 2], Index3 = m->indices[3 * t + 1];
-        const V3 V1 = P(Index1), V2 = P(Index2), V3_ = P(Index3);
-        tt_cuda_triangle& tri = agg[t];
-        std::memset(&tri, 0, sizeof(tri));
-        for (int k = 0; k < 2; k++) {
-            tri.tex0[k] = m->uvs ? m->uvs[2 * Index1 + k] : 0.0f;
-            tri.texedge1[k] = m->uvs ? m->uvs[2 * Index2 + k] : 0.0f;
-            tri.texedge2[k] = m->uvs ? m->uvs[2 * Index3 + k] : 0.0f;
+    auto range = [&](uint32_t t0, uint32_t t1) {
+        for (uint32_t t = t0; t < t1; t++) {
+            const int Index1 = m->indices[3 * t], Index2 = m->indices[3 * t + 2], Index3 = m->indices[3 * t + 1];
+            const V3 V1 = P3(Index1), V2 = P3(Index2), V3_ = P3(Index3);
+            tt_cuda_triangle& tri = P.agg[t];
+            std::memset(&tri, 0, sizeof(tri));
+            for (int k = 0; k < 2; k++) {
+                tri.tex0[k] = m->uvs ? m->uvs[2 * Index1 + k] : 0.0f;
+                tri.texedge1[k] = m->uvs ? m->uvs[2 * Index2 + k] : 0.0f;
+                tri.texedge2[k] = m->uvs ? m->uvs[2 * Index3 + k] : 0.0f;
+            }
+            const V3 e1 = V2 - V1, e2 = V3_ - V1;
+            tri.pos0[0] = V1.x; tri.pos0[1] = V1.y; tri.pos0[2] = V1.z;
+            tri.posedge1[0] = e1.x; tri.posedge1[1] = e1.y; tri.posedge1[2] = e1.z;
+            tri.posedge2[0] = e2.x; tri.posedge2[1] = e2.y; tri.posedge2[2] = e2.z;
+            const int idx[3] = {Index1, Index2, Index3};
+            for (int k = 0; k < 3; k++) {
+                const V3 n = normalized(N(idx[k]));
+                tri.norms[k] = tt_pack_octahedral(n.x, n.y, n.z);
+                const V3 tg = normalized(T(idx[k]));
+                tri.tans[k] = tt_pack_octahedral(tg.x, tg.y, tg.z);
+            }
+            tri.MatDat = m->matdat ? (uint32_t)m->matdat[t] : 0u;
+            P.Triangles[t].Create(V1, V2);
+            P.Triangles[t].Extend(V3_);
+            P.Triangles[t].Validate(ParentScale);
         }
-        const V3 e1 = V2 - V1, e2 = V3_ - V1;
-        tri.pos0[0] = V1.x; tri.pos0[1] = V1.y; tri.pos0[2] = V1.z;
-        tri.posedge1[0] = e1.x; tri.posedge1[1] = e1.y; tri.posedge1[2] = e1.z;
-        tri.posedge2[0] = e2.x; tri.posedge2[1] = e2.y; tri.posedge2[2] = e2.z;
-        const int idx[3] = {Index1, Index2, Index3};
-        for (int k = 0; k < 3; k++) {
-            const V3 n = normalized(N(idx[k]));
-            tri.norms[k] = tt_pack_octahedral(n.x, n.y, n.z);
-            const V3 tg = normalized(T(idx[k]));
-            tri.tans[k] = tt_pack_octahedral(tg.x, tg.y, tg.z);
-        }
-        tri.MatDat = m->matdat ? (uint32_t)m->matdat[t] : 0u;
-        Triangles[t].Create(V1, V2);
-        Triangles[t].Extend(V3_);
-        Triangles[t].Validate(ParentScale);
+    };
+    const uint32_t nth = (ntri >= (1u << 16) && std::getenv("TT_BUILD_SERIAL") == nullptr)
+                             ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    if (nth > 1) {
+        std::vector<std::thread> th;
+        for (uint32_t k = 1; k < nth; k++)
+            th.emplace_back(range, (uint32_t)((uint64_t)ntri * k / nth), (uint32_t)((uint64_t)ntri * (k + 1) / nth));
+        range(0, (uint32_t)((uint64_t)ntri / nth));
+        for (auto& t : th) t.join();
+    } else {
+        range(0, ntri);
     }
     // ConstructAABB (:1143-1149)
-    b->aabb_untransformed.init();
-    for (uint32_t t = 0; t < ntri; t++) b->aabb_untransformed.Extend(Triangles[t]);
+    P.aabb_untransformed.init();
+    for (uint32_t t = 0; t < ntri; t++) P.aabb_untransformed.Extend(P.Triangles[t]);
+    return TT_OK;
+}
 
+// Construct's BVH8 stage (:679-742), the cwbvh_indices permutation (:1084-1090) and Aggregate
+// (:1091-1092) over a finished BVH2.
+tt_status blas_finish(BlasPrep& P, BVH2Builder& bvh2, tt_blas* b) {
+    const uint32_t ntri = (uint32_t)P.agg.size();
     bool ok = false;
-    BVH2Builder bvh2;
     BVH8Builder bvh8;
+    double t_bvh8 = 0.0;
     run_big_stack([&] {
-        bvh2.build(Triangles.data(), (int)ntri);
+        const auto t8 = std::chrono::steady_clock::now();
         ok = bvh8.build(bvh2);
+        t_bvh8 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t8).count();
     });
-    if (!ok) {
-        delete b;
-        return TT_ERR_UNSUPPORTED;
-    }
+    if (std::getenv("TT_BUILD_TIMES")) std::fprintf(stderr, "[build] blas n=%u bvh8 %.3f s\n", ntri, t_bvh8);
+    if (!ok) return TT_ERR_UNSUPPORTED;
+    b->aabb_untransformed = P.aabb_untransformed;
     b->bvh2_depth = bvh2.max_depth;
     b->tris.resize(ntri);
     b->leaf_of.assign(ntri, 0);
     for (uint32_t i = 0; i < ntri; i++) {
-        b->tris[i] = agg[bvh8.cwbvh_indices[i]];
+        b->tris[i] = P.agg[bvh8.cwbvh_indices[i]];
         b->leaf_of[bvh8.cwbvh_indices[i]] = (int32_t)i;
     }
     b->nodes.resize(bvh8.BVH8Nodes.size());
     Aggregate(bvh8.BVH8Nodes, b->nodes.data());
+    return TT_OK;
+}
+}  // namespace
+
+tt_status tt_blas_build(const tt_mesh_input* m, tt_blas** out) {
+    if (!out) return TT_ERR_INVALID_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    BlasPrep P;
+    tt_status st = blas_prepare(m, P);
+    if (st != TT_OK) return st;
+    if (std::getenv("TT_BUILD_TIMES"))
+        std::fprintf(stderr, "[build] blas n=%zu triangles+boxes %.3f s\n", P.agg.size(),
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    tt_blas* b = new (std::nothrow) tt_blas();
+    if (!b) return TT_ERR_OOM;
+    BVH2Builder bvh2;
+    run_big_stack([&] { bvh2.build(P.Triangles.data(), (int)P.Triangles.size()); });
+    st = blas_finish(P, bvh2, b);
+    if (st != TT_OK) {
+        delete b;
+        return st;
+    }
+    b->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    *out = b;
+    return TT_OK;
+}
+
+tt_status tt_blas_prepare_aabbs(const tt_mesh_input* m, float* aabbs) {
+    if (!aabbs) return TT_ERR_INVALID_ARG;
+    BlasPrep P;
+    const tt_status st = blas_prepare(m, P);
+    if (st != TT_OK) return st;
+    for (size_t t = 0; t < P.Triangles.size(); t++) {
+        const AABB& a = P.Triangles[t];
+        float* o = aabbs + 6 * t;
+        o[0] = a.BBMax.x; o[1] = a.BBMax.y; o[2] = a.BBMax.z;
+        o[3] = a.BBMin.x; o[4] = a.BBMin.y; o[5] = a.BBMin.z;
+    }
+    return TT_OK;
+}
+
+tt_status tt_bvh2_presort(const float* aabbs, uint32_t n, int32_t* presorted) {
+    if (!aabbs || !n || !presorted) return TT_ERR_INVALID_ARG;
+    std::vector<float> c[3];
+    for (int d = 0; d < 3; d++) c[d].resize(n);
+    for (uint32_t i = 0; i < n; i++) {  // BVH2Builder's centroid: (max - min) / 2 + min
+        const float* a = aabbs + 6 * (size_t)i;
+        for (int d = 0; d < 3; d++) c[d][i] = (a[d] - a[3 + d]) / 2.0f + a[3 + d];
+    }
+    auto sort_axis = [&](int d) {
+        int32_t* seg = presorted + (size_t)n * d;
+        for (uint32_t i = 0; i < n; i++) seg[i] = (int32_t)i;
+        DotNetSort s{seg, KeyCmp{c[d].data()}};
+        s.Sort((int)n);
+    };
+    if (n >= (1u << 16) && std::getenv("TT_BUILD_SERIAL") == nullptr) {
+        std::thread t1(sort_axis, 1), t2(sort_axis, 2);
+        sort_axis(0);
+        t1.join();
+        t2.join();
+    } else {
+        for (int d = 0; d < 3; d++) sort_axis(d);
+    }
+    return TT_OK;
+}
+
+tt_status tt_blas_build_from_bvh2(const tt_mesh_input* m, const int32_t* final_indices, const float* node_aabbs,
+                                  const int32_t* node_left, const uint32_t* node_count, uint32_t max_depth,
+                                  tt_blas** out) {
+    if (!out || !final_indices || !node_aabbs || !node_left || !node_count) return TT_ERR_INVALID_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    BlasPrep P;
+    tt_status st = blas_prepare(m, P);
+    if (st != TT_OK) return st;
+    const uint32_t n = (uint32_t)P.Triangles.size();
+    BVH2Builder bvh2;
+    bvh2.PrimCount = (int)n;
+    bvh2.parallel = std::getenv("TT_BUILD_SERIAL") == nullptr;
+    bvh2.max_depth = max_depth;
+    bvh2.FinalIndices.assign(final_indices, final_indices + n);
+    bvh2.BVH2Nodes.resize(2 * (size_t)n);
+    for (size_t i = 0; i < 2 * (size_t)n; i++) {
+        const float* a = node_aabbs + 6 * i;
+        BVHNode2Data& nd = bvh2.BVH2Nodes[i];
+        nd.aabb.BBMax = v3(a[0], a[1], a[2]);
+        nd.aabb.BBMin = v3(a[3], a[4], a[5]);
+        nd.left = node_left[i];
+        nd.count = node_count[i];
+    }
+    {  // structure check: a binary tree over the n positions (children after their parent), a permutation
+        std::vector<char> seen(n, 0);
+        std::vector<int> stack{0};
+        uint32_t leaves = 0;
+        while (!stack.empty()) {
+            const int i = stack.back();
+            stack.pop_back();
+            const BVHNode2Data& nd = bvh2.BVH2Nodes[(size_t)i];
+            if (nd.count == 1) {
+                if (nd.left < 0 || (uint32_t)nd.left >= n || seen[(size_t)nd.left]) return TT_ERR_INVALID_ARG;
+                seen[(size_t)nd.left] = 1;
+                leaves++;
+            } else if (nd.count == 0) {
+                if (nd.left <= i || (size_t)nd.left + 1 >= 2 * (size_t)n) return TT_ERR_INVALID_ARG;
+                stack.push_back(nd.left);
+                stack.push_back(nd.left + 1);
+            } else {
+                return TT_ERR_INVALID_ARG;
+            }
+        }
+        if (leaves != n) return TT_ERR_INVALID_ARG;
+        std::fill(seen.begin(), seen.end(), 0);
+        for (uint32_t k = 0; k < n; k++) {
+            if (final_indices[k] < 0 || (uint32_t)final_indices[k] >= n || seen[(size_t)final_indices[k]])
+                return TT_ERR_INVALID_ARG;
+            seen[(size_t)final_indices[k]] = 1;
+        }
+    }
+    tt_blas* b = new (std::nothrow) tt_blas();
+    if (!b) return TT_ERR_OOM;
+    st = blas_finish(P, bvh2, b);
+    if (st != TT_OK) {
+        delete b;
+        return st;
+    }
     b->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *out = b;
     return TT_OK;

@@ -160,6 +160,11 @@ class TTError(RuntimeError):
         self.status = status
 
 
+def _check(st: int, what: str):
+    if st != TT_OK:
+        raise TTError(st, what)
+
+
 def _ptr(a) -> Optional[int]:
     if a is None:
         return None
@@ -184,7 +189,8 @@ SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_f
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
                  "tt_synth_prop", "tt_synth_ground", "tt_synth_san_miguel", "tt_synth_mesh_view", "tt_synth_mesh_free",
-                 "tt_synth_mesh_from_arrays", "tt_blas_copy_leaf_order"]
+                 "tt_synth_mesh_from_arrays", "tt_blas_copy_leaf_order", "tt_blas_prepare_aabbs", "tt_bvh2_presort",
+                 "tt_blas_build_from_bvh2"]
 
 
 def scene_lib():
@@ -211,6 +217,9 @@ def scene_lib():
         L.tt_pack_octahedral.argtypes = [C.c_float, C.c_float, C.c_float]
         L.tt_pack_octahedral.restype = u32
         L.tt_bvh2_build.argtypes = [vp, u32, vp, vp, vp, vp]
+        L.tt_blas_prepare_aabbs.argtypes = [C.POINTER(MeshInput), vp]
+        L.tt_bvh2_presort.argtypes = [vp, u32, vp]
+        L.tt_blas_build_from_bvh2.argtypes = [C.POINTER(MeshInput), vp, vp, vp, vp, u32, C.POINTER(vp)]
         L.tt_dotnet_sort_by_key.argtypes = [vp, u32, vp]
         L.tt_dotnet_sort_by_key.restype = None
         L.tt_synth_cornell.argtypes = [C.POINTER(vp)]
@@ -267,6 +276,7 @@ def hip_lib():
         L.tt_scene_read_nodes.argtypes = [vp, u32, u32, vp]
         L.tt_scene_read_tris.argtypes = [vp, u32, u32, vp]
         L.tt_blas_refit.argtypes = [vp, C.POINTER(BlasRefitParams), vp, vp, vp]
+        L.tt_bvh2_build_device.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, C.POINTER(u32)]
         L.tt_sync.argtypes = [vp]
         L.tt_async_overflows.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_ctx_stream.argtypes = [vp]
@@ -410,16 +420,45 @@ class Mesh:
 class Blas:
     """A built ParentObject: CWBVH8 nodes + leaf-ordered CudaTriangles (ParentObject.BuildTotal)."""
 
-    def __init__(self, mesh: Mesh, lossy_scale=(1.0, 1.0, 1.0)):
+    def __init__(self, mesh: Mesh, lossy_scale=(1.0, 1.0, 1.0), engine: "Engine" = None, timings: dict = None):
+        """engine: run the BVH2 stage on that engine's GPU (tt_bvh2_build_device); the result is
+        byte-identical to the host build. timings (dict): filled with the stage times in seconds."""
         v = mesh.view()
         v.lossy_scale[:] = lossy_scale
         h = C.c_void_p()
-        st = scene_lib().tt_blas_build(C.byref(v), C.byref(h))
-        if st != TT_OK:
-            raise TTError(st, "tt_blas_build")
+        L = scene_lib()
+        if engine is None:
+            st = L.tt_blas_build(C.byref(v), C.byref(h))
+            if st != TT_OK:
+                raise TTError(st, "tt_blas_build")
+        else:
+            import time
+            t0 = time.perf_counter()
+            n = v.n_indices // 3
+            aabbs = np.zeros((n, 6), np.float32)
+            _check(L.tt_blas_prepare_aabbs(C.byref(v), aabbs.ctypes.data), "tt_blas_prepare_aabbs")
+            t1 = time.perf_counter()
+            pre = np.zeros((3, n), np.int32)
+            _check(L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data), "tt_bvh2_presort")
+            t2 = time.perf_counter()
+            fi = np.zeros(n, np.int32)
+            boxes = np.zeros((2 * n, 6), np.float32)
+            left = np.zeros(2 * n, np.int32)
+            count = np.zeros(2 * n, np.uint32)
+            depth = C.c_uint32(0)
+            st = engine.L.tt_bvh2_build_device(engine.h, aabbs.ctypes.data, n, pre.ctypes.data, fi.ctypes.data,
+                                               boxes.ctypes.data, left.ctypes.data, count.ctypes.data, C.byref(depth))
+            if st != TT_OK:
+                raise TTError(st, "tt_bvh2_build_device")
+            t3 = time.perf_counter()
+            _check(L.tt_blas_build_from_bvh2(C.byref(v), fi.ctypes.data, boxes.ctypes.data, left.ctypes.data,
+                                             count.ctypes.data, depth.value, C.byref(h)), "tt_blas_build_from_bvh2")
+            if timings is not None:
+                timings.update(prepare_s=t1 - t0, presort_s=t2 - t1, bvh2_device_s=t3 - t2,
+                               bvh8_s=time.perf_counter() - t3)
         self.h = h.value
         info = BlasInfo()
-        scene_lib().tt_blas_get_info(self.h, C.byref(info))
+        L.tt_blas_get_info(self.h, C.byref(info))
         self.info = info
 
     @property
