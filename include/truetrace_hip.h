@@ -314,6 +314,18 @@ tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, cons
                                int32_t* final_indices, float* node_aabbs, int32_t* node_left, uint32_t* node_count,
                                uint32_t* max_depth);
 
+/* The whole BLAS build after the host's presort on the GPU (row f4's builder half): the BVH2 stage
+ * above, then BVH8Builder (BVH8Builder.cs:30-392) -- the cost pass bottom up over the BVH2's levels,
+ * get_children / order_children / collapse top down over the CWBVH8's levels with the sequential
+ * depth-first node and triangle numbering recovered from per-subtree counts -- and Aggregate
+ * (CommonVars.cs:662-688). Outputs are byte-identical to tt_blas_build's: the 80-B nodes (capacity
+ * max_nodes >= n - 1 suffices), their count, cwbvh_indices (n: leaf position -> source triangle)
+ * and the BVH2 depth; tt_blas_build_from_cwbvh (truetrace_scene.h) assembles the tt_blas.
+ * TT_ERR_UNSUPPORTED where the reference's BVH8Builder.build fails. */
+tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
+                               tt_cwbvh_node* nodes, uint32_t max_nodes, uint32_t* n_nodes, int32_t* cwbvh_indices,
+                               uint32_t* bvh2_depth);
+
 /* Copies AggTris [first, first+count) back from HBM (e.g. after tt_blas_refit). */
 tt_status tt_scene_read_tris(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cuda_triangle* out);
 

@@ -61,6 +61,9 @@ tt_status tt_bvh2_presort(const float* aabbs_maxmin, uint32_t n, int32_t* presor
 tt_status tt_blas_build_from_bvh2(const tt_mesh_input* mesh, const int32_t* final_indices, const float* node_aabbs,
                                   const int32_t* node_left, const uint32_t* node_count, uint32_t bvh2_depth,
                                   tt_blas** out);
+/* ... or over finished CWBVH8 nodes + cwbvh_indices (tt_blas_build_device in truetrace_hip.h). */
+tt_status tt_blas_build_from_cwbvh(const tt_mesh_input* mesh, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                                   const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out);
 tt_status tt_blas_get_info(const tt_blas* b, tt_blas_info* info);
 /* Copies the packed nodes (80 B) and the leaf-ordered triangles (88 B). */
 tt_status tt_blas_copy(const tt_blas* b, tt_cwbvh_node* nodes, tt_cuda_triangle* tris);

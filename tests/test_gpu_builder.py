@@ -86,10 +86,11 @@ def test_device_bvh2_equals_host_bvh2(engine, name):
     assert depth == tthip.Blas(mesh).info.bvh2_depth
 
 
-@pytest.mark.parametrize("name", ["pedestal", "grid_40x25", "duplicates", "soup_50k"])
-def test_blas_built_with_device_bvh2_is_identical(engine, name):
+@pytest.mark.parametrize("stages", ["bvh2", "bvh2+bvh8"])
+@pytest.mark.parametrize("name", list(_meshes().keys()))
+def test_blas_built_on_the_device_is_identical(engine, name, stages):
     mesh = _meshes()[name]
-    _same_blas(tthip.Blas(mesh), tthip.Blas(mesh, engine=engine))
+    _same_blas(tthip.Blas(mesh), tthip.Blas(mesh, engine=engine, device_stages=stages))
 
 
 def test_sponza_c2_blas_device_build_identical_and_traces(engine):
@@ -97,4 +98,19 @@ def test_sponza_c2_blas_device_build_identical_and_traces(engine):
     t = {}
     a, b = tthip.Blas(mesh), tthip.Blas(mesh, engine=engine, timings=t)
     _same_blas(a, b)
-    assert set(t) == {"prepare_s", "presort_s", "bvh2_device_s", "bvh8_s"}
+    assert set(t) == {"prepare_s", "presort_s", "device_s", "assemble_s"}
+    # and the device-built BLAS traces exactly like the host-built one (the same buffers)
+    import ttconfigs as T
+    am = tthip.AssetManager()
+    am.add_parent(b, None, np.zeros(7, tthip.MAT_DTYPE))
+    sc = am.build()
+    W, H = 320, 180
+    c2w, ip = T.C2_VIEW.camera(W, H)
+    rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+    engine.upload(sc)
+    engine.generate(rays, c2w, ip, W, H, T.NEAR, T.FAR, jitter=1, frames=0, max_bounce=1)
+    import oracle_ctypes as O
+    ref = rays.copy()
+    engine.trace(rays, W * H, 0, T.FAR, W, H)
+    assert O.trace(sc, ref, W * H, 0, T.FAR, W, H, nthreads=8)[0] == 0
+    assert np.array_equal(rays["hits"], ref["hits"])

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""BLAS build times, host vs GPU BVH2 stage (row f4's builder half), on the BASELINE meshes:
+"""BLAS build times, host vs the GPU stages (row f4's builder half: BVH2 only, BVH2 + BVH8), on the BASELINE meshes:
 C2 Sponza-shaped (262k tris) and C5 San-Miguel-shaped (10M tris). Both builds must be byte-identical
 (nodes, leaf-ordered triangles, leaf order). Usage: build_bench.py [--meshes c2,c5]
 Prints one JSON document (commit under profiles/)."""
@@ -29,6 +29,12 @@ def main():
         t0 = time.perf_counter()
         host = tthip.Blas(mesh)
         t_host = time.perf_counter() - t0
+        tim2 = {}
+        t0 = time.perf_counter()
+        dev2 = tthip.Blas(mesh, engine=eng, timings=tim2, device_stages="bvh2")
+        t_dev2 = time.perf_counter() - t0
+        same2 = dev2.arrays()[0].tobytes() == host.arrays()[0].tobytes()
+        del dev2
         tim = {}
         t0 = time.perf_counter()
         dev = tthip.Blas(mesh, engine=eng, timings=tim)
@@ -38,8 +44,10 @@ def main():
         same = (nh.tobytes() == nd.tobytes() and th.tobytes() == td.tobytes()
                 and bool(np.array_equal(host.leaf_order(), dev.leaf_order())))
         row = {"mesh": name, "tris": host.n_tris, "cwbvh_nodes": host.n_nodes, "bvh2_depth": host.info.bvh2_depth,
-               "host_build_s": round(t_host, 3), "gpu_bvh2_build_s": round(t_dev, 3),
-               "gpu_stages_s": {k: round(v, 3) for k, v in tim.items()}, "identical": same}
+               "host_build_s": round(t_host, 3),
+               "device_bvh2_host_bvh8_s": round(t_dev2, 3), "device_bvh2_host_bvh8_stages_s": {k: round(v, 3) for k, v in tim2.items()},
+               "device_bvh2_bvh8_s": round(t_dev, 3), "device_bvh2_bvh8_stages_s": {k: round(v, 3) for k, v in tim.items()},
+               "identical": same and same2}
         out["rows"].append(row)
         print(f"[build] {row}", file=sys.stderr, flush=True)
         del host, dev

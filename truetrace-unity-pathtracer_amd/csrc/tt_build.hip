@@ -316,6 +316,313 @@ inline unsigned grid_of(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock)
 
 }  // namespace
 
+// ------------------------------------------------------------------------------- BVH8 stage
+// BVH8Builder (BVH8Builder.cs:30-392) restated for the GPU: the cost pass bottom up over the BVH2's
+// depth levels, the collapse top down over the CWBVH8's levels. The sequential collapse numbers the
+// nodes and the leaf triangles with two running counters in depth-first order; here each CWBVH8 node
+// first learns how many nodes (A) and triangles (T) its subtree allocates (bottom up), then its
+// counters on entry (top down), so every node is written independently with the reference's numbers.
+
+__device__ inline float surface_area_h(const Box& a) { return surface_area(a); }
+
+// BFS of the BVH2 from the root: lvl_out gets the internal children of the frontier's internal nodes
+__global__ void k_bvh2_level(int m, const int* __restrict__ frontier, const int* __restrict__ left,
+                             const uint32_t* __restrict__ count, int* __restrict__ next, int* __restrict__ n_next) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= m) return;
+    const int v = frontier[t];
+    if (count[v] > 0) return;
+    const int l = left[v];
+    const int o = atomicAdd(n_next, 2);
+    next[o] = l;
+    next[o + 1] = l + 1;
+}
+
+struct Dec {
+    int8_t type, dl, dr;  // 0 LEAF, 1 INTERNAL, 2 DISTRIBUTE
+};
+
+// calculate_cost (BVH8Builder.cs) of one BVH2 node whose children are done; nprim / firstpos: the
+// subtree's primitive count and first leaf position (count_primitives' range)
+__global__ void k_cost8(int m, const int* __restrict__ nodes_lvl, const Box* __restrict__ box, const int* __restrict__ left,
+                        const uint32_t* __restrict__ count, float* __restrict__ cost, Dec* __restrict__ dec,
+                        int* __restrict__ nprim, int* __restrict__ firstpos, int* __restrict__ err) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= m) return;
+    const int v = nodes_lvl[t];
+    const Box a = box[v];
+    if (count[v] > 0) {
+        const int np = (int)count[v];
+        nprim[v] = np;
+        firstpos[v] = left[v];
+        if (np != 1) {
+            atomicOr(err, 2);
+            return;
+        }
+        const float cl = surface_area(a) * (float)np;
+        for (int i = 0; i < 7; i++) {
+            cost[v * 7 + i] = cl;
+            dec[v * 7 + i] = Dec{0, 0, 0};
+        }
+        return;
+    }
+    const int l = left[v], r = l + 1;
+    const int np = nprim[l] + nprim[r];
+    nprim[v] = np;
+    firstpos[v] = firstpos[l];
+    const float cost_leaf = np <= 3 ? (float)np * surface_area(a) : FLT_MAX;
+    float cost_distribute = FLT_MAX;
+    int dist_left = -1, dist_right = -1;
+    for (int k = 0; k < 7; k++) {
+        const float c = cost[l * 7 + k] + cost[r * 7 + 6 - k];
+        if (c < cost_distribute) {
+            cost_distribute = c;
+            dist_left = k;
+            dist_right = 6 - k;
+        }
+    }
+    const float cost_internal = cost_distribute + surface_area(a);
+    Dec d0;
+    if (cost_leaf < cost_internal) {
+        cost[v * 7] = cost_leaf;
+        d0.type = 0;
+    } else {
+        cost[v * 7] = cost_internal;
+        d0.type = 1;
+    }
+    d0.dl = (int8_t)dist_left;
+    d0.dr = (int8_t)dist_right;
+    dec[v * 7] = d0;
+    Dec prev = d0;
+    for (int i = 1; i < 7; i++) {
+        float cd = cost[v * 7 + i - 1];
+        int dl = -1, dr = -1;
+        for (int k = 0; k < i; k++) {
+            const float c = cost[l * 7 + k] + cost[r * 7 + i - k - 1];
+            if (c < cd) {
+                cd = c;
+                dl = k;
+                dr = i - k - 1;
+            }
+        }
+        cost[v * 7 + i] = cd;
+        if (dl != -1) prev = Dec{2, (int8_t)dl, (int8_t)dr};
+        dec[v * 7 + i] = prev;
+    }
+}
+
+struct Rec8 {
+    int bvh2;       // the BVH2 node this CWBVH8 node collapses
+    int child[8];   // BVH2 children by slot (order_children), -1 empty
+    int crec[8];    // records of the internal children by internal rank
+    int k, t;       // internal children, triangles of the leaf children
+    int A, T;       // CWBVH8 nodes / triangles the subtree's collapse allocates
+    int idx, C, Ct; // node index, node and triangle counters on entry to collapse()
+};
+
+// get_children + order_children + the child checks of collapse() for one CWBVH8 node; appends its
+// internal children as records of the next level.
+__global__ void k_expand8(int lo, int hi, Rec8* __restrict__ rec, int* __restrict__ n_rec, const Box* __restrict__ box,
+                          const int* __restrict__ left, const uint32_t* __restrict__ count, const Dec* __restrict__ dec,
+                          const int* __restrict__ nprim, int* __restrict__ err) {
+    const int x = lo + blockIdx.x * kBlock + threadIdx.x;
+    if (x >= hi) return;
+    Rec8& R = rec[x];
+    const int N = R.bvh2;
+    int children[8];
+    int cc = 0;
+    bool ok = true;
+    if (count[N] > 0) {
+        children[cc++] = N;
+    } else {
+        int stn[24], sti[24], sp = 0;  // pending (node, i) expansions, processed depth first
+        stn[sp] = N;
+        sti[sp] = 0;
+        sp++;
+        bool root = true;
+        while (sp > 0 && ok) {
+            sp--;
+            const int v = stn[sp], i = sti[sp];
+            if (!root && dec[v * 7 + i].type != 2) {  // a plain child
+                if (cc >= 8) { ok = false; break; }
+                children[cc++] = v;
+                continue;
+            }
+            root = false;
+            const Dec d = dec[v * 7 + i];
+            if (!(d.dl >= 0 && d.dl < 7) || !(d.dr >= 0 && d.dr < 7) || cc >= 8) { ok = false; break; }
+            const int l = left[v];
+            stn[sp] = l + 1; sti[sp] = d.dr; sp++;  // right after left
+            stn[sp] = l; sti[sp] = d.dl; sp++;
+        }
+    }
+    if (!ok) { atomicOr(err, 4); return; }
+    // order_children: greedy slot assignment by octant direction costs
+    const Box nb = box[N];
+    const float px = (nb.mx[0] + nb.mn[0]) / 2.0f, py = (nb.mx[1] + nb.mn[1]) / 2.0f, pz = (nb.mx[2] + nb.mn[2]) / 2.0f;
+    float cost2[8][8];
+    for (int c = 0; c < cc; c++) {
+        const Box ca = box[children[c]];
+        const float dx = (ca.mx[0] + ca.mn[0]) / 2.0f - px, dy = (ca.mx[1] + ca.mn[1]) / 2.0f - py,
+                    dz = (ca.mx[2] + ca.mn[2]) / 2.0f - pz;
+        for (int s = 0; s < 8; s++) {
+            const float sx = ((s >> 2) & 1) ? -1.0f : 1.0f, sy = ((s >> 1) & 1) ? -1.0f : 1.0f, sz = (s & 1) ? -1.0f : 1.0f;
+            cost2[c][s] = dx * sx + dy * sy + dz * sz;
+        }
+    }
+    int assignment[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    bool slot_filled[8] = {false, false, false, false, false, false, false, false};
+    while (true) {
+        float min_cost = FLT_MAX;
+        int min_slot = -1, min_index = -1;
+        for (int c = 0; c < cc; c++) {
+            if (assignment[c] != -1) continue;
+            for (int s = 0; s < 8; s++) {
+                if (!slot_filled[s] && cost2[c][s] < min_cost) {
+                    min_cost = cost2[c][s];
+                    min_slot = s;
+                    min_index = c;
+                }
+            }
+        }
+        if (min_slot == -1) break;
+        slot_filled[min_slot] = true;
+        assignment[min_index] = min_slot;
+    }
+    int slots[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    for (int c = 0; c < cc; c++) {
+        if (assignment[c] < 0) { atomicOr(err, 8); return; }  // a child no slot could take (NaN boxes)
+        slots[assignment[c]] = children[c];
+    }
+    int k = 0, t = 0;
+    for (int s = 0; s < 8; s++) {
+        R.child[s] = slots[s];
+        const int c = slots[s];
+        if (c < 0) continue;
+        const int ty = dec[c * 7].type;
+        if (ty == 0) {
+            const int tc = nprim[c];
+            if (!(tc > 0 && tc <= 3)) { atomicOr(err, 16); return; }
+            t += tc;
+            if (t > 24) { atomicOr(err, 16); return; }
+        } else if (ty == 1) {
+            const int o = atomicAdd(n_rec, 1);
+            rec[o].bvh2 = c;
+            R.crec[k++] = o;
+        } else {
+            atomicOr(err, 32);
+            return;
+        }
+    }
+    R.k = k;
+    R.t = t;
+}
+
+__global__ void k_up8(int lo, int hi, Rec8* __restrict__ rec) {
+    const int x = lo + blockIdx.x * kBlock + threadIdx.x;
+    if (x >= hi) return;
+    Rec8& R = rec[x];
+    int A = R.k, T = R.t;
+    for (int r = 0; r < R.k; r++) {
+        A += rec[R.crec[r]].A;
+        T += rec[R.crec[r]].T;
+    }
+    R.A = A;
+    R.T = T;
+}
+
+__global__ void k_down8(int lo, int hi, Rec8* __restrict__ rec) {
+    const int x = lo + blockIdx.x * kBlock + threadIdx.x;
+    if (x >= hi) return;
+    const Rec8& R = rec[x];
+    int C = R.C + R.k, Ct = R.Ct + R.t;
+    for (int r = 0; r < R.k; r++) {
+        Rec8& c = rec[R.crec[r]];
+        c.idx = R.C + r;
+        c.C = C;
+        c.Ct = Ct;
+        C += c.A;
+        Ct += c.T;
+    }
+}
+
+// Mathf.Log2 / Ceil / Floor / Pow: float wrappers over System.Math (double)
+__device__ inline float mathf_log2(float f) { return (float)(log((double)f) / log(2.0)); }
+__device__ inline float mathf_ceil(float f) { return (float)ceil((double)f); }
+__device__ inline float mathf_floor(float f) { return (float)floor((double)f); }
+__device__ inline float mathf_pow2(float p) { return (float)pow(2.0, (double)p); }
+// (byte)(uint)x of a C# float (unchecked): truncate toward zero, wrap to 8 bits
+__device__ inline uint32_t to_byte(float x) {
+    if (!(x == x)) return 0u;
+    if (x <= -1.0f || x >= 4294967296.0f) return 0u;
+    return (uint32_t)x & 0xffu;
+}
+
+// collapse()'s node body + Aggregate (CommonVars.cs:662-688): the 80-B node at R.idx, and the leaf
+// children's primitives (count_primitives) at cwbvh_indices[R.Ct ...]
+__global__ void k_fill8(int m, const Rec8* __restrict__ rec, const Box* __restrict__ box, const Dec* __restrict__ dec,
+                        const int* __restrict__ nprim, const int* __restrict__ firstpos, const int* __restrict__ final_idx,
+                        tt_cwbvh_node* __restrict__ out, int* __restrict__ cwbvh_indices, int* __restrict__ err) {
+    const int x = blockIdx.x * kBlock + threadIdx.x;
+    if (x >= m) return;
+    const Rec8& R = rec[x];
+    const Box a = box[R.bvh2];
+    const float denom = 1.0f / (float)((1 << 8) - 1);
+    const float ex = mathf_pow2(mathf_ceil(mathf_log2((a.mx[0] - a.mn[0]) * denom)));
+    const float ey = mathf_pow2(mathf_ceil(mathf_log2((a.mx[1] - a.mn[1]) * denom)));
+    const float ez = mathf_pow2(mathf_ceil(mathf_log2((a.mx[2] - a.mn[2]) * denom)));
+    const float ox = 1.0f / ex, oy = 1.0f / ey, oz = 1.0f / ez;
+    const uint32_t ux = __float_as_uint(ex), uy = __float_as_uint(ey), uz = __float_as_uint(ez);
+    if ((ux & 0x807FFFFFu) || (uy & 0x807FFFFFu) || (uz & 0x807FFFFFu)) {
+        atomicOr(err, 64);
+        return;
+    }
+    uint32_t meta[2] = {0u, 0u}, qlx[2] = {0u, 0u}, qhx[2] = {0u, 0u}, qly[2] = {0u, 0u}, qhy[2] = {0u, 0u},
+             qlz[2] = {0u, 0u}, qhz[2] = {0u, 0u};
+    uint32_t imask = 0;
+    int internal = 0, tri = 0;
+    for (int s = 0; s < 8; s++) {
+        const int c = R.child[s];
+        if (c < 0) continue;
+        const Box ca = box[c];
+        const int w = s >> 2, sh = (s & 3) * 8;
+        qlx[w] |= to_byte(mathf_floor((ca.mn[0] - a.mn[0]) * ox)) << sh;
+        qly[w] |= to_byte(mathf_floor((ca.mn[1] - a.mn[1]) * oy)) << sh;
+        qlz[w] |= to_byte(mathf_floor((ca.mn[2] - a.mn[2]) * oz)) << sh;
+        qhx[w] |= to_byte(mathf_ceil((ca.mx[0] - a.mn[0]) * ox)) << sh;
+        qhy[w] |= to_byte(mathf_ceil((ca.mx[1] - a.mn[1]) * oy)) << sh;
+        qhz[w] |= to_byte(mathf_ceil((ca.mx[2] - a.mn[2]) * oz)) << sh;
+        uint32_t mb;
+        if (dec[c * 7].type == 0) {
+            const int tc = nprim[c], f = firstpos[c];
+            mb = 0u;
+            for (int j = 0; j < tc; j++) {
+                mb |= 1u << (j + 5);
+                cwbvh_indices[R.Ct + tri + j] = final_idx[f + j];
+            }
+            mb |= (uint32_t)tri;
+            tri += tc;
+        } else {
+            mb = (uint32_t)((internal + 24) | 0x20);
+            imask |= (1u << internal) & 0xffu;
+            internal++;
+        }
+        meta[w] |= (mb & 0xffu) << sh;
+    }
+    tt_cwbvh_node o;
+    o.p[0] = a.mn[0];
+    o.p[1] = a.mn[1];
+    o.p[2] = a.mn[2];
+    o.e_imask = (ux >> 23) | ((uy >> 23) << 8) | ((uz >> 23) << 16) | (imask << 24);
+    o.base_child = (uint32_t)R.C;
+    o.base_tri = (uint32_t)R.Ct;
+    o.meta[0] = meta[0]; o.meta[1] = meta[1];
+    o.qlo_x[0] = qlx[0]; o.qlo_x[1] = qlx[1]; o.qhi_x[0] = qhx[0]; o.qhi_x[1] = qhx[1];
+    o.qlo_y[0] = qly[0]; o.qlo_y[1] = qly[1]; o.qhi_y[0] = qhy[0]; o.qhi_y[1] = qhy[1];
+    o.qlo_z[0] = qlz[0]; o.qlo_z[1] = qlz[1]; o.qhi_z[0] = qhz[0]; o.qhi_z[1] = qhz[1];
+    out[R.idx] = o;
+}
+
 // exclusive-scan input: live children per segment (0 past the last segment, so base[S] = total)
 struct NextCount {
     const SplitOut* so;
@@ -329,14 +636,16 @@ struct NextCount {
         if (e_ != hipSuccess) return TT_ERR_HIP;  \
     } while (0)
 
-extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n_u, const int32_t* presorted,
-                                          int32_t* final_indices, float* node_aabbs, int32_t* node_left,
-                                          uint32_t* node_count, uint32_t* max_depth) {
-    if (!ctx || !aabbs || !n_u || !presorted || !final_indices || n_u >= (1u << 30)) return TT_ERR_INVALID_ARG;
-    const int n = (int)n_u;
-    hipStream_t st = tt_ctx_stream_of(ctx);
-    for (size_t i = 0; i < 3 * (size_t)n; i++)
-        if (presorted[i] < 0 || presorted[i] >= n) return TT_ERR_INVALID_ARG;
+// The BVH2 stage's result, left on the device for the BVH8 stage: BVH2Nodes (boxes, left, count; 2n
+// slots) and FinalIndices.
+struct Bvh2Dev {
+    DBuf<Box> box;
+    DBuf<int> left, final_idx;
+    DBuf<uint32_t> count;
+    uint32_t depth = 0;
+};
+
+static tt_status bvh2_stage(hipStream_t st, const float* aabbs, int n, const int32_t* presorted, Bvh2Dev& R) {
 
     // root box: Extend over the primitives in index order (BVH2Builder.cs: BVH2Nodes[0].aabb)
     Box root = box_init();
@@ -349,23 +658,27 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
     }
     const size_t n2 = 2 * (size_t)n;
     uint32_t depth = 0;
-    if (n == 1) {
-        if (node_aabbs) {
-            std::memset(node_aabbs, 0, n2 * sizeof(Box));
-            std::memcpy(node_aabbs, &root, sizeof(Box));
-        }
-        if (node_left) std::memset(node_left, 0, n2 * sizeof(int32_t));
-        if (node_count) {
-            std::memset(node_count, 0, n2 * sizeof(uint32_t));
-            node_count[0] = 1u;
-        }
-        final_indices[0] = presorted[0];
-        if (max_depth) *max_depth = 0;
+    TT_BH(R.box.alloc(n2));
+    TT_BH(R.left.alloc(n2));
+    TT_BH(R.count.alloc(n2));
+    TT_BH(R.final_idx.alloc(n));
+    if (n == 1) {  // BuildRecursive(0, 2, 0, 1, 0): the root is a leaf
+        const uint32_t one = 1u;
+        TT_BH(hipMemsetAsync(R.box.p, 0, n2 * sizeof(Box), st));
+        TT_BH(hipMemcpyAsync(R.box.p, &root, sizeof(Box), hipMemcpyHostToDevice, st));
+        TT_BH(hipMemsetAsync(R.left.p, 0, n2 * sizeof(int), st));
+        TT_BH(hipMemsetAsync(R.count.p, 0, n2 * sizeof(uint32_t), st));
+        TT_BH(hipMemcpyAsync(R.count.p, &one, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        TT_BH(hipMemcpyAsync(R.final_idx.p, presorted, sizeof(int), hipMemcpyHostToDevice, st));
+        TT_BH(hipStreamSynchronize(st));
+        R.depth = 0;
         return TT_OK;
     }
-    DBuf<Box> prims, pre, sufr, box, c_left, c_right;
-    DBuf<int> idxb[4], seg, lrank, nleft, c_pos, dimv, base, err;
-    DBuf<uint32_t> ncount;
+    DBuf<Box> prims, pre, sufr, c_left, c_right;
+    DBuf<int> idxb[4], seg, lrank, c_pos, dimv, base, err;
+    Box* box_p = R.box.p;
+    int* nleft_p = R.left.p;
+    uint32_t* ncount_p = R.count.p;
     DBuf<unsigned char> going_left;
     DBuf<Seg> segs, next;
     DBuf<SplitOut> so;
@@ -376,9 +689,6 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
     TT_BH(prims.alloc(n));
     TT_BH(pre.alloc(n));
     TT_BH(sufr.alloc(n));
-    TT_BH(box.alloc(n2));
-    TT_BH(nleft.alloc(n2));
-    TT_BH(ncount.alloc(n2));
     for (auto& b : idxb) TT_BH(b.alloc(n));
     TT_BH(seg.alloc(n));
     TT_BH(lrank.alloc(n));
@@ -401,10 +711,10 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
     TT_BH(hipMemcpyAsync(prims.p, aabbs, (size_t)n * sizeof(Box), hipMemcpyHostToDevice, st));
     for (int d = 0; d < 3; d++)
         TT_BH(hipMemcpyAsync(idx[d], presorted + (size_t)d * n, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
-    TT_BH(hipMemsetAsync(box.p, 0, n2 * sizeof(Box), st));  // NativeArrayOptions.ClearMemory
-    TT_BH(hipMemcpyAsync(box.p, &root, sizeof(Box), hipMemcpyHostToDevice, st));
-    TT_BH(hipMemsetAsync(nleft.p, 0, n2 * sizeof(int), st));
-    TT_BH(hipMemsetAsync(ncount.p, 0, n2 * sizeof(uint32_t), st));
+    TT_BH(hipMemsetAsync(box_p, 0, n2 * sizeof(Box), st));  // NativeArrayOptions.ClearMemory
+    TT_BH(hipMemcpyAsync(box_p, &root, sizeof(Box), hipMemcpyHostToDevice, st));
+    TT_BH(hipMemsetAsync(nleft_p, 0, n2 * sizeof(int), st));
+    TT_BH(hipMemsetAsync(ncount_p, 0, n2 * sizeof(uint32_t), st));
     TT_BH(hipMemsetAsync(seg.p, 0, (size_t)n * sizeof(int), st));  // every position in segment 0 (the root)
     TT_BH(hipMemsetAsync(err.p, 0, sizeof(int), st));
     const Seg root_seg{0, 2, 0, n};
@@ -456,7 +766,7 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
                                c_left.p + (size_t)d * S, c_right.p + (size_t)d * S);
         }
         hipLaunchKernelGGL(k_split, dim3(grid_of(S)), dim3(kBlock), 0, st, S, segs.p, c_cost.p, c_pos.p, c_left.p,
-                           c_right.p, so.p, box.p, nleft.p, ncount.p, err.p);
+                           c_right.p, so.p, box_p, nleft_p, ncount_p, err.p);
         size_t t = tb;
         auto nc = rocprim::make_transform_iterator(cnt, NextCount{so.p, S});
         TT_BH(rocprim::exclusive_scan(tstore.p, t, nc, base.p, 0, (size_t)S + 1, rocprim::plus<int>(), st));
@@ -484,11 +794,134 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
         std::swap(segs.p, next.p);
         S = h[0];
     }
-    TT_BH(hipMemcpyAsync(final_indices, idx[0], (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
-    if (node_aabbs) TT_BH(hipMemcpyAsync(node_aabbs, box.p, n2 * sizeof(Box), hipMemcpyDeviceToHost, st));
-    if (node_left) TT_BH(hipMemcpyAsync(node_left, nleft.p, n2 * sizeof(int), hipMemcpyDeviceToHost, st));
-    if (node_count) TT_BH(hipMemcpyAsync(node_count, ncount.p, n2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    TT_BH(hipMemcpyAsync(R.final_idx.p, idx[0], (size_t)n * sizeof(int), hipMemcpyDeviceToDevice, st));
     TT_BH(hipStreamSynchronize(st));
-    if (max_depth) *max_depth = depth;
+    R.depth = depth;
+    return TT_OK;
+}
+
+static tt_status check_inputs(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted) {
+    if (!ctx || !aabbs || !n || !presorted || n >= (1u << 30)) return TT_ERR_INVALID_ARG;
+    for (size_t i = 0; i < 3 * (size_t)n; i++)
+        if (presorted[i] < 0 || (uint32_t)presorted[i] >= n) return TT_ERR_INVALID_ARG;
+    return TT_OK;
+}
+
+extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
+                                          int32_t* final_indices, float* node_aabbs, int32_t* node_left,
+                                          uint32_t* node_count, uint32_t* max_depth) {
+    tt_status s = check_inputs(ctx, aabbs, n, presorted);
+    if (s != TT_OK || !final_indices) return s != TT_OK ? s : TT_ERR_INVALID_ARG;
+    hipStream_t st = tt_ctx_stream_of(ctx);
+    Bvh2Dev R;
+    if ((s = bvh2_stage(st, aabbs, (int)n, presorted, R)) != TT_OK) return s;
+    const size_t n2 = 2 * (size_t)n;
+    TT_BH(hipMemcpyAsync(final_indices, R.final_idx.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (node_aabbs) TT_BH(hipMemcpyAsync(node_aabbs, R.box.p, n2 * sizeof(Box), hipMemcpyDeviceToHost, st));
+    if (node_left) TT_BH(hipMemcpyAsync(node_left, R.left.p, n2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (node_count) TT_BH(hipMemcpyAsync(node_count, R.count.p, n2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    TT_BH(hipStreamSynchronize(st));
+    if (max_depth) *max_depth = R.depth;
+    return TT_OK;
+}
+
+extern "C" tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
+                                          tt_cwbvh_node* nodes, uint32_t max_nodes, uint32_t* n_nodes,
+                                          int32_t* cwbvh_indices, uint32_t* bvh2_depth) {
+    tt_status s = check_inputs(ctx, aabbs, n, presorted);
+    if (s != TT_OK) return s;
+    if (!nodes || !n_nodes || !cwbvh_indices) return TT_ERR_INVALID_ARG;
+    hipStream_t st = tt_ctx_stream_of(ctx);
+    Bvh2Dev B;
+    if ((s = bvh2_stage(st, aabbs, (int)n, presorted, B)) != TT_OK) return s;
+    const size_t n2 = 2 * (size_t)n;
+    // BVH2 levels, root first (for the bottom-up cost pass)
+    DBuf<int> order, cnt1, err;
+    TT_BH(order.alloc(n2));
+    TT_BH(cnt1.alloc(1));
+    TT_BH(err.alloc(1));
+    TT_BH(hipMemsetAsync(err.p, 0, sizeof(int), st));
+    const int zero = 0;
+    TT_BH(hipMemcpyAsync(order.p, &zero, sizeof(int), hipMemcpyHostToDevice, st));
+    std::vector<int> lvl{0, 1};
+    while (lvl.back() > lvl[lvl.size() - 2]) {
+        const int lo = lvl[lvl.size() - 2], hi = lvl.back();
+        TT_BH(hipMemcpyAsync(cnt1.p, &zero, sizeof(int), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_bvh2_level, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, hi - lo, order.p + lo, B.left.p,
+                           B.count.p, order.p + hi, cnt1.p);
+        int m = 0;
+        TT_BH(hipMemcpyAsync(&m, cnt1.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        TT_BH(hipStreamSynchronize(st));
+        if ((size_t)hi + (size_t)m > n2) return TT_ERR_INVALID_ARG;
+        lvl.push_back(hi + m);
+    }
+    // cost pass, deepest level first
+    DBuf<float> cost;
+    DBuf<Dec> dec;
+    DBuf<int> nprim, firstpos;
+    TT_BH(cost.alloc(n2 * 7));
+    TT_BH(dec.alloc(n2 * 7));
+    TT_BH(nprim.alloc(n2));
+    TT_BH(firstpos.alloc(n2));
+    for (size_t L = lvl.size() - 1; L-- > 0;) {
+        const int lo = lvl[L], hi = lvl[L + 1];
+        if (hi > lo)
+            hipLaunchKernelGGL(k_cost8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, hi - lo, order.p + lo, B.box.p,
+                               B.left.p, B.count.p, cost.p, dec.p, nprim.p, firstpos.p, err.p);
+    }
+    // collapse: CWBVH8 levels top down (records appended per level)
+    const size_t cap = std::max<size_t>(1, (size_t)n);
+    DBuf<Rec8> rec;
+    DBuf<int> nrec;
+    TT_BH(rec.alloc(cap));
+    TT_BH(nrec.alloc(1));
+    Rec8 root{};
+    root.bvh2 = 0;
+    root.idx = 0;
+    root.C = 1;
+    root.Ct = 0;
+    const int one = 1;
+    TT_BH(hipMemcpyAsync(rec.p, &root, sizeof(Rec8), hipMemcpyHostToDevice, st));
+    TT_BH(hipMemcpyAsync(nrec.p, &one, sizeof(int), hipMemcpyHostToDevice, st));
+    std::vector<int> r8{0, 1};
+    while (r8.back() > r8[r8.size() - 2]) {
+        const int lo = r8[r8.size() - 2], hi = r8.back();
+        hipLaunchKernelGGL(k_expand8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, lo, hi, rec.p, nrec.p, B.box.p,
+                           B.left.p, B.count.p, dec.p, nprim.p, err.p);
+        int h[2] = {0, 0};
+        TT_BH(hipMemcpyAsync(&h[0], nrec.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        TT_BH(hipMemcpyAsync(&h[1], err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        TT_BH(hipStreamSynchronize(st));
+        if (h[1]) return TT_ERR_UNSUPPORTED;  // BVH8Builder.build returns false on the same inputs
+        if ((size_t)h[0] > cap) return TT_ERR_UNSUPPORTED;
+        r8.push_back(h[0]);
+    }
+    const int total = r8.back();
+    if ((uint32_t)total > max_nodes) return TT_ERR_INVALID_ARG;
+    for (size_t L = r8.size() - 1; L-- > 0;) {
+        const int lo = r8[L], hi = r8[L + 1];
+        if (hi > lo) hipLaunchKernelGGL(k_up8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, lo, hi, rec.p);
+    }
+    for (size_t L = 0; L + 1 < r8.size(); L++) {
+        const int lo = r8[L], hi = r8[L + 1];
+        if (hi > lo) hipLaunchKernelGGL(k_down8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, lo, hi, rec.p);
+    }
+    DBuf<tt_cwbvh_node> out;
+    DBuf<int> idxo;
+    TT_BH(out.alloc((size_t)total));
+    TT_BH(idxo.alloc(n));
+    TT_BH(hipMemsetAsync(out.p, 0, (size_t)total * sizeof(tt_cwbvh_node), st));
+    TT_BH(hipMemsetAsync(idxo.p, 0, (size_t)n * sizeof(int), st));
+    hipLaunchKernelGGL(k_fill8, dim3(grid_of(total)), dim3(kBlock), 0, st, total, rec.p, B.box.p, dec.p, nprim.p,
+                       firstpos.p, B.final_idx.p, out.p, idxo.p, err.p);
+    TT_BH(hipGetLastError());
+    int e = 0;
+    TT_BH(hipMemcpyAsync(&e, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    TT_BH(hipMemcpyAsync(nodes, out.p, (size_t)total * sizeof(tt_cwbvh_node), hipMemcpyDeviceToHost, st));
+    TT_BH(hipMemcpyAsync(cwbvh_indices, idxo.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+    TT_BH(hipStreamSynchronize(st));
+    if (e) return TT_ERR_UNSUPPORTED;
+    *n_nodes = (uint32_t)total;
+    if (bvh2_depth) *bvh2_depth = B.depth;
     return TT_OK;
 }

@@ -1037,6 +1037,36 @@ tt_status tt_blas_build_from_bvh2(const tt_mesh_input* m, const int32_t* final_i
     return TT_OK;
 }
 
+tt_status tt_blas_build_from_cwbvh(const tt_mesh_input* m, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                                   const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out) {
+    if (!out || !nodes || !n_nodes || !cwbvh_indices) return TT_ERR_INVALID_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    BlasPrep P;
+    tt_status st = blas_prepare(m, P);
+    if (st != TT_OK) return st;
+    const uint32_t ntri = (uint32_t)P.agg.size();
+    std::vector<char> seen(ntri, 0);
+    for (uint32_t i = 0; i < ntri; i++) {
+        const int32_t k = cwbvh_indices[i];
+        if (k < 0 || (uint32_t)k >= ntri || seen[(size_t)k]) return TT_ERR_INVALID_ARG;
+        seen[(size_t)k] = 1;
+    }
+    tt_blas* b = new (std::nothrow) tt_blas();
+    if (!b) return TT_ERR_OOM;
+    b->aabb_untransformed = P.aabb_untransformed;
+    b->bvh2_depth = bvh2_depth;
+    b->tris.resize(ntri);
+    b->leaf_of.assign(ntri, 0);
+    for (uint32_t i = 0; i < ntri; i++) {
+        b->tris[i] = P.agg[(size_t)cwbvh_indices[i]];
+        b->leaf_of[(size_t)cwbvh_indices[i]] = (int32_t)i;
+    }
+    b->nodes.assign(nodes, nodes + n_nodes);
+    b->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    *out = b;
+    return TT_OK;
+}
+
 tt_status tt_blas_copy_leaf_order(const tt_blas* b, int32_t* out) {
     if (!b || !out) return TT_ERR_INVALID_ARG;
     std::copy(b->leaf_of.begin(), b->leaf_of.end(), out);

@@ -190,7 +190,7 @@ SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_f
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
                  "tt_synth_prop", "tt_synth_ground", "tt_synth_san_miguel", "tt_synth_mesh_view", "tt_synth_mesh_free",
                  "tt_synth_mesh_from_arrays", "tt_blas_copy_leaf_order", "tt_blas_prepare_aabbs", "tt_bvh2_presort",
-                 "tt_blas_build_from_bvh2"]
+                 "tt_blas_build_from_bvh2", "tt_blas_build_from_cwbvh"]
 
 
 def scene_lib():
@@ -220,6 +220,7 @@ def scene_lib():
         L.tt_blas_prepare_aabbs.argtypes = [C.POINTER(MeshInput), vp]
         L.tt_bvh2_presort.argtypes = [vp, u32, vp]
         L.tt_blas_build_from_bvh2.argtypes = [C.POINTER(MeshInput), vp, vp, vp, vp, u32, C.POINTER(vp)]
+        L.tt_blas_build_from_cwbvh.argtypes = [C.POINTER(MeshInput), vp, u32, vp, u32, C.POINTER(vp)]
         L.tt_dotnet_sort_by_key.argtypes = [vp, u32, vp]
         L.tt_dotnet_sort_by_key.restype = None
         L.tt_synth_cornell.argtypes = [C.POINTER(vp)]
@@ -277,6 +278,7 @@ def hip_lib():
         L.tt_scene_read_tris.argtypes = [vp, u32, u32, vp]
         L.tt_blas_refit.argtypes = [vp, C.POINTER(BlasRefitParams), vp, vp, vp]
         L.tt_bvh2_build_device.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, C.POINTER(u32)]
+        L.tt_blas_build_device.argtypes = [vp, vp, u32, vp, vp, u32, C.POINTER(u32), vp, C.POINTER(u32)]
         L.tt_sync.argtypes = [vp]
         L.tt_async_overflows.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_ctx_stream.argtypes = [vp]
@@ -420,9 +422,11 @@ class Mesh:
 class Blas:
     """A built ParentObject: CWBVH8 nodes + leaf-ordered CudaTriangles (ParentObject.BuildTotal)."""
 
-    def __init__(self, mesh: Mesh, lossy_scale=(1.0, 1.0, 1.0), engine: "Engine" = None, timings: dict = None):
-        """engine: run the BVH2 stage on that engine's GPU (tt_bvh2_build_device); the result is
-        byte-identical to the host build. timings (dict): filled with the stage times in seconds."""
+    def __init__(self, mesh: Mesh, lossy_scale=(1.0, 1.0, 1.0), engine: "Engine" = None, timings: dict = None,
+                 device_stages: str = "bvh2+bvh8"):
+        """engine: build on that engine's GPU after the host's presort -- device_stages "bvh2+bvh8"
+        (tt_blas_build_device) or "bvh2" (tt_bvh2_build_device, BVH8 on the host); either way the
+        result is byte-identical to the host build. timings (dict): the stage times in seconds."""
         v = mesh.view()
         v.lossy_scale[:] = lossy_scale
         h = C.c_void_p()
@@ -441,6 +445,26 @@ class Blas:
             pre = np.zeros((3, n), np.int32)
             _check(L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data), "tt_bvh2_presort")
             t2 = time.perf_counter()
+            if device_stages == "bvh2+bvh8":
+                cap = max(1, n - 1)
+                nodes = np.zeros(cap, NODE_DTYPE)
+                cw = np.zeros(n, np.int32)
+                nn, depth = C.c_uint32(0), C.c_uint32(0)
+                st = engine.L.tt_blas_build_device(engine.h, aabbs.ctypes.data, n, pre.ctypes.data, nodes.ctypes.data,
+                                                   cap, C.byref(nn), cw.ctypes.data, C.byref(depth))
+                if st != TT_OK:
+                    raise TTError(st, "tt_blas_build_device")
+                t3 = time.perf_counter()
+                _check(L.tt_blas_build_from_cwbvh(C.byref(v), nodes.ctypes.data, nn.value, cw.ctypes.data, depth.value,
+                                                  C.byref(h)), "tt_blas_build_from_cwbvh")
+                if timings is not None:
+                    timings.update(prepare_s=t1 - t0, presort_s=t2 - t1, device_s=t3 - t2,
+                                   assemble_s=time.perf_counter() - t3)
+                self.h = h.value
+                info = BlasInfo()
+                L.tt_blas_get_info(self.h, C.byref(info))
+                self.info = info
+                return
             fi = np.zeros(n, np.int32)
             boxes = np.zeros((2 * n, 6), np.float32)
             left = np.zeros(2 * n, np.int32)
