@@ -405,6 +405,9 @@ def main():
     assert eng.stream == stream.cuda_stream == torch.cuda.current_stream(dev).cuda_stream != 0, \
         "engine and torch must share one (non-NULL) stream"
     eng.upload(scene)
+    # the BASELINE meshes of >= 100k triangles built later (aux configs, C5 tiles) use the GPU BLAS
+    # builder (tt_blas_build_device, byte-identical to the host build; tests/test_gpu_builder.py)
+    tthip.set_build_engine(eng, min_tris=100_000)
 
     # ------------------------------------------------------------------ resident rays
     rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)

@@ -419,6 +419,17 @@ class Mesh:
             self.h = None
 
 
+_BUILD_ENGINE = None
+_BUILD_MIN_TRIS = 0
+
+
+def set_build_engine(engine: "Engine" = None, min_tris: int = 100_000):
+    """Route every later Blas(mesh) of at least ``min_tris`` triangles through ``engine``'s GPU
+    (tt_blas_build_device; byte-identical to the host build). None: host builds again."""
+    global _BUILD_ENGINE, _BUILD_MIN_TRIS
+    _BUILD_ENGINE, _BUILD_MIN_TRIS = engine, int(min_tris)
+
+
 class Blas:
     """A built ParentObject: CWBVH8 nodes + leaf-ordered CudaTriangles (ParentObject.BuildTotal)."""
 
@@ -431,6 +442,8 @@ class Blas:
         v.lossy_scale[:] = lossy_scale
         h = C.c_void_p()
         L = scene_lib()
+        if engine is None and _BUILD_ENGINE is not None and v.n_indices // 3 >= _BUILD_MIN_TRIS:
+            engine = _BUILD_ENGINE
         if engine is None:
             st = L.tt_blas_build(C.byref(v), C.byref(h))
             if st != TT_OK:
