@@ -125,6 +125,12 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern unsafe TTStatus tt_blas_refit(IntPtr ctx, ref TTBlasRefitParams p, float* vertices,
             int* indices, int* leafOfTriangle);
         [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
+        // ParentObject.BuildTotal's BVH2Builder + BVH8Builder + Aggregate on the GPU, after the host's presort
+        // (byte-identical to the C# build): triangle AABBs {max, min}, 3 x n presorted indices, nodes out.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_blas_build_device(IntPtr ctx, float* aabbs, uint n,
+            int* presorted, void* nodes, uint maxNodes, out uint nNodes, int* cwbvhIndices, out uint bvh2Depth);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_bvh2_build_device(IntPtr ctx, float* aabbs, uint n,
+            int* presorted, int* finalIndices, float* nodeAabbs, int* nodeLeft, uint* nodeCount, out uint maxDepth);
     }
 
     /// Replaces `cmd.DispatchCompute(IntersectionShader, TraceKernel, CurBounceInfoBuffer, 0)`
