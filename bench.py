@@ -352,6 +352,10 @@ def main():
                          "to ranks, each traces its pixels and their bounce-1 rays, and the primary hit records are "
                          "RCCL-gathered to rank 0 inside every timed step (strong scaling). sample: every rank "
                          "traces its own full-frame sample, no collective (weak scaling)")
+    ap.add_argument("--parts", type=int, default=2,
+                    help="N > 1 (tiles): a rank's tiles are traced as this many tile-interleaved parts, each by its "
+                         "own engine on its own stream (each part's bounce-1 after its own primary), so one part's "
+                         "launch drain overlaps the other parts' work (tools/exp_streams.py). N = 1: one launch per bounce")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     ap.add_argument("--no-recur", action="store_true",
                     help="skip the auxiliary unjittered (UseReCur) primary + bounce launches (profiling runs: they "
@@ -422,60 +426,92 @@ def main():
     # its screen column x = W/2 has direction.z == -0.0 exactly, whose NaN z slabs make ~1,000 rays
     # walk ~900 nodes each (tools/long_rays.py). The sample layout jitters with frames = rank.
     jitter, frames = 1, (rank if (world > 1 and not tiles) else 0)
-    if tiles:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), at the buffer's start
-        pix = torch.from_numpy(ttdist.tile_pixels(W, H, world, rank)).to(dev)
-        n_prim = int(pix.shape[0])
+    P = max(1, args.parts) if tiles else 1
+
+    class Part:  # one launch stream of this rank: its engine, stream, rays and counts
+        pass
+
+    parts = []
+    if tiles:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), split into P parts
         full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
-        rays.view(2 * WH, 48)[:n_prim] = full.view(WH, 48)[pix]
+        for s, pix_np in enumerate(ttdist.part_pixels(W, H, world, rank, P)):
+            p = Part()
+            if s == 0:
+                p.eng, p.stream, p.rays = eng, stream, rays
+            else:
+                p.stream = torch.cuda.Stream(dev)
+                p.eng = tthip.Engine(gpu, stream=p.stream.cuda_stream)
+                p.eng.upload(scene)
+                p.rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            pix = torch.from_numpy(pix_np).to(dev)
+            p.n = int(pix.shape[0])
+            p.rays.view(2 * WH, 48)[:p.n] = full.view(WH, 48)[pix]
+            parts.append(p)
         del full
+        torch.cuda.synchronize(dev)  # the other parts' engines run on their own streams
     else:
-        n_prim = WH
+        p = Part()
+        p.eng, p.stream, p.rays, p.n = eng, stream, rays, WH
         eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
-    s_prim = eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, stats=True)
-    nb = eng.enqueue_bounce(rays, n_prim, 0, far, W, H, frames=frames, max_bounce=1, device=True)
-    s_bnc = eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
+        parts.append(p)
+    for p in parts:
+        p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, stats=True)
+        p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+        p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
+        p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
     torch.cuda.synchronize(dev)
+    n_prim, nb = sum(p.n for p in parts), sum(p.nb for p in parts)
     rays_per_step = n_prim + nb
-    B_prim = alg_bytes(s_prim, 0, n_prim)
-    B_bnc = alg_bytes(s_bnc, 1, nb)
-    log(f"rank {rank}: primary {n_prim} rays nodes/ray {s_prim.node_visits / max(n_prim, 1):.2f} "
-        f"tris/ray {s_prim.tri_tests / max(n_prim, 1):.2f} "
-        f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(nb, 1):.2f} "
-        f"tris/ray {s_bnc.tri_tests / max(nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}")
+    s_prim, s_bnc = parts[0].s_prim, parts[0].s_bnc
+    B_prim = alg_bytes(s_prim, 0, parts[0].n)  # the roofline is part 0's launches' (the engine ring below)
+    B_bnc = alg_bytes(s_bnc, 1, parts[0].nb)
+    log(f"rank {rank}: primary {n_prim} rays nodes/ray {s_prim.node_visits / max(parts[0].n, 1):.2f} "
+        f"tris/ray {s_prim.tri_tests / max(parts[0].n, 1):.2f} "
+        f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(parts[0].nb, 1):.2f} "
+        f"tris/ray {s_bnc.tri_tests / max(parts[0].nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}"
+        f"; parts {P}")
 
     # tiles: the frame's primary hit records go to rank 0 in one gather per step (shards padded to
-    # the largest so every rank sends one equal-size message). The gather runs on its own stream,
-    # overlapped with the bounce-1 trace (which reads and writes only the other half of the
-    # ping-pong buffer); the step ends when both are done, so the timed step includes the collective.
+    # the largest so every rank sends one equal-size message; a rank's parts back to back). The
+    # gather runs on its own stream, overlapped with the bounce-1 traces (which read and write only
+    # the other half of the ping-pong buffers); the step ends when both are done, so the timed step
+    # includes the collective.
     sizes, hits_buf, gather_list, comm = None, None, None, None
     if tiles:
-        n_t = torch.tensor([n_prim], dtype=torch.int64, device=red_dev)
+        n_t = torch.tensor([p.n for p in parts], dtype=torch.int64, device=red_dev)
         sz = [torch.zeros_like(n_t) for _ in range(world)]
         dist.all_gather(sz, n_t)
-        sizes = [int(x.item()) for x in sz]
-        hits_buf = torch.zeros((max(sizes), 4), dtype=torch.int32, device=red_dev)
+        sizes = [[int(v) for v in x.tolist()] for x in sz]
+        hits_buf = torch.zeros((max(sum(x) for x in sizes), 4), dtype=torch.int32, device=red_dev)
         gather_list = [torch.empty_like(hits_buf) for _ in range(world)] if rank == 0 else None
         comm = torch.cuda.Stream(dev)
-    prim_hits = rays[: n_prim * 48].view(n_prim, 48)[:, 32:48].view(torch.int32)
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
 
     def step():
-        eng.trace(rays, n_prim, 0, far, W, H, info=info, device=True, asynchronous=True)
+        for p in parts:
+            p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True)
         if tiles:
-            comm.wait_stream(stream)  # the primary hit records are final
+            for p in parts:
+                comm.wait_stream(p.stream)  # the primary hit records are final
             with torch.cuda.stream(comm):
-                hits_buf[:n_prim].copy_(prim_hits)
+                o = 0
+                for p in parts:
+                    hits_buf[o:o + p.n].copy_(p.prim_hits)
+                    o += p.n
                 dist.gather(hits_buf, gather_list, dst=0)
-        eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+        for p in parts:
+            p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
         if tiles:
-            stream.wait_stream(comm)  # the next step's primary trace rewrites the gathered half
+            for p in parts:
+                p.stream.wait_stream(comm)  # the next step's primary trace rewrites the gathered half
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    eng.timing_reset()
+    for p in parts:
+        p.eng.timing_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -488,6 +524,8 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     launch_ms = eng.timing_read()
+    for p in parts[1:]:
+        assert len(p.eng.timing_read()) == 2 * args.steps
     assert len(launch_ms) == 2 * args.steps, (len(launch_ms), args.steps)
     total_rays = float(rays_per_step * args.steps)
     trace_ms_rank = float(np.sum(launch_ms)) / args.steps
@@ -512,7 +550,7 @@ def main():
     # tiles: SURVEY 8(e) parity -- the gathered frame must equal one GPU tracing the whole frame
     gather_parity = None
     if tiles and rank == 0:
-        frame = ttdist.assemble_tiles([g[:n] for g, n in zip(gather_list, sizes)], W, H, world)
+        frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
         one = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         eng.trace(one, WH, 0, far, W, H, device=True)
@@ -521,6 +559,8 @@ def main():
         del one
         log(f"gathered frame: {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels, "
             f"identical to a single-GPU trace: {gather_parity}")
+    for p in parts[1:]:
+        p.eng.close()
 
     # secondary N > 1 layout: every rank traces its own full-frame jittered sample (weak scaling)
     sample_sharded = None
@@ -581,7 +621,7 @@ def main():
     # pristine rays (occluded rays get t = 0 in place) on the shared stream; only the kernel is timed.
     shadow = None
     if not args.no_shadow:
-        sr = nee_rays(torch, rays, n_prim, far, light=(0.0, 9.0, 0.5))
+        sr = nee_rays(torch, rays, parts[0].n, far, light=(0.0, 9.0, 0.5))  # part 0's primary hits
         ns = int(sr.shape[0]) // 48
         work = torch.empty_like(sr)
         work.copy_(sr)
@@ -681,12 +721,15 @@ def main():
                    "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "jitter": jitter,
                    "seed": hex(args.seed),
                    "parallelism": ("single GPU, full frame" if world == 1 else
-                                   (f"64x64 screen tiles round-robin over {world} ranks + one RCCL gather of the "
+                                   (f"64x64 screen tiles round-robin over {world} ranks, each rank's tiles as {P} "
+                                    f"tile-interleaved parts on {P} streams, + one RCCL gather of the "
                                     f"primary hit records to rank 0 per step (inside the timed step"
                                     + (", overlapped with the bounce-1 trace on a second stream)" if gather_overlapped
                                        else ")") if tiles
                                     else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
-                   "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it",
+                   "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it"
+                             + (f" (part 0 of {P}: its launches overlap the other parts')" if P > 1 else ""),
+                   "parts_per_rank": P,
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
                    "trace_ms_primary_median": round(float(np.median(prim_ms)), 4),

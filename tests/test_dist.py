@@ -75,3 +75,21 @@ def test_gloo_two_rank_tile_shard_and_gather():
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) is True
+
+
+def test_part_split_partitions_each_rank_and_reassembles():
+    """bench.py --parts: a rank's tiles split into tile-interleaved parts traced on concurrent
+    streams; the parts cover the rank's pixels exactly and the per-rank blocks (parts back to back)
+    reassemble into the screen."""
+    W, H = 1920, 1080
+    for world, parts in ((2, 2), (8, 2), (4, 3), (1, 2)):
+        frame = np.zeros((W * H, 4), np.uint32)
+        frame[:, 0] = np.arange(W * H, dtype=np.uint32)  # every pixel's record names its pixel
+        blocks, sizes = [], []
+        for r in range(world):
+            ps = ttdist.part_pixels(W, H, world, r, parts)
+            assert np.array_equal(np.sort(np.concatenate(ps)), np.sort(ttdist.tile_pixels(W, H, world, r)))
+            blocks.append(np.concatenate([frame[p] for p in ps]))
+            sizes.append([len(p) for p in ps])
+        got = ttdist.assemble_parts(blocks, sizes, W, H, world, parts)
+        assert np.array_equal(got, frame)

@@ -69,3 +69,25 @@ def assemble_tiles(parts, width: int, height: int, world: int, tile: int = 64) -
         arr = part.cpu().numpy() if hasattr(part, "cpu") else np.asarray(part)
         full[pix] = arr.view(np.uint32).reshape(-1, 4)
     return full
+
+
+def part_pixels(width: int, height: int, world: int, rank: int, parts: int, tile: int = 64):
+    """A rank's tiles split into ``parts`` tile-interleaved parts (traced on concurrent streams):
+    part s of rank r is virtual rank s * world + r of world * parts, so the union over s is exactly
+    tile_pixels(width, height, world, rank)."""
+    return [tile_pixels(width, height, world * parts, s * world + rank, tile) for s in range(parts)]
+
+
+def assemble_parts(gathered, part_sizes, width: int, height: int, world: int, parts: int, tile: int = 64) -> np.ndarray:
+    """Screen-order hit records from one gathered block per rank: rank r's block holds its parts'
+    records back to back (part_sizes[r][s] records each)."""
+    virt = [None] * (world * parts)
+    for r in range(world):
+        arr = gathered[r].cpu().numpy() if hasattr(gathered[r], "cpu") else np.asarray(gathered[r])
+        arr = arr.view(np.uint32).reshape(-1, 4)
+        o = 0
+        for s in range(parts):
+            n = int(part_sizes[r][s])
+            virt[s * world + r] = arr[o:o + n]
+            o += n
+    return assemble_tiles(virt, width, height, world * parts, tile)
