@@ -942,6 +942,9 @@ MatView mat_view(const tt_ctx* c) {
 }  // namespace
 
 hipStream_t tt_ctx_stream_of(tt_ctx* c) { return c->stream; }  // tt_build.hip
+void tt_ctx_set_error(tt_ctx* c, const char* msg) {                // tt_build.hip
+    if (c) c->err = msg ? msg : "";
+}
 
 tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
                            const tt_col_data* colors, tt_stats* stats) {

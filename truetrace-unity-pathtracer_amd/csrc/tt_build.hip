@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -30,6 +31,11 @@
 #include "../../include/truetrace_hip.h"
 
 extern "C" hipStream_t tt_ctx_stream_of(tt_ctx* c);  // tt_api.hip (C linkage there)
+extern "C" void tt_ctx_set_error(tt_ctx* c, const char* msg);
+
+namespace {
+thread_local char g_err[256];  // the failing step of the current build, for tt_last_error
+}
 
 namespace {
 
@@ -327,13 +333,15 @@ __device__ inline float surface_area_h(const Box& a) { return surface_area(a); }
 
 // BFS of the BVH2 from the root: lvl_out gets the internal children of the frontier's internal nodes
 __global__ void k_bvh2_level(int m, const int* __restrict__ frontier, const int* __restrict__ left,
-                             const uint32_t* __restrict__ count, int* __restrict__ next, int* __restrict__ n_next) {
+                             const uint32_t* __restrict__ count, int* __restrict__ next, int* __restrict__ n_next,
+                             int cap) {
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= m) return;
     const int v = frontier[t];
     if (count[v] > 0) return;
     const int l = left[v];
     const int o = atomicAdd(n_next, 2);
+    if (o + 1 >= cap) return;  // not a tree: the host sees the count and fails
     next[o] = l;
     next[o + 1] = l + 1;
 }
@@ -422,7 +430,7 @@ struct Rec8 {
 
 // get_children + order_children + the child checks of collapse() for one CWBVH8 node; appends its
 // internal children as records of the next level.
-__global__ void k_expand8(int lo, int hi, Rec8* __restrict__ rec, int* __restrict__ n_rec, const Box* __restrict__ box,
+__global__ void k_expand8(int lo, int hi, int cap, Rec8* __restrict__ rec, int* __restrict__ n_rec, const Box* __restrict__ box,
                           const int* __restrict__ left, const uint32_t* __restrict__ count, const Dec* __restrict__ dec,
                           const int* __restrict__ nprim, int* __restrict__ err) {
     const int x = lo + blockIdx.x * kBlock + threadIdx.x;
@@ -507,6 +515,7 @@ __global__ void k_expand8(int lo, int hi, Rec8* __restrict__ rec, int* __restric
             if (t > 24) { atomicOr(err, 16); return; }
         } else if (ty == 1) {
             const int o = atomicAdd(n_rec, 1);
+            if (o >= cap) { atomicOr(err, 128); return; }
             rec[o].bvh2 = c;
             R.crec[k++] = o;
         } else {
@@ -630,10 +639,18 @@ struct NextCount {
     __device__ int operator()(int q) const { return q < S ? so[q].n_next : 0; }
 };
 
-#define TT_BH(x)                                  \
-    do {                                          \
-        const hipError_t e_ = (x);                \
-        if (e_ != hipSuccess) return TT_ERR_HIP;  \
+#define TT_BH(x)                                                                                  \
+    do {                                                                                          \
+        const hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                                   \
+            std::snprintf(g_err, sizeof(g_err), "%s: %s", #x, hipGetErrorString(e_));             \
+            return e_ == hipErrorOutOfMemory ? TT_ERR_OOM : TT_ERR_HIP;                            \
+        }                                                                                         \
+    } while (0)
+#define TT_BFAIL(status, msg)                                  \
+    do {                                                       \
+        std::snprintf(g_err, sizeof(g_err), "%s", msg);        \
+        return status;                                         \
     } while (0)
 
 // The BVH2 stage's result, left on the device for the BVH8 stage: BVH2Nodes (boxes, left, count; 2n
@@ -774,7 +791,7 @@ static tt_status bvh2_stage(hipStream_t st, const float* aabbs, int n, const int
         TT_BH(hipMemcpyAsync(&h[0], base.p + S, sizeof(int), hipMemcpyDeviceToHost, st));
         TT_BH(hipMemcpyAsync(&h[1], err.p, sizeof(int), hipMemcpyDeviceToHost, st));
         TT_BH(hipStreamSynchronize(st));
-        if (h[1]) return TT_ERR_UNSUPPORTED;  // a node without a finite SAH split (the C# recursion misbehaves there too)
+        if (h[1]) TT_BFAIL(TT_ERR_UNSUPPORTED, "BVH2 stage: a node has no finite SAH split");  // the C# misbehaves too
         hipLaunchKernelGGL(k_children, dim3(grid_of(S)), dim3(kBlock), 0, st, S, segs.p, so.p, base.p, next.p,
                            child_id.p);
         hipLaunchKernelGGL(k_dim_of, dim3(grid_of(S)), dim3(kBlock), 0, st, S, so.p, dimv.p);
@@ -814,7 +831,10 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
     if (s != TT_OK || !final_indices) return s != TT_OK ? s : TT_ERR_INVALID_ARG;
     hipStream_t st = tt_ctx_stream_of(ctx);
     Bvh2Dev R;
-    if ((s = bvh2_stage(st, aabbs, (int)n, presorted, R)) != TT_OK) return s;
+    if ((s = bvh2_stage(st, aabbs, (int)n, presorted, R)) != TT_OK) {
+        tt_ctx_set_error(ctx, g_err);
+        return s;
+    }
     const size_t n2 = 2 * (size_t)n;
     TT_BH(hipMemcpyAsync(final_indices, R.final_idx.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
     if (node_aabbs) TT_BH(hipMemcpyAsync(node_aabbs, R.box.p, n2 * sizeof(Box), hipMemcpyDeviceToHost, st));
@@ -825,9 +845,22 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
     return TT_OK;
 }
 
+static tt_status blas_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
+                             tt_cwbvh_node* nodes, uint32_t max_nodes, uint32_t* n_nodes, int32_t* cwbvh_indices,
+                             uint32_t* bvh2_depth);
+
 extern "C" tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
                                           tt_cwbvh_node* nodes, uint32_t max_nodes, uint32_t* n_nodes,
                                           int32_t* cwbvh_indices, uint32_t* bvh2_depth) {
+    g_err[0] = 0;
+    const tt_status s = blas_device(ctx, aabbs, n, presorted, nodes, max_nodes, n_nodes, cwbvh_indices, bvh2_depth);
+    if (s != TT_OK) tt_ctx_set_error(ctx, g_err[0] ? g_err : "tt_blas_build_device: invalid argument");
+    return s;
+}
+
+static tt_status blas_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
+                             tt_cwbvh_node* nodes, uint32_t max_nodes, uint32_t* n_nodes, int32_t* cwbvh_indices,
+                             uint32_t* bvh2_depth) {
     tt_status s = check_inputs(ctx, aabbs, n, presorted);
     if (s != TT_OK) return s;
     if (!nodes || !n_nodes || !cwbvh_indices) return TT_ERR_INVALID_ARG;
@@ -848,11 +881,11 @@ extern "C" tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint3
         const int lo = lvl[lvl.size() - 2], hi = lvl.back();
         TT_BH(hipMemcpyAsync(cnt1.p, &zero, sizeof(int), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_bvh2_level, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, hi - lo, order.p + lo, B.left.p,
-                           B.count.p, order.p + hi, cnt1.p);
+                           B.count.p, order.p + hi, cnt1.p, (int)(n2 - (size_t)hi));
         int m = 0;
         TT_BH(hipMemcpyAsync(&m, cnt1.p, sizeof(int), hipMemcpyDeviceToHost, st));
         TT_BH(hipStreamSynchronize(st));
-        if ((size_t)hi + (size_t)m > n2) return TT_ERR_INVALID_ARG;
+        if ((size_t)hi + (size_t)m > n2) TT_BFAIL(TT_ERR_INVALID_ARG, "BVH2 levels: not a binary tree");
         lvl.push_back(hi + m);
     }
     // cost pass, deepest level first
@@ -886,18 +919,18 @@ extern "C" tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint3
     std::vector<int> r8{0, 1};
     while (r8.back() > r8[r8.size() - 2]) {
         const int lo = r8[r8.size() - 2], hi = r8.back();
-        hipLaunchKernelGGL(k_expand8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, lo, hi, rec.p, nrec.p, B.box.p,
+        hipLaunchKernelGGL(k_expand8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, lo, hi, (int)cap, rec.p, nrec.p, B.box.p,
                            B.left.p, B.count.p, dec.p, nprim.p, err.p);
         int h[2] = {0, 0};
         TT_BH(hipMemcpyAsync(&h[0], nrec.p, sizeof(int), hipMemcpyDeviceToHost, st));
         TT_BH(hipMemcpyAsync(&h[1], err.p, sizeof(int), hipMemcpyDeviceToHost, st));
         TT_BH(hipStreamSynchronize(st));
-        if (h[1]) return TT_ERR_UNSUPPORTED;  // BVH8Builder.build returns false on the same inputs
-        if ((size_t)h[0] > cap) return TT_ERR_UNSUPPORTED;
+        if (h[1]) TT_BFAIL(TT_ERR_UNSUPPORTED, "BVH8 stage: BVH8Builder.build fails on this tree");
+        if ((size_t)h[0] > cap) TT_BFAIL(TT_ERR_UNSUPPORTED, "BVH8 stage: more CWBVH8 nodes than BVH2 nodes");
         r8.push_back(h[0]);
     }
     const int total = r8.back();
-    if ((uint32_t)total > max_nodes) return TT_ERR_INVALID_ARG;
+    if ((uint32_t)total > max_nodes) TT_BFAIL(TT_ERR_INVALID_ARG, "tt_blas_build_device: max_nodes too small");
     for (size_t L = r8.size() - 1; L-- > 0;) {
         const int lo = r8[L], hi = r8[L + 1];
         if (hi > lo) hipLaunchKernelGGL(k_up8, dim3(grid_of(hi - lo)), dim3(kBlock), 0, st, lo, hi, rec.p);
@@ -920,7 +953,7 @@ extern "C" tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint3
     TT_BH(hipMemcpyAsync(nodes, out.p, (size_t)total * sizeof(tt_cwbvh_node), hipMemcpyDeviceToHost, st));
     TT_BH(hipMemcpyAsync(cwbvh_indices, idxo.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
     TT_BH(hipStreamSynchronize(st));
-    if (e) return TT_ERR_UNSUPPORTED;
+    if (e) TT_BFAIL(TT_ERR_UNSUPPORTED, "BVH8 stage: a node's quantization exponent is not a power of two");
     *n_nodes = (uint32_t)total;
     if (bvh2_depth) *bvh2_depth = B.depth;
     return TT_OK;
