@@ -125,7 +125,11 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern unsafe TTStatus tt_blas_refit(IntPtr ctx, ref TTBlasRefitParams p, float* vertices,
             int* indices, int* leafOfTriangle);
         [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
-        // ParentObject.BuildTotal's BVH2Builder + BVH8Builder + Aggregate on the GPU, after the host's presort
+        // BVH2Builder's three Array.Sort centroid presorts (introsort replayed, same tie order); returns
+        // TTStatus.Unsupported for n <= 16 or non-finite centroids: then Array.Sort on the C# side.
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_bvh2_presort_device(IntPtr ctx, float* aabbs, uint n,
+            int* presorted);
+        // ParentObject.BuildTotal's BVH2Builder + BVH8Builder + Aggregate on the GPU, after the presort
         // (byte-identical to the C# build): triangle AABBs {max, min}, 3 x n presorted indices, nodes out.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_blas_build_device(IntPtr ctx, float* aabbs, uint n,
             int* presorted, void* nodes, uint maxNodes, out uint nNodes, int* cwbvhIndices, out uint bvh2Depth);

@@ -322,6 +322,14 @@ tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, cons
  * max_nodes >= n - 1 suffices), their count, cwbvh_indices (n: leaf position -> source triangle)
  * and the BVH2 depth; tt_blas_build_from_cwbvh (truetrace_scene.h) assembles the tt_blas.
  * TT_ERR_UNSUPPORTED where the reference's BVH8Builder.build fails. */
+/* BVH2Builder's three centroid presorts (.NET Array.Sort: IntrospectiveSort with the float-key
+ * Comparison, BVH2Builder.cs:137-147) on the GPU, with the same output as tt_bvh2_presort -- the
+ * unstable sort's exact swap sequence replayed level by level (median of three, the two-pointer
+ * partition in closed form, insertion sort <= 16, heapsort at the depth limit). TT_ERR_UNSUPPORTED
+ * (use tt_bvh2_presort) for n <= 16, non-finite centroids, or a depth-exhausted partition above
+ * 65536 elements. aabbs: n x {BBMax[3], BBMin[3]} (host); presorted: 3 x n (host). */
+tt_status tt_bvh2_presort_device(tt_ctx* ctx, const float* aabbs, uint32_t n, int32_t* presorted);
+
 tt_status tt_blas_build_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const int32_t* presorted,
                                tt_cwbvh_node* nodes, uint32_t max_nodes, uint32_t* n_nodes, int32_t* cwbvh_indices,
                                uint32_t* bvh2_depth);

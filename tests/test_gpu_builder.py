@@ -114,3 +114,35 @@ def test_sponza_c2_blas_device_build_identical_and_traces(engine):
     engine.trace(rays, W * H, 0, T.FAR, W, H)
     assert O.trace(sc, ref, W * H, 0, T.FAR, W, H, nthreads=8)[0] == 0
     assert np.array_equal(rays["hits"], ref["hits"])
+
+
+def _presorts(engine, mesh):
+    L = tthip.scene_lib()
+    v = mesh.view()
+    n = v.n_indices // 3
+    aabbs = np.zeros((n, 6), np.float32)
+    assert L.tt_blas_prepare_aabbs(v, aabbs.ctypes.data) == 0
+    host = np.zeros((3, n), np.int32)
+    assert L.tt_bvh2_presort(aabbs.ctypes.data, n, host.ctypes.data) == 0
+    dev = np.full((3, n), -1, np.int32)
+    st = engine.L.tt_bvh2_presort_device(engine.h, aabbs.ctypes.data, n, dev.ctypes.data)
+    return st, host, dev
+
+
+def _snapped(n, seed):  # grid-snapped triangles: most centroid keys tie (the introsort's swap order decides)
+    rng = np.random.default_rng(seed)
+    pos = (np.round(rng.uniform(-4, 4, (3 * n, 3)) * 2) / 2).astype(np.float32)
+    return tthip.Mesh.from_arrays(pos, np.arange(3 * n, dtype=np.int32))
+
+
+@pytest.mark.parametrize("name", ["pedestal", "grid_40x25", "duplicates", "signed_zeros", "soup_50k", "snapped_80k"])
+def test_device_presort_replays_the_dotnet_introsort(engine, name):
+    mesh = _snapped(80_000, 5) if name == "snapped_80k" else _meshes()[name]
+    st, host, dev = _presorts(engine, mesh)
+    assert st == 0
+    assert np.array_equal(host, dev)
+
+
+def test_device_presort_declines_tiny_inputs(engine):
+    st, _, _ = _presorts(engine, _meshes()["unity_cube"])  # 12 triangles: the host sorts
+    assert st == tthip.TT_ERR_UNSUPPORTED

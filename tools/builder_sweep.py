@@ -59,6 +59,14 @@ def main():
         n = int(np.exp(rng.uniform(0, np.log(200_000))))
         mesh = mesh_for(tthip, rng, kind, n)
         host = tthip.Blas(mesh)
+        v = mesh.view()
+        aabbs = np.zeros((host.n_tris, 6), np.float32)
+        tthip.scene_lib().tt_blas_prepare_aabbs(v, aabbs.ctypes.data)
+        ph = np.zeros((3, host.n_tris), np.int32)
+        pd = np.zeros((3, host.n_tris), np.int32)
+        tthip.scene_lib().tt_bvh2_presort(aabbs.ctypes.data, host.n_tris, ph.ctypes.data)
+        st = eng.L.tt_bvh2_presort_device(eng.h, aabbs.ctypes.data, host.n_tris, pd.ctypes.data)
+        presort_same = bool(np.array_equal(ph, pd)) if st == 0 else None  # None: declined (host sorts)
         try:
             dev = tthip.Blas(mesh, engine=eng)
             nh, th = host.arrays()
@@ -69,8 +77,10 @@ def main():
         except tthip.TTError as e:
             same = False
             print(f"[sweep] case {c} {kind} n={n}: {e}", file=sys.stderr)
+        same = same and presort_same is not False
         bad += 0 if same else 1
-        rows.append({"case": c, "kind": kind, "tris": host.n_tris, "nodes": host.n_nodes, "identical": same})
+        rows.append({"case": c, "kind": kind, "tris": host.n_tris, "nodes": host.n_nodes, "identical": same,
+                     "device_presort": presort_same})
         if not same:
             print(f"[sweep] MISMATCH case {c} {kind} n={n}", file=sys.stderr, flush=True)
     eng.close()

@@ -632,6 +632,253 @@ __global__ void k_fill8(int m, const Rec8* __restrict__ rec, const Box* __restri
     out[R.idx] = o;
 }
 
+// ------------------------------------------------------------------------ presort (introsort)
+// .NET Framework's ArraySortHelper IntrospectiveSort with BVH2Builder's float-key Comparison
+// (BVH2Builder.cs:137-147; host restatement DotNetSort in host/tt_scene.cpp), run level by level.
+// The sort is unstable, so its output order of equal keys is whatever its exact sequence of swaps
+// produces -- the GPU must replay that sequence, not just sort. Partitions of one recursion level are
+// disjoint and independent, so they run together; within a partition, PickPivotAndPartition's
+// two-pointer scan is replayed in closed form: after the median-of-three and the pivot parked at
+// hi - 1, the k-th stop of the left pointer is the k-th position (from lo + 1) whose key is >= the
+// pivot's (a_k), the k-th stop of the right pointer the k-th position (from hi - 2 down) whose key
+// is <= it (b_k); pairs k < K swap, where K is the first k with a_k >= b_k, and the pivot lands at
+// min(a_K, b_(K-1)) (b_0 = hi - 1). Small partitions (<= 16) and partitions whose depth limit ran
+// out (heapsort) are finished by one thread each, exactly as the sequential code does them.
+struct SortPart {
+    int lo, hi, depth;
+};
+
+__device__ inline int key_cmp(const float* __restrict__ k, int a, int b) {  // KeyCmp
+    const float sign = k[a] - k[b];
+    return sign < 0 ? -1 : (sign == 0 ? 0 : 1);
+}
+// position p of the 3n-long index array -> the axis it sorts (keys of axis d at cent + d * n)
+__device__ inline const float* axis_keys(const float* cent, int n, int p) { return cent + (size_t)(p / n) * n; }
+
+__device__ void swap_if_greater(int* it, const float* k, int a, int b) {
+    if (a != b && key_cmp(k, it[a], it[b]) > 0) {
+        const int t = it[a];
+        it[a] = it[b];
+        it[b] = t;
+    }
+}
+__device__ void small_sort(int* it, const float* k, int lo, int hi) {  // IntroSort's <= 16 branch
+    const int size = hi - lo + 1;
+    if (size <= 1) return;
+    if (size == 2) {
+        swap_if_greater(it, k, lo, hi);
+        return;
+    }
+    if (size == 3) {
+        swap_if_greater(it, k, lo, hi - 1);
+        swap_if_greater(it, k, lo, hi);
+        swap_if_greater(it, k, hi - 1, hi);
+        return;
+    }
+    for (int i = lo; i < hi; i++) {  // InsertionSort
+        int j = i;
+        const int t = it[i + 1];
+        while (j >= lo && key_cmp(k, t, it[j]) < 0) {
+            it[j + 1] = it[j];
+            j--;
+        }
+        it[j + 1] = t;
+    }
+}
+__device__ void down_heap(int* it, const float* k, int i, int n, int lo) {
+    const int d = it[lo + i - 1];
+    while (i <= n / 2) {
+        int child = 2 * i;
+        if (child < n && key_cmp(k, it[lo + child - 1], it[lo + child]) < 0) child++;
+        if (!(key_cmp(k, d, it[lo + child - 1]) < 0)) break;
+        it[lo + i - 1] = it[lo + child - 1];
+        i = child;
+    }
+    it[lo + i - 1] = d;
+}
+__device__ void heap_sort(int* it, const float* k, int lo, int hi) {
+    const int n = hi - lo + 1;
+    for (int i = n / 2; i >= 1; i--) down_heap(it, k, i, n, lo);
+    for (int i = n; i > 1; i--) {
+        const int t = it[lo];
+        it[lo] = it[lo + i - 1];
+        it[lo + i - 1] = t;
+        down_heap(it, k, 1, i - 1, lo);
+    }
+}
+
+// median of three, the pivot parked at hi - 1; pk = the pivot item
+__global__ void k_pivot(int P, const SortPart* __restrict__ parts, int* __restrict__ it, const float* __restrict__ cent,
+                        int n, int* __restrict__ pk) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= P) return;
+    const SortPart q = parts[s];
+    const float* k = axis_keys(cent, n, q.lo);
+    const int middle = q.lo + ((q.hi - q.lo) >> 1);
+    swap_if_greater(it, k, q.lo, middle);
+    swap_if_greater(it, k, q.lo, q.hi);
+    swap_if_greater(it, k, middle, q.hi);
+    const int pivot = it[middle];
+    if (middle != q.hi - 1) {
+        it[middle] = it[q.hi - 1];
+        it[q.hi - 1] = pivot;
+    }
+    pk[s] = pivot;
+}
+
+// left-pointer stops (ge: key >= pivot, over [lo+1, hi-1]) and right-pointer stops (le: key <=
+// pivot, over [lo, hi-2]) as 0/1 flags
+struct GeFlag {
+    const int* it;
+    const int* part;
+    const SortPart* parts;
+    const int* pk;
+    const float* cent;
+    int n;
+    __device__ int operator()(int p) const {
+        const int s = part[p];
+        if (s < 0) return 0;
+        const SortPart q = parts[s];
+        if (p < q.lo + 1 || p > q.hi - 1) return 0;
+        const float* k = axis_keys(cent, n, p);
+        return key_cmp(k, it[p], pk[s]) < 0 ? 0 : 1;
+    }
+};
+struct LeFlagRev {  // indexed by q = 3n - 1 - p (the right pointer's direction)
+    const int* it;
+    const int* part;
+    const SortPart* parts;
+    const int* pk;
+    const float* cent;
+    int n, n3;
+    __device__ int operator()(int qi) const {
+        const int p = n3 - 1 - qi;
+        const int s = part[p];
+        if (s < 0) return 0;
+        const SortPart q = parts[s];
+        if (p < q.lo || p > q.hi - 2) return 0;
+        const float* k = axis_keys(cent, n, p);
+        return key_cmp(k, pk[s], it[p]) < 0 ? 0 : 1;
+    }
+};
+struct PartKeyRev {
+    const int* part;
+    int n3;
+    __device__ int operator()(int qi) const { return part[n3 - 1 - qi]; }
+};
+
+// aList[lo + k] = k-th left stop, bList[lo + k] = k-th right stop (k from 0)
+__global__ void k_stops(int n3, const int* __restrict__ part, const SortPart* __restrict__ parts, const int* __restrict__ it,
+                        const int* __restrict__ pk, const float* __restrict__ cent, int n, const int* __restrict__ gerank,
+                        const int* __restrict__ lerank_rev, int* __restrict__ alist, int* __restrict__ blist) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n3) return;
+    const int s = part[p];
+    if (s < 0) return;
+    const SortPart q = parts[s];
+    const float* k = axis_keys(cent, n, p);
+    if (p >= q.lo + 1 && p <= q.hi - 1 && key_cmp(k, it[p], pk[s]) >= 0) alist[q.lo + gerank[p]] = p;
+    if (p >= q.lo && p <= q.hi - 2 && key_cmp(k, pk[s], it[p]) >= 0) blist[q.lo + lerank_rev[n3 - 1 - p]] = p;
+}
+
+// K (first k with a_k >= b_k) by binary search; the swap count K - 1 and the pivot's final slot
+__global__ void k_crossing(int P, const SortPart* __restrict__ parts, const int* __restrict__ gerank,
+                           const int* __restrict__ lerank_rev, const int* __restrict__ alist, const int* __restrict__ blist,
+                           int n3, int2* __restrict__ res) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= P) return;
+    const SortPart q = parts[s];
+    const int cnt_ge = gerank[q.hi - 1] + 1;       // hi - 1 (the pivot) is always a stop
+    const int cnt_le = lerank_rev[n3 - 1 - q.lo] + 1;  // lo (<= pivot after the median of three) is too
+    auto pred = [&](int K) {  // a_K >= b_K (1-based K); b_K = -1 past the last right stop
+        const int a = alist[q.lo + K - 1];
+        const int b = K <= cnt_le ? blist[q.lo + K - 1] : -1;
+        return a >= b;
+    };
+    int lo = 1, hi = cnt_ge;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pred(mid)) hi = mid;
+        else lo = mid + 1;
+    }
+    const int K = lo;
+    const int aK = alist[q.lo + K - 1];
+    const int bK1 = K >= 2 ? blist[q.lo + K - 2] : q.hi - 1;
+    res[s] = make_int2(K - 1, aK < bK1 ? aK : bK1);
+}
+
+__global__ void k_pswap(int n3, const int* __restrict__ part, const SortPart* __restrict__ parts, const int2* __restrict__ res,
+                        const int* __restrict__ alist, const int* __restrict__ blist, int* __restrict__ it) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n3) return;
+    const int s = part[p];
+    if (s < 0) return;
+    const int kk = p - parts[s].lo;
+    if (kk >= res[s].x) return;
+    const int a = alist[p], b = blist[p];
+    const int t = it[a];
+    it[a] = it[b];
+    it[b] = t;
+}
+
+// the pivot into its slot; children: finished here (<= 16, or heapsort at depth 0) or the next level
+__global__ void k_children_sort(int P, const SortPart* __restrict__ parts, const int2* __restrict__ res, int* __restrict__ it,
+                                const float* __restrict__ cent, int n, SortPart* __restrict__ next, int* __restrict__ n_next,
+                                int2* __restrict__ child, int* __restrict__ err) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= P) return;
+    const SortPart q = parts[s];
+    const int left = res[s].y;
+    if (left != q.hi - 1) {
+        const int t = it[left];
+        it[left] = it[q.hi - 1];
+        it[q.hi - 1] = t;
+    }
+    const float* k = axis_keys(cent, n, q.lo);
+    const int d = q.depth - 1;
+    int2 id = make_int2(-1, -1);
+    const int bounds[2][2] = {{q.lo, left - 1}, {left + 1, q.hi}};
+    for (int c = 0; c < 2; c++) {
+        const int lo = bounds[c][0], hi = bounds[c][1];
+        const int size = hi - lo + 1;
+        if (size <= 16) {
+            small_sort(it, k, lo, hi);
+        } else if (d == 0) {
+            if (size > 65536) atomicOr(err, 1);  // left to the host: one thread would take too long
+            else heap_sort(it, k, lo, hi);
+        } else {
+            const int o = atomicAdd(n_next, 1);
+            next[o] = SortPart{lo, hi, d};
+            if (c == 0) id.x = o;
+            else id.y = o;
+        }
+    }
+    child[s] = id;
+}
+
+__global__ void k_repart(int n3, int* __restrict__ part, const int2* __restrict__ res, const int2* __restrict__ child) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n3) return;
+    const int s = part[p];
+    if (s < 0) return;
+    const int left = res[s].y;
+    part[p] = p < left ? child[s].x : (p > left ? child[s].y : -1);
+}
+
+// BVH2Builder's centroids, (max - min) / 2 + min per axis, axis-major; flags non-finite keys
+__global__ void k_centroids(int n, const Box* __restrict__ prims, float* __restrict__ cent, int* __restrict__ it,
+                            int* __restrict__ bad) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const Box b = prims[i];
+    for (int d = 0; d < 3; d++) {
+        const float c = (b.mx[d] - b.mn[d]) / 2.0f + b.mn[d];
+        cent[(size_t)d * n + i] = c;
+        it[(size_t)d * n + i] = i;
+        if (!(c - c == 0.0f)) atomicOr(bad, 1);  // NaN or infinity: the comparator is not an order there
+    }
+}
+
 // exclusive-scan input: live children per segment (0 past the last segment, so base[S] = total)
 struct NextCount {
     const SplitOut* so;
@@ -957,4 +1204,108 @@ static tt_status blas_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const 
     *n_nodes = (uint32_t)total;
     if (bvh2_depth) *bvh2_depth = B.depth;
     return TT_OK;
+}
+
+// The three presorts of BVH2Builder on the GPU. TT_ERR_UNSUPPORTED (the caller sorts on the host,
+// tt_bvh2_presort) when a key is not finite or a depth-exhausted partition is too large for the
+// one-thread heapsort.
+static tt_status presort_device(hipStream_t st, const float* aabbs, int n, int32_t* presorted) {
+    const int n3 = 3 * n;
+    DBuf<Box> prims;
+    DBuf<float> cent;
+    DBuf<int> it, part, gerank, lerank, alist, blist, pk, cnt, err;
+    DBuf<SortPart> parts, next;
+    DBuf<int2> res, child;
+    const size_t pmax = (size_t)n3 / 17 + 4;  // live partitions per level (> 16 elements each)
+    TT_BH(prims.alloc(n));
+    TT_BH(cent.alloc(n3));
+    TT_BH(it.alloc(n3));
+    TT_BH(part.alloc(n3));
+    TT_BH(gerank.alloc(n3));
+    TT_BH(lerank.alloc(n3));
+    TT_BH(alist.alloc(n3));
+    TT_BH(blist.alloc(n3));
+    TT_BH(pk.alloc(pmax));
+    TT_BH(parts.alloc(pmax));
+    TT_BH(next.alloc(pmax));
+    TT_BH(res.alloc(pmax));
+    TT_BH(child.alloc(pmax));
+    TT_BH(cnt.alloc(1));
+    TT_BH(err.alloc(1));
+    TT_BH(hipMemcpyAsync(prims.p, aabbs, (size_t)n * sizeof(Box), hipMemcpyHostToDevice, st));
+    TT_BH(hipMemsetAsync(err.p, 0, sizeof(int), st));
+    hipLaunchKernelGGL(k_centroids, dim3(grid_of(n)), dim3(kBlock), 0, st, n, prims.p, cent.p, it.p, err.p);
+    int bad = 0;
+    TT_BH(hipMemcpyAsync(&bad, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    TT_BH(hipStreamSynchronize(st));
+    if (bad) TT_BFAIL(TT_ERR_UNSUPPORTED, "presort: non-finite centroid keys (host sort)");
+    if (n <= 16) TT_BFAIL(TT_ERR_UNSUPPORTED, "presort: tiny inputs are sorted on the host");
+    // Sort(length): IntroSort(0, length - 1, 2 * FloorLog2(length)), FloorLog2 = bit length
+    int fl = 0;
+    for (int m = n; m >= 1; m /= 2) fl++;
+    std::vector<SortPart> roots;
+    std::vector<int> part_h(n3, -1);
+    for (int d = 0; d < 3; d++) roots.push_back(SortPart{d * n, d * n + n - 1, 2 * fl});
+    int P = (int)roots.size();
+    for (int s = 0; s < P; s++)
+        for (int p = roots[s].lo; p <= roots[s].hi; p++) part_h[p] = s;
+    TT_BH(hipMemcpyAsync(parts.p, roots.data(), (size_t)P * sizeof(SortPart), hipMemcpyHostToDevice, st));
+    TT_BH(hipMemcpyAsync(part.p, part_h.data(), (size_t)n3 * sizeof(int), hipMemcpyHostToDevice, st));
+    auto cnt_it = rocprim::make_counting_iterator<int>(0);
+    size_t tb = 0, t1 = 0;
+    {
+        auto ge = rocprim::make_transform_iterator(cnt_it, GeFlag{it.p, part.p, parts.p, pk.p, cent.p, n});
+        TT_BH(rocprim::exclusive_scan_by_key(nullptr, t1, part.p, ge, gerank.p, 0, (size_t)n3, rocprim::plus<int>(),
+                                             rocprim::equal_to<int>(), st));
+        tb = std::max(tb, t1);
+        auto le = rocprim::make_transform_iterator(cnt_it, LeFlagRev{it.p, part.p, parts.p, pk.p, cent.p, n, n3});
+        auto rk = rocprim::make_transform_iterator(cnt_it, PartKeyRev{part.p, n3});
+        TT_BH(rocprim::exclusive_scan_by_key(nullptr, t1, rk, le, lerank.p, 0, (size_t)n3, rocprim::plus<int>(),
+                                             rocprim::equal_to<int>(), st));
+        tb = std::max(tb, t1);
+    }
+    DBuf<unsigned char> tstore;
+    TT_BH(tstore.alloc(tb));
+    while (P > 0) {
+        hipLaunchKernelGGL(k_pivot, dim3(grid_of(P)), dim3(kBlock), 0, st, P, parts.p, it.p, cent.p, n, pk.p);
+        size_t t = tb;
+        auto ge = rocprim::make_transform_iterator(cnt_it, GeFlag{it.p, part.p, parts.p, pk.p, cent.p, n});
+        TT_BH(rocprim::exclusive_scan_by_key(tstore.p, t, part.p, ge, gerank.p, 0, (size_t)n3, rocprim::plus<int>(),
+                                             rocprim::equal_to<int>(), st));
+        t = tb;
+        auto le = rocprim::make_transform_iterator(cnt_it, LeFlagRev{it.p, part.p, parts.p, pk.p, cent.p, n, n3});
+        auto rk = rocprim::make_transform_iterator(cnt_it, PartKeyRev{part.p, n3});
+        TT_BH(rocprim::exclusive_scan_by_key(tstore.p, t, rk, le, lerank.p, 0, (size_t)n3, rocprim::plus<int>(),
+                                             rocprim::equal_to<int>(), st));
+        hipLaunchKernelGGL(k_stops, dim3(grid_of(n3)), dim3(kBlock), 0, st, n3, part.p, parts.p, it.p, pk.p, cent.p, n,
+                           gerank.p, lerank.p, alist.p, blist.p);
+        hipLaunchKernelGGL(k_crossing, dim3(grid_of(P)), dim3(kBlock), 0, st, P, parts.p, gerank.p, lerank.p, alist.p,
+                           blist.p, n3, res.p);
+        hipLaunchKernelGGL(k_pswap, dim3(grid_of(n3)), dim3(kBlock), 0, st, n3, part.p, parts.p, res.p, alist.p, blist.p,
+                           it.p);
+        TT_BH(hipMemsetAsync(cnt.p, 0, sizeof(int), st));
+        hipLaunchKernelGGL(k_children_sort, dim3(grid_of(P)), dim3(kBlock), 0, st, P, parts.p, res.p, it.p, cent.p, n,
+                           next.p, cnt.p, child.p, err.p);
+        hipLaunchKernelGGL(k_repart, dim3(grid_of(n3)), dim3(kBlock), 0, st, n3, part.p, res.p, child.p);
+        TT_BH(hipGetLastError());
+        int h[2] = {0, 0};
+        TT_BH(hipMemcpyAsync(&h[0], cnt.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        TT_BH(hipMemcpyAsync(&h[1], err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        TT_BH(hipStreamSynchronize(st));
+        if (h[1]) TT_BFAIL(TT_ERR_UNSUPPORTED, "presort: a depth-exhausted partition is too large (host sort)");
+        if ((size_t)h[0] > pmax) TT_BFAIL(TT_ERR_UNSUPPORTED, "presort: too many partitions");
+        std::swap(parts.p, next.p);
+        P = h[0];
+    }
+    TT_BH(hipMemcpyAsync(presorted, it.p, (size_t)n3 * sizeof(int), hipMemcpyDeviceToHost, st));
+    TT_BH(hipStreamSynchronize(st));
+    return TT_OK;
+}
+
+extern "C" tt_status tt_bvh2_presort_device(tt_ctx* ctx, const float* aabbs, uint32_t n, int32_t* presorted) {
+    if (!ctx || !aabbs || !n || !presorted || n >= (1u << 29)) return TT_ERR_INVALID_ARG;
+    g_err[0] = 0;
+    const tt_status s = presort_device(tt_ctx_stream_of(ctx), aabbs, (int)n, presorted);
+    if (s != TT_OK) tt_ctx_set_error(ctx, g_err[0] ? g_err : "tt_bvh2_presort_device failed");
+    return s;
 }

@@ -279,6 +279,7 @@ def hip_lib():
         L.tt_blas_refit.argtypes = [vp, C.POINTER(BlasRefitParams), vp, vp, vp]
         L.tt_bvh2_build_device.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, C.POINTER(u32)]
         L.tt_blas_build_device.argtypes = [vp, vp, u32, vp, vp, u32, C.POINTER(u32), vp, C.POINTER(u32)]
+        L.tt_bvh2_presort_device.argtypes = [vp, vp, u32, vp]
         L.tt_sync.argtypes = [vp]
         L.tt_async_overflows.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_ctx_stream.argtypes = [vp]
@@ -456,7 +457,8 @@ class Blas:
             _check(L.tt_blas_prepare_aabbs(C.byref(v), aabbs.ctypes.data), "tt_blas_prepare_aabbs")
             t1 = time.perf_counter()
             pre = np.zeros((3, n), np.int32)
-            _check(L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data), "tt_bvh2_presort")
+            if engine.L.tt_bvh2_presort_device(engine.h, aabbs.ctypes.data, n, pre.ctypes.data) != TT_OK:
+                _check(L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data), "tt_bvh2_presort")
             t2 = time.perf_counter()
             if device_stages == "bvh2+bvh8":
                 cap = max(1, n - 1)
