@@ -353,10 +353,13 @@ def main():
                          "RCCL-gathered to rank 0 inside every timed step (strong scaling). sample: every rank "
                          "traces its own full-frame sample, no collective (weak scaling)")
     ap.add_argument("--parts", type=int, default=2,
-                    help="N > 1 (tiles): a rank's tiles are traced as this many tile-interleaved parts, each by its "
-                         "own engine on its own stream (each part's bounce-1 after its own primary), so one part's "
-                         "launch drain overlaps the other parts' work (tools/exp_streams.py). N = 1: one launch per bounce")
+                    help="a rank's pixels (N = 1: the frame; N > 1: its tiles) are traced as this many tile-interleaved "
+                         "parts, each by its own engine on its own stream (each part's bounce-1 after its own primary), "
+                         "so one part's launch drain overlaps the other parts' work (tools/exp_streams.py). 1: one "
+                         "launch per bounce")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
+    ap.add_argument("--no-single", action="store_true",
+                    help="N = 1, parts > 1: skip the single-stream leg (one launch at a time; roofline.single_stream)")
     ap.add_argument("--no-recur", action="store_true",
                     help="skip the auxiliary unjittered (UseReCur) primary + bounce launches (profiling runs: they "
                          "use the metric's kernel instantiation and would mix into its rocprof average)")
@@ -426,13 +429,17 @@ def main():
     # its screen column x = W/2 has direction.z == -0.0 exactly, whose NaN z slabs make ~1,000 rays
     # walk ~900 nodes each (tools/long_rays.py). The sample layout jitters with frames = rank.
     jitter, frames = 1, (rank if (world > 1 and not tiles) else 0)
-    P = max(1, args.parts) if tiles else 1
+    # a rank's pixels (the whole frame at N = 1) as P tile-interleaved parts, each traced by its own
+    # engine context on its own stream: a part's launches overlap the other parts' launch drains
+    # (tools/exp_streams.py); P = 1 is one full-frame launch per bounce in the kernel's own tile order
+    P = max(1, args.parts) if (tiles or world == 1) else 1
+    split = tiles or P > 1
 
     class Part:  # one launch stream of this rank: its engine, stream, rays and counts
         pass
 
     parts = []
-    if tiles:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), split into P parts
+    if split:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), split into P parts
         full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         for s, pix_np in enumerate(ttdist.part_pixels(W, H, world, rank, P)):
@@ -464,8 +471,9 @@ def main():
     n_prim, nb = sum(p.n for p in parts), sum(p.nb for p in parts)
     rays_per_step = n_prim + nb
     s_prim, s_bnc = parts[0].s_prim, parts[0].s_bnc
-    B_prim = alg_bytes(s_prim, 0, parts[0].n)  # the roofline is part 0's launches' (the engine ring below)
+    B_prim = alg_bytes(s_prim, 0, parts[0].n)  # part 0's launches (the engine ring below)
     B_bnc = alg_bytes(s_bnc, 1, parts[0].nb)
+    B_step = sum(alg_bytes(p.s_prim, 0, p.n) + alg_bytes(p.s_bnc, 1, p.nb) for p in parts)  # all parts
     log(f"rank {rank}: primary {n_prim} rays nodes/ray {s_prim.node_visits / max(parts[0].n, 1):.2f} "
         f"tris/ray {s_prim.tri_tests / max(parts[0].n, 1):.2f} "
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(parts[0].nb, 1):.2f} "
@@ -528,7 +536,7 @@ def main():
         assert len(p.eng.timing_read()) == 2 * args.steps
     assert len(launch_ms) == 2 * args.steps, (len(launch_ms), args.steps)
     total_rays = float(rays_per_step * args.steps)
-    trace_ms_rank = float(np.sum(launch_ms)) / args.steps
+    trace_ms_rank = float(np.sum(launch_ms)) / args.steps  # part 0's two launches per step
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -545,12 +553,20 @@ def main():
     prim_ms = launch_ms[0::2]
     bnc_ms = launch_ms[1::2]
     avg_ms = float(np.mean(launch_ms))
-    achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9  # GB/s per launch, averaged over both launches
+    if P == 1:  # GB/s per launch, averaged over both launches
+        achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9
+    else:  # the P parts' launches overlap: all of a step's algorithmic bytes over the step's wall time
+        achieved = B_step / (elapsed / args.steps) / 1e9
 
-    # tiles: SURVEY 8(e) parity -- the gathered frame must equal one GPU tracing the whole frame
+    # SURVEY 8(e) parity -- the gathered (N > 1) or the parts' (N = 1) frame must equal one launch
+    # tracing the whole frame
     gather_parity = None
-    if tiles and rank == 0:
-        frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
+    if split and rank == 0:
+        if tiles:
+            frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
+        else:
+            own = torch.cat([p.prim_hits for p in parts]).cpu()
+            frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
         one = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         eng.trace(one, WH, 0, far, W, H, device=True)
@@ -561,6 +577,31 @@ def main():
             f"identical to a single-GPU trace: {gather_parity}")
     for p in parts[1:]:
         p.eng.close()
+
+    # the kernel alone, one launch at a time (N = 1, P > 1): the full frame in the kernel's own tile
+    # order on the shared stream, per-launch HIP events -- the per-launch roofline and the launch
+    # times rocprofv3 reports for this command's trace kernels
+    single = None
+    frame_rays, frame_nb = (rays, nb) if (P == 1 and world == 1) else (None, None)  # a full-frame, traced ray buffer (N = 1)
+    if world == 1 and P > 1:
+        one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
+        o_prim = eng.trace(one, WH, 0, far, W, H, info=info, device=True, stats=True)
+        onb = eng.enqueue_bounce(one, WH, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+        o_bnc = eng.trace(one, onb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
+        frame_rays, frame_nb = one, onb
+        if not args.no_single:
+            launches = [lambda: eng.trace(one, WH, 0, far, W, H, info=info, device=True, asynchronous=True),
+                        lambda: eng.trace(one, onb, 1, far, W, H, info=info, colors=colors_t, device=True,
+                                          asynchronous=True)]
+            oms = timed_launches(eng, launches, args.warmup, args.steps)
+            o_avg = float(oms.mean())
+            o_ach = ((alg_bytes(o_prim, 0, WH) + alg_bytes(o_bnc, 1, onb)) / 2.0) / (o_avg * 1e-3) / 1e9
+            single = {"achieved": round(o_ach, 1), "frac": round(o_ach / HBM_PEAK_GBS, 4),
+                      "avg_launch_ms": round(o_avg, 4), "trace_ms_primary": round(float(oms[:, 0].mean()), 4),
+                      "trace_ms_bounce": round(float(oms[:, 1].mean()), 4),
+                      "mrays_s": round((WH + onb) / float(oms.sum(1).mean()) / 1e3, 2)}
+            log(f"single-stream leg (the kernel alone, one launch at a time): {single}")
 
     # secondary N > 1 layout: every rank traces its own full-frame jittered sample (weak scaling)
     sample_sharded = None
@@ -621,7 +662,9 @@ def main():
     # pristine rays (occluded rays get t = 0 in place) on the shared stream; only the kernel is timed.
     shadow = None
     if not args.no_shadow:
-        sr = nee_rays(torch, rays, parts[0].n, far, light=(0.0, 9.0, 0.5))  # part 0's primary hits
+        # the frame's primary hits at N = 1, part 0's at N > 1
+        sr = (nee_rays(torch, frame_rays, WH, far, light=(0.0, 9.0, 0.5)) if frame_rays is not None else
+              nee_rays(torch, rays, parts[0].n, far, light=(0.0, 9.0, 0.5)))
         ns = int(sr.shape[0]) // 48
         work = torch.empty_like(sr)
         work.copy_(sr)
@@ -644,16 +687,16 @@ def main():
     # Generate (1080p primary rays) and the diffuse-bounce enqueue with wave-ballot compaction (counter
     # reset + kernel), on a scratch copy of the traced rays restored before every call; engine timing ring.
     producers = None
-    if world == 1:
-        scratch = rays.clone()
+    if world == 1:  # on the full-frame buffer in the kernel's own order (the parts hold compacted tiles)
+        scratch = frame_rays.clone()
         eng.timing_reset()
         for k in range(args.steps):
             eng.generate(scratch, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         gen_ms = eng.timing_read()
         eng.timing_reset()
         for k in range(args.steps):
-            scratch.copy_(rays)
-            eng.enqueue_bounce(scratch, n_prim, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+            scratch.copy_(frame_rays)
+            eng.enqueue_bounce(scratch, WH, 0, far, W, H, frames=frames, max_bounce=1, device=True)
         enq_ms = eng.timing_read()
         producers = {"generate_ms": round(float(np.median(gen_ms)), 4), "primary_rays": n_prim,
                      "enqueue_compact_ms": round(float(np.median(enq_ms)), 4), "bounce_rays": nb}
@@ -680,7 +723,10 @@ def main():
     # ------------------------------------------------------------------ CPU baseline (rank 0, N=1)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(scene, rays, WH, n_prim, nb, colors, far, W, H, args.cpu_seconds)
+        # the same step workload on the full-frame buffer (the parts' buffers hold compacted tiles)
+        if frame_nb != nb:
+            log(f"note: full-frame bounce batch {frame_nb} rays, the parts' {nb}")
+        cpu = cpu_baseline(scene, frame_rays, WH, WH, frame_nb, colors, far, W, H, args.cpu_seconds)
 
     # fabric traffic per launch from the round's separate rocprofv3 --pmc pass of this same command
     # (tools/profile_round.sh -> profiles/traffic_latest.json); null when no such pass was committed
@@ -720,7 +766,8 @@ def main():
                    "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_rank0": int(rays_per_step),
                    "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "jitter": jitter,
                    "seed": hex(args.seed),
-                   "parallelism": ("single GPU, full frame" if world == 1 else
+                   "parallelism": ((f"single GPU, full frame as {P} tile-interleaved parts on {P} streams"
+                                    if P > 1 else "single GPU, full frame") if world == 1 else
                                    (f"64x64 screen tiles round-robin over {world} ranks, each rank's tiles as {P} "
                                     f"tile-interleaved parts on {P} streams, + one RCCL gather of the "
                                     f"primary hit records to rank 0 per step (inside the timed step"
@@ -735,17 +782,22 @@ def main():
                    "trace_ms_primary_median": round(float(np.median(prim_ms)), 4),
                    "trace_ms_bounce_median": round(float(np.median(bnc_ms)), 4),
                    "trace_ms_per_step_slowest_rank": round(trace_ms_slowest, 4),
-                   "kernel_mrays_s_trace_only": round(rays_per_step / trace_ms_rank / 1e3, 2),
+                   "kernel_mrays_s_trace_only": round((parts[0].n + parts[0].nb) / trace_ms_rank / 1e3, 2),
                    "gather_identical_to_1gpu": gather_parity,
                    "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0),
-                     "units_busy": units,
-                     "note": "achieved = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean HIP-event "
-                             "launch time; bytes are served mostly from L2/MALL, so the loop is bound by VALU issue "
+                     "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0) if P == 1 else round(B_step / (2 * P)),
+                     "alg_bytes_per_step": round(B_step),
+                     "units_busy": units, "single_stream": single,
+                     "note": ("achieved = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean HIP-event "
+                              "launch time" if P == 1 else
+                              f"achieved = algorithmic bytes (B_ray, SURVEY §8d) of all 2 x {P} trace launches of a "
+                              "step / the step's wall time (the parts' launches overlap, so a per-launch time is not "
+                              "the kernel's; single_stream = the per-launch figure with one launch at a time)")
+                             + "; bytes are served mostly from L2/MALL, so the loop is bound by VALU issue "
                              "and load latency, not HBM (DESIGN.md §5). traffic = fabric bytes per launch from "
                              + (traffic_src or "no PMC pass") + " (2 x FETCH_SIZE + WRITE_SIZE, includes "
                              "Infinity-Cache hits); units_busy = VALU-issue / texture-data / texture-address "

@@ -7,7 +7,11 @@ finish on ever fewer, sparser waves. On one stream the next la
 tail; with S streams, part s's launches overlap the other parts' tails. Dependencies are kept per
 part: part s's bounce-1 launch follows its own primary launch on its stream (as shading would).
 
-Usage: exp_streams.py [--world N --rank R] [--parts 1,2,3,4] [--steps 20]
+Usage: exp_streams.py [--world N --rank R] [--parts 1,2,3,4] [--weights "2:1;3:2"] [--native] [--steps 20]
+--weights: unequal splits (part s takes w_s of every sum(w) consecutive tiles of the shard), so the
+parts' launches end at different times. --native (world 1): a row for the single full-frame launch
+in the kernel's own 8x8-tile swizzle order (a 1-part tile-order batch of W*H rays would be
+swizzled a second time).
 Prints one JSON document: per S, wall ms per frame step and Grays/s, and whether the union of the
 parts' primary hit records equals one launch over the whole shard.
 """
@@ -30,6 +34,8 @@ def main():
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--parts", default="1,2,3,4")
+    ap.add_argument("--weights", default="")
+    ap.add_argument("--native", action="store_true")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     a = ap.parse_args()
@@ -64,7 +70,49 @@ def main():
     out = {"tool": "tools/exp_streams.py", "world": a.world, "rank": a.rank, "shard_rays": int(shard.shape[0]),
            "rows": []}
     engines = [eng0]
-    for S in [int(x) for x in a.parts.split(",")]:
+    shard_np = ttdist.tile_pixels(W, H, a.world, a.rank)
+    # tile id (within the shard's tile sequence) of every shard pixel, for the weighted splits
+    tx = (W + 63) // 64
+    gt = (shard_np // W) // 64 * tx + (shard_np % W) // 64
+    _, tile_of = np.unique(gt, return_inverse=True)  # shard tiles are in increasing global id order
+
+    def split_pixels(weights):
+        SW = sum(weights)
+        cum = np.cumsum([0] + list(weights))
+        slot = tile_of % SW
+        return [shard_np[(slot >= cum[s]) & (slot < cum[s + 1])] for s in range(len(weights))]
+
+    def timed(step, parts_rays):
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / a.steps
+
+    if a.native and a.world == 1:
+        rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        info = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+        rays[: WH * 48] = full
+        eng0.trace(rays, WH, 0, far, W, H, info=info, device=True)
+        nb = eng0.enqueue_bounce(rays, WH, 0, far, W, H, frames=0, max_bounce=1, device=True)
+
+        def nstep():
+            eng0.trace(rays, WH, 0, far, W, H, info=info, device=True, asynchronous=True)
+            eng0.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+
+        dt = timed(nstep, None)
+        row = {"parts": "native", "ms_per_step": round(dt * 1e3, 4), "grays_s": round((WH + nb) / dt / 1e9, 3),
+               "rays_per_step": WH + nb}
+        out["rows"].append(row)
+        print(f"[streams] {row}", file=sys.stderr, flush=True)
+        del rays, info
+    specs = [[1] * int(x) for x in a.parts.split(",") if x] + \
+        [[int(w) for w in x.split(":")] for x in a.weights.split(";") if x]
+    for weights in specs:
+        S = len(weights)
         streams = [base] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
         while len(engines) < S:
             e = tthip.Engine(0, stream=streams[len(engines)].cuda_stream)
@@ -73,7 +121,7 @@ def main():
         parts = []
         for s in range(S):
             eng = engines[s]
-            pix = torch.from_numpy(ttdist.tile_pixels(W, H, a.world * S, s * a.world + a.rank)).to(dev)
+            pix = torch.from_numpy(split_pixels(weights)[s]).to(dev)
             n = int(pix.shape[0])
             with torch.cuda.stream(streams[s]):
                 rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
@@ -97,16 +145,9 @@ def main():
             for eng, rays, info, pix, n, nb in parts:
                 eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
 
-        for _ in range(a.warmup):
-            step()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            step()
-        torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t0) / a.steps
+        dt = timed(step, None)
         rays_step = sum(p[4] + p[5] for p in parts)
-        row = {"parts": S, "ms_per_step": round(dt * 1e3, 4), "grays_s": round(rays_step / dt / 1e9, 3),
+        row = {"parts": S, "weights": weights, "ms_per_step": round(dt * 1e3, 4), "grays_s": round(rays_step / dt / 1e9, 3),
                "rays_per_step": rays_step, "identical_primary_hits": same}
         out["rows"].append(row)
         print(f"[streams] {row}", file=sys.stderr, flush=True)

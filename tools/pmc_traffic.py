@@ -34,7 +34,10 @@ for k, cs in vals.items():
                      "bytes": 2.0 * fetch * 1024.0 + write * 1024.0, "dispatches": len(cs.get("FETCH_SIZE", []))}
 # bench.py launches the primary and the bounce instantiation equally often
 # (the timed launches are the non-STATS closest-hit instantiations; STATS launches run once in setup)
-timed = {k: v for k, v in per_kernel.items() if k.startswith("void tt_trace_kernel<false")}
+# (<false, false, 1>: primary with _PrimaryTriangleInfo, <false, false, 2>: bounce-1 with the Data.w-gated
+# info; the parity check's full-frame <false, false, 0> launch and the aux configs are not the metric's)
+timed = {k: v for k, v in per_kernel.items()
+         if k.replace(" ", "") in ("voidtt_trace_kernel<false,false,1>", "voidtt_trace_kernel<false,false,2>")}
 res = {"file": out.split("/")[-1], "source": src,
        "correction": "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; includes Infinity-Cache hits",
        "per_kernel": per_kernel, "timed_kernels": sorted(timed),
