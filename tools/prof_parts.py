@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Cross-checks bench.py's roofline against a rocprofv3 --kernel-trace of the same command when the
+N = 1 frame is traced as P parts on P streams (bench.py --parts P, the default 2).
+
+The parts' launches overlap, so rocprofv3's per-kernel average duration is not the kernel's time per
+frame: this tool takes the timed steps' dispatches from the kernel trace (the first 2P x (warmup +
+steps) non-STATS closest-hit launches, <false, false, 1> primary and <false, false, 2> bounce-1, on
+the part streams), drops the warmup, and reports the wall span per step (first start to last end of
+the timed steps / steps), the per-stream launch averages, and the single-stream leg that follows (one
+launch at a time on stream 0; its averages are bench.py's roofline.single_stream.avg_launch_ms).
+With --bench the bench JSON line, it also recomputes roofline.achieved from the trace span.
+
+Usage: prof_parts.py <run_kernel_trace.csv> [--parts 2 --warmup 3 --steps 20] [--bench bench.json]"""
+import argparse
+import csv
+import json
+
+TIMED = ("voidtt_trace_kernel<false,false,1>", "voidtt_trace_kernel<false,false,2>")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--parts", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--bench", default="")
+    a = ap.parse_args()
+    rows = [r for r in csv.DictReader(open(a.trace))
+            if r["Kernel_Name"].split("(")[0].replace(" ", "") in TIMED]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    n_parts = 2 * a.parts * (a.warmup + a.steps)
+    parts, rest = rows[:n_parts], rows[n_parts:]
+    timed = parts[2 * a.parts * a.warmup:]
+    t0 = min(int(r["Start_Timestamp"]) for r in timed)
+    t1 = max(int(r["End_Timestamp"]) for r in timed)
+    per_stream = {}
+    for r in timed:
+        k = (r["Stream_Id"], r["Kernel_Name"].split("(")[0])
+        per_stream.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    out = {"tool": "tools/prof_parts.py", "trace": a.trace, "parts": a.parts, "steps": a.steps,
+           "step_span_ms": round((t1 - t0) / 1e6 / a.steps, 4),
+           "per_stream_launch_ms": {f"stream {s} {k}": round(sum(v) / len(v), 4)
+                                    for (s, k), v in sorted(per_stream.items())}}
+    single = rest[2 * a.warmup: 2 * (a.warmup + a.steps)]
+    if single:
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in single]
+        out["single_stream_avg_launch_ms"] = round(sum(d) / len(d), 4)
+        out["single_stream_streams"] = sorted({r["Stream_Id"] for r in single})
+    if a.bench:
+        b = json.loads(open(a.bench).read().strip().splitlines()[-1])
+        rf = b["roofline"]
+        out["bench_ms_per_step"] = b["ms_per_step"]
+        out["bench_achieved_GBs"] = rf["achieved"]
+        out["trace_achieved_GBs"] = round(rf["alg_bytes_per_step"] / (out["step_span_ms"] * 1e-3) / 1e9, 1)
+        if rf.get("single_stream"):
+            out["bench_single_stream_avg_launch_ms"] = rf["single_stream"]["avg_launch_ms"]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
