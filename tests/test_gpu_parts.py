@@ -1,0 +1,81 @@
+"""Two engine contexts on two streams of one GPU tracing the C2 1080p frame as two tile-interleaved
+parts (bench.py's default layout), launches pipelined asynchronously (primary A,
+primary B, bounce A, bounce B, several times over) so the contexts' kernels overlap. The parts'
+primary hit records and _PrimaryTriangleInfo, reassembled in screen order, and their bounce-1 hit
+records, matched by PixelIndex, must equal one context tracing the whole frame."""
+import numpy as np
+import pytest
+
+import ttconfigs as T
+import ttdist
+import tthip
+from parity_util import FAR
+
+pytestmark = pytest.mark.gpu
+
+
+def test_two_parts_on_two_streams_equal_one_launch():
+    import torch
+
+    W, H = 1920, 1080
+    WH = W * H
+    dev = torch.device("cuda:0")
+    scene = T.c2_sponza()
+    c2w, ip = T.C2_VIEW.camera(W, H)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    engines = [tthip.Engine(0, stream=s.cuda_stream) for s in streams]
+    try:
+        for e in engines:
+            e.upload(scene)
+        colors = np.zeros(WH, tthip.COL_DTYPE)
+        colors["Data"][:, 3] = 1.0
+        colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+        e0 = engines[0]
+        with torch.cuda.stream(streams[0]):
+            one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            info1 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        e0.generate(one, c2w, ip, W, H, T.NEAR, FAR, jitter=1, frames=0, max_bounce=1, device=True)
+        full = one[: WH * 48].clone()
+        e0.trace(one, WH, 0, FAR, W, H, info=info1, device=True)
+        nb1 = e0.enqueue_bounce(one, WH, 0, FAR, W, H, frames=0, max_bounce=1, device=True)
+        e0.trace(one, nb1, 1, FAR, W, H, info=info1, colors=colors_t, device=True)
+        torch.cuda.synchronize(dev)
+        ref_prim = one.view(2 * WH, 48)[:WH, 32:48].cpu().numpy()
+        ref_bnc = one.view(2 * WH, 48)[WH:WH + nb1].cpu().numpy()
+        ref_info = info1.cpu().numpy()
+        del one
+
+        parts = []
+        info = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)  # shared: the parts' pixels are disjoint
+        for s, pix_np in enumerate(ttdist.part_pixels(W, H, 1, 0, 2)):
+            with torch.cuda.stream(streams[s]):
+                rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            n = int(pix_np.shape[0])
+            rays.view(2 * WH, 48)[:n] = full.view(WH, 48)[torch.from_numpy(pix_np).to(dev)]
+            torch.cuda.synchronize(dev)
+            engines[s].trace(rays, n, 0, FAR, W, H, info=info, device=True)
+            nb = engines[s].enqueue_bounce(rays, n, 0, FAR, W, H, frames=0, max_bounce=1, device=True)
+            parts.append((engines[s], rays, n, nb))
+        torch.cuda.synchronize(dev)
+        assert sum(p[3] for p in parts) == nb1
+        for _ in range(3):  # pipelined, as bench.py's step
+            for e, rays, n, nb in parts:
+                e.trace(rays, n, 0, FAR, W, H, info=info, device=True, asynchronous=True)
+            for e, rays, n, nb in parts:
+                e.trace(rays, nb, 1, FAR, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+        torch.cuda.synchronize(dev)
+
+        own = np.concatenate([rays.view(2 * WH, 48)[:n, 32:48].cpu().numpy() for e, rays, n, nb in parts])
+        frame = ttdist.assemble_parts([own.view(np.uint32).reshape(-1, 4)], [[p[2] for p in parts]], W, H, 1, 2)
+        assert np.array_equal(frame, ref_prim.view(np.uint32).reshape(-1, 4))
+        assert np.array_equal(info.cpu().numpy(), ref_info)
+        # bounce-1: the parts compact their survivors in their own order; match records by PixelIndex
+        got = np.concatenate([rays.view(2 * WH, 48)[WH:WH + nb].cpu().numpy() for e, rays, n, nb in parts])
+        pix_of = lambda recs: recs[:, 12:16].copy().view(np.uint32)[:, 0]  # RayData.PixelIndex (bytes 12-15)
+        og, orf = np.argsort(pix_of(got), kind="stable"), np.argsort(pix_of(ref_bnc), kind="stable")
+        assert np.array_equal(got[og], ref_bnc[orf])
+    finally:
+        for e in engines:
+            e.close()
