@@ -128,7 +128,56 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         torch.cuda.synchronize(dev)
         return bufs, counts
 
-    def run(name, scene_fn, view, W, H, nb, extra_fn):
+    def parts2(sc, view, W, H, nb, info, colors_t):
+        """The same frame as 2 tile-interleaved parts, each with its own engine context on its own
+        stream and its own chain of bounce launches (bench.py's metric layout): wall
+        ms per frame over all launches of both parts."""
+        import ttdist
+
+        WH = W * H
+        c2w, ip = view.camera(W, H)
+        base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(base, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=max(nb, 1), device=True)
+        s1 = torch.cuda.Stream(dev)
+        e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
+        try:
+            e1.upload(sc)
+            chains = []
+            for e, pix_np in zip((eng, e1), ttdist.part_pixels(W, H, 1, 0, 2)):
+                cur = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+                n = int(pix_np.shape[0])
+                cur.view(2 * WH, 48)[:n] = base.view(WH, 48)[torch.from_numpy(pix_np).to(dev)]
+                torch.cuda.synchronize(dev)
+                bufs, counts = [cur.clone()], [n]
+                for b in range(nb):
+                    e.trace(cur, counts[-1], b, far, W, H, device=True)
+                    counts.append(e.enqueue_bounce(cur, counts[-1], b, far, W, H, frames=0,
+                                                   max_bounce=max(nb, 1), device=True))
+                    bufs.append(cur.clone())
+                torch.cuda.synchronize(dev)
+                chains.append((e, bufs, counts))
+
+            def frame():
+                for b in range(nb + 1):
+                    for e, bufs, counts in chains:
+                        e.trace(bufs[b], counts[b], b, far, W, H, info=info, colors=colors_t if b > 0 else None,
+                                device=True, asynchronous=True)
+
+            reps = max(3, args.steps // 2)
+            for _ in range(max(1, args.warmup)):
+                frame()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                frame()
+            torch.cuda.synchronize(dev)
+            ms = (time.perf_counter() - t0) * 1e3 / reps
+            rays = sum(sum(c) for _, _, c in chains)
+            return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": int(rays)}
+        finally:
+            e1.close()
+
+    def run(name, scene_fn, view, W, H, nb, extra_fn, with_parts=False):
         try:
             t0 = time.time()
             sc = scene_fn()
@@ -143,8 +192,15 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                                                colors=colors_t if b > 0 else None, device=True,
                                                asynchronous=True)) for b in range(nb + 1)]
             ms = timed_launches(eng, launches, max(1, args.warmup), max(3, args.steps // 2))
-            pack(name, counts, ms, dict(extra_fn(sc), width=W, height=H, build_s=round(build_s, 1)))
-            del bufs, info, colors_t
+            extra = dict(extra_fn(sc), width=W, height=H, build_s=round(build_s, 1))
+            del bufs
+            if with_parts:
+                try:
+                    extra["two_parts_two_streams"] = parts2(sc, view, W, H, nb, info, colors_t)
+                except Exception as e:  # noqa: BLE001
+                    extra["two_parts_two_streams"] = {"error": f"{type(e).__name__}: {e}"}
+            pack(name, counts, ms, extra)
+            del info, colors_t
             return sc
         except Exception as e:  # auxiliary: record, never lose the metric line
             out[name] = {"error": f"{type(e).__name__}: {e}"}
@@ -165,12 +221,13 @@ def aux_configs(torch, tthip, eng, dev, args, which):
 
     if "c3" in which:
         run("c3_sponza_primary_plus_3_bounces_1080p", T.c2_sponza, T.C2_VIEW, 1920, 1080, 3,
-            lambda sc: {"tris": int(len(sc.tris))})
+            lambda sc: {"tris": int(len(sc.tris))}, with_parts=True)
     sc4 = None
     if "c4" in which:
         sc4 = run("c4_bistro_primary_plus_1_bounce_1080p", T.c4_bistro, T.C4_VIEW, 1920, 1080, 1,
             lambda sc: {"unique_tris": int(len(sc.tris)), "instanced_tris": sc.meta["instanced_tris"],
-                        "unique_blas": 600, "instances": 2400, "cwbvh_nodes": int(len(sc.nodes))})
+                        "unique_blas": 600, "instances": 2400, "cwbvh_nodes": int(len(sc.nodes))},
+            with_parts=True)
     if "refit" in which:
         # row f4 per frame: the GPU TLAS refit of the C4 scene (AssetManager.RefitTLAS, 2,400
         # instance boxes -> TLAS nodes) and the BLAS refit of the C2 mesh as a deforming mesh
