@@ -551,6 +551,7 @@ def main():
         hits_buf = torch.zeros((max(sum(x) for x in sizes), 4), dtype=torch.int32, device=red_dev)
         gather_list = [torch.empty_like(hits_buf) for _ in range(world)] if rank == 0 else None
         comm = torch.cuda.Stream(dev)
+        copied = torch.cuda.Event()
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
 
@@ -565,12 +566,15 @@ def main():
                 for p in parts:
                     hits_buf[o:o + p.n].copy_(p.prim_hits)
                     o += p.n
+                copied.record(comm)
                 dist.gather(hits_buf, gather_list, dst=0)
         for p in parts:
             p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
         if tiles:
             for p in parts:
-                p.stream.wait_stream(comm)  # the next step's primary trace rewrites the gathered half
+                # the next step's primary trace rewrites the records copied out above: it waits for the
+                # copy, not for the gather (which reads hits_buf; the next copy is ordered after it on comm)
+                p.stream.wait_event(copied)
 
     for _ in range(args.warmup):
         step()
