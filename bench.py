@@ -409,11 +409,12 @@ def main():
                          "to ranks, each traces its pixels and their bounce-1 rays, and the primary hit records are "
                          "RCCL-gathered to rank 0 inside every timed step (strong scaling). sample: every rank "
                          "traces its own full-frame sample, no collective (weak scaling)")
-    ap.add_argument("--parts", type=int, default=2,
+    ap.add_argument("--parts", type=int, default=0,
                     help="a rank's pixels (N = 1: the frame; N > 1: its tiles) are traced as this many tile-interleaved "
                          "parts, each by its own engine on its own stream (each part's bounce-1 after its own primary), "
                          "so one part's launch drain overlaps the other parts' work (tools/exp_streams.py). 1: one "
-                         "launch per bounce")
+                         "launch per bounce; 0 (default): 2, or 3 at N >= 4 (shards of <= 1/4 frame: measured "
+                         "-11%% / -4%% step time at the N = 4 / 8 shards vs 2 parts, profiles/r02/exp_streams_2v3_w*.json)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     ap.add_argument("--no-single", action="store_true",
                     help="N = 1, parts > 1: skip the single-stream leg (one launch at a time; roofline.single_stream)")
@@ -489,6 +490,8 @@ def main():
     # a rank's pixels (the whole frame at N = 1) as P tile-interleaved parts, each traced by its own
     # engine context on its own stream: a part's launches overlap the other parts' launch drains
     # (tools/exp_streams.py); P = 1 is one full-frame launch per bounce in the kernel's own tile order
+    if args.parts <= 0:
+        args.parts = 3 if world >= 4 else 2
     P = max(1, args.parts) if (tiles or world == 1) else 1
     split = tiles or P > 1
 
