@@ -83,9 +83,18 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
                                                    const uint4 n3, const uint4 n4, const LaneRay& r,
                                                    uint32_t oct_inv4, float max_distance) {
     const uint32_t w = n0.w;
-    const float adjx = __uint_as_float((w & 0xffu) << 23) * r.ix;
-    const float adjy = __uint_as_float(((w >> 8) & 0xffu) << 23) * r.iy;
-    const float adjz = __uint_as_float(((w >> 16) & 0xffu) << 23) * r.iz;
+    // asfloat(e << 23) per axis: the exponent byte shifted into place by ONE v_lshlrev_b32_sdwa
+    // (byte-selected source, so no mask), instead of a shift + an AND each
+    uint32_t ex, ey, ez;
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+        : "=v"(ex) : "s"(23u), "v"(w));
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+        : "=v"(ey) : "s"(23u), "v"(w));
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+        : "=v"(ez) : "s"(23u), "v"(w));
+    const float adjx = __uint_as_float(ex) * r.ix;
+    const float adjy = __uint_as_float(ey) * r.iy;
+    const float adjz = __uint_as_float(ez) * r.iz;
     const float orgx = r.ix * (__uint_as_float(n0.x) - r.ox);
     const float orgy = r.iy * (__uint_as_float(n0.y) - r.oy);
     const float orgz = r.iz * (__uint_as_float(n0.z) - r.oz);
@@ -115,7 +124,11 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
             const float tmaxy = fma_((float)((y_max >> (j * 8)) & 0xffu), adjy, orgy);
             const float tmaxz = fma_((float)((z_max >> (j * 8)) & 0xffu), adjz, orgz);
             const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
-            const float tmax = fminf(fminf(tmaxx, tmaxy), fminf(tmaxz, max_distance));
+            // min(tmaxz, t_max) as a plain v_min_f32: max_distance is never a signalling NaN (FarPlane or
+            // an accepted t), so the per-step canonicalize fminf would add is dropped
+            float tmaxz_c;
+            asm("v_min_f32 %0, %1, %2" : "=v"(tmaxz_c) : "v"(tmaxz), "v"(max_distance));
+            const float tmax = fminf(fminf(tmaxx, tmaxy), tmaxz_c);
             // child_bits byte j << bit_index byte j in ONE v_lshlrev_b32_sdwa (both operands byte-selected)
             uint32_t bits;
             if (j == 0)
