@@ -64,6 +64,15 @@ tt_status tt_blas_build_from_bvh2(const tt_mesh_input* mesh, const int32_t* fina
 /* ... or over finished CWBVH8 nodes + cwbvh_indices (tt_blas_build_device in truetrace_hip.h). */
 tt_status tt_blas_build_from_cwbvh(const tt_mesh_input* mesh, const tt_cwbvh_node* nodes, uint32_t n_nodes,
                                    const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out);
+/* The same with the triangle preparation done once: tt_blas_prepare keeps BuildTotal's AggTriangles
+ * (and writes the AABBs the device builder consumes); tt_blas_build_from_cwbvh_prepared then only
+ * permutes them into leaf order. The handle is consumed (freed) by the build call on success and
+ * on failure; tt_blas_prep_free releases one that is not built. */
+typedef struct tt_blas_prep tt_blas_prep;
+tt_status tt_blas_prepare(const tt_mesh_input* mesh, float* aabbs_maxmin, tt_blas_prep** out);
+tt_status tt_blas_build_from_cwbvh_prepared(tt_blas_prep* prep, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                                            const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out);
+void tt_blas_prep_free(tt_blas_prep* prep);
 tt_status tt_blas_get_info(const tt_blas* b, tt_blas_info* info);
 /* Copies the packed nodes (80 B) and the leaf-ordered triangles (88 B). */
 tt_status tt_blas_copy(const tt_blas* b, tt_cwbvh_node* nodes, tt_cuda_triangle* tris);

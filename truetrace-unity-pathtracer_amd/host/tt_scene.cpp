@@ -935,19 +935,64 @@ tt_status tt_blas_build(const tt_mesh_input* m, tt_blas** out) {
     return TT_OK;
 }
 
+extern "C++" {
+namespace {
+// splits [0, n) over up to 16 threads for large n (independent iterations)
+template <class F>
+void parallel_range(uint32_t n, F&& f) {
+    const uint32_t nth = (n >= (1u << 16) && std::getenv("TT_BUILD_SERIAL") == nullptr)
+                             ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    if (nth == 1) {
+        f(0u, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t k = 1; k < nth; k++)
+        th.emplace_back(f, (uint32_t)((uint64_t)n * k / nth), (uint32_t)((uint64_t)n * (k + 1) / nth));
+    f(0u, (uint32_t)((uint64_t)n / nth));
+    for (auto& t : th) t.join();
+}
+void write_aabbs(const BlasPrep& P, float* aabbs) {
+    parallel_range((uint32_t)P.Triangles.size(), [&](uint32_t t0, uint32_t t1) {
+        for (uint32_t t = t0; t < t1; t++) {
+            const AABB& a = P.Triangles[t];
+            float* o = aabbs + 6 * (size_t)t;
+            o[0] = a.BBMax.x; o[1] = a.BBMax.y; o[2] = a.BBMax.z;
+            o[3] = a.BBMin.x; o[4] = a.BBMin.y; o[5] = a.BBMin.z;
+        }
+    });
+}
+}  // namespace
+}  // extern "C++"
+
+struct tt_blas_prep {
+    BlasPrep P;
+};
+
 tt_status tt_blas_prepare_aabbs(const tt_mesh_input* m, float* aabbs) {
     if (!aabbs) return TT_ERR_INVALID_ARG;
     BlasPrep P;
     const tt_status st = blas_prepare(m, P);
     if (st != TT_OK) return st;
-    for (size_t t = 0; t < P.Triangles.size(); t++) {
-        const AABB& a = P.Triangles[t];
-        float* o = aabbs + 6 * t;
-        o[0] = a.BBMax.x; o[1] = a.BBMax.y; o[2] = a.BBMax.z;
-        o[3] = a.BBMin.x; o[4] = a.BBMin.y; o[5] = a.BBMin.z;
-    }
+    write_aabbs(P, aabbs);
     return TT_OK;
 }
+
+tt_status tt_blas_prepare(const tt_mesh_input* m, float* aabbs, tt_blas_prep** out) {
+    if (!aabbs || !out) return TT_ERR_INVALID_ARG;
+    tt_blas_prep* p = new (std::nothrow) tt_blas_prep();
+    if (!p) return TT_ERR_OOM;
+    const tt_status st = blas_prepare(m, p->P);
+    if (st != TT_OK) {
+        delete p;
+        return st;
+    }
+    write_aabbs(p->P, aabbs);
+    *out = p;
+    return TT_OK;
+}
+
+void tt_blas_prep_free(tt_blas_prep* p) { delete p; }
 
 tt_status tt_bvh2_presort(const float* aabbs, uint32_t n, int32_t* presorted) {
     if (!aabbs || !n || !presorted) return TT_ERR_INVALID_ARG;
@@ -1037,16 +1082,13 @@ tt_status tt_blas_build_from_bvh2(const tt_mesh_input* m, const int32_t* final_i
     return TT_OK;
 }
 
-tt_status tt_blas_build_from_cwbvh(const tt_mesh_input* m, const tt_cwbvh_node* nodes, uint32_t n_nodes,
-                                   const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out) {
-    if (!out || !nodes || !n_nodes || !cwbvh_indices) return TT_ERR_INVALID_ARG;
-    const auto t0 = std::chrono::steady_clock::now();
-    BlasPrep P;
-    tt_status st = blas_prepare(m, P);
-    if (st != TT_OK) return st;
+namespace {
+tt_status blas_from_cwbvh(const BlasPrep& P, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                          const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out,
+                          std::chrono::steady_clock::time_point t0) {
     const uint32_t ntri = (uint32_t)P.agg.size();
     std::vector<char> seen(ntri, 0);
-    for (uint32_t i = 0; i < ntri; i++) {
+    for (uint32_t i = 0; i < ntri; i++) {  // a permutation of the triangles (sequential: duplicate check)
         const int32_t k = cwbvh_indices[i];
         if (k < 0 || (uint32_t)k >= ntri || seen[(size_t)k]) return TT_ERR_INVALID_ARG;
         seen[(size_t)k] = 1;
@@ -1057,14 +1099,37 @@ tt_status tt_blas_build_from_cwbvh(const tt_mesh_input* m, const tt_cwbvh_node* 
     b->bvh2_depth = bvh2_depth;
     b->tris.resize(ntri);
     b->leaf_of.assign(ntri, 0);
-    for (uint32_t i = 0; i < ntri; i++) {
-        b->tris[i] = P.agg[(size_t)cwbvh_indices[i]];
-        b->leaf_of[(size_t)cwbvh_indices[i]] = (int32_t)i;
-    }
+    parallel_range(ntri, [&](uint32_t i0, uint32_t i1) {  // disjoint writes: cwbvh_indices is a permutation
+        for (uint32_t i = i0; i < i1; i++) {
+            b->tris[i] = P.agg[(size_t)cwbvh_indices[i]];
+            b->leaf_of[(size_t)cwbvh_indices[i]] = (int32_t)i;
+        }
+    });
     b->nodes.assign(nodes, nodes + n_nodes);
     b->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *out = b;
     return TT_OK;
+}
+}  // namespace
+
+tt_status tt_blas_build_from_cwbvh(const tt_mesh_input* m, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                                   const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out) {
+    if (!out || !nodes || !n_nodes || !cwbvh_indices) return TT_ERR_INVALID_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    BlasPrep P;
+    tt_status st = blas_prepare(m, P);
+    if (st != TT_OK) return st;
+    return blas_from_cwbvh(P, nodes, n_nodes, cwbvh_indices, bvh2_depth, out, t0);
+}
+
+tt_status tt_blas_build_from_cwbvh_prepared(tt_blas_prep* prep, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                                            const int32_t* cwbvh_indices, uint32_t bvh2_depth, tt_blas** out) {
+    if (!prep) return TT_ERR_INVALID_ARG;
+    tt_status st = TT_ERR_INVALID_ARG;
+    if (out && nodes && n_nodes && cwbvh_indices)
+        st = blas_from_cwbvh(prep->P, nodes, n_nodes, cwbvh_indices, bvh2_depth, out, std::chrono::steady_clock::now());
+    delete prep;
+    return st;
 }
 
 tt_status tt_blas_copy_leaf_order(const tt_blas* b, int32_t* out) {

@@ -190,7 +190,8 @@ SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_f
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
                  "tt_synth_prop", "tt_synth_ground", "tt_synth_san_miguel", "tt_synth_mesh_view", "tt_synth_mesh_free",
                  "tt_synth_mesh_from_arrays", "tt_blas_copy_leaf_order", "tt_blas_prepare_aabbs", "tt_bvh2_presort",
-                 "tt_blas_build_from_bvh2", "tt_blas_build_from_cwbvh"]
+                 "tt_blas_build_from_bvh2", "tt_blas_build_from_cwbvh", "tt_blas_prepare",
+                 "tt_blas_build_from_cwbvh_prepared", "tt_blas_prep_free"]
 
 
 def scene_lib():
@@ -221,6 +222,10 @@ def scene_lib():
         L.tt_bvh2_presort.argtypes = [vp, u32, vp]
         L.tt_blas_build_from_bvh2.argtypes = [C.POINTER(MeshInput), vp, vp, vp, vp, u32, C.POINTER(vp)]
         L.tt_blas_build_from_cwbvh.argtypes = [C.POINTER(MeshInput), vp, u32, vp, u32, C.POINTER(vp)]
+        L.tt_blas_prepare.argtypes = [C.POINTER(MeshInput), vp, C.POINTER(vp)]
+        L.tt_blas_build_from_cwbvh_prepared.argtypes = [vp, vp, u32, vp, u32, C.POINTER(vp)]
+        L.tt_blas_prep_free.argtypes = [vp]
+        L.tt_blas_prep_free.restype = None
         L.tt_dotnet_sort_by_key.argtypes = [vp, u32, vp]
         L.tt_dotnet_sort_by_key.restype = None
         L.tt_synth_cornell.argtypes = [C.POINTER(vp)]
@@ -454,11 +459,19 @@ class Blas:
             t0 = time.perf_counter()
             n = v.n_indices // 3
             aabbs = np.zeros((n, 6), np.float32)
-            _check(L.tt_blas_prepare_aabbs(C.byref(v), aabbs.ctypes.data), "tt_blas_prepare_aabbs")
+            prep = C.c_void_p()  # the prepared triangles, kept for the final assembly (bvh2+bvh8)
+            if device_stages == "bvh2+bvh8":
+                _check(L.tt_blas_prepare(C.byref(v), aabbs.ctypes.data, C.byref(prep)), "tt_blas_prepare")
+            else:
+                _check(L.tt_blas_prepare_aabbs(C.byref(v), aabbs.ctypes.data), "tt_blas_prepare_aabbs")
             t1 = time.perf_counter()
             pre = np.zeros((3, n), np.int32)
             if engine.L.tt_bvh2_presort_device(engine.h, aabbs.ctypes.data, n, pre.ctypes.data) != TT_OK:
-                _check(L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data), "tt_bvh2_presort")
+                st = L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data)
+                if st != TT_OK:
+                    if prep:
+                        L.tt_blas_prep_free(prep)
+                    raise TTError(st, "tt_bvh2_presort")
             t2 = time.perf_counter()
             if device_stages == "bvh2+bvh8":
                 cap = max(1, n - 1)
@@ -468,10 +481,12 @@ class Blas:
                 st = engine.L.tt_blas_build_device(engine.h, aabbs.ctypes.data, n, pre.ctypes.data, nodes.ctypes.data,
                                                    cap, C.byref(nn), cw.ctypes.data, C.byref(depth))
                 if st != TT_OK:
+                    L.tt_blas_prep_free(prep)
                     raise TTError(st, "tt_blas_build_device")
                 t3 = time.perf_counter()
-                _check(L.tt_blas_build_from_cwbvh(C.byref(v), nodes.ctypes.data, nn.value, cw.ctypes.data, depth.value,
-                                                  C.byref(h)), "tt_blas_build_from_cwbvh")
+                _check(L.tt_blas_build_from_cwbvh_prepared(prep, nodes.ctypes.data, nn.value, cw.ctypes.data,
+                                                           depth.value, C.byref(h)),
+                       "tt_blas_build_from_cwbvh_prepared")  # consumes prep
                 if timings is not None:
                     timings.update(prepare_s=t1 - t0, presort_s=t2 - t1, device_s=t3 - t2,
                                    assemble_s=time.perf_counter() - t3)
