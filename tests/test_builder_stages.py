@@ -69,3 +69,40 @@ def test_malformed_bvh2_is_rejected():
     leaf = int(np.nonzero(count == 1)[0][0])
     bad[2][leaf] = 10 ** 6  # leaf position out of range
     assert _from_bvh2(L, v, bad, 1)[0] != 0
+
+
+@pytest.mark.parametrize("mesh_fn", [tthip.Mesh.cornell, lambda: tthip.Mesh.prop(4, 80_000)])
+def test_prepared_handle_reassembles_the_host_blas(mesh_fn):
+    """tt_blas_prepare + tt_blas_build_from_cwbvh_prepared (the device build's assembly, triangles
+    prepared once) over the host build's own nodes and leaf order reproduce it byte for byte; a
+    leaf order that is not a permutation is rejected, and the handle is consumed either way."""
+    mesh = mesh_fn()
+    ref = tthip.Blas(mesh)
+    nodes, tris = ref.arrays()
+    cw = np.argsort(ref.leaf_order()).astype(np.int32)  # leaf position -> source triangle
+    L = tthip.scene_lib()
+    v = mesh.view()
+    n = v.n_indices // 3
+    aabbs = np.zeros((n, 6), np.float32)
+    ref_aabbs = np.zeros((n, 6), np.float32)
+    assert L.tt_blas_prepare_aabbs(v, ref_aabbs.ctypes.data) == 0
+    prep = tthip.C.c_void_p()
+    assert L.tt_blas_prepare(v, aabbs.ctypes.data, tthip.C.byref(prep)) == 0
+    assert np.array_equal(aabbs.view(np.uint32), ref_aabbs.view(np.uint32))
+    h = tthip.C.c_void_p()
+    assert L.tt_blas_build_from_cwbvh_prepared(prep, nodes.ctypes.data, len(nodes), cw.ctypes.data,
+                                               ref.info.bvh2_depth, tthip.C.byref(h)) == 0
+    got = tthip.Blas.__new__(tthip.Blas)
+    got.h = h.value
+    got.info = tthip.BlasInfo()
+    L.tt_blas_get_info(got.h, tthip.C.byref(got.info))
+    for a, b in zip((nodes, tris), got.arrays()):
+        assert a.tobytes() == b.tobytes()
+    assert np.array_equal(ref.leaf_order(), got.leaf_order())
+    bad = cw.copy()
+    bad[-1] = bad[0]  # a duplicate: not a permutation
+    prep2 = tthip.C.c_void_p()
+    assert L.tt_blas_prepare(v, aabbs.ctypes.data, tthip.C.byref(prep2)) == 0
+    h2 = tthip.C.c_void_p()
+    assert L.tt_blas_build_from_cwbvh_prepared(prep2, nodes.ctypes.data, len(nodes), bad.ctypes.data,
+                                               ref.info.bvh2_depth, tthip.C.byref(h2)) == tthip.TT_ERR_INVALID_ARG
