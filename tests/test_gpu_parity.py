@@ -88,6 +88,19 @@ def test_malformed_scene_is_refused(engine):
     assert e.value.status == tthip.TT_ERR_INVALID_ARG
 
 
+def test_nan_far_plane_is_refused(engine):
+    """FarPlane seeds best.t, the node test's t_max, which the kernel's clamp assumes is not a NaN:
+    tt_trace_closest refuses a NaN far plane (an infinite one is traced)."""
+    sc = tthip.single_object_scene(tthip.Mesh.soup(3, 200, 1.0, 0.1))
+    engine.upload(sc)
+    rays = np.zeros(2 * 64, tthip.RAY_DTYPE)
+    rays["direction"][:, 2] = 1.0
+    with pytest.raises(tthip.TTError) as e:
+        engine.trace(rays, 64, 0, float("nan"), 8, 8)
+    assert e.value.status == tthip.TT_ERR_INVALID_ARG
+    engine.trace(rays, 64, 0, float("inf"), 8, 8)
+
+
 # ------------------------------------------------------------------ golden fixtures
 @pytest.mark.parametrize("name", golden_io.NAMES)
 def test_golden_on_gpu(engine, name):

@@ -953,6 +953,9 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or rays");
     if (p->screen_width == 0 || p->screen_height == 0) return fail(c, TT_ERR_INVALID_ARG, "zero screen size");
     if (p->bounce < 0) return fail(c, TT_ERR_INVALID_ARG, "negative bounce");
+    // FarPlane (camera.farClipPlane) seeds best.t, the node test's t_max; the kernel's t_max clamp
+    // assumes it is not a NaN (tt_traverse.h)
+    if (p->far_plane != p->far_plane) return fail(c, TT_ERR_INVALID_ARG, "far_plane is NaN");
     if (info && p->bounce > 0 && !colors)
         return fail(c, TT_ERR_INVALID_ARG, "GlobalColors required for _PrimaryTriangleInfo at bounce > 0");
     if (c->any_cutout && !c->atlas.p)

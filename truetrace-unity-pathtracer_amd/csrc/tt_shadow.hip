@@ -417,7 +417,9 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
                 ray.dy = __uint_as_float(r1.y);
                 ray.dz = __uint_as_float(r1.z);
                 // |t| (:356); VisabilityCheckCompute takes its dist as given, throughput 0 (:732)
-                max_distance = vis_check ? __uint_as_float(r1.w) : fabsf(__uint_as_float(r1.w));
+                // canonicalized once per ray: node_intersect's t_max clamp is a plain v_min_f32
+                max_distance = __builtin_canonicalizef(vis_check ? __uint_as_float(r1.w)
+                                                                 : fabsf(__uint_as_float(r1.w)));
                 thr = vis_check ? make_float3(0.0f, 0.0f, 0.0f) : make_float3(1.0f, 1.0f, 1.0f);
                 ray.ix = rcp_rn(ray.dx);
                 ray.iy = rcp_rn(ray.dy);

@@ -124,8 +124,9 @@ __device__ __forceinline__ uint32_t node_intersect(const uint4 n0, const uint4 n
             const float tmaxy = fma_((float)((y_max >> (j * 8)) & 0xffu), adjy, orgy);
             const float tmaxz = fma_((float)((z_max >> (j * 8)) & 0xffu), adjz, orgz);
             const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
-            // min(tmaxz, t_max) as a plain v_min_f32: max_distance is never a signalling NaN (FarPlane or
-            // an accepted t), so the per-step canonicalize fminf would add is dropped
+            // min(tmaxz, t_max) as a plain v_min_f32 without the per-step canonicalize fminf adds: t_max is
+            // never a signalling NaN -- FarPlane (tt_trace_closest rejects a NaN) or an accepted t in the
+            // closest-hit kernel, the ray's distance canonicalized at ray start in the any-hit kernel
             float tmaxz_c;
             asm("v_min_f32 %0, %1, %2" : "=v"(tmaxz_c) : "v"(tmaxz), "v"(max_distance));
             const float tmax = fminf(fminf(tmaxx, tmaxy), tmaxz_c);
