@@ -448,12 +448,15 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    # TT_BENCH_RCCL_WORLD1=1 (rehearsal, not a bench mode): one rank runs the N > 1 tile path with a
+    # real RCCL communicator of size 1 -- the gather on RCCL's own stream beside the part streams
+    rccl1 = world == 1 and os.environ.get("TT_BENCH_RCCL_WORLD1") == "1"
+    if world > 1 or rccl1:
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=dev)
         else:
             dist.init_process_group(backend=backend)
-    tiles = world > 1 and args.shard == "tiles"
+    tiles = (world > 1 or rccl1) and args.shard == "tiles"
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -869,7 +872,7 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or rccl1:
         dist.destroy_process_group()
 
 
