@@ -22,16 +22,22 @@ from parity_util import CPU_THREADS, FAR  # noqa: E402
 from test_gpu_parity import glass_soup, instanced_scene  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+SEED0 = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+# "variants": every case also draws the compile-time trace variants of GlobalDefines.cginc:4,11 as
+# launch flags (IgnoreGlassMain / IgnoreBackfacing, both, or neither) for its closest-hit traces
+VARIANTS = len(sys.argv) > 3 and sys.argv[3] == "variants"
+FLAG_SETS = (0, tthip.TT_TRACE_IGNORE_GLASS, tthip.TT_TRACE_IGNORE_BACKFACING,
+             tthip.TT_TRACE_IGNORE_GLASS | tthip.TT_TRACE_IGNORE_BACKFACING)
 eng = tthip.Engine(0)
 bad_total, rays_total = 0, 0
 
 
-def compare(sc, rays, n, bounce, W, H, info=True):
+def compare(sc, rays, n, bounce, W, H, info=True, flags=0):
     rg, rc = rays.copy(), rays.copy()
     ig = np.zeros((W * H, 4), np.uint32) if info else None
     ic = np.zeros((W * H, 4), np.uint32) if info else None
-    eng.trace(rg, n, bounce, FAR, W, H, info=ig)
-    st, _ = O.trace(sc, rc, n, bounce, FAR, W, H, info=ic, nthreads=CPU_THREADS)
+    eng.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags)
+    st, _ = O.trace(sc, rc, n, bounce, FAR, W, H, info=ic, nthreads=CPU_THREADS, flags=flags)
     assert st == 0
     off = W * H if bounce % 2 else 0
     bad = int((rg["hits"][off:off + n] != rc["hits"][off:off + n]).any(1).sum())
@@ -59,8 +65,9 @@ def shadow_compare(sc, sr, W, H):
 
 t0 = time.time()
 for k in range(N):
-    seed = 1000 + k
+    seed = SEED0 + k
     rng = np.random.default_rng(seed)
+    flags = FLAG_SETS[int(rng.integers(0, 4))] if VARIANTS else 0
     kind = ("soup", "instanced", "glass")[k % 3]
     if kind == "soup":
         sc = tthip.single_object_scene(tthip.Mesh.soup(seed, int(rng.integers(500, 120000)), 1.0,
@@ -79,17 +86,17 @@ for k in range(N):
     c2w, ip = tthip.unity_camera(pos, look, (0, 1, 0), float(rng.uniform(30, 90)), W, H, 0.05, FAR)
     rays = O.generate(c2w, ip, W, H, 0.05, FAR)
     eng.upload(sc)
-    b0, rg = compare(sc, rays, W * H, 0, W, H)
+    b0, rg = compare(sc, rays, W * H, 0, W, H, flags=flags)
     # bounce 1 from the GPU's primary hits (identical to the oracle's when b0 == 0)
     r1 = rg.copy()
     nb = eng.enqueue_bounce(r1, W * H, 0, FAR, W, H, frames=k, max_bounce=2)
-    b1, _ = compare(sc, r1, nb, 1, W, H, info=False) if nb else (0, None)
+    b1, _ = compare(sc, r1, nb, 1, W, H, info=False, flags=flags) if nb else (0, None)
     sr = hb.nee_rays_from_hits(rg, W * H, tuple(rng.uniform(-2, 2, 3) + [0, 3, 0]), seed)
     bs = shadow_compare(sc, sr, W, H) if len(sr) else 0
     n_rays = W * H + nb + len(sr)
     rays_total += n_rays
     bad_total += b0 + b1 + bs
-    print(f"case {k:3d} {kind:9s} seed {seed} tris {len(sc.tris):6d} {W}x{H}: primary+info mismatches {b0}, "
+    print(f"case {k:3d} {kind:9s} seed {seed} flags {flags:#04x} tris {len(sc.tris):6d} {W}x{H}: primary+info mismatches {b0}, "
           f"bounce-1 ({nb} rays) {b1}, shadow ({len(sr)} rays) {bs}", flush=True)
 print(f"SUMMARY: {N} cases, {rays_total} rays traced on the GPU and the oracle, {bad_total} mismatching records, "
       f"{time.time() - t0:.0f} s", flush=True)
