@@ -128,22 +128,25 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         torch.cuda.synchronize(dev)
         return bufs, counts
 
-    def parts2(sc, view, W, H, nb, info, colors_t):
-        """The same frame as 2 tile-interleaved parts, each with its own engine context on its own
+    def parts_layout(sc, view, W, H, nb, info, colors_t, P=2):
+        """The same frame as P tile-interleaved parts, each with its own engine context on its own
         stream and its own chain of bounce launches (bench.py's metric layout): wall
-        ms per frame over all launches of both parts."""
+        ms per frame over all launches of all parts."""
         import ttdist
 
         WH = W * H
         c2w, ip = view.camera(W, H)
         base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(base, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=max(nb, 1), device=True)
-        s1 = torch.cuda.Stream(dev)
-        e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
+        extra_engs = []
         try:
-            e1.upload(sc)
+            for _ in range(P - 1):
+                s1 = torch.cuda.Stream(dev)
+                e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
+                extra_engs.append(e1)
+                e1.upload(sc)
             chains = []
-            for e, pix_np in zip((eng, e1), ttdist.part_pixels(W, H, 1, 0, 2)):
+            for e, pix_np in zip([eng] + extra_engs, ttdist.part_pixels(W, H, 1, 0, P)):
                 cur = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
                 n = int(pix_np.shape[0])
                 cur.view(2 * WH, 48)[:n] = base.view(WH, 48)[torch.from_numpy(pix_np).to(dev)]
@@ -175,7 +178,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             rays = sum(sum(c) for _, _, c in chains)
             return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": int(rays)}
         finally:
-            e1.close()
+            for e1 in extra_engs:
+                e1.close()
 
     def run(name, scene_fn, view, W, H, nb, extra_fn, with_parts=False):
         try:
@@ -195,10 +199,11 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             extra = dict(extra_fn(sc), width=W, height=H, build_s=round(build_s, 1))
             del bufs
             if with_parts:
-                try:
-                    extra["two_parts_two_streams"] = parts2(sc, view, W, H, nb, info, colors_t)
-                except Exception as e:  # noqa: BLE001
-                    extra["two_parts_two_streams"] = {"error": f"{type(e).__name__}: {e}"}
+                for P, key in ((2, "two_parts_two_streams"), (3, "three_parts_three_streams")):
+                    try:
+                        extra[key] = parts_layout(sc, view, W, H, nb, info, colors_t, P)
+                    except Exception as e:  # noqa: BLE001
+                        extra[key] = {"error": f"{type(e).__name__}: {e}"}
             pack(name, counts, ms, extra)
             del info, colors_t
             return sc
@@ -265,7 +270,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         log(f"aux refit: {rec}")
     if "c5" in which:
         run("c5_san_miguel_primary_4k", T.c5_san_miguel, T.C5_VIEW, 3840, 2160, 0,
-            lambda sc: {"tris": int(len(sc.tris)), "cwbvh_nodes": int(len(sc.nodes))})
+            lambda sc: {"tris": int(len(sc.tris)), "cwbvh_nodes": int(len(sc.nodes))}, with_parts=True)
     return out
 
 
