@@ -138,11 +138,11 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         c2w, ip = view.camera(W, H)
         base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(base, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=max(nb, 1), device=True)
-        extra_engs = []
+        extra_engs, streams = [], []
         try:
             for _ in range(P - 1):
-                s1 = torch.cuda.Stream(dev)
-                e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
+                streams.append(torch.cuda.Stream(dev))
+                e1 = tthip.Engine(dev.index, stream=streams[-1].cuda_stream)
                 extra_engs.append(e1)
                 e1.upload(sc)
             chains = []
@@ -284,7 +284,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     import ttconfigs as T
     import ttdist
 
-    rec, ok, ms = {}, 1, 0.0
+    rec, ok, ms, ms_parts = {}, 1, 0.0, 0.0
     W, H, far = 3840, 2160, T.FAR
     WH = W * H
     try:
@@ -301,6 +301,33 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         launch = [lambda: eng.trace(mine, n, 0, far, W, H, device=True, asynchronous=True)]
         ms = float(np.median(timed_launches(eng, launch, max(1, args.warmup), max(3, args.steps // 2))))
         rec.update(rays_this_rank=n, build_s=round(build_s, 1))
+        # the metric's layout: the rank's tiles as 2 tile-interleaved parts, each on its own engine
+        # context and stream, frames back to back (a part's launch drain overlaps the other's work)
+        s1 = torch.cuda.Stream(dev)
+        e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
+        try:
+            e1.upload(sc)
+            chains = []
+            for e, pp in zip((eng, e1), ttdist.part_pixels(W, H, world, rank, 2)):
+                chains.append((e, full.view(WH, 48)[torch.from_numpy(pp).to(dev)].contiguous(), int(pp.shape[0])))
+            torch.cuda.synchronize(dev)
+
+            def frame():
+                for e, buf, m in chains:
+                    e.trace(buf, m, 0, far, W, H, device=True, asynchronous=True)
+
+            for _ in range(max(1, args.warmup)):
+                frame()
+            torch.cuda.synchronize(dev)
+            reps = max(3, args.steps // 2)
+            tp = time.perf_counter()
+            for _ in range(reps):
+                frame()
+            torch.cuda.synchronize(dev)
+            ms_parts = (time.perf_counter() - tp) * 1e3 / reps
+            hits_parts = torch.cat([buf.view(m, 48)[:, 32:48] for _, buf, m in chains]).contiguous()
+        finally:
+            e1.close()
     except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
         ok = 0
         rec["error"] = f"rank {rank}: {type(e).__name__}: {e}"
@@ -311,6 +338,8 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     if flags[0].item() < 1.0:
         return rec if rank == 0 else None
+    tp_max = torch.tensor([ms_parts], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(tp_max, op=dist.ReduceOp.MAX)
     hits = mine.view(n, 48)[:, 32:48].contiguous().view(torch.int32).to(red_dev)
     torch.cuda.synchronize(dev)
     dist.barrier()
@@ -318,16 +347,24 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     parts = ttdist.gather_hits(hits, world, rank)
     torch.cuda.synchronize(dev)
     gather_ms = (time.perf_counter() - tg) * 1e3
+    # the two-part records, one gather too (each rank's parts back to back)
+    parts2 = ttdist.gather_hits(hits_parts.view(torch.int32).to(red_dev), world, rank)
     if rank != 0:
         return None
     frame = ttdist.assemble_tiles(parts, W, H, world)
+    sizes2 = [[int(pp.shape[0]) for pp in ttdist.part_pixels(W, H, world, r, 2)] for r in range(world)]
+    frame2 = ttdist.assemble_parts(parts2, sizes2, W, H, world, 2)
     eng.trace(full, WH, 0, far, W, H, device=True)
     ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
     frame_ms = float(t_max.item())
+    frame_ms_parts = float(tp_max.item())
     rec.update(config="c5_san_miguel_4k_tiles", ranks=world, tile=64, frame_rays=WH,
                trace_ms_slowest_rank=round(frame_ms, 4), trace_ms_rank0=round(ms, 4),
                mrays_s_frame=round(WH / frame_ms / 1e3, 1), gather_ms=round(gather_ms, 3),
-               identical_to_1gpu=bool(np.array_equal(frame, ref)))
+               identical_to_1gpu=bool(np.array_equal(frame, ref)),
+               two_parts=dict(ms_per_frame_slowest_rank=round(frame_ms_parts, 4),
+                              mrays_s_frame=round(WH / frame_ms_parts / 1e3, 1),
+                              identical_to_1gpu=bool(np.array_equal(frame2, ref))))
     log(f"c5 tiles: {rec}")
     return rec
 
