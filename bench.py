@@ -458,6 +458,8 @@ def main():
                          "launch per bounce; 0 (default): 2, or 3 at N >= 4 (shards of <= 1/4 frame: measured "
                          "-11%% / -4%% step time at the N = 4 / 8 shards vs 2 parts, profiles/r02/exp_streams_2v3_w*.json)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
+    ap.add_argument("--steady-steps", type=int, default=200,
+                    help="N = 1: steps of the secondary steady-state leg after the timed region (0 = skip)")
     ap.add_argument("--no-single", action="store_true",
                     help="N = 1, parts > 1: skip the single-stream leg (one launch at a time; roofline.single_stream)")
     ap.add_argument("--no-recur", action="store_true",
@@ -666,6 +668,22 @@ def main():
         achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9
     else:  # the P parts' launches overlap: all of a step's algorithmic bytes over the step's wall time
         achieved = B_step / (elapsed / args.steps) / 1e9
+
+    # the same step for longer, right after the timed region (N = 1): the rate once clocks and caches
+    # have settled -- with W = 5, K = 20 the first post-warmup steps run ~2% slower.
+    # A secondary field; `value` is always the W/K protocol's measurement above.
+    steady = None
+    if world == 1 and args.steady_steps > 0:
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        for _ in range(args.steady_steps):
+            step()
+        torch.cuda.synchronize(dev)
+        es = time.perf_counter() - ts
+        steady = {"steps": args.steady_steps, "ms_per_step": round(es * 1e3 / args.steady_steps, 4),
+                  "mrays_s": round(rays_per_step * args.steady_steps / es / 1e6, 2),
+                  "note": "untimed-for-value: the same step repeated after the timed region"}
+        log(f"steady state: {steady}")
 
     # SURVEY 8(e) parity -- the gathered (N > 1) or the parts' (N = 1) frame must equal one launch
     # tracing the whole frame
@@ -893,6 +911,7 @@ def main():
                    "trace_ms_per_step_slowest_rank": round(trace_ms_slowest, 4),
                    "kernel_mrays_s_trace_only": round((parts[0].n + parts[0].nb) / trace_ms_rank / 1e3, 2),
                    "gather_identical_to_1gpu": gather_parity,
+                   "steady_state": steady,
                    "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},
