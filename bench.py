@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import shutil
 import sys
@@ -73,9 +74,22 @@ def nee_rays(torch, rays, n, far, light):
     return sr.contiguous().view(torch.uint8).view(-1)
 
 
+TIMING_RING = 256  # the engine's HIP-event ring (tt_api.hip TT_RING): tt_timing_read returns the last 256
+
+
+def ring_tail(eng, per_step, steps):
+    """The engine ring's per-call times (ms) of the last min(steps, 256 // per_step) steps, shape
+    (rows, per_step): with more calls than the ring holds, the oldest are overwritten, so per-launch
+    statistics cover the last rows steps (the wall-clock `value` always covers all of them)."""
+    rows = min(steps, TIMING_RING // per_step)
+    ms = np.asarray(eng.timing_read(), np.float64)
+    assert len(ms) == rows * per_step, (len(ms), rows, per_step)
+    return ms.reshape(rows, per_step)
+
+
 def timed_launches(eng, launches, warmup, steps):
     """Runs the list of launch closures warmup + steps times; returns per-launch HIP-event times
-    (ms) as an array of shape (steps, len(launches))."""
+    (ms) as an array of shape (rows, len(launches)) over the last rows <= steps repetitions."""
     import torch
 
     for _ in range(warmup):
@@ -87,7 +101,7 @@ def timed_launches(eng, launches, warmup, steps):
         for f in launches:
             f()
     torch.cuda.synchronize()
-    return np.asarray(eng.timing_read(), np.float64).reshape(steps, len(launches))
+    return ring_tail(eng, len(launches), steps)
 
 
 def aux_configs(torch, tthip, eng, dev, args, which):
@@ -220,9 +234,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         eng.timing_reset()
         for _ in range(steps):
             fn()
-        ms = np.asarray(eng.timing_read(), np.float64)
-        assert len(ms) == steps, (len(ms), steps)
-        return ms
+        return ring_tail(eng, 1, steps)[:, 0]
 
     if "c3" in which:
         run("c3_sponza_primary_plus_3_bounces_1080p", T.c2_sponza, T.C2_VIEW, 1920, 1080, 3,
@@ -412,32 +424,94 @@ def cpu_baseline(scene, rays, info_n, n_prim, nb, colors, far, W, H, seconds):
         t = time.perf_counter() - tc0
         return done / t / 1e6, reps, t
 
-    v_all, reps, tcpu = run(aff, seconds)
-    v16 = None
-    if aff != 16:
-        v16, _, _ = run(16, seconds / 2)
+    # thread counts tried: 16 (the per-GPU CPU share the GPU box grants), the cgroup quota rounded up
+    # (capped at the affinity mask), and every CPU of the affinity mask; the baseline is the best
+    # of them (an oversubscribed quota runs slower than the threads it can actually use)
+    cands = sorted({min(16, aff), min(aff, math.ceil(quota)) if quota else aff, aff})
+    runs = {}
+    for nt in cands:
+        runs[nt] = run(nt, seconds / len(cands))
+        log(f"cpu baseline candidate: {nt} threads -> {runs[nt][0]:.3f} Mrays/s ({runs[nt][1]} reps)")
+    best = max(runs, key=lambda k: runs[k][0])
+    v_best, reps, tcpu = runs[best]
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
     except OSError:
         pass
-    cpu = {"value": round(v_all, 3), "unit": "Mrays/s", "cores": aff, "kind": "port",
-           "host_cpu": model, "hardware_threads": hw, "cgroup_cpu_quota": quota,
-           "value_16_threads": None if v16 is None else round(v16, 3),
+    cpu = {"value": round(v_best, 3), "unit": "Mrays/s", "cores": best, "kind": "port",
+           "host_cpu": model, "hardware_threads": hw, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+           "candidates": {str(k): round(v[0], 3) for k, v in runs.items()},
            "sample": f"full step workload ({n_prim} primary + {nb} bounce-1 rays) x {reps} in {tcpu:.1f}s, "
-                     f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {aff} threads "
-                     f"(all CPUs of the process' affinity mask; cgroup quota {quota}); "
-                     f"C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
+                     f"oracle/tt_oracle.c scalar C ({os.path.basename(O.lib()._path)}), {best} threads "
+                     f"(the best of {cands} threads: 16, the cgroup quota {quota} rounded up, the affinity mask's "
+                     f"{aff}); C# scalar baseline (bindings/csharp/ScalarTraversal.cs) "
                      + ("not run: no .NET runtime (dotnet) on the box" if shutil.which("dotnet") is None
                         else "not run by bench.py: see tools/dump_scene_raw.py")}
-    log(f"cpu baseline {cpu['value']} Mrays/s on {aff} threads ({reps} reps, {tcpu:.1f}s); 16 threads: {v16}")
+    log(f"cpu baseline {cpu['value']} Mrays/s on {best} threads ({reps} reps, {tcpu:.1f}s); all: {cpu['candidates']}")
     return cpu
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_ranks(n: int, argv, timeout=None) -> int:
+    """`bench.py --gpus N` without a launcher: starts N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, as torchrun would),
+    before this process touches the GPU. Rank 0 prints the JSON line. Returns the worst exit code
+    (a rank killed by a signal counts as 128 + signal); once one rank fails the others are
+    terminated so none is left blocked in a collective."""
+    import signal
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TT_BENCH_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      start_new_session=False))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}), master 127.0.0.1:{port}")
+    t0 = time.time()
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        failed = [rc for rc in rcs if rc not in (None, 0)]
+        late = timeout is not None and time.time() - t0 > timeout
+        if (failed or late) and any(rc is None for rc in rcs):
+            log(f"rank exit codes {rcs}{' (timeout)' if late else ''}: terminating the remaining ranks")
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            if late and not failed:
+                rcs = [rc if rc else 124 for rc in rcs]
+            break
+        time.sleep(0.2)
+    codes = [(128 - rc) if rc < 0 else rc for rc in rcs]  # Popen: -signal for a killed child
+    log(f"rank exit codes {codes}")
+    return max(codes)
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU). Under a launcher (torchrun: WORLD_SIZE set) it must equal "
+                         "WORLD_SIZE; without one, N > 1 starts N rank processes of this script itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
@@ -472,9 +546,32 @@ def main():
                          " '' = none)")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            # no launcher: become one (nothing has touched the GPU in this process)
+            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+        if args.gpus is not None and args.gpus < 1:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} must be >= 1")
+    elif args.gpus is not None and args.gpus != int(env_world):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks; "
+                         "refusing to report a measurement for a different GPU count")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("TT_BENCH_LAUNCH_CHECK") == "1":
+        # launcher rehearsal (tests/test_bench_launch.py): the rank wiring and a gloo world, no GPU work
+        import torch.distributed as dist
+
+        dist.init_process_group(backend="gloo")
+        rec = {"rank": rank, "world": world, "dist_world_size": dist.get_world_size(),
+               "dist_rank": dist.get_rank(), "local_rank": local_rank,
+               "self_launched": os.environ.get("TT_BENCH_SELF_LAUNCHED") == "1"}
+        dist.barrier()
+        dist.destroy_process_group()
+        print(json.dumps(rec), flush=True)
+        fail = os.environ.get("TT_BENCH_LAUNCH_CHECK_FAIL_RANK")
+        raise SystemExit(3 if fail is not None and int(fail) == rank else 0)
     import torch  # first: tthip must bind to torch's HIP runtime (see tthip.hip_lib)
     import torch.distributed as dist
     import tthip
@@ -485,6 +582,9 @@ def main():
     # RCCL ("nccl") over xGMI, one process per GPU. TT_BENCH_DIST_BACKEND=gloo is a rehearsal mode for
     # boxes with fewer GPUs than ranks (ranks share devices, host-side collectives); not a bench mode.
     backend = os.environ.get("TT_BENCH_DIST_BACKEND", "nccl")
+    if backend == "nccl" and local_rank >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} (local {local_rank}) needs GPU {local_rank}, but "
+                         f"{torch.cuda.device_count()} are visible: one process per GPU")
     gpu = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -500,7 +600,10 @@ def main():
             dist.init_process_group(backend="nccl", device_id=dev)
         else:
             dist.init_process_group(backend=backend)
-    tiles = (world > 1 or rccl1) and args.shard == "tiles"
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: the process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
+    dist_world = dist.get_world_size() if (world > 1 or rccl1) else None
+    tiles =(world > 1 or rccl1) and args.shard == "tiles"
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -642,12 +745,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
-    launch_ms = eng.timing_read()
+    launch_ms = ring_tail(eng, 2, args.steps).reshape(-1)  # part 0's launches, the last <= 128 steps
     for p in parts[1:]:
-        assert len(p.eng.timing_read()) == 2 * args.steps
-    assert len(launch_ms) == 2 * args.steps, (len(launch_ms), args.steps)
+        ring_tail(p.eng, 2, args.steps)
     total_rays = float(rays_per_step * args.steps)
-    trace_ms_rank = float(np.sum(launch_ms)) / args.steps  # part 0's two launches per step
+    trace_ms_rank = float(np.sum(launch_ms)) / (len(launch_ms) // 2)  # part 0's two launches per step
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -801,8 +903,7 @@ def main():
                 eng.timing_reset()
             work.copy_(sr)
             eng.trace_shadow(work, ns, 0, W, H, device=True, asynchronous=True)
-        sh_ms = eng.timing_read()
-        assert len(sh_ms) == args.steps
+        sh_ms = ring_tail(eng, 1, args.steps)[:, 0]
         shadow = {"rays": ns, "trace_ms": round(float(np.mean(sh_ms)), 4),
                   "trace_ms_median": round(float(np.median(sh_ms)), 4),
                   "mrays_s": round(ns / float(np.mean(sh_ms)) / 1e3, 1),
@@ -867,11 +968,35 @@ def main():
 
     # unit utilisation of the same kernels from the round's separate PMC passes (tools/pmc_units.sh
     # -> profiles/units_latest.json): the binding units, since the scene is cache-resident
-    units = None
+    units, units_k, units_src = None, {}, None
     upath = os.path.join(REPO, "profiles", "units_latest.json")
     if os.path.exists(upath) and (W, H, args.tris) == (1920, 1080, 262267):
         with open(upath) as f:
-            units = json.load(f).get("mean")
+            uj = json.load(f)
+        units, units_src = uj.get("mean"), uj.get("source")
+        units_k = {k.rstrip(">").split(",")[-1].strip(): v for k, v in uj.get("per_kernel", {}).items()}
+
+    # the binding unit is VALU issue: per launch, rays/s against the rate the same
+    # instruction stream reaches with VALU issue 100% busy on all 1,024 SIMDs at the 2.4 GHz peak
+    # clock (valu_ceiling_grays_s, from the PMC pass's VALU issue cycles per ray). One launch at a
+    # time (P = 1: the metric's launches; P > 1: the single-stream leg), so a launch's duration is
+    # the kernel's. The dominant kernel is the longer launch.
+    if P == 1:
+        per_launch = {"1": (n_prim, float(np.mean(prim_ms))), "2": (nb, float(np.mean(bnc_ms)))}
+    elif single is not None:
+        per_launch = {"1": (WH, single["trace_ms_primary"]), "2": (frame_nb, single["trace_ms_bounce"])}
+    else:
+        per_launch = {}
+    valu = {}
+    for info, (n, ms) in per_launch.items():
+        u = units_k.get(info, {})
+        rate = n / (ms * 1e-3) / 1e9
+        ceil = u.get("valu_ceiling_grays_s")
+        valu[info] = {"kernel": f"tt_trace_kernel<false,false,{info}>", "rays": int(n), "launch_ms": round(ms, 4),
+                      "grays_s": round(rate, 4), "valu_ceiling_grays_s": ceil,
+                      "valu_issue_cycles_per_ray": u.get("valu_issue_cycles_per_ray"),
+                      "frac": round(rate / ceil, 4) if ceil else None}
+    dom = max(valu.values(), key=lambda v: v["launch_ms"]) if valu else None
 
     ms_per_step = elapsed * 1e3 / args.steps
     result = {
@@ -904,6 +1029,9 @@ def main():
                    "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it"
                              + (f" (part 0 of {P}: its launches overlap the other parts')" if P > 1 else ""),
                    "parts_per_rank": P,
+                   "dist_world_size": dist_world, "dist_backend": backend if dist_world else None,
+                   "launcher": ("bench.py self-launch" if os.environ.get("TT_BENCH_SELF_LAUNCHED") == "1"
+                                else "external (WORLD_SIZE set)" if env_world is not None else "none (1 rank)"),
                    "trace_ms_primary": round(float(np.mean(prim_ms)), 4),
                    "trace_ms_bounce": round(float(np.mean(bnc_ms)), 4),
                    "trace_ms_primary_median": round(float(np.median(prim_ms)), 4),
@@ -915,21 +1043,31 @@ def main():
                    "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0) if P == 1 else round(B_step / (2 * P)),
-                     "alg_bytes_per_step": round(B_step),
+        "roofline": {"bound": "valu_issue", "unit": "Grays/s",
+                     "achieved": dom["grays_s"] if dom else None,
+                     "peak": dom["valu_ceiling_grays_s"] if dom else None,
+                     "frac": dom["frac"] if dom else None,
+                     "kernel": dom["kernel"] if dom else None,
+                     "traffic": traffic,
+                     "per_launch": valu,
+                     "hbm": {"achieved_alg_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
+                             "frac_alg": round(achieved / HBM_PEAK_GBS, 4),
+                             "traffic_bytes_per_launch": traffic,
+                             "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0) if P == 1 else round(B_step / (2 * P)),
+                             "alg_bytes_per_step": round(B_step),
+                             "note": ("achieved_alg_gbs = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean "
+                                      "HIP-event launch time" if P == 1 else
+                                      f"achieved_alg_gbs = algorithmic bytes (B_ray, SURVEY §8d) of all 2 x {P} trace "
+                                      "launches of a step / the step's wall time") + "; the bytes are served mostly "
+                                     "from L2 / MALL: traffic = fabric bytes per launch from " + (traffic_src or "no PMC pass")
+                                     + " (2 x FETCH_SIZE + WRITE_SIZE, includes Infinity-Cache hits), so HBM does not "
+                                     "bind this loop"},
                      "units_busy": units, "single_stream": single,
-                     "note": ("achieved = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean HIP-event "
-                              "launch time" if P == 1 else
-                              f"achieved = algorithmic bytes (B_ray, SURVEY §8d) of all 2 x {P} trace launches of a "
-                              "step / the step's wall time (the parts' launches overlap, so a per-launch time is not "
-                              "the kernel's; single_stream = the per-launch figure with one launch at a time)")
-                             + "; bytes are served mostly from L2/MALL, so the loop is bound by VALU issue "
-                             "and load latency, not HBM (DESIGN.md §5). traffic = fabric bytes per launch from "
-                             + (traffic_src or "no PMC pass") + " (2 x FETCH_SIZE + WRITE_SIZE, includes "
-                             "Infinity-Cache hits); units_busy = VALU-issue / texture-data / texture-address "
-                             "busy fractions of the same kernels (profiles/units_latest.json, tools/pmc_units.sh)"},
+                     "note": "bound = VALU issue (DESIGN.md §3.1): achieved = rays/s of the dominant launch (one launch "
+                             "at a time, HIP events on its stream), peak = the same launch's VALU-issue ceiling = 1024 "
+                             "SIMDs x 2.4 GHz / VALU issue cycles per ray from the PMC pass " + (units_src or "(none)")
+                             + " (tools/pmc_units.sh -> tools/pmc_units_summary.py -> profiles/units_latest.json); "
+                             "frac <= 1 by construction up to run-to-run variation of the cycles per ray"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(result), flush=True)

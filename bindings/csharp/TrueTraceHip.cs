@@ -199,14 +199,32 @@ namespace TrueTrace.Hip
             return s;
         }
 
-        /// One kernel_shadow dispatch (IntersectionKernels.compute:264-505) for bounce `curBounce`;
-        /// `cacheBuffer` (PropogatedCacheData per pixel) and `flags` (RadianceCache, VisibilityCheck,
-        /// UseReSTIRGI) select the :457-485 accumulations of the reference's define set.
-        public unsafe TTStats TraceShadow<TShadow, TCol, TCache>(TShadow[] shadowRays, uint nRays, int curBounce, int width,
-                                                                 int height, float[] visibility = null,
-                                                                 TCol[] globalColors = null, float[] neePos = null,
-                                                                 TCache[] cacheBuffer = null,
-                                                                 TTTraceFlags flags = TTTraceFlags.RadianceCache)
+        /// tt_trace_shadow (the original signature and contract): visibility, t write-back,
+        /// Direct += at bounce 0 and NEEPosA only; the caller does the other :457-485 accumulations.
+        public unsafe TTStats TraceShadow<TShadow, TCol>(TShadow[] shadowRays, uint nRays, int curBounce, int width,
+                                                         int height, float[] visibility = null,
+                                                         TCol[] globalColors = null, float[] neePos = null,
+                                                         TTTraceFlags flags = 0)
+            where TShadow : unmanaged where TCol : unmanaged
+        {
+            var p = new TTShadowParams { nRays = nRays, bounce = curBounce, screenWidth = (uint)width,
+                                         screenHeight = (uint)height, flags = flags };
+            TTStats s;
+            fixed (TShadow* r = shadowRays) fixed (float* vis = visibility) fixed (TCol* col = globalColors)
+            fixed (float* nee = neePos)
+                Check(Native.tt_trace_shadow(m_ctx, ref p, r, vis, col, nee, out s));
+            return s;
+        }
+
+        /// One kernel_shadow dispatch (IntersectionKernels.compute:264-505) for bounce `curBounce`
+        /// with the full :457-485 output contract (tt_trace_shadow_ex); `cacheBuffer`
+        /// (PropogatedCacheData per pixel) and `flags` (RadianceCache, VisibilityCheck, UseReSTIRGI)
+        /// select the accumulations of the reference's define set.
+        public unsafe TTStats TraceShadowEx<TShadow, TCol, TCache>(TShadow[] shadowRays, uint nRays, int curBounce, int width,
+                                                                   int height, float[] visibility = null,
+                                                                   TCol[] globalColors = null, float[] neePos = null,
+                                                                   TCache[] cacheBuffer = null,
+                                                                   TTTraceFlags flags = TTTraceFlags.RadianceCache)
             where TShadow : unmanaged where TCol : unmanaged where TCache : unmanaged
         {
             var p = new TTShadowParams { nRays = nRays, bounce = curBounce, screenWidth = (uint)width,

@@ -529,8 +529,11 @@ tt_status tt_generate_primary(tt_ctx* ctx, const tt_camera* cam, tt_ray_data* gl
 /* Diffuse-lobe next-bounce enqueue for the rays traced at p->bounce (the subset of kernel_shade
  * in RayTracingShader.compute:52-84, 99-122, 293, 498-506 that produces the next ray): hits
  * spawn a cosine-weighted ray about the shading normal, offset 1e-4 along the geometric normal;
- * misses terminate. Survivors are compacted (wave ballot, one atomic per wave) into the other
- * half of the ping-pong buffer; *n_next receives their count. */
+ * misses terminate. Survivors are compacted into the other half of the ping-pong buffer in
+ * source order (a stable single-pass scan: 4096-ray tiles, block ballot / LDS prefix, decoupled
+ * look-back over the preceding tiles' counts; the reference's InterlockedAdd order,
+ * RayTracingShader.compute:500, is whatever its atomics serialise to); *n_next receives their
+ * count. */
 tt_status tt_enqueue_diffuse_bounce(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
                                     int32_t frames_accumulated, int32_t max_bounce, uint32_t* n_next);
 

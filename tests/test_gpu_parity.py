@@ -908,6 +908,52 @@ def test_shadow_accumulations_match_oracle(engine, bounce, flags):
         assert (cc["PrimaryNEERay"] != col["PrimaryNEERay"]).sum() > 20
 
 
+@pytest.mark.parametrize("bounce", [0, 1])
+def test_legacy_shadow_entry_contract(engine, bounce):
+    """tt_trace_shadow keeps its original contract (include/truetrace_hip.h): visibility, the t = 0
+    write-back, Direct += at bounce 0 and NEEPosA -- and none of tt_trace_shadow_ex's Indirect /
+    PrimaryNEERay accumulations, so a caller doing those itself does not double-count. Against the
+    oracle, with t < 0 on a quarter of the rays and Data.w == bounce (the rays tt_trace_shadow_ex
+    would accumulate into Indirect / PrimaryNEERay)."""
+    seed = 90 + bounce
+    sc = glass_soup(seed)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 3.0), (0, 0, -1), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    O.trace(sc, rays, W * H, 0, FAR, W, H)
+    rng = np.random.default_rng(seed)
+    sr = hb.nee_rays_from_hits(rays, W * H, (0.5, 2.0, 2.5), seed)
+    assert (sr["t"] < 0).sum() > 100
+    col = np.zeros(W * H, tthip.COL_DTYPE)
+    col["Direct"] = rng.uniform(0, 2, (W * H, 3))
+    col["Indirect"] = rng.uniform(0, 2, (W * H, 3))
+    col["PrimaryNEERay"] = (rng.integers(12, 24, W * H).astype(np.uint32) << 27) | \
+        rng.integers(0, 1 << 27, W * H).astype(np.uint32)
+    col["Data"][:, 3] = float(bounce)
+    engine.upload(sc)
+    n = len(sr)
+    rg, cg = sr.copy(), col.copy()
+    vg = np.full((n, 4), 7.0, np.float32)
+    ng = np.full((W * H, 4), 9.0, np.float32)
+    engine.trace_shadow(rg, n, bounce, W, H, visibility=vg, colors=cg, nee_pos=ng, legacy=True)
+    rc, cc = sr.copy(), col.copy()
+    vc = np.full((n, 4), 7.0, np.float32)
+    nc = np.full((W * H, 4), 9.0, np.float32)
+    st, _ = O.shadow(sc, rc, n, bounce, W, H, visibility=vc, colors=cc, nee_pos=nc, nthreads=CPU_THREADS)
+    assert st == 0
+    b = lambda x: np.ascontiguousarray(x).view(np.uint8)  # noqa: E731
+    assert np.array_equal(b(rg), b(rc)), "shadow ray bytes differ"
+    assert same_floats(vg, vc), "visibility differs"
+    assert same_floats(ng, nc), "NEEPosA differs"
+    assert same_floats(cg["Direct"], cc["Direct"]), "GlobalColors.Direct differs"
+    # the accumulations tt_trace_shadow leaves to the caller: untouched
+    assert np.array_equal(b(cg["Indirect"]), b(col["Indirect"]))
+    assert np.array_equal(cg["PrimaryNEERay"], col["PrimaryNEERay"])
+    # ... which the full contract (the oracle) does change on this input
+    changed = (cc["PrimaryNEERay"] != col["PrimaryNEERay"]).sum() + (cc["Indirect"] != col["Indirect"]).any(1).sum()
+    assert changed > 20
+
+
 @pytest.mark.parametrize("seed", [81, 82])
 def test_visibility_check_mode(engine, seed):
     """VisabilityCheckCompute (CommonData.cginc:710-819): the distance as given, visibility only,

@@ -942,6 +942,7 @@ MatView mat_view(const tt_ctx* c) {
 }  // namespace
 
 hipStream_t tt_ctx_stream_of(tt_ctx* c) { return c->stream; }  // tt_build.hip
+hipError_t tt_ctx_bind_device(tt_ctx* c) { return hipSetDevice(c->device); }  // tt_build.hip
 void tt_ctx_set_error(tt_ctx* c, const char* msg) {                // tt_build.hip
     if (c) c->err = msg ? msg : "";
 }
@@ -1016,11 +1017,6 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.ctl_next = c->ctl + (ci ^ 1u);
     a.sticky_overflow = c->sticky;
     a.spill = c->spill.p;
-#if defined(TT_DIAG_TIMES) || defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST) || \
-    defined(TT_DIAG_BLOCKS) || defined(TT_DIAG_SOLO)
-    // diagnostic builds only: a device buffer for the kernel's timing records
-    if (const char* e = std::getenv("TT_DIAG_TIMES_PTR")) a.diag_times = reinterpret_cast<unsigned long long*>(std::strtoull(e, nullptr, 0));
-#endif
     a.n_rays = p->n_rays;
     a.ray_offset = off;
     a.width = p->screen_width;
@@ -1091,13 +1087,12 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     return TT_OK;
 }
 
-tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
-                          tt_col_data* colors, float* nee_pos, tt_stats* stats) {
-    return tt_trace_shadow_ex(c, p, rays, visibility, colors, nee_pos, nullptr, stats);
-}
+}  // extern "C"
 
-tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
-                             tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats) {
+// full = false: tt_trace_shadow's contract (Direct at bounce 0 + NEEPosA only, the caller does the
+// rest); full = true: tt_trace_shadow_ex's (plus CacheBuffer / Indirect / PrimaryNEERay)
+static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
+                             tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats, bool full) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or shadow rays");
@@ -1155,7 +1150,7 @@ tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     // the accumulations beyond Direct / NEEPosA run in a second pass that reads the visibility
     // records: give the traversal one when the caller passed none
     const bool vis_check = (p->flags & TT_SHADOW_VISIBILITY_CHECK) != 0;
-    const bool accumulate = !vis_check && (d_col || d_cache);
+    const bool accumulate = full && !vis_check && (d_col || d_cache);
     if (accumulate && !d_vis) {
         if (c->st_vis.n < p->n_rays) TT_HIP(c, c->st_vis.alloc(p->n_rays));
         d_vis = c->st_vis.p;
@@ -1231,6 +1226,18 @@ tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
         return fail(c, TT_ERR_STACK_OVERFLOW, "%u shadow rays needed more than %d traversal stack entries",
                     ctl.err_overflow, TT_STACK_SIZE);
     return TT_OK;
+}
+
+extern "C" {
+
+tt_status tt_trace_shadow(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
+                          tt_col_data* colors, float* nee_pos, tt_stats* stats) {
+    return shadow_call(c, p, rays, visibility, colors, nee_pos, nullptr, stats, false);
+}
+
+tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
+                             tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats) {
+    return shadow_call(c, p, rays, visibility, colors, nee_pos, cache, stats, true);
 }
 
 tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_data* rays, float* normals6) {

@@ -31,6 +31,7 @@
 #include "../../include/truetrace_hip.h"
 
 extern "C" hipStream_t tt_ctx_stream_of(tt_ctx* c);  // tt_api.hip (C linkage there)
+extern "C" hipError_t tt_ctx_bind_device(tt_ctx* c);  // hipSetDevice(the context's device)
 extern "C" void tt_ctx_set_error(tt_ctx* c, const char* msg);
 
 namespace {
@@ -369,8 +370,8 @@ __global__ void k_cost8(int m, const int* __restrict__ nodes_lvl, const Box* __r
         }
         const float cl = surface_area(a) * (float)np;
         for (int i = 0; i < 7; i++) {
-            cost[v * 7 + i] = cl;
-            dec[v * 7 + i] = Dec{0, 0, 0};
+            cost[(size_t)v * 7 + i] = cl;
+            dec[(size_t)v * 7 + i] = Dec{0, 0, 0};
         }
         return;
     }
@@ -382,7 +383,7 @@ __global__ void k_cost8(int m, const int* __restrict__ nodes_lvl, const Box* __r
     float cost_distribute = FLT_MAX;
     int dist_left = -1, dist_right = -1;
     for (int k = 0; k < 7; k++) {
-        const float c = cost[l * 7 + k] + cost[r * 7 + 6 - k];
+        const float c = cost[(size_t)l * 7 + k] + cost[(size_t)r * 7 + 6 - k];
         if (c < cost_distribute) {
             cost_distribute = c;
             dist_left = k;
@@ -392,30 +393,30 @@ __global__ void k_cost8(int m, const int* __restrict__ nodes_lvl, const Box* __r
     const float cost_internal = cost_distribute + surface_area(a);
     Dec d0;
     if (cost_leaf < cost_internal) {
-        cost[v * 7] = cost_leaf;
+        cost[(size_t)v * 7] = cost_leaf;
         d0.type = 0;
     } else {
-        cost[v * 7] = cost_internal;
+        cost[(size_t)v * 7] = cost_internal;
         d0.type = 1;
     }
     d0.dl = (int8_t)dist_left;
     d0.dr = (int8_t)dist_right;
-    dec[v * 7] = d0;
+    dec[(size_t)v * 7] = d0;
     Dec prev = d0;
     for (int i = 1; i < 7; i++) {
-        float cd = cost[v * 7 + i - 1];
+        float cd = cost[(size_t)v * 7 + i - 1];
         int dl = -1, dr = -1;
         for (int k = 0; k < i; k++) {
-            const float c = cost[l * 7 + k] + cost[r * 7 + i - k - 1];
+            const float c = cost[(size_t)l * 7 + k] + cost[(size_t)r * 7 + i - k - 1];
             if (c < cd) {
                 cd = c;
                 dl = k;
                 dr = i - k - 1;
             }
         }
-        cost[v * 7 + i] = cd;
+        cost[(size_t)v * 7 + i] = cd;
         if (dl != -1) prev = Dec{2, (int8_t)dl, (int8_t)dr};
-        dec[v * 7 + i] = prev;
+        dec[(size_t)v * 7 + i] = prev;
     }
 }
 
@@ -451,13 +452,13 @@ __global__ void k_expand8(int lo, int hi, int cap, Rec8* __restrict__ rec, int* 
         while (sp > 0 && ok) {
             sp--;
             const int v = stn[sp], i = sti[sp];
-            if (!root && dec[v * 7 + i].type != 2) {  // a plain child
+            if (!root && dec[(size_t)v * 7 + i].type != 2) {  // a plain child
                 if (cc >= 8) { ok = false; break; }
                 children[cc++] = v;
                 continue;
             }
             root = false;
-            const Dec d = dec[v * 7 + i];
+            const Dec d = dec[(size_t)v * 7 + i];
             if (!(d.dl >= 0 && d.dl < 7) || !(d.dr >= 0 && d.dr < 7) || cc >= 8) { ok = false; break; }
             const int l = left[v];
             stn[sp] = l + 1; sti[sp] = d.dr; sp++;  // right after left
@@ -507,7 +508,7 @@ __global__ void k_expand8(int lo, int hi, int cap, Rec8* __restrict__ rec, int* 
         R.child[s] = slots[s];
         const int c = slots[s];
         if (c < 0) continue;
-        const int ty = dec[c * 7].type;
+        const int ty = dec[(size_t)c * 7].type;
         if (ty == 0) {
             const int tc = nprim[c];
             if (!(tc > 0 && tc <= 3)) { atomicOr(err, 16); return; }
@@ -602,7 +603,7 @@ __global__ void k_fill8(int m, const Rec8* __restrict__ rec, const Box* __restri
         qhy[w] |= to_byte(mathf_ceil((ca.mx[1] - a.mn[1]) * oy)) << sh;
         qhz[w] |= to_byte(mathf_ceil((ca.mx[2] - a.mn[2]) * oz)) << sh;
         uint32_t mb;
-        if (dec[c * 7].type == 0) {
+        if (dec[(size_t)c * 7].type == 0) {
             const int tc = nprim[c], f = firstpos[c];
             mb = 0u;
             for (int j = 0; j < tc; j++) {
@@ -1076,6 +1077,7 @@ extern "C" tt_status tt_bvh2_build_device(tt_ctx* ctx, const float* aabbs, uint3
                                           uint32_t* node_count, uint32_t* max_depth) {
     tt_status s = check_inputs(ctx, aabbs, n, presorted);
     if (s != TT_OK || !final_indices) return s != TT_OK ? s : TT_ERR_INVALID_ARG;
+    TT_BH(tt_ctx_bind_device(ctx));  // allocations and launches on the context's GPU
     hipStream_t st = tt_ctx_stream_of(ctx);
     Bvh2Dev R;
     if ((s = bvh2_stage(st, aabbs, (int)n, presorted, R)) != TT_OK) {
@@ -1111,6 +1113,7 @@ static tt_status blas_device(tt_ctx* ctx, const float* aabbs, uint32_t n, const 
     tt_status s = check_inputs(ctx, aabbs, n, presorted);
     if (s != TT_OK) return s;
     if (!nodes || !n_nodes || !cwbvh_indices) return TT_ERR_INVALID_ARG;
+    TT_BH(tt_ctx_bind_device(ctx));  // allocations and launches on the context's GPU
     hipStream_t st = tt_ctx_stream_of(ctx);
     Bvh2Dev B;
     if ((s = bvh2_stage(st, aabbs, (int)n, presorted, B)) != TT_OK) return s;
@@ -1305,6 +1308,10 @@ static tt_status presort_device(hipStream_t st, const float* aabbs, int n, int32
 extern "C" tt_status tt_bvh2_presort_device(tt_ctx* ctx, const float* aabbs, uint32_t n, int32_t* presorted) {
     if (!ctx || !aabbs || !n || !presorted || n >= (1u << 29)) return TT_ERR_INVALID_ARG;
     g_err[0] = 0;
+    if (tt_ctx_bind_device(ctx) != hipSuccess) {  // allocations and launches on the context's GPU
+        tt_ctx_set_error(ctx, "tt_bvh2_presort_device: hipSetDevice failed");
+        return TT_ERR_HIP;
+    }
     const tt_status s = presort_device(tt_ctx_stream_of(ctx), aabbs, (int)n, presorted);
     if (s != TT_OK) tt_ctx_set_error(ctx, g_err[0] ? g_err : "tt_bvh2_presort_device failed");
     return s;

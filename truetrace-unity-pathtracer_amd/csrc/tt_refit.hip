@@ -188,6 +188,12 @@ __global__ void refit_tree(RefitTreeArgs t) {
         const int32_t p = t.parent[id];
         const uint32_t prev = __hip_atomic_fetch_add(t.arrive + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev != 7u) return;  // not the last of the parent's 8 slots
+        // the other 7 boxes were stored sc1 by threads of other workgroups (often other CUs / XCDs):
+        // one agent-scope acquire before reading them (MI355X_MICROARCH.md, inter-workgroup
+        // visibility: with several workgroups per CU the sc1-loads-only hand-off is outside the
+        // measured table, so the acquire stays), then wait for its invalidate to complete
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(t.arrive + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         id = p;
         internal_pair(id, t.fwd, bb, t.nodes + t.node_of[id], box);

@@ -104,18 +104,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
     uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
     uint32_t d_lead_same = 0, d_uniform = 0;  // node-step uniformity (lanes sharing the first lane's node)
-#ifdef TT_DIAG_TL
-    uint32_t d_tl = 0;
-#endif
-#ifdef TT_DIAG_BLOCKS  // wave executions of each loop block -> diag_times[k] (uint64)
-    uint32_t db[10] = {};
-#define DB(k) do { if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) db[k]++; } while (0)
-#else
-#define DB(k) do { } while (0)
-#endif
-#ifdef TT_DIAG_RAYS  // per-ray (start, end, iterations, node visits): diag_times -> uint4[n_rays]
-    uint32_t r_t0 = 0, r_iter = 0, r_nodes = 0;
-#endif
     // the world-space ray (ray2, IntersectionKernels.compute:151), kept in registers
     auto world_ray = [&]() -> LaneRay { return wray; };
 
@@ -123,19 +111,9 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     auto finish_ray = [&]() {
         const bool hit = write_record<INFO>(A, ray_index, pix, col_w, best, world_ray());
         if (STATS) c_hits += hit ? 1u : 0u;
-#ifdef TT_DIAG_RAYS
-        if (A.diag_times)
-            reinterpret_cast<uint4*>(A.diag_times)[ray_index - A.ray_offset] =
-                make_uint4(r_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), r_iter, r_nodes);
-#endif
         (void)hit;
     };
-#ifdef TT_DIAG_TIMES
-    const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
-    uint64_t t_wide = 0;  // when the wave entered the cooperative drain phase (0: never)
-#endif
     while (true) {
-        DB(0);
         // ---------------------------------------------------------------- refill
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
@@ -145,7 +123,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         // finished rays write their records in batches, right before their lanes are refilled
         if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry) || to_wide) {
             if (pending) {
-                DB(9);
                 finish_ray();
                 pending = false;
             }
@@ -153,9 +130,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         if (n_idle == TT_WAVE && pool_dry) break;
 #if TT_WIDE
         if (to_wide) {
-#ifdef TT_DIAG_TIMES
-            t_wide = __builtin_amdgcn_s_memrealtime();
-#endif
             WideState st{ray, wray, best, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset,
                          mesh_id, Reps, ray_index, pix, col_w, tid, gtid, active};
             regroup<2>(st, __ballot(active), lane);
@@ -170,7 +144,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
 #endif
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
-            DB(1);
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
@@ -230,34 +203,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 mesh_id = -1;
                 Reps = 0;
                 active = true;
-#ifdef TT_DIAG_RAYS
-                r_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                r_iter = 0;
-                r_nodes = 0;
-#endif
-#ifdef TT_DIAG_TIMES
-                c_rays++;
-#else
                 if (STATS) c_rays++;
-#endif
             }
         }
 
-#ifdef TT_DIAG_TL  // per-wave timeline: every 4th iteration (time, active lanes) -> diag_times
-        if (A.diag_times) {
-            const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
-            if ((d_tl & 3u) == 0u && (d_tl >> 2) < 64u && lane == 0) {
-                const uint32_t na = (uint32_t)__popcll(__ballot(active));
-                reinterpret_cast<uint2*>(A.diag_times)[(size_t)w * 64u + (d_tl >> 2)] =
-                    make_uint2((uint32_t)__builtin_amdgcn_s_memrealtime(), na | (more << 8) | ((uint32_t)__builtin_amdgcn_s_memtime() << 12));
-            }
-            d_tl++;
-        }
-#endif
         // ------------------------------------------------------------- node phase
-#ifdef TT_DIAG_RAYS
-        r_iter += active ? 1u : 0u;
-#endif
         if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)
             const uint64_t nm = __ballot(active && tg.y == 0u && Reps < TT_MAX_REPS && (cg.y & 0xff000000u));
             const uint64_t am = __ballot(active);  // outside the lane-0 branch: a ballot there sees lane 0 only
@@ -270,7 +220,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
         // A lane is at the top of the reference's loop exactly when no leaf triangles are pending.
         if (active && tg.y == 0u) {
-            DB(2);
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
@@ -294,18 +243,12 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                                 n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
                                 n4 = buffer_load16(nodes, no + 64u);
                     const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
-#ifdef TT_DIAG_NODEHIST  // diagnostic: visits per node index -> diag_times (as uint32[n_nodes])
-                    if (A.diag_times) atomicAdd(reinterpret_cast<uint32_t*>(A.diag_times) + child, 1u);
-#endif
                     cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
                     tg.y = hitmask & 0x00ffffffu;
                     cg.x = n1.x + (uint32_t)NodeOffset;
                     tg.x = n1.y + (uint32_t)TriOffset;
                     Reps++;
                     if (STATS) c_nodes++;
-#ifdef TT_DIAG_RAYS
-                    r_nodes++;
-#endif
                 } else {
                     active = false;
                     if (STATS) c_ovf++;
@@ -316,7 +259,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                 cg = make_uint2(0u, 0u);
             }
             if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
-                DB(3);
                 const uint32_t mo = firstbithigh(tg.y);
                 tg.y &= ~(1u << mo);
                 const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
@@ -364,7 +306,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         }
         // --------------------------------------------------------- triangle phase
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
-            DB(4);
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool acc = intersect_triangle<MATCHECK>(tris, A.mat, A.bounce == 0, A.flags, (int32_t)(tg.x + ti),
@@ -379,10 +320,8 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
         // One place for every lane whose group is used up, whether it came from a node step or
         // from its last triangle this pass (equivalent order: the reference pops right after).
         if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
-            DB(5);
             if (stack_size != 0) {
                 if (stack_size == tlas_ss) {
-                    DB(6);
                     NodeOffset = 0;
                     TriOffset = 0;
                     tlas_ss = -1;
@@ -390,28 +329,13 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
                     oct = octant_inv4(ray);
                 }
                 TT_POP(cg);
-                DB(7);
             } else {
                 pending = true;  // written at the next refill (or when the wave drains)
-                DB(8);
                 active = false;
             }
         }
     }
 
-#ifdef TT_DIAG_TIMES
-    {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        const uint32_t rays_done = wave_sum(c_rays);
-        if (lane == 0 && A.diag_times) {
-            const uint32_t w = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
-            A.diag_times[4 * w + 0] = t_begin;
-            A.diag_times[4 * w + 1] = t_end;
-            A.diag_times[4 * w + 2] = rays_done;
-            A.diag_times[4 * w + 3] = t_wide;
-        }
-    }
-#endif
     if (STATS) {
         const uint32_t v[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
                                wave_sum(c_hits), wave_sum(c_reps), wave_sum(c_ovf), wave_sum(c_acc)};
@@ -429,13 +353,6 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             atomicAdd(&A.ctl->diag[7], (unsigned long long)un);
         }
     }
-#ifdef TT_DIAG_BLOCKS
-    if (A.diag_times)
-        for (int k = 0; k < 10; k++) {
-            const uint32_t v = wave_sum(db[k]);
-            if (lane == 0 && v) atomicAdd(A.diag_times + k, (unsigned long long)v);
-        }
-#endif
 }
 
 // ------------------------------------------------------------------ launchers

@@ -22,10 +22,6 @@
 #endif
 // G = 2 lanes per ray: more than 32 live rays do not fit a wave (measured: 48 gives wrong hits)
 static_assert(TT_WIDE_ENTER >= 1 && TT_WIDE_ENTER <= 32, "TT_WIDE_ENTER must be in [1, 32]");
-#if defined(TT_DIAG_RAYS) || defined(TT_DIAG_TL) || defined(TT_DIAG_NODEHIST)
-#undef TT_WIDE
-#define TT_WIDE 0
-#endif
 
 namespace {
 
@@ -178,9 +174,6 @@ __device__ __forceinline__ uint32_t node_intersect_part(const uint4 n0, const ui
     return hit_mask;
 }
 
-}  // namespace
-#include "tt_solo.h"
-namespace {
 
 // The drain loop for groups of G lanes; regroups into 2G-lane groups when the live rays fit and
 // returns when every ray of the wave has finished. `finish(st)` writes a finished ray's records
@@ -197,19 +190,6 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
         const uint64_t lead = __ballot(st.active && sub == 0u);
         const uint32_t n = (uint32_t)__popcll(lead);
         if (n == 0u) return;
-#if TT_SOLO
-        if (n == 1u) {  // one live ray left: give it the whole wave (tt_solo.h)
-            WideState s = st;
-            solo_take(s, (uint32_t)__builtin_ctzll(lead));
-            uint2 stk = make_uint2(0u, 0u);  // lane i <- stack entry i of the ray's LDS / spill column
-            if (lane < (uint32_t)s.stack_size) {
-                if (TT_LDS_STACK >= TT_STACK_SIZE || lane < TT_LDS_STACK) stk = s_stack[lane][s.scol];
-                else stk = spill[(size_t)(lane - TT_LDS_STACK) * spill_stride + s.gcol];
-            }
-            solo_run<STATS, MATCHECK>(A, s, stk, nodes, tris, lane, C, finish);
-            return;
-        }
-#endif
         if constexpr (G < 8) {
             if (n * (2 * G) <= TT_WAVE) {
                 regroup<2 * G>(st, lead, lane);

@@ -6,12 +6,14 @@ gather of the 16-byte hit records to rank 0 (RCCL via torch.distributed "nccl", 
 CPU in the tests).
 
 Two shardings:
-  * ``sample`` (weak scaling, bench.py default): every rank traces its own full-frame sample of
-    the same view (``frames_accumulated = rank`` selects the sub-pixel jitter).
-  * ``tiles`` (strong scaling): the screen is cut into ``tile``×``tile`` pixel
-    tiles dealt round-robin to ranks (balances sky-heavy and geometry-heavy regions); each rank
-    builds a compact ray list of its pixels and the hit records are gathered and scattered back
+  * ``tiles`` (strong scaling, SURVEY.md §8(e), bench.py default): the screen is cut into
+    ``tile``×``tile`` pixel tiles dealt round-robin to ranks (balances sky-heavy and geometry-heavy
+    regions); each rank builds a compact ray list of its pixels (optionally split into
+    tile-interleaved parts, ``part_pixels``) and the hit records are gathered and scattered back
     into screen order on rank 0.
+  * ``sample`` (weak scaling, ``bench.py --shard sample`` and the ``aux_sample_sharded`` line):
+    every rank traces its own full-frame sample of the same view (``frames_accumulated = rank``
+    selects the sub-pixel jitter).
 """
 from __future__ import annotations
 

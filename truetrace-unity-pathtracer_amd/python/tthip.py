@@ -806,17 +806,23 @@ class Engine:
 
     def trace_shadow(self, shadow_rays, n_rays: int, bounce: int, width: int, height: int, visibility=None,
                      colors=None, nee_pos=None, device: bool = False, stats: bool = False, check: bool = True,
-                     asynchronous: bool = False, flags: int = 0, cache=None):
+                     asynchronous: bool = False, flags: int = 0, cache=None, legacy: bool = False):
         """tt_trace_shadow_ex (kernel_shadow replacement): any-hit visibility of ShadowRayData rays and
-        the GlobalColors / CacheBuffer accumulations (flags: TT_SHADOW_*, TT_TRACE_USE_RESTIRGI)."""
+        the GlobalColors / CacheBuffer accumulations (flags: TT_SHADOW_*, TT_TRACE_USE_RESTIRGI).
+        legacy=True calls tt_trace_shadow instead (Direct at bounce 0 + NEEPosA only, no cache)."""
         p = ShadowParams(n_rays=n_rays, bounce=bounce, screen_width=width, screen_height=height,
                          flags=flags | (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0)
                          | (TT_TRACE_ASYNC if asynchronous else 0))
         s = Stats()
-        st = self.L.tt_trace_shadow_ex(self.h, C.byref(p), _ptr(shadow_rays), _ptr(visibility), _ptr(colors),
-                                       _ptr(nee_pos), _ptr(cache), C.byref(s))
+        if legacy:
+            assert cache is None, "tt_trace_shadow takes no CacheBuffer"
+            st = self.L.tt_trace_shadow(self.h, C.byref(p), _ptr(shadow_rays), _ptr(visibility), _ptr(colors),
+                                        _ptr(nee_pos), C.byref(s))
+        else:
+            st = self.L.tt_trace_shadow_ex(self.h, C.byref(p), _ptr(shadow_rays), _ptr(visibility), _ptr(colors),
+                                           _ptr(nee_pos), _ptr(cache), C.byref(s))
         if check:
-            self._check(st, "tt_trace_shadow_ex")
+            self._check(st, "tt_trace_shadow" if legacy else "tt_trace_shadow_ex")
         return (s, st) if not check else s
 
     def resolve_normals(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int,
