@@ -245,6 +245,87 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             lambda sc: {"unique_tris": int(len(sc.tris)), "instanced_tris": sc.meta["instanced_tris"],
                         "unique_blas": 600, "instances": 2400, "cwbvh_nodes": int(len(sc.nodes))},
             with_parts=True)
+    if "dyn" in which:
+        # the reference's per-frame dynamic-scene update on C4 (AssetManager.cs:1767-1826): every
+        # frame rewrites all _MeshData records (MeshDataBuffer.SetData, :1825) and refits the TLAS
+        # (RefitTLAS, :1821-1823, :1473-1606) before tracing. Here: tt_scene_update_meshdata of all
+        # 2,401 records from a host array + tt_tlas_refit from device AABBs + Generate + primary
+        # trace + diffuse enqueue + bounce-1 trace, the instances alternating between two poses (a
+        # 5 cm shift of every instance). Wall time per frame and the host time of the update call.
+        rec = {}
+        try:
+            if sc4 is None:
+                sc4 = T.c4_bistro()
+            eng.upload(sc4)
+            W, H = 1920, 1080
+            n_md = len(sc4.meshdata)
+            md_a = sc4.meshdata.copy()
+            md_b = sc4.meshdata.copy()
+            box_a = np.ascontiguousarray(sc4.meta["mesh_aabbs"], np.float32).reshape(n_md, 6)
+            box_b = box_a.copy()
+            d = np.array([0.05, 0.0, 0.02])
+            shift = np.eye(4)
+            shift[:3, 3] = -d
+            for i in range(1, n_md):  # record 0: the static street parent
+                w2l = md_a["W2L"][i].astype(np.float64).reshape(4, 4).T
+                md_b["W2L"][i] = tthip.unity_colmajor(w2l @ shift)
+                box_b[i, 0:3] += d.astype(np.float32)
+                box_b[i, 3:6] += d.astype(np.float32)
+            boxes = [torch.from_numpy(box_a).to(dev), torch.from_numpy(box_b).to(dev)]
+            mds = [md_a, md_b]
+            c2w, ip = T.C4_VIEW.camera(W, H)
+            rays = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
+            info = torch.zeros(W * H * 16, dtype=torch.uint8, device=dev)
+            colors = np.zeros(W * H, tthip.COL_DTYPE)
+            colors["Data"][:, 3] = 1.0
+            colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+            host_upd, host_refit, nbs = [], [], []
+
+            def frame(k, record):
+                t0 = time.perf_counter()
+                eng.update_meshdata(0, mds[k])
+                t1 = time.perf_counter()
+                eng.tlas_refit(sc4.tlas_nodes, boxes[k], device=True, asynchronous=True)
+                t2 = time.perf_counter()
+                eng.generate(rays, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=1, device=True)
+                eng.trace(rays, W * H, 0, far, W, H, info=info, device=True, asynchronous=True)
+                nb_ = eng.enqueue_bounce(rays, W * H, 0, far, W, H, frames=0, max_bounce=1, device=True)
+                eng.trace(rays, nb_, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+                if record:
+                    host_upd.append(t1 - t0)
+                    host_refit.append(t2 - t1)
+                    nbs.append(nb_)
+
+            for k in range(max(2, args.warmup)):
+                frame(k & 1, False)
+            torch.cuda.synchronize(dev)
+            reps = max(6, args.steps // 2)
+            tf = time.perf_counter()
+            for k in range(reps):
+                frame(k & 1, True)
+            torch.cuda.synchronize(dev)
+            ms = (time.perf_counter() - tf) * 1e3 / reps
+            # the update + refit alone on the stream (HIP events around the refit; the update's
+            # device work is one H2D copy + one small kernel)
+            eng.timing_reset()
+            for k in range(reps):
+                eng.update_meshdata(0, mds[k & 1])
+                eng.tlas_refit(sc4.tlas_nodes, boxes[k & 1], device=True, asynchronous=True)
+            refit_ms = ring_tail(eng, 1, reps)[:, 0]
+            eng.upload(sc4)  # leave the scene as built
+            rays_f = W * H + float(np.mean(nbs))
+            rec = {"instances_updated": n_md, "tlas_nodes": int(sc4.tlas_nodes), "frames": reps,
+                   "ms_per_frame": round(ms, 4), "mrays_s": round(rays_f / ms / 1e3, 1),
+                   "update_meshdata_host_ms_median": round(float(np.median(host_upd)) * 1e3, 4),
+                   "update_meshdata_host_ms_max": round(float(np.max(host_upd)) * 1e3, 4),
+                   "tlas_refit_host_ms_median": round(float(np.median(host_refit)) * 1e3, 4),
+                   "tlas_refit_gpu_ms_median": round(float(np.median(refit_ms)), 4),
+                   "note": "frame = update_meshdata (all records, host array, async) + tlas_refit (device boxes) + "
+                           "Generate + primary trace + enqueue (returns the count: one sync) + bounce-1 trace"}
+        except Exception as e:  # auxiliary: record, never lose the metric line
+            rec["error"] = f"{type(e).__name__}: {e}"
+        out["c4_dynamic_frame"] = rec
+        log(f"aux c4 dynamic frame: {rec}")
     if "refit" in which:
         # row f4 per frame: the GPU TLAS refit of the C4 scene (AssetManager.RefitTLAS, 2,400
         # instance boxes -> TLAS nodes) and the BLAS refit of the C2 mesh as a deforming mesh
@@ -541,8 +622,8 @@ def main():
                          "use the metric's kernel instantiation and would mix into its rocprof average)")
     ap.add_argument("--no-c5-tiles", action="store_true",
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
-    ap.add_argument("--aux", default="c3,c4,refit,c5",
-                    help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,refit,c5;"
+    ap.add_argument("--aux", default="c3,c4,dyn,refit,c5",
+                    help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,dyn,refit,c5;"
                          " '' = none)")
     args = ap.parse_args()
 

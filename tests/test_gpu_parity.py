@@ -235,6 +235,59 @@ def test_update_meshdata_and_nodes(engine):
         engine.update_nodes(0, bad)
 
 
+def test_incremental_async_updates(engine):
+    """The per-frame update paths are incremental and asynchronous (no host sync): a sub-range of
+    _MeshData records (the caller's buffer overwritten right after the call: the library staged
+    it), back-to-back updates (pinned staging slots reused), a record re-pointed at another
+    validated BLAS, a rejected record (out-of-range BLAS: nothing changes), a BLAS-node rewrite
+    (full validation) -- every state traced against the oracle on the same buffers."""
+    sc = instanced_scene(11, n_props=4, n_inst=30)
+    W, H = 96, 64
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.3, FAR)
+    engine.upload(sc)
+    md = sc.meshdata.copy()
+    rng = np.random.default_rng(11)
+    for step in range(3):  # three updates back to back, no trace or sync between them
+        buf = md.copy()
+        for i in range(5, 17):
+            buf["W2L"][i] = tthip.unity_colmajor(np.linalg.inv(tthip.trs_matrix(
+                rng.uniform(-30, 30, 3) * [1, 0.1, 1], float(rng.uniform(0, 360)), float(rng.uniform(0.5, 1.5)))))
+        engine.update_meshdata(5, buf[5:17])
+        md[5:17] = buf[5:17]
+        buf["W2L"][:] = np.nan  # the caller reuses its buffer at once
+    sc2 = tthip.Scene(sc.nodes, sc.tris, sc.tlas, md, sc.materials)
+    rg, rc, ig, ic, _, _ = trace_both(engine, sc2, rays, W * H, 0, W, H, upload=False)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    # re-point instance 3 at the BLAS of instance 4 (validated at upload)
+    if (md["NodeOffset"][3], md["TriOffset"][3]) == (md["NodeOffset"][4], md["TriOffset"][4]):
+        j = next(k for k in range(5, len(md)) if md["NodeOffset"][k] != md["NodeOffset"][3])
+    else:
+        j = 4
+    rec = md[3:4].copy()
+    for f in ("NodeOffset", "TriOffset", "mesh_data_bvh_offsets"):
+        rec[f] = md[f][j]
+    engine.update_meshdata(3, rec)
+    md[3:4] = rec
+    # a record naming an out-of-range BLAS root is refused and changes nothing
+    bad = md[6:7].copy()
+    bad["mesh_data_bvh_offsets"] = len(sc.nodes) + 5
+    bad["W2L"][:] = 0.0
+    with pytest.raises(tthip.TTError):
+        engine.update_meshdata(6, bad)
+    sc3 = tthip.Scene(sc.nodes, sc.tris, sc.tlas, md, sc.materials)
+    rg, rc, ig, ic, _, _ = trace_both(engine, sc3, rays, W * H, 0, W, H, upload=False)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+    # a BLAS node (outside the TLAS) rewritten: the root of instance 5's BLAS grown conservatively
+    nodes = sc.nodes.copy()
+    r5 = int(md["mesh_data_bvh_offsets"][5]) & 0x7FFFFFFF
+    nodes[r5]["p"] = nodes[r5]["p"] - 0.25
+    engine.update_nodes(r5, nodes[r5:r5 + 1])
+    sc4 = tthip.Scene(nodes, sc.tris, sc.tlas, md, sc.materials)
+    rg, rc, ig, ic, _, _ = trace_both(engine, sc4, rays, W * H, 0, W, H, upload=False)
+    assert_same(rg, rc, ig, ic, 0, W * H)
+
+
 def test_info_forms_at_later_bounce(engine):
     g = golden_io.load("soup")
     sc, W, H = g["scene"], g["W"], g["H"]

@@ -50,7 +50,17 @@ for _ in range(10):
     eng.trace(rays, nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
 ms = eng.timing_read()
 p, b = float(np.median(ms[0::2])), float(np.median(ms[1::2]))
-print(json.dumps({"ok": ok, "primary_ms": round(p, 4), "bounce_ms": round(b, 4), "grays": round((W * H + nb) / (p + b) / 1e6, 3)}))
+rec = {"ok": ok, "primary_ms": round(p, 4), "bounce_ms": round(b, 4), "grays": round((W * H + nb) / (p + b) / 1e6, 3)}
+if os.environ.get("RV_RECUR") == "1":  # + the unjittered (UseReCur) primary launch: the long-ray tail
+    rr = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
+    eng.generate(rr, c2w, ip, W, H, 0.3, far, jitter=0, frames=0, max_bounce=1, device=True)
+    for _ in range(2):
+        eng.trace(rr, W * H, 0, far, W, H, info=info, device=True, asynchronous=True)
+    eng.timing_reset()
+    for _ in range(5):
+        eng.trace(rr, W * H, 0, far, W, H, info=info, device=True, asynchronous=True)
+    rec["recur_primary_ms"] = round(float(np.median(eng.timing_read())), 4)
+print(json.dumps(rec))
 '''
 libs = sorted(glob.glob(os.path.join(REPO, "truetrace-unity-pathtracer_amd", "lib", "variants", "*.so")))
 names = [os.path.basename(l)[len("libtruetrace_hip_"):-3] for l in libs]

@@ -72,6 +72,20 @@ struct SceneHost {
     bool any_cutout = false;       // Cutout materials present (need the alpha atlas)
     std::vector<CutoutMat> cut;    // per material, when any_cutout
     std::vector<GlassMat> glass;   // per material, when any_atlas_shadow
+    // incremental per-frame updates (tt_scene_update_*): what the last full validation established
+    struct BlasKey {
+        uint32_t root, node_offset, tri_offset;
+        bool operator<(const BlasKey& o) const {
+            return root != o.root ? root < o.root : node_offset != o.node_offset ? node_offset < o.node_offset
+                                                                                  : tri_offset < o.tri_offset;
+        }
+        bool operator==(const BlasKey& o) const {
+            return root == o.root && node_offset == o.node_offset && tri_offset == o.tri_offset;
+        }
+    };
+    std::vector<BlasKey> blas_ok;       // sorted: (root, NodeOffset, TriOffset) triples walked and valid
+    std::vector<uint8_t> is_tlas_node;  // node reached by the TLAS-level walk
+    std::vector<uint32_t> tlas_nodes;   // the same, as a list
 };
 
 }  // namespace
@@ -145,6 +159,16 @@ struct tt_ctx {
     DevBuf<float4> st_nee;
     DevBuf<tt_cache_data> st_cache;
     unsigned long long last_diag[8] = {};
+    // pinned host staging for the asynchronous per-frame updates: two slots, each reused once the
+    // copy enqueued from it has completed (its event)
+    struct Pinned {
+        void* p = nullptr;
+        size_t n = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    Pinned pin[2];
+    uint32_t pin_cur = 0;
 };
 
 // Per-call timing ring entries (tt_timing_read) around device work issued on the context stream.
@@ -195,9 +219,12 @@ struct Validator {
     explicit Validator(const SceneHost& h) : s(h), epoch_of(h.nodes.size(), 0u) {}
 
     uint32_t max_matdat = 0;
+    std::vector<uint32_t> tlas_visit;  // nodes reached by the last TLAS-level walk
+    std::vector<SceneHost::BlasKey> keys;  // BLAS (root, NodeOffset, TriOffset) walked by run()
     bool walk(uint32_t root, uint32_t node_offset, uint32_t tri_offset, bool tlas_level) {
         epoch++;
         max_matdat = 0;
+        if (tlas_level) tlas_visit.clear();
         std::vector<uint32_t> work{root};
         while (!work.empty()) {
             const uint32_t ni = work.back();
@@ -208,6 +235,7 @@ struct Validator {
             }
             if (epoch_of[ni] == epoch) continue;
             epoch_of[ni] = epoch;
+            if (tlas_level) tlas_visit.push_back(ni);
             const tt_cwbvh_node& n = s.nodes[ni];
             const uint32_t imask = n.e_imask >> 24;
             for (int k = 0; k < 8; k++) {
@@ -254,6 +282,16 @@ struct Validator {
         return true;
     }
 
+    // one mesh record's BLAS (IntersectionKernels.compute:197-213 reach it through the TLAS)
+    bool walk_mesh(const tt_mesh_data& md) {
+        if (md.NodeOffset < 0 || md.TriOffset < 0) {
+            why = "negative mesh offsets";
+            return false;
+        }
+        return walk((uint32_t)(md.mesh_data_bvh_offsets & 0x7fffffff), (uint32_t)md.NodeOffset,
+                    (uint32_t)md.TriOffset, false);
+    }
+
     bool run() {
         if (s.nodes.empty() || s.mesh.empty()) {
             why = "empty scene";
@@ -286,12 +324,22 @@ struct Validator {
                 if (!walk(root, (uint32_t)md.NodeOffset, (uint32_t)md.TriOffset, false)) return false;
                 mm = max_matdat;
                 seen.push_back(Seen{key, root, mm});
+                keys.push_back(SceneHost::BlasKey{root, (uint32_t)md.NodeOffset, (uint32_t)md.TriOffset});
             }
 
         }
+        std::sort(keys.begin(), keys.end());
         return true;
     }
 };
+
+// Records what a full validation established, for the incremental per-frame update paths.
+void remember_validation(SceneHost& h, const Validator& v) {
+    h.blas_ok = v.keys;
+    h.is_tlas_node.assign(h.nodes.size(), 0u);
+    h.tlas_nodes = v.tlas_visit;
+    for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
+}
 
 tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris, uint32_t n_tris,
                       const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md, uint32_t n_mesh,
@@ -352,10 +400,11 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
         why = v.why;
         return TT_ERR_INVALID_ARG;
     }
+    remember_validation(h, v);
     return TT_OK;
 }
 
-void derive_mesh(const tt_mesh_data& in, MeshGpu& o) {
+__host__ __device__ inline void derive_mesh(const tt_mesh_data& in, MeshGpu& o) {
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 4; c++) o.m[r * 4 + c] = in.W2L[c * 4 + r];
     o.TriOffset = in.TriOffset;
@@ -389,6 +438,29 @@ void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
     o.e2z = t.posedge2[2];
     o.matdat = t.MatDat;
     o.pad0 = o.pad1 = 0;
+}
+
+// The traversal records of updated _MeshData entries [first, first + count) (derive_mesh), and
+// every TLAS leaf record whose TLASBVH8Indices entry names one of them (derive_leaves).
+__global__ void tt_update_mesh_kernel(const tt_mesh_data* __restrict__ raw, MeshGpu* __restrict__ mesh,
+                                      LeafMesh* __restrict__ leaf, const int32_t* __restrict__ tlas, uint32_t n_tlas,
+                                      uint32_t first, uint32_t count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) {
+        MeshGpu g;
+        derive_mesh(raw[first + i], g);
+        mesh[first + i] = g;
+    }
+    if (i < n_tlas) {
+        const int32_t m = tlas[i];
+        if (m >= 0 && (uint32_t)m - first < count) {
+            LeafMesh l;
+            derive_mesh(raw[m], l.m);
+            l.mesh_id = m;
+            l.pad[0] = l.pad[1] = l.pad[2] = 0;
+            leaf[i] = l;
+        }
+    }
 }
 
 bool is_device_ptr(const void* p) {
@@ -550,6 +622,10 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     for (uint32_t i = 0; i < TT_RING; i++) {
         if (c->ring0[i]) (void)hipEventDestroy(c->ring0[i]);
         if (c->ring1[i]) (void)hipEventDestroy(c->ring1[i]);
+    }
+    for (auto& pn : c->pin) {
+        if (pn.p) (void)hipHostFree(pn.p);
+        if (pn.ev) (void)hipEventDestroy(pn.ev);
     }
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -862,8 +938,38 @@ tt_status tt_scene_validate(const tt_cwbvh_node* nodes, uint32_t n_nodes, const 
 }
 
 namespace {
-// Rebuilds the TLAS leaf records from the host mirror (on upload and after node / mesh-record
-// updates, which may change the topology) and uploads them on the stream.
+// Copies `bytes` of caller memory into the next pinned staging slot (waiting, if needed, until the
+// copy last enqueued from that slot has completed), so the H2D copy can be asynchronous and the
+// caller may reuse its buffer as soon as the call returns. stage_end() marks the slot in use by the
+// copies enqueued since.
+hipError_t stage_begin(tt_ctx* c, const void* src, size_t bytes, void*& out) {
+    tt_ctx::Pinned& pn = c->pin[c->pin_cur];
+    hipError_t e;
+    if (!pn.ev && (e = hipEventCreateWithFlags(&pn.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (pn.pending) {
+        if ((e = hipEventSynchronize(pn.ev)) != hipSuccess) return e;
+        pn.pending = false;
+    }
+    if (pn.n < bytes) {
+        if (pn.p) (void)hipHostFree(pn.p);
+        pn.p = nullptr;
+        pn.n = 0;
+        if ((e = hipHostMalloc(&pn.p, bytes, hipHostMallocDefault)) != hipSuccess) return e;
+        pn.n = bytes;
+    }
+    std::memcpy(pn.p, src, bytes);
+    out = pn.p;
+    return hipSuccess;
+}
+hipError_t stage_end(tt_ctx* c) {
+    tt_ctx::Pinned& pn = c->pin[c->pin_cur];
+    c->pin_cur ^= 1u;
+    const hipError_t e = hipEventRecord(pn.ev, c->stream);
+    pn.pending = e == hipSuccess;
+    return e;
+}
+
+// Rebuilds the TLAS leaf records from the host mirror (on upload) and uploads them on the stream.
 tt_status refresh_leaves(tt_ctx* c) {
     std::vector<LeafMesh> lv = derive_leaves(c->host.tlas, c->host.mesh);
     if (c->leaf.n < lv.size()) {
@@ -882,18 +988,35 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!nodes || (uint64_t)first + count > c->host.nodes.size())
         return fail(c, TT_ERR_INVALID_ARG, "node update range out of bounds");
-    std::vector<tt_cwbvh_node> saved(c->host.nodes.begin() + first, c->host.nodes.begin() + first + count);
-    std::copy(nodes, nodes + count, c->host.nodes.begin() + first);
-    Validator v(c->host);
-    if (!v.run()) {
-        std::copy(saved.begin(), saved.end(), c->host.nodes.begin() + first);
+    if (count == 0) return TT_OK;
+    SceneHost& h = c->host;
+    std::vector<tt_cwbvh_node> saved(h.nodes.begin() + first, h.nodes.begin() + first + count);
+    std::copy(nodes, nodes + count, h.nodes.begin() + first);
+    // A rewrite of TLAS-level nodes only (the per-frame case: BVH8AggregatedBuffer.SetData of the
+    // TLAS region) re-walks the TLAS level; the BLASes were validated at upload and are unchanged.
+    // Any other rewrite re-validates the whole scene.
+    bool tlas_only = true;
+    for (uint32_t i = first; i < first + count && tlas_only; i++) tlas_only = h.is_tlas_node[i] != 0;
+    Validator v(h);
+    const bool ok = tlas_only ? v.walk(0, 0, 0, true) : v.run();
+    if (!ok) {
+        std::copy(saved.begin(), saved.end(), h.nodes.begin() + first);
         return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after node update: %s", v.why.c_str());
     }
+    if (tlas_only) {
+        for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 0u;
+        h.tlas_nodes = v.tlas_visit;
+        for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
+    } else {
+        remember_validation(h, v);
+    }
     TT_HIP(c, hipSetDevice(c->device));
-    TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, nodes, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
-    TT_HIP(c, hipStreamSynchronize(c->stream));
+    void* pinned = nullptr;
+    TT_HIP(c, stage_begin(c, nodes, sizeof(tt_cwbvh_node) * count, pinned));
+    TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, pinned, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
+    TT_HIP(c, stage_end(c));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
-    return refresh_leaves(c);
+    return TT_OK;
 }
 
 tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, const tt_mesh_data* md) {
@@ -901,19 +1024,48 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!md || (uint64_t)first + count > c->host.mesh.size())
         return fail(c, TT_ERR_INVALID_ARG, "meshdata update range out of bounds");
-    std::vector<tt_mesh_data> saved(c->host.mesh.begin() + first, c->host.mesh.begin() + first + count);
-    std::copy(md, md + count, c->host.mesh.begin() + first);
-    Validator v(c->host);
-    if (!v.run()) {
-        std::copy(saved.begin(), saved.end(), c->host.mesh.begin() + first);
-        return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: %s", v.why.c_str());
+    if (count == 0) return TT_OK;
+    SceneHost& h = c->host;
+    // Only records whose BLAS reference (root, NodeOffset, TriOffset) changed need a check, and only
+    // against the BLASes validated so far; a BLAS never seen is walked once and remembered. The
+    // per-frame transform update (MeshDataBuffer.SetData, AssetManager.cs:1825) changes none.
+    std::vector<SceneHost::BlasKey> added;
+    for (uint32_t i = 0; i < count; i++) {
+        const tt_mesh_data& r = md[i];
+        const tt_mesh_data& o = h.mesh[first + i];
+        if (r.NodeOffset == o.NodeOffset && r.TriOffset == o.TriOffset &&
+            ((r.mesh_data_bvh_offsets ^ o.mesh_data_bvh_offsets) & 0x7fffffff) == 0)
+            continue;
+        if (r.NodeOffset < 0 || r.TriOffset < 0)
+            return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: negative mesh offsets");
+        const SceneHost::BlasKey k{(uint32_t)(r.mesh_data_bvh_offsets & 0x7fffffff), (uint32_t)r.NodeOffset,
+                                   (uint32_t)r.TriOffset};
+        if (std::binary_search(h.blas_ok.begin(), h.blas_ok.end(), k) ||
+            std::find(added.begin(), added.end(), k) != added.end())
+            continue;
+        Validator v(h);
+        if (!v.walk_mesh(r))
+            return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: %s", v.why.c_str());
+        added.push_back(k);
     }
-    std::vector<MeshGpu> mg(count);
-    for (uint32_t i = 0; i < count; i++) derive_mesh(md[i], mg[i]);
+    if (!added.empty()) {
+        h.blas_ok.insert(h.blas_ok.end(), added.begin(), added.end());
+        std::sort(h.blas_ok.begin(), h.blas_ok.end());
+    }
+    std::memcpy(h.mesh.data() + first, md, sizeof(tt_mesh_data) * count);
     TT_HIP(c, hipSetDevice(c->device));
-    TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, md, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
-    TT_HIP(c, hipMemcpyAsync(c->mesh.p + first, mg.data(), sizeof(MeshGpu) * count, hipMemcpyHostToDevice, c->stream));
-    return refresh_leaves(c);
+    // the raw records go to _MeshData in HBM; one small kernel derives the traversal records
+    // (MeshGpu) and patches the TLAS leaf records that name an updated mesh, on the stream
+    void* pinned = nullptr;
+    TT_HIP(c, stage_begin(c, md, sizeof(tt_mesh_data) * count, pinned));
+    TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, pinned, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
+    TT_HIP(c, stage_end(c));
+    const uint32_t n_tlas = (uint32_t)h.tlas.size();
+    const uint32_t n = std::max(count, n_tlas);
+    hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream, c->mesh_raw.p, c->mesh.p,
+                       c->leaf.p, c->tlas.p, n_tlas, first, count);
+    TT_HIP(c, hipGetLastError());
+    return TT_OK;
 }
 
 tt_status tt_scene_bytes(const tt_ctx* c, uint64_t* bytes) {
