@@ -54,7 +54,7 @@ __device__ __forceinline__ bool shadow_triangle(__amdgpu_buffer_rsrc_t tris, con
     const float qz = fma_(sx, e1y, -(sy * e1x));
     const float v = f * fma_(r.dz, qz, fma_(r.dy, qy, r.dx * qx));
     const float t = f * fma_(e2z, qz, fma_(e2y, qy, e2x * qx));
-    const bool in_tri = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f);
+    const bool in_tri = (u >= 0.0f) && (v >= 0.0f && u + v <= 1.0f);  // u <= 1 implied (tt_traverse.h)
     bool occ = in_tri && (t > 0.0f && t < max_distance);
     if (MATCHECK && in_tri) {
         // IsBackground / ShadowCaster surfaces never occlude (:612); Cutout with the point sampler

@@ -286,7 +286,10 @@ __device__ __forceinline__ TriCand triangle_test(const TriData& d, const MatView
     R.t = t;
     R.u = u;
     R.v = v;
-    R.cand = (u >= 0.0f && u <= 1.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best_t);
+    // IntersectionKernels.compute:29-31: (u >= 0 && u <= 1) && (v >= 0 && u + v <= 1) && (t > 0 && t < best).
+    // u <= 1 is implied by v >= 0 && fl(u + v) <= 1 (v >= 0 gives u + v >= u, rounding is monotonic and u
+    // is representable; an infinite or NaN u fails u + v <= 1), so it is not evaluated: same predicate.
+    R.cand = (u >= 0.0f) && (v >= 0.0f && u + v <= 1.0f) && (t > 0.0f && t < best_t);
     R.accept = R.cand;
     if (MATCHECK && R.accept) {
         // _Materials[MatOffset + MatDat]; an out-of-range StructuredBuffer read returns zeros in
