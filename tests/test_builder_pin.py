@@ -83,26 +83,40 @@ def test_build_total_rounding_is_needed():
 
 # ---------------------------------------------------------------------------------------------
 # Unity built-in Cube ParentObjects of the same scene (tools/unity_prim_pin.py --write-fixture):
-# 18 serialized 12-entry leaf orders (4 distinct), positions = Unity's Cube mesh through BuildTotal's
-# (v + Ofst) -> TransMat -> - Ofst2 path with each object's transform chain.
+# 18 serialized 12-entry leaf orders (6 distinct). Inputs, all from the scene's serialized fields:
+# positions = Unity's Cube mesh through BuildTotal's (v + Ofst) -> TransMat -> - Ofst2 path on each
+# object's CachedTransforms (exact float32 worldToLocalMatrix + position; Matrix4x4.inverse evaluated
+# in double, rounded once), and the lossy scale whose 0.001f / lossy is the serialized ParentScale --
+# the AABB.Validate padding of the flat faces (CommonVars.cs:385-395), which decides the SAH ties of
+# the scaled cubes.
 
 
 def _cube_pins():
     return np.load(os.path.join(HERE, "golden", "unity_cube_pins.npz"))
 
 
+def _cube_order(pos, idx, lossy):
+    return tthip.Blas(tthip.Mesh.from_arrays(pos.astype(np.float32), idx),
+                      lossy_scale=tuple(float(x) for x in lossy)).leaf_order()
+
+
 def test_unity_cube_leaf_orders_reproduced():
     z = _cube_pins()
-    ok = []
-    for pos, order in zip(z["positions"], z["orders"]):
-        lo = tthip.Blas(tthip.Mesh.from_arrays(pos.astype(np.float32), z["cube_i"])).leaf_order()
-        ok.append(bool(np.array_equal(lo, order)))
+    ok = [bool(np.array_equal(_cube_order(p, z["cube_i"], l), o))
+          for p, o, l in zip(z["positions"], z["orders"], z["lossy"])]
     assert ok == z["reproduced"].tolist()
-    assert sum(ok) >= 14
-    # the reproduced set includes orders other than the unit cube's: BuildTotal's float offset path
-    # decides SAH ties there, exactly as in the reference's build
-    repro = {tuple(o) for o, k in zip(z["orders"].tolist(), ok) if k}
-    assert len(repro) >= 3
+    assert all(ok), f"{sum(ok)}/18 serialized cube leaf orders reproduced"
+    assert len({tuple(o) for o in z["orders"].tolist()}) == 6  # all 6 distinct serialized orders are covered
+
+
+def test_unity_cube_parent_scale_padding_is_needed():
+    """Without the serialized ParentScale (lossy scale 1: padding 0.001 on every axis) the scaled cubes'
+    ties break differently: the padding is an input of the reference's build, not a detail."""
+    z = _cube_pins()
+    ok = [bool(np.array_equal(_cube_order(p, z["cube_i"], (1.0, 1.0, 1.0)), o))
+          for p, o in zip(z["positions"], z["orders"])]
+    assert sum(ok) < 18
+    assert not all(np.allclose(l, 1.0) for l in z["lossy"])
 
 
 def test_unity_cube_raw_mesh_gives_the_common_order():
@@ -110,3 +124,22 @@ def test_unity_cube_raw_mesh_gives_the_common_order():
     lo = tthip.Blas(tthip.Mesh.from_arrays(z["cube_v"], z["cube_i"])).leaf_order()
     common = max({tuple(o) for o in z["orders"].tolist()}, key=lambda o: sum(tuple(x) == o for x in z["orders"].tolist()))
     assert tuple(lo.tolist()) == common
+
+
+# Multi-child ParentObjects made of built-in meshes (tools/unity_prim_pin.py --write-fixture): "Ceiling"
+# (4 cubes, 48 triangles) and "Wall1" (4 cubes + a Quad, 50) reproduce every leaf position, "Quad" its 2.
+# "Entrance" (3 cubes, one under a 90-degree x rotation stored with 1e-8-level float noise) matches 32 of
+# 36: two within-leaf swaps of the two triangles of a face whose boxes tie up to that noise.
+
+
+def test_unity_multi_object_leaf_orders():
+    z = np.load(os.path.join(HERE, "golden", "unity_multi_pins.npz"))
+    got = {}
+    for k, name in enumerate(z["names"].tolist()):
+        lo = tthip.Blas(tthip.Mesh.from_arrays(z[f"positions_{k}"], z[f"indices_{k}"]),
+                        lossy_scale=tuple(float(x) for x in z[f"lossy_{k}"])).leaf_order()
+        got[name] = int((lo == z[f"order_{k}"]).sum())
+        assert sorted(lo.tolist()) == list(range(len(lo)))
+    assert got == dict(zip(z["names"].tolist(), z["matched"].tolist()))
+    assert got["Ceiling"] == 48 and got["Wall1"] == 50 and got["Quad"] == 2
+    assert got["Entrance"] >= 32
