@@ -9,14 +9,17 @@ rays (bounce 1, _PrimaryTriangleInfo written where GlobalColors.Data.w == 1), bo
 resident in HBM in the reference's 2*W*H ping-pong RayData buffer. Ray generation and the
 bounce enqueue run once during setup (they are the caller's kernels, not the trace).
 
-Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): one process per GPU, scene
-replicated per GPU, the 1080p frame's 64x64 screen tiles dealt round-robin to the ranks (SURVEY.md
-§8(e)). Each rank traces its tiles' primary rays and their bounce-1 rays, then the primary hit
-records go to rank 0 in ONE RCCL gather over xGMI -- inside the timed step (on a second stream,
-overlapped with the bounce-1 trace), so a step is a whole frame and ``value`` is frame rays / frame
-time (strong scaling). ``--shard sample`` instead has
-every rank trace its own full-frame sample (weak scaling, no data-path collective); that layout is
-also reported as ``config.aux_sample_sharded``.
+Multi-GPU (``bench.py --gpus N``, self-launched, or under ``torchrun --nproc-per-node N``): one process
+per GPU, scene replicated per GPU. Default layout ``--shard spp`` (weak scaling, per-GPU work fixed):
+the job at N GPUs is an N-sample 1080p frame (sample k = the reference's Generate with
+frames_accumulated = k); its (sample, 64x64 screen tile) units are dealt round-robin to the ranks
+(SURVEY.md §8(e)'s tile sharding), so each rank traces one frame's worth of tiles' primary rays and
+their bounce-1 rays, and the primary hit records of all N samples go to rank 0 in ONE RCCL gather
+over xGMI -- inside the timed step (on a second stream, overlapped with the bounce-1 trace).
+``value`` = all ranks' rays / the slowest rank's time. The strong-scaling layout (ONE 1-sample
+frame's tiles over the ranks, same gather) is measured beside it as ``config.aux_strong_tiles`` and
+is the headline with ``--shard tiles``; ``--shard sample`` has every rank trace its own full-frame
+sample with no collective (``config.aux_sample_sharded``).
 
 Streams: torch and the engine share ONE stream (a torch.cuda.Stream made current before any
 allocation and passed to tt_ctx_create), so every torch copy / collective and every engine launch
@@ -601,11 +604,14 @@ def main():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x53504F4E)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", choices=["tiles", "sample"], default="tiles",
-                    help="N > 1 layout. tiles (default, SURVEY 8e): the frame's 64x64 tiles are dealt round-robin "
-                         "to ranks, each traces its pixels and their bounce-1 rays, and the primary hit records are "
-                         "RCCL-gathered to rank 0 inside every timed step (strong scaling). sample: every rank "
-                         "traces its own full-frame sample, no collective (weak scaling)")
+    ap.add_argument("--shard", choices=["spp", "tiles", "sample"], default="spp",
+                    help="N > 1 layout. spp (default, weak scaling): the job at N ranks is an N-sample 1080p frame "
+                         "whose (sample, 64x64 tile) units are dealt round-robin to the ranks (ttdist.spp_part_pixels): "
+                         "every rank traces one frame's worth of screen tiles and their bounce-1 rays, and the primary "
+                         "hit records of all N samples are RCCL-gathered to rank 0 inside every timed step. tiles "
+                         "(strong scaling, also reported as config.aux_strong_tiles): ONE 1-sample frame's tiles dealt "
+                         "round-robin, same gather. sample: every rank traces its own full-frame sample, no collective "
+                         "(weak scaling)")
     ap.add_argument("--parts", type=int, default=0,
                     help="a rank's pixels (N = 1: the frame; N > 1: its tiles) are traced as this many tile-interleaved "
                          "parts, each by its own engine on its own stream (each part's bounce-1 after its own primary), "
@@ -684,7 +690,8 @@ def main():
         if dist.get_world_size() != world:
             raise SystemExit(f"bench.py: the process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
     dist_world = dist.get_world_size() if (world > 1 or rccl1) else None
-    tiles =(world > 1 or rccl1) and args.shard == "tiles"
+    tiles = (world > 1 or rccl1) and args.shard in ("tiles", "spp")
+    spp = tiles and args.shard == "spp"  # the N-sample frame (weak scaling); "tiles": one frame (strong)
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -729,36 +736,116 @@ def main():
     class Part:  # one launch stream of this rank: its engine, stream, rays and counts
         pass
 
-    parts = []
-    if split:  # this rank's pixels, compacted in tile order (ttdist.tile_pixels), split into P parts
-        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
-        for s, pix_np in enumerate(ttdist.part_pixels(W, H, world, rank, P)):
+    # part s always runs on the same engine context and stream (part 0: the shared main stream)
+    lanes = [(eng, stream)]
+
+    def lane(s):
+        while len(lanes) <= s:
+            st = torch.cuda.Stream(dev)
+            e = tthip.Engine(gpu, stream=st.cuda_stream)
+            e.upload(scene)
+            lanes.append((e, st))
+        return lanes[s]
+
+    def build_parts(plan, fresh=False):
+        """plan: per part, [(sample k, pixel indices)]: the rays of sample k (Generate with
+        frames_accumulated = k) at those pixels, compacted back to back into the part's ping-pong
+        buffer (part 0: the main buffer `rays` unless fresh); then one stats trace of each bounce and
+        the bounce-1 enqueue (setup, untimed)."""
+        ps = []
+        for s_, lst in enumerate(plan):
             p = Part()
-            if s == 0:
-                p.eng, p.stream, p.rays = eng, stream, rays
-            else:
-                p.stream = torch.cuda.Stream(dev)
-                p.eng = tthip.Engine(gpu, stream=p.stream.cuda_stream)
-                p.eng.upload(scene)
-                p.rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-            pix = torch.from_numpy(pix_np).to(dev)
-            p.n = int(pix.shape[0])
-            p.rays.view(2 * WH, 48)[:p.n] = full.view(WH, 48)[pix]
-            parts.append(p)
+            p.eng, p.stream = lane(s_)
+            p.rays = rays if (s_ == 0 and not fresh) else torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            p.n = int(sum(len(pix) for _, pix in lst))
+            ps.append(p)
+        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        for k in sorted({k for lst in plan for k, _ in lst}):
+            eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=k, max_bounce=1, device=True)
+            for p, lst in zip(ps, plan):
+                o = 0
+                for kk, pix in lst:
+                    if kk == k and len(pix):
+                        p.rays.view(2 * WH, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
+                    o += len(pix)
         del full
         torch.cuda.synchronize(dev)  # the other parts' engines run on their own streams
-    else:
-        p = Part()
-        p.eng, p.stream, p.rays, p.n = eng, stream, rays, WH
-        eng.generate(rays, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
-        parts.append(p)
-    for p in parts:
-        p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, stats=True)
-        p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=frames, max_bounce=1, device=True)
-        p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
-        p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
-    torch.cuda.synchronize(dev)
+        for p in ps:
+            p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, stats=True)
+            p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+            p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
+            p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
+        torch.cuda.synchronize(dev)
+        return ps
+
+    class Gather:  # the per-step RCCL gather of the primary hit records to rank 0
+        pass
+
+    def make_gather(ps):
+        # shards padded to the largest so every rank sends one equal-size message; a rank's parts back
+        # to back. The gather runs on its own stream, overlapped with the bounce-1 traces (which read and
+        # write only the other half of the ping-pong buffers); the step ends when both are done, so the
+        # timed step includes the collective.
+        g = Gather()
+        n_t = torch.tensor([p.n for p in ps], dtype=torch.int64, device=red_dev)
+        sz = [torch.zeros_like(n_t) for _ in range(world)]
+        dist.all_gather(sz, n_t)
+        g.sizes = [[int(v) for v in x.tolist()] for x in sz]
+        g.hits_buf = torch.zeros((max(sum(x) for x in g.sizes), 4), dtype=torch.int32, device=red_dev)
+        g.gather_list = [torch.empty_like(g.hits_buf) for _ in range(world)] if rank == 0 else None
+        g.comm = torch.cuda.Stream(dev)
+        g.copied = torch.cuda.Event()
+        return g
+
+    def make_step(ps, g):
+        def step_fn():
+            for p in ps:
+                p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True)
+            if g is not None:
+                for p in ps:
+                    g.comm.wait_stream(p.stream)  # the primary hit records are final
+                with torch.cuda.stream(g.comm):
+                    o = 0
+                    for p in ps:
+                        g.hits_buf[o:o + p.n].copy_(p.prim_hits)
+                        o += p.n
+                    g.copied.record(g.comm)
+                    dist.gather(g.hits_buf, g.gather_list, dst=0)
+            for p in ps:
+                p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+            if g is not None:
+                for p in ps:
+                    # the next step's primary trace rewrites the records copied out above: it waits for the
+                    # copy, not for the gather (which reads hits_buf; the next copy is ordered after it on comm)
+                    p.stream.wait_event(g.copied)
+        return step_fn
+
+    def timed(ps, step_fn):
+        """W untimed steps, then exactly K steps between barrier + synchronize pairs: this rank's seconds."""
+        for _ in range(args.warmup):
+            step_fn()
+        torch.cuda.synchronize(dev)
+        for p in ps:
+            p.eng.timing_reset()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0_ = time.perf_counter()
+        for _ in range(args.steps):
+            step_fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0_
+
+    if spp:  # this rank's (sample, tile) units of the N-sample frame (ttdist.spp_part_pixels)
+        plan = ttdist.spp_part_pixels(W, H, world, rank, P)
+    elif split:  # this rank's pixels of the one frame, compacted in tile order, split into P parts
+        plan = [[(frames, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)]
+    else:  # the whole frame, one launch per bounce in the kernel's own tile order
+        plan = [[(frames, np.arange(WH, dtype=np.int64))]]
+    parts = build_parts(plan)
     n_prim, nb = sum(p.n for p in parts), sum(p.nb for p in parts)
     rays_per_step = n_prim + nb
     s_prim, s_bnc = parts[0].s_prim, parts[0].s_bnc
@@ -769,63 +856,14 @@ def main():
         f"tris/ray {s_prim.tri_tests / max(parts[0].n, 1):.2f} "
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(parts[0].nb, 1):.2f} "
         f"tris/ray {s_bnc.tri_tests / max(parts[0].nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}"
-        f"; parts {P}")
+        f"; parts {P}" + (f"; {world}-sample frame (spp)" if spp else ""))
 
-    # tiles: the frame's primary hit records go to rank 0 in one gather per step (shards padded to
-    # the largest so every rank sends one equal-size message; a rank's parts back to back). The
-    # gather runs on its own stream, overlapped with the bounce-1 traces (which read and write only
-    # the other half of the ping-pong buffers); the step ends when both are done, so the timed step
-    # includes the collective.
-    sizes, hits_buf, gather_list, comm = None, None, None, None
-    if tiles:
-        n_t = torch.tensor([p.n for p in parts], dtype=torch.int64, device=red_dev)
-        sz = [torch.zeros_like(n_t) for _ in range(world)]
-        dist.all_gather(sz, n_t)
-        sizes = [[int(v) for v in x.tolist()] for x in sz]
-        hits_buf = torch.zeros((max(sum(x) for x in sizes), 4), dtype=torch.int32, device=red_dev)
-        gather_list = [torch.empty_like(hits_buf) for _ in range(world)] if rank == 0 else None
-        comm = torch.cuda.Stream(dev)
-        copied = torch.cuda.Event()
+    G = make_gather(parts) if tiles else None
+    sizes, gather_list = (G.sizes, G.gather_list) if G is not None else (None, None)
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
-
-    def step():
-        for p in parts:
-            p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True)
-        if tiles:
-            for p in parts:
-                comm.wait_stream(p.stream)  # the primary hit records are final
-            with torch.cuda.stream(comm):
-                o = 0
-                for p in parts:
-                    hits_buf[o:o + p.n].copy_(p.prim_hits)
-                    o += p.n
-                copied.record(comm)
-                dist.gather(hits_buf, gather_list, dst=0)
-        for p in parts:
-            p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
-        if tiles:
-            for p in parts:
-                # the next step's primary trace rewrites the records copied out above: it waits for the
-                # copy, not for the gather (which reads hits_buf; the next copy is ordered after it on comm)
-                p.stream.wait_event(copied)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    for p in parts:
-        p.eng.timing_reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t_start
+    step = make_step(parts, G)
+    elapsed = timed(parts, step)
     launch_ms = ring_tail(eng, 2, args.steps).reshape(-1)  # part 0's launches, the last <= 128 steps
     for p in parts[1:]:
         ring_tail(p.eng, 2, args.steps)
@@ -868,25 +906,61 @@ def main():
                   "note": "untimed-for-value: the same step repeated after the timed region"}
         log(f"steady state: {steady}")
 
-    # SURVEY 8(e) parity -- the gathered (N > 1) or the parts' (N = 1) frame must equal one launch
-    # tracing the whole frame
+    # SURVEY 8(e) parity -- the gathered (N > 1) or the parts' (N = 1) frame(s) must equal one launch
+    # tracing each whole frame
+    def one_gpu_frame(k):
+        one = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=k, max_bounce=1, device=True)
+        eng.trace(one, WH, 0, far, W, H, device=True)
+        return one.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+
     gather_parity = None
     if split and rank == 0:
-        if tiles:
-            frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
+        if spp:
+            fr = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gather_list, sizes)], W, H, world, P)
+            gather_parity = all(bool(np.array_equal(fr[k], one_gpu_frame(k))) for k in range(world))
+            frame = fr[0]
         else:
-            own = torch.cat([p.prim_hits for p in parts]).cpu()
-            frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
-        one = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
-        eng.trace(one, WH, 0, far, W, H, device=True)
-        ref = one.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
-        gather_parity = bool(np.array_equal(frame, ref))
-        del one
-        log(f"gathered frame: {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels, "
-            f"identical to a single-GPU trace: {gather_parity}")
-    for p in parts[1:]:
-        p.eng.close()
+            if tiles:
+                frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
+            else:
+                own = torch.cat([p.prim_hits for p in parts]).cpu()
+                frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
+            gather_parity = bool(np.array_equal(frame, one_gpu_frame(frames)))
+        log(f"gathered frame(s): {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels in sample 0, "
+            f"{world if spp else 1} sample(s) identical to single-GPU traces: {gather_parity}")
+
+    # N > 1 with the spp headline: the strong-scaling layout beside it -- ONE 1-sample frame's tiles dealt
+    # round-robin (P parts per rank), the same per-step gather; frame time = the slowest rank's
+    strong = None
+    if spp and world > 1:
+        ps_s = build_parts([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)], fresh=True)
+        g_s = make_gather(ps_s)
+        el_s = timed(ps_s, make_step(ps_s, g_s))
+        for p in ps_s:
+            ring_tail(p.eng, 2, args.steps)
+        st_ = torch.tensor([el_s, float(sum(p.n + p.nb for p in ps_s) * args.steps)], dtype=torch.float64,
+                           device=red_dev)
+        tmax = st_[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        rsum = st_[1:].clone()
+        dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
+        par = None
+        if rank == 0:
+            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(g_s.gather_list, g_s.sizes)], g_s.sizes, W, H,
+                                        world, P)
+            par = bool(np.array_equal(fr1, one_gpu_frame(0)))
+        strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
+                  "scaling": "strong", "ranks": world, "parts_per_rank": P,
+                  "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4),
+                  "rays_per_step_all_ranks": int(round(float(rsum.item()) / args.steps)),
+                  "gather_identical_to_1gpu": par,
+                  "layout": "one 1080p frame (1 sample): 64x64 tiles round-robin over the ranks + one RCCL gather "
+                            "of its primary hit records per step"}
+        del ps_s, g_s
+        log(f"strong-scaling tile layout: {strong}")
+    for e_, _ in lanes[1:]:
+        e_.close()
 
     # the kernel alone, one launch at a time (N = 1, P > 1): the full frame in the kernel's own tile
     # order on the shared stream, per-launch HIP events -- the per-launch roofline and the launch
@@ -1089,7 +1163,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak" if (world > 1 and not tiles) else "strong",
+        "scaling": "weak" if (world > 1 and (spp or not tiles)) else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza); primary rays from the reference's "
@@ -1101,7 +1175,11 @@ def main():
                    "seed": hex(args.seed),
                    "parallelism": ((f"single GPU, full frame as {P} tile-interleaved parts on {P} streams"
                                     if P > 1 else "single GPU, full frame") if world == 1 else
-                                   (f"64x64 screen tiles round-robin over {world} ranks, each rank's tiles as {P} "
+                                   ((f"{world}-sample 1080p frame (sample k = Generate with frames_accumulated = k), "
+                                     f"its (sample, 64x64 tile) units round-robin over {world} ranks (one frame's "
+                                     f"worth each: weak scaling), " if spp else
+                                     f"one 1080p frame's 64x64 screen tiles round-robin over {world} ranks, ")
+                                    + f"each rank's tiles as {P} "
                                     f"tile-interleaved parts on {P} streams, + one RCCL gather of the "
                                     f"primary hit records to rank 0 per step (inside the timed step"
                                     + (", overlapped with the bounce-1 trace on a second stream)" if gather_overlapped
@@ -1109,7 +1187,7 @@ def main():
                                     else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
                    "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it"
                              + (f" (part 0 of {P}: its launches overlap the other parts')" if P > 1 else ""),
-                   "parts_per_rank": P,
+                   "parts_per_rank": P, "samples_per_frame": world if spp else 1,
                    "dist_world_size": dist_world, "dist_backend": backend if dist_world else None,
                    "launcher": ("bench.py self-launch" if os.environ.get("TT_BENCH_SELF_LAUNCHED") == "1"
                                 else "external (WORLD_SIZE set)" if env_world is not None else "none (1 rank)"),
@@ -1121,6 +1199,7 @@ def main():
                    "kernel_mrays_s_trace_only": round((parts[0].n + parts[0].nb) / trace_ms_rank / 1e3, 2),
                    "gather_identical_to_1gpu": gather_parity,
                    "steady_state": steady,
+                   "aux_strong_tiles": strong,
                    "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},

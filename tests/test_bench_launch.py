@@ -80,15 +80,20 @@ def _port():
 @pytest.mark.gpu
 def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
     """The full bench through the self-launch path: 2 ranks on the one GPU (gloo collectives),
-    the metric's tile layout with one gather per step; rank 0's JSON line reports 2 GPUs and a
-    gathered frame identical to one GPU tracing the whole frame."""
+    the metric's spp layout (a 2-sample frame's tiles over the ranks, weak scaling) with one gather per
+    step; rank 0's JSON line reports 2 GPUs and gathered samples identical to one GPU tracing each
+    whole frame, and the strong-scaling tile layout beside it (one frame, same gather) identical too."""
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
                         "--no-shadow", "--no-c5-tiles", "--steady-steps", "0"],
-                       env=_env(TT_BENCH_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=110)
+                       env=_env(TT_BENCH_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=115)
     assert r.returncode == 0, r.stderr[-3000:]
     (d,) = _json_lines(r.stdout)
     assert d["n_gpus"] == 2
     c = d["config"]
     assert c["dist_world_size"] == 2 and c["launcher"] == "bench.py self-launch"
     assert c["gather_identical_to_1gpu"] is True
-    assert c["rays_per_step_all_ranks"] > 4_000_000
+    assert d["scaling"] == "weak" and c["samples_per_frame"] == 2
+    assert c["rays_per_step_all_ranks"] > 8_000_000  # two 1080p samples, primary + bounce 1
+    st = c["aux_strong_tiles"]
+    assert st["scaling"] == "strong" and st["gather_identical_to_1gpu"] is True
+    assert 4_000_000 < st["rays_per_step_all_ranks"] < 4_200_000

@@ -93,3 +93,92 @@ def test_part_split_partitions_each_rank_and_reassembles():
             sizes.append([len(p) for p in ps])
         got = ttdist.assemble_parts(blocks, sizes, W, H, world, parts)
         assert np.array_equal(got, frame)
+
+
+def test_spp_units_partition_every_sample_and_balance_ranks():
+    """bench.py default at N > 1 (weak scaling): an N-sample frame's (sample, tile) units dealt round-robin
+    cover every (sample, pixel) exactly once and give every rank one frame's worth of tiles."""
+    W, H = 1920, 1080
+    T = ttdist.n_tiles(W, H)
+    for world, parts in ((1, 2), (2, 2), (3, 2), (4, 3), (8, 3)):
+        seen = np.zeros((world, W * H), np.int32)
+        for r in range(world):
+            units = ttdist.spp_part_pixels(W, H, world, r, parts)
+            assert len(units) == parts
+            n_pix = 0
+            for lst in units:
+                for k, pix in lst:
+                    seen[k, pix] += 1
+                    n_pix += len(pix)
+            # T units per rank: the frame's pixel count up to the partial edge tiles
+            assert abs(n_pix - W * H) <= 64 * 64 * world, (world, r, n_pix)
+        assert (seen == 1).all()
+    # N = 1 is exactly the single-GPU parts layout
+    a = [pix for lst in ttdist.spp_part_pixels(W, H, 1, 0, 2) for _, pix in lst]
+    b = ttdist.part_pixels(W, H, 1, 0, 2)
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    assert T == 30 * 17
+
+
+def test_spp_assemble_reorders_gathered_blocks():
+    W, H = 200, 130
+    for world, parts in ((2, 2), (3, 1), (4, 3)):
+        frames = np.zeros((world, W * H, 4), np.uint32)
+        frames[:, :, 0] = np.arange(W * H, dtype=np.uint32)[None, :]
+        frames[:, :, 1] = np.arange(world, dtype=np.uint32)[:, None]
+        blocks = []
+        for r in range(world):
+            blocks.append(np.concatenate([frames[k, pix] for lst in ttdist.spp_part_pixels(W, H, world, r, parts)
+                                          for k, pix in lst]))
+        assert np.array_equal(ttdist.assemble_spp(blocks, W, H, world, parts), frames)
+
+
+def _spp_worker(rank, world, port, q):
+    sys.path.insert(0, HERE)
+    import torch
+    import torch.distributed as dist
+
+    import oracle_ctypes as O
+    import tthip
+    import ttdist as td
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    W, H, P = 96, 70, 2
+    sc = tthip.single_object_scene(tthip.Mesh.soup(78, 3000, 1.0, 0.08))
+    c2w, ip = tthip.unity_camera((0.2, 0.1, 3.0), (0, 0, -1), (0, 1, 0), 55, W, H, 0.3, 1000.0)
+    samples = [O.generate(c2w, ip, W, H, 0.3, 1000.0, jitter=1, frames=k) for k in range(world)]
+    block = []
+    for lst in td.spp_part_pixels(W, H, world, rank, P, tile=16):
+        for k, pix in lst:
+            mine = np.zeros(2 * max(len(pix), 1), samples[0].dtype)
+            mine[: len(pix)] = samples[k][pix]
+            st, _ = O.trace(sc, mine, len(pix), 0, 1000.0, len(pix), 1)
+            assert st == 0
+            block.append(mine["hits"][: len(pix)])
+    hits = torch.from_numpy(np.concatenate(block).astype(np.int64).astype(np.int32))
+    got = td.gather_hits(hits, world, rank)
+    if rank == 0:
+        frames = td.assemble_spp(got, W, H, world, P, tile=16)
+        ok = True
+        for k in range(world):
+            ref = samples[k].copy()
+            st, _ = O.trace(sc, ref, W * H, 0, 1000.0, W, H)
+            ok = ok and bool(np.array_equal(frames[k], ref["hits"][: W * H]))
+        q.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_spp_shard_and_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True

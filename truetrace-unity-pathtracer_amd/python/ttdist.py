@@ -5,8 +5,13 @@ The reference is single-GPU. On an 8×MI355X node the scene is replicated per GP
 gather of the 16-byte hit records to rank 0 (RCCL via torch.distributed "nccl", or "gloo" on
 CPU in the tests).
 
-Two shardings:
-  * ``tiles`` (strong scaling, SURVEY.md §8(e), bench.py default): the screen is cut into
+Three shardings:
+  * ``spp`` (weak scaling, bench.py default at N > 1): the job at N ranks is an N-sample 1080p frame
+    (sample k = the reference's Generate with frames_accumulated = k); its (sample, 64x64 tile) units
+    are dealt round-robin to the ranks (``spp_part_pixels``), so every rank traces one frame's worth of
+    screen tiles -- the north star's tile sharding at fixed per-GPU work -- and the primary hit records
+    of all N samples are gathered to rank 0 (``assemble_spp``).
+  * ``tiles`` (strong scaling, SURVEY.md §8(e), ``bench.py --shard tiles``): the screen is cut into
     ``tile``×``tile`` pixel tiles dealt round-robin to ranks (balances sky-heavy and geometry-heavy
     regions); each rank builds a compact ray list of its pixels (optionally split into
     tile-interleaved parts, ``part_pixels``) and the hit records are gathered and scattered back
@@ -93,3 +98,38 @@ def assemble_parts(gathered, part_sizes, width: int, height: int, world: int, pa
             virt[s * world + r] = arr[o:o + n]
             o += n
     return assemble_tiles(virt, width, height, world * parts, tile)
+
+
+def n_tiles(width: int, height: int, tile: int = 64) -> int:
+    return ((width + tile - 1) // tile) * ((height + tile - 1) // tile)
+
+
+def spp_part_pixels(width: int, height: int, world: int, rank: int, parts: int, tile: int = 64):
+    """``rank``'s share of an ``world``-sample frame, as ``parts`` lists of (sample k, pixel indices).
+
+    Unit u = k * T + t (sample k, tile t of T) goes to rank u % world, so rank r holds, for sample k,
+    the tiles t = (r - k * T) mod world (mod world) -- exactly tile_pixels of virtual rank
+    (r - k * T) % world -- and every rank holds T units, one frame's worth. Each sample's tiles are
+    then split into ``parts`` tile-interleaved parts (part_pixels); part s concatenates them over k."""
+    T = n_tiles(width, height, tile)
+    out = [[] for _ in range(parts)]
+    for k in range(world):
+        v = (rank - k * T) % world
+        for s, pix in enumerate(part_pixels(width, height, world, v, parts, tile)):
+            out[s].append((k, pix))
+    return out
+
+
+def assemble_spp(gathered, width: int, height: int, world: int, parts: int, tile: int = 64) -> np.ndarray:
+    """(world, W*H, 4) per-sample screen-order hit records from one gathered block per rank, each
+    holding its parts' records back to back in spp_part_pixels order."""
+    out = np.zeros((world, width * height, 4), np.uint32)
+    for r in range(world):
+        arr = gathered[r].cpu().numpy() if hasattr(gathered[r], "cpu") else np.asarray(gathered[r])
+        arr = arr.view(np.uint32).reshape(-1, 4)
+        o = 0
+        for lst in spp_part_pixels(width, height, world, r, parts, tile):
+            for k, pix in lst:
+                out[k, pix] = arr[o:o + len(pix)]
+                o += len(pix)
+    return out
