@@ -109,6 +109,12 @@ namespace TrueTrace.Hip
         [DllImport(Lib, EntryPoint = "tt_trace_shadow_ex")] public static extern TTStatus tt_trace_shadow_dev(IntPtr ctx,
             ref TTShadowParams p, IntPtr shadowRays, IntPtr visibility, IntPtr globalColors, IntPtr neePos,
             IntPtr cacheBuffer, out TTStats stats);
+        // Indirect dispatch (BufferSizes[CurBounce].tracerays / .shadow_rays kept on the GPU, the reference's
+        // TransferKernel + DispatchIndirect): traces min(*nRaysDev, p.nRays) rays; device pointers, async.
+        [DllImport(Lib)] public static extern TTStatus tt_trace_closest_indirect(IntPtr ctx, ref TTTraceParams p,
+            IntPtr nRaysDev, IntPtr globalRays, IntPtr primaryInfo, IntPtr globalColors);
+        [DllImport(Lib)] public static extern TTStatus tt_trace_shadow_ex_indirect(IntPtr ctx, ref TTShadowParams p,
+            IntPtr nRaysDev, IntPtr shadowRays, IntPtr visibility, IntPtr globalColors, IntPtr neePos, IntPtr cacheBuffer);
         [DllImport(Lib)] public static extern TTStatus tt_async_overflows(IntPtr ctx, out ulong count);
         [DllImport(Lib)] public static extern IntPtr tt_ctx_stream(IntPtr ctx);
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
@@ -197,6 +203,21 @@ namespace TrueTrace.Hip
             };
             Check(Native.tt_trace_closest_dev(m_ctx, ref p, globalRays, primaryInfo, globalColors, out TTStats s));
             return s;
+        }
+
+        /// kernel_trace as DispatchIndirect: the ray count is the uint at `nRaysDevice` (HIP device memory,
+        /// written by an earlier operation on the context stream, e.g. the shading pass's BufferSizes),
+        /// clamped to `capacity`; the call never waits for the GPU.
+        public void TraceDeviceIndirect(IntPtr globalRays, IntPtr nRaysDevice, uint capacity, int curBounce, float farPlane,
+                                        int width, int height, IntPtr primaryInfo = default, IntPtr globalColors = default,
+                                        TTTraceFlags extra = TTTraceFlags.None)
+        {
+            var p = new TTTraceParams
+            {
+                nRays = capacity, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width, screenHeight = (uint)height,
+                flags = extra | TTTraceFlags.DevicePtrs
+            };
+            Check(Native.tt_trace_closest_indirect(m_ctx, ref p, nRaysDevice, globalRays, primaryInfo, globalColors));
         }
 
         /// tt_trace_shadow (the original signature and contract): visibility, t write-back,

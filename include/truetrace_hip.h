@@ -396,6 +396,17 @@ typedef struct tt_stats {
 tt_status tt_trace_closest(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
                            uint32_t* primary_info, const tt_col_data* global_colors,
                            tt_stats* stats);
+/* kernel_trace dispatched indirectly (the reference keeps BufferSizes[CurBounce].tracerays on the
+ * GPU; TransferKernel turns it into DispatchIndirect arguments, RayTracingShader.compute:736-747,
+ * RayTracingMaster.cs:964-970): the launch traces min(*n_rays_dev, p->n_rays) rays, the count read
+ * on the device when the kernel starts, so a bounce chain (trace -> enqueue -> trace ...) runs on the
+ * context stream with no host round trip. p->n_rays is the capacity (e.g. W*H); n_rays_dev is a
+ * device uint32 written by an earlier operation on the stream (tt_enqueue_diffuse_bounce_indirect,
+ * or the caller's own kernel / copy). Requires TT_TRACE_DEVICE_PTRS, implies TT_TRACE_ASYNC, and
+ * rejects TT_TRACE_STATS. Results are identical to tt_trace_closest with the same count. */
+tt_status tt_trace_closest_indirect(tt_ctx* ctx, const tt_trace_params* p, const uint32_t* n_rays_dev,
+                                    tt_ray_data* global_rays, uint32_t* primary_info,
+                                    const tt_col_data* global_colors);
 /* Per-call GPU durations (HIP events on the context stream, in issue order) since the last
  * tt_timing_reset (ring of 256 entries). One entry per call of tt_trace_closest and
  * tt_trace_shadow (the trace kernel alone), tt_generate_primary (the generate kernel),
@@ -497,6 +508,12 @@ tt_status tt_trace_shadow(tt_ctx* ctx, const tt_shadow_params* p, tt_shadow_ray*
 tt_status tt_trace_shadow_ex(tt_ctx* ctx, const tt_shadow_params* p, tt_shadow_ray* shadow_rays, float* visibility,
                              tt_col_data* global_colors, float* nee_pos, tt_cache_data* cache_buffer,
                              tt_stats* stats);
+/* tt_trace_shadow_ex dispatched indirectly (BufferSizes[CurBounce].shadow_rays on the GPU,
+ * TransferKernel Type 1): traces min(*n_rays_dev, p->n_rays) shadow rays; as
+ * tt_trace_closest_indirect (device pointers, asynchronous, no stats). */
+tt_status tt_trace_shadow_ex_indirect(tt_ctx* ctx, const tt_shadow_params* p, const uint32_t* n_rays_dev,
+                                      tt_shadow_ray* shadow_rays, float* visibility, tt_col_data* global_colors,
+                                      float* nee_pos, tt_cache_data* cache_buffer);
 
 /* ------------------------------------------------- attribute resolve */
 /* Parity aid for "normals within 1e-5": per hit, the interpolated shading normal
@@ -536,6 +553,13 @@ tt_status tt_generate_primary(tt_ctx* ctx, const tt_camera* cam, tt_ray_data* gl
  * count. */
 tt_status tt_enqueue_diffuse_bounce(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
                                     int32_t frames_accumulated, int32_t max_bounce, uint32_t* n_next);
+/* The same enqueue with device-resident counts: reads the traced count from n_rays_dev (nullable:
+ * p->n_rays; otherwise p->n_rays is the capacity) and writes the survivor count to the device uint32
+ * n_next_dev (BufferSizes[CurBounce + 1].tracerays) instead of returning it: no synchronization, so
+ * it chains with tt_trace_closest_indirect. Requires TT_TRACE_DEVICE_PTRS. */
+tt_status tt_enqueue_diffuse_bounce_indirect(tt_ctx* ctx, const tt_trace_params* p, const uint32_t* n_rays_dev,
+                                             tt_ray_data* global_rays, int32_t frames_accumulated,
+                                             int32_t max_bounce, uint32_t* n_next_dev);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -1054,3 +1054,118 @@ def test_async_chain_stack_overflow_is_reported(engine):
         engine.trace(buf, 1, 0, FAR, 1, 1, device=True, asynchronous=True)
     assert engine.async_overflows() == 3
     assert engine.async_overflows() == 0  # reset by the read
+
+
+# ------------------------------------------------------------------ indirect dispatch (§8 f2, TransferKernel)
+def test_indirect_bounce_chain_matches_host_counts(engine):
+    """Primary + 3 bounces with device-resident counts (the reference's BufferSizes[].tracerays +
+    TransferKernel + DispatchIndirect): trace_indirect -> enqueue_bounce_indirect -> ... issued back to
+    back on the context stream with no host round trip, bit-identical to the host-count chain
+    (rays, hit records, _PrimaryTriangleInfo, every bounce's survivor count); the full-frame tile order
+    at bounce 0 is chosen on the device (count == W*H)."""
+    import torch
+
+    sc = tthip.single_object_scene(tthip.Mesh.soup(31, 25000, 1.0, 0.1))
+    W, H = 256, 160
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 2.4), (-0.1, -0.05, -1.0), (0, 1, 0), 60.0, W, H, 0.05, FAR)
+    engine.upload(sc)
+    dev = torch.device("cuda:0")
+    WH = W * H
+    base = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+    engine.generate(base, c2w, ip, W, H, 0.05, FAR, jitter=1, frames=3, max_bounce=4, device=True)
+    colors = np.zeros(WH, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = 2.0  # _PrimaryTriangleInfo written at bounce 2
+    col_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+    # host-count reference chain
+    ref = base.clone()
+    info_ref = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+    counts = [WH]
+    for b in range(3):
+        engine.trace(ref, counts[-1], b, FAR, W, H, info=info_ref, colors=col_t if b else None, device=True)
+        counts.append(engine.enqueue_bounce(ref, counts[-1], b, FAR, W, H, frames=3, max_bounce=4, device=True))
+    engine.trace(ref, counts[-1], 3, FAR, W, H, device=True)
+    # device-count chain: nothing read back until the end
+    got = base.clone()
+    info_got = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+    n_dev = torch.zeros(5, dtype=torch.int32, device=dev)
+    n_dev[0] = WH
+    torch.cuda.synchronize()
+    for b in range(3):
+        engine.trace_indirect(got, n_dev[b:], WH, b, FAR, W, H, info=info_got, colors=col_t if b else None)
+        engine.enqueue_bounce_indirect(got, n_dev[b:], WH, n_dev[b + 1:], b, FAR, W, H, frames=3, max_bounce=4)
+    engine.trace_indirect(got, n_dev[3:], WH, 3, FAR, W, H)
+    torch.cuda.synchronize()
+    assert n_dev[:4].tolist() == counts
+    assert counts[1] > WH // 3 and counts[3] > 0
+    assert torch.equal(got, ref)
+    assert torch.equal(info_got, info_ref)
+
+
+def test_indirect_counts_clamp_zero_and_refusals(engine):
+    import torch
+
+    sc = tthip.single_object_scene(tthip.Mesh.soup(32, 8000, 1.0, 0.1))
+    W, H = 120, 90
+    c2w, ip = tthip.unity_camera((0.2, 0.1, 2.8), (0, 0, -1), (0, 1, 0), 55.0, W, H, 0.05, FAR)
+    engine.upload(sc)
+    dev = torch.device("cuda:0")
+    WH = W * H
+    base = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+    engine.generate(base, c2w, ip, W, H, 0.05, FAR, jitter=1, frames=0, max_bounce=2, device=True)
+    for count, capacity in ((0, WH), (777, WH), (WH + 1000, 5000), (4097, 4097)):
+        ref = base.clone()
+        engine.trace(ref, min(count, capacity), 0, FAR, W, H, device=True)
+        got = base.clone()
+        n = torch.tensor([count], dtype=torch.int32, device=dev)
+        engine.trace_indirect(got, n, capacity, 0, FAR, W, H)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (count, capacity)
+        # enqueue: traced count from the device (clamped), survivors to the device
+        ref_n = engine.enqueue_bounce(ref, min(count, capacity), 0, FAR, W, H, frames=0, max_bounce=2, device=True)
+        nn = torch.zeros(1, dtype=torch.int32, device=dev)
+        engine.enqueue_bounce_indirect(got, n, capacity, nn, 0, FAR, W, H, frames=0, max_bounce=2)
+        torch.cuda.synchronize()
+        assert int(nn.item()) == ref_n and torch.equal(got, ref), (count, capacity)
+    # host pointers, host count buffers and stats are refused
+    host_rays = np.zeros(2 * WH, tthip.RAY_DTYPE)
+    n = torch.tensor([10], dtype=torch.int32, device=dev)
+    p = tthip.TraceParams(n_rays=WH, bounce=0, far_plane=FAR, screen_width=W, screen_height=H, flags=0)
+    assert engine.L.tt_trace_closest_indirect(engine.h, tthip.C.byref(p), n.data_ptr(), host_rays.ctypes.data,
+                                              None, None) == tthip.TT_ERR_INVALID_ARG
+    hn = np.array([10], np.uint32)
+    assert engine.trace_indirect(base, hn, WH, 0, FAR, W, H, check=False) == tthip.TT_ERR_INVALID_ARG
+    assert engine.trace_indirect(base, n, WH, 0, FAR, W, H, flags=tthip.TT_TRACE_STATS,
+                                 check=False) == tthip.TT_ERR_INVALID_ARG
+    assert engine.trace_indirect(base, None, WH, 0, FAR, W, H, check=False) == tthip.TT_ERR_INVALID_ARG
+
+
+def test_indirect_shadow_matches_host_count(engine):
+    import torch
+
+    seed = 33
+    sc = tthip.single_object_scene(tthip.Mesh.soup(seed, 12000, 1.0, 0.1))
+    W, H = 140, 100
+    pos = np.array([1.5, 1.0, 2.0])
+    c2w, ip = tthip.unity_camera(pos, -pos, (0, 1, 0), 60.0, W, H, 0.05, FAR)
+    rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    engine.upload(sc)
+    engine.trace(rays, W * H, 0, FAR, W, H)
+    sr = hb.nee_rays_from_hits(rays, W * H, pos * 1.2, seed)
+    ns = len(sr)
+    assert ns > 100
+    dev = torch.device("cuda:0")
+    colors = np.zeros(W * H, tthip.COL_DTYPE)
+    for count in (ns, ns // 3, 0):
+        outs = []
+        for indirect in (False, True):
+            rt = torch.from_numpy(sr.view(np.uint8).copy()).to(dev)
+            vt = torch.zeros((ns, 4), dtype=torch.float32, device=dev)
+            ct = torch.from_numpy(colors.view(np.uint8).copy()).to(dev)
+            if indirect:
+                engine.trace_shadow_indirect(rt, torch.tensor([count], dtype=torch.int32, device=dev), ns, 0, W, H,
+                                             visibility=vt, colors=ct)
+            elif count:
+                engine.trace_shadow(rt, count, 0, W, H, visibility=vt, colors=ct, device=True)
+            torch.cuda.synchronize()
+            outs.append((rt.cpu(), vt.cpu(), ct.cpu()))
+        assert all(torch.equal(a, b) for a, b in zip(*outs)), count

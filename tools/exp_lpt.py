@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Experiment: how much of a launch is load-balance tail? Traces the C2 primary (and bounce-1) rays
+"""Experiment: how much of a launch is load-balance tail? Traces the C2 (--config c4: C4) primary (and bounce-1) rays
 in three chunk orders -- the natural tile order, longest-chunk-first (LPT, per-ray step counts from
 the oracle) and shortest-first -- as compacted batches (n_rays = W*H - 1 disables the tile swizzle, so
 chunk c = records [64c, 64c+64)). Results are order-independent (each ray's traversal is its own);
@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 def main():
     ranks = int(sys.argv[sys.argv.index("--ranks") + 1]) if "--ranks" in sys.argv else 1
+    cfg = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
     import torch
     import tthip
     import ttconfigs as T
@@ -28,11 +29,11 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     eng = tthip.Engine(0, stream=stream.cuda_stream)
-    sc = T.c2_sponza()
+    sc, view = (T.c2_sponza(), T.C2_VIEW) if cfg == "c2" else (T.c4_bistro(), T.C4_VIEW)
     eng.upload(sc)
-    W, H = 1920, 1080
+    W, H = view.width, view.height
     WH = W * H
-    c2w, ip = T.C2_VIEW.camera()
+    c2w, ip = view.camera()
     r = O.generate(c2w, ip, W, H, T.NEAR, T.FAR, jitter=1, frames=0, max_bounce=1)
     # tile order (8x8 tiles row-major), or rank 0's 64x64 tiles of an N-rank frame
     if ranks > 1:
@@ -42,9 +43,9 @@ def main():
     base = np.zeros(2 * WH, tthip.RAY_DTYPE)
     n0 = len(pix)
     base[:n0] = r[pix]
-    st, cnt = O.trace(sc, base.copy(), n0, 0, T.FAR, W, H, counts=True, nthreads=os.cpu_count() or 8)
+    st, cnt = O.trace(sc, base.copy(), n0, 0, T.FAR, W, H, counts=True, nthreads=16)
     steps0 = cnt["node_visits"].astype(np.int64) + cnt["tri_tests"].astype(np.int64)
-    out = {"tool": "tools/exp_lpt.py", "ranks": ranks, "launches": {}}
+    out = {"tool": "tools/exp_lpt.py", "config": cfg, "ranks": ranks, "launches": {}}
 
     def run(name, recs, n, bounce, steps):
         nch = (n + 63) // 64
@@ -77,10 +78,10 @@ def main():
     run("primary", base[:n0], n0, 0, steps0)
     # bounce-1 rays from the oracle's own enqueue of the traced primaries
     traced = base.copy()
-    O.trace(sc, traced, n0, 0, T.FAR, W, H, nthreads=os.cpu_count() or 8)
+    O.trace(sc, traced, n0, 0, T.FAR, W, H, nthreads=16)
     nb = O.enqueue_bounce(sc, traced, n0, 0, T.FAR, W, H)
     brec = traced[WH: WH + nb].copy()
-    st, cb = O.trace(sc, traced, nb, 1, T.FAR, W, H, counts=True, nthreads=os.cpu_count() or 8)
+    st, cb = O.trace(sc, traced, nb, 1, T.FAR, W, H, counts=True, nthreads=16)
     steps1 = cb["node_visits"].astype(np.int64) + cb["tri_tests"].astype(np.int64)
     run("bounce1", brec, nb, 1, steps1)
     print(json.dumps(out, indent=1))

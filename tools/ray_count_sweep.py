@@ -9,7 +9,7 @@ launches each rank of an N-GPU run would issue (rank 0's tiles = the largest sha
     t_frame(N) = t_primary(shard_N) + t_bounce(shard_N) [+ gather, reported separately]
     eff(N)     = t_frame(1) / (N * t_frame(N))
 
-C2 (Sponza-shaped 1080p, primary + bounce 1, the reference's default jittered Generate) and C5 (San-Miguel-shaped 4K primary). Every time is
+C2 (Sponza-shaped 1080p, primary + bounce 1, the reference's default jittered Generate), C4 (Bistro-shaped two-level 1080p, primary + bounce 1; --configs c4) and C5 (San-Miguel-shaped 4K primary). Every time is
 a HIP-event launch time on the shared torch/engine stream (tt_timing_read), median of --steps.
 Output: one JSON document on stdout (commit under profiles/).
 """
@@ -87,6 +87,11 @@ def main():
     which = set(args.configs.split(","))
     if "c2" in which:
         sweep("c2_sponza_1080p_primary_plus_bounce1", T.c2_sponza(), T.C2_VIEW, 1920, 1080, True)
+    if "c4" in which:
+        t0 = time.time()
+        sc = T.c4_bistro()
+        print(f"[sweep] c4 build {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+        sweep("c4_bistro_1080p_primary_plus_bounce1", sc, T.C4_VIEW, T.C4_VIEW.width, T.C4_VIEW.height, True)
     if "c5" in which:
         t0 = time.time()
         sc = T.c5_san_miguel()

@@ -29,7 +29,8 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
                               int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays, hipStream_t st);
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
-                            const tt_mesh_data* md, uint32_t* counter, hipStream_t st);
+                            const tt_mesh_data* md, uint32_t* counter, hipStream_t st, const uint32_t* n_dev,
+                            uint32_t* n_next_dev);
 uint32_t tt_bounce_tiles(uint32_t n);
 hipError_t tt_launch_resolve(const tt_ray_data* rays, uint32_t ray_offset, uint32_t n, float far_plane,
                              const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* md, uint32_t n_mesh,
@@ -1099,8 +1100,12 @@ void tt_ctx_set_error(tt_ctx* c, const char* msg) {                // tt_build.h
     if (c) c->err = msg ? msg : "";
 }
 
-tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
-                           const tt_col_data* colors, tt_stats* stats) {
+}  // extern "C"
+
+// n_dev (nullable): the device-resident ray count (tt_trace_closest_indirect); p->n_rays is then the
+// capacity the launch covers, and the call is asynchronous with device pointers.
+static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_dev, tt_ray_data* rays,
+                                    uint32_t* info, const tt_col_data* colors, tt_stats* stats) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or rays");
@@ -1119,9 +1124,14 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     const uint32_t off = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u;
     if ((uint64_t)off + p->n_rays > 0xffffffffull) return fail(c, TT_ERR_INVALID_ARG, "ray range overflows");
     const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
-    const bool async = dev && (p->flags & TT_TRACE_ASYNC);
+    const bool async = dev && ((p->flags & TT_TRACE_ASYNC) || n_dev);
     const bool want_stats = (p->flags & TT_TRACE_STATS) != 0;
     const int info_mode = info ? (p->bounce == 0 ? 1 : 2) : 0;
+    if (n_dev) {
+        if (!dev) return fail(c, TT_ERR_INVALID_ARG, "a device-resident ray count needs TT_TRACE_DEVICE_PTRS");
+        if (want_stats) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_STATS needs a host ray count");
+        if (!is_device_ptr(n_dev)) return fail(c, TT_ERR_INVALID_ARG, "the ray count pointer is not device memory");
+    }
     if (stats) std::memset(stats, 0, sizeof(*stats));
     if (p->n_rays == 0) return TT_OK;
     if (reinterpret_cast<uintptr_t>(rays) % 16 || (info && reinterpret_cast<uintptr_t>(info) % 16))
@@ -1170,13 +1180,16 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     a.sticky_overflow = c->sticky;
     a.spill = c->spill.p;
     a.n_rays = p->n_rays;
+    a.n_rays_dev = n_dev;
     a.ray_offset = off;
     a.width = p->screen_width;
     a.height = p->screen_height;
     a.far_plane = p->far_plane;
     a.bounce = p->bounce;
     a.flags = p->flags;
-    a.tile_swizzle = (p->n_rays == wh && p->screen_width % 8 == 0 && p->screen_height % 8 == 0) ? 1u : 0u;
+    // (the kernel also requires its actual count to be W*H: a device count decides at run time)
+    a.tile_swizzle = ((n_dev ? p->n_rays >= wh : p->n_rays == wh) && p->screen_width % 8 == 0 &&
+                      p->screen_height % 8 == 0) ? 1u : 0u;
     a.div_width = fastdiv_make(std::max(1u, p->screen_width));
     a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
     const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout ||
@@ -1239,12 +1252,26 @@ tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* ray
     return TT_OK;
 }
 
+extern "C" {
+
+tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
+                           const tt_col_data* colors, tt_stats* stats) {
+    return trace_closest_call(c, p, nullptr, rays, info, colors, stats);
+}
+
+tt_status tt_trace_closest_indirect(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_rays_dev, tt_ray_data* rays,
+                                    uint32_t* info, const tt_col_data* colors) {
+    if (!n_rays_dev) return c ? fail(c, TT_ERR_INVALID_ARG, "null device ray count") : TT_ERR_INVALID_ARG;
+    return trace_closest_call(c, p, n_rays_dev, rays, info, colors, nullptr);
+}
+
 }  // extern "C"
 
 // full = false: tt_trace_shadow's contract (Direct at bounce 0 + NEEPosA only, the caller does the
 // rest); full = true: tt_trace_shadow_ex's (plus CacheBuffer / Indirect / PrimaryNEERay)
 static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray* rays, float* visibility,
-                             tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats, bool full) {
+                             tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats, bool full,
+                             const uint32_t* n_dev = nullptr) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or shadow rays");
@@ -1260,8 +1287,13 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
     if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
     const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
-    const bool async = dev && (p->flags & TT_TRACE_ASYNC);
+    const bool async = dev && ((p->flags & TT_TRACE_ASYNC) || n_dev);
     const bool want_stats = (p->flags & TT_TRACE_STATS) != 0;
+    if (n_dev) {
+        if (!dev) return fail(c, TT_ERR_INVALID_ARG, "a device-resident ray count needs TT_TRACE_DEVICE_PTRS");
+        if (want_stats) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_STATS needs a host ray count");
+        if (!is_device_ptr(n_dev)) return fail(c, TT_ERR_INVALID_ARG, "the ray count pointer is not device memory");
+    }
     if (stats) std::memset(stats, 0, sizeof(*stats));
     if (p->n_rays == 0) return TT_OK;
     if (reinterpret_cast<uintptr_t>(rays) % 16 || (visibility && reinterpret_cast<uintptr_t>(visibility) % 16) ||
@@ -1328,6 +1360,7 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     a.sticky_overflow = c->sticky;
     a.spill = c->spill.p;
     a.n_rays = p->n_rays;
+    a.n_rays_dev = n_dev;
     a.width = p->screen_width;
     a.height = p->screen_height;
     a.bounce = p->bounce;
@@ -1392,6 +1425,13 @@ tt_status tt_trace_shadow_ex(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     return shadow_call(c, p, rays, visibility, colors, nee_pos, cache, stats, true);
 }
 
+tt_status tt_trace_shadow_ex_indirect(tt_ctx* c, const tt_shadow_params* p, const uint32_t* n_rays_dev,
+                                      tt_shadow_ray* rays, float* visibility, tt_col_data* colors, float* nee_pos,
+                                      tt_cache_data* cache) {
+    if (!n_rays_dev) return c ? fail(c, TT_ERR_INVALID_ARG, "null device ray count") : TT_ERR_INVALID_ARG;
+    return shadow_call(c, p, rays, visibility, colors, nee_pos, cache, nullptr, true, n_rays_dev);
+}
+
 tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_data* rays, float* normals6) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
@@ -1447,19 +1487,29 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
     return TT_OK;
 }
 
-tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, int32_t frames,
-                                    int32_t max_bounce, uint32_t* n_next) {
+}  // extern "C"
+
+// n_dev (nullable): device-resident count of the rays traced at p->bounce (p->n_rays = capacity);
+// n_next_dev (nullable): the survivor count is written there on the device and the call returns
+// without synchronizing (n_next may then be null).
+static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_dev, tt_ray_data* rays,
+                              int32_t frames, int32_t max_bounce, uint32_t* n_next, uint32_t* n_next_dev) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
-    if (!p || !rays || !n_next) return fail(c, TT_ERR_INVALID_ARG, "null argument");
+    if (!p || !rays || (!n_next && !n_next_dev)) return fail(c, TT_ERR_INVALID_ARG, "null argument");
     const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
     if (!wh || wh > 0x7fffffffull || p->n_rays > wh) return fail(c, TT_ERR_INVALID_ARG, "bad ray count / screen");
     const uint32_t src = (p->bounce % 2 == 1) ? (uint32_t)wh : 0u, dst = (p->bounce % 2 == 1) ? 0u : (uint32_t)wh;
+    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    if (n_dev || n_next_dev) {
+        if (!dev) return fail(c, TT_ERR_INVALID_ARG, "device-resident ray counts need TT_TRACE_DEVICE_PTRS");
+        if ((n_dev && !is_device_ptr(n_dev)) || (n_next_dev && !is_device_ptr(n_next_dev)))
+            return fail(c, TT_ERR_INVALID_ARG, "a ray count pointer is not device memory");
+    }
     TT_HIP(c, hipSetDevice(c->device));
     // [0] survivor count, [1] tile ticket, [2..3] pad, then one 64-bit look-back word per tile
     const size_t ctl_words = 4 + 2 * (size_t)tt_bounce_tiles(p->n_rays);
     if (c->counter.n < ctl_words) TT_HIP(c, c->counter.alloc(ctl_words));
-    const bool dev = (p->flags & TT_TRACE_DEVICE_PTRS) != 0;
     tt_ray_data* d = rays;
     if (!dev) {
         if (c->st_rays.n < 2 * wh) {
@@ -1473,8 +1523,12 @@ tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 4 * ctl_words, c->stream));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
-                               c->mesh_raw.p, c->counter.p, c->stream));
+                               c->mesh_raw.p, c->counter.p, c->stream, n_dev, n_next_dev));
     TT_HIP(c, ring_close(c, slot));
+    if (n_next_dev) {  // BufferSizes[CurBounce + 1].tracerays stays on the GPU: no host round trip
+        if (n_next) *n_next = 0;
+        return TT_OK;
+    }
     uint32_t cnt = 0;
     TT_HIP(c, hipMemcpyAsync(&cnt, c->counter.p, 4, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
@@ -1483,6 +1537,21 @@ tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_
     }
     *n_next = cnt;
     return TT_OK;
+}
+
+extern "C" {
+
+tt_status tt_enqueue_diffuse_bounce(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, int32_t frames,
+                                    int32_t max_bounce, uint32_t* n_next) {
+    if (c && !n_next) return fail(c, TT_ERR_INVALID_ARG, "null argument");
+    return enqueue_call(c, p, nullptr, rays, frames, max_bounce, n_next, nullptr);
+}
+
+tt_status tt_enqueue_diffuse_bounce_indirect(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_rays_dev,
+                                             tt_ray_data* rays, int32_t frames, int32_t max_bounce,
+                                             uint32_t* n_next_dev) {
+    if (!n_next_dev) return c ? fail(c, TT_ERR_INVALID_ARG, "null device survivor count") : TT_ERR_INVALID_ARG;
+    return enqueue_call(c, p, n_rays_dev, rays, frames, max_bounce, nullptr, n_next_dev);
 }
 
 }  // extern "C"

@@ -138,7 +138,9 @@ struct TraceArgs {
     uint32_t* sticky_overflow;   // stack overflows since the last tt_async_overflows (never reset by launches)
     uint2* spill;                // traversal-stack entries beyond TT_LDS_STACK, [entry][thread]
     unsigned long long* diag_times;  // TT_DIAG_TIMES builds: per wave (start, end, rays)
-    uint32_t n_rays;
+    uint32_t n_rays;             // rays to trace; with n_rays_dev: the capacity
+    const uint32_t* n_rays_dev;  // nullable: device-resident count (BufferSizes[CurBounce].tracerays),
+                                 // traced = min(*n_rays_dev, n_rays) -- the reference's DispatchIndirect
     uint32_t ray_offset;         // W*H on odd bounces
     uint32_t width, height;
     float far_plane;
@@ -170,10 +172,18 @@ struct ShadowArgs {
     TraceControl* ctl;
     uint32_t* sticky_overflow;
     uint2* spill;
-    uint32_t n_rays;
+    uint32_t n_rays;             // rays to trace; with n_rays_dev: the capacity
+    const uint32_t* n_rays_dev;  // nullable: device-resident count (BufferSizes[CurBounce].shadow_rays)
     uint32_t width, height;
     int32_t bounce;
     uint32_t flags;
 };
+
+// The launch's ray count: the host value, or the device-resident count clamped to it (a wave-uniform
+// load of a word an earlier operation on the stream wrote).
+template <class Args>
+__device__ __forceinline__ uint32_t launch_ray_count(const Args& A) {
+    return A.n_rays_dev ? min(*A.n_rays_dev, A.n_rays) : A.n_rays;
+}
 
 #endif

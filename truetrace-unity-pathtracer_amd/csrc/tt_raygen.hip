@@ -239,7 +239,8 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
                                                         uint32_t n, float far_plane, int32_t cur_bounce, int32_t frames,
                                                         int32_t max_bounce, const tt_cuda_triangle* __restrict__ tris,
                                                         const tt_mesh_data* __restrict__ md, uint32_t* __restrict__ ctl,
-                                                        unsigned long long* __restrict__ lb, uint32_t n_tiles) {
+                                                        unsigned long long* __restrict__ lb, uint32_t n_tiles,
+                                                        const uint32_t* __restrict__ n_dev, uint32_t* __restrict__ n_next_dev) {
     __shared__ uint32_t s_tile, s_prefix;
     __shared__ uint32_t s_cnt[TT_BOUNCE_K][TT_BOUNCE_WAVES];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -247,6 +248,9 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
     __syncthreads();
     const uint32_t tile = s_tile;
     const uint32_t base = tile * TT_BOUNCE_TILE;
+    // device-resident count (the reference's BufferSizes[CurBounce].tracerays): tiles past it find no
+    // rays, publish 0 and keep the look-back chain complete up to the grid's last tile
+    if (n_dev) n = min(*n_dev, n);
     // pass 1: which rays survive (hit, and the cosine sample's pdf > 0); keep the ray and omega_o
     Ray3 R[TT_BOUNCE_K];
     float3 om[TT_BOUNCE_K];
@@ -287,7 +291,10 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
         }
         if (lane == 0) {
             s_prefix = prefix;
-            if (tile == n_tiles - 1u) ctl[0] = prefix + total;  // the survivor count tt_enqueue returns
+            if (tile == n_tiles - 1u) {
+                ctl[0] = prefix + total;  // the survivor count tt_enqueue returns
+                if (n_next_dev) *n_next_dev = prefix + total;  // BufferSizes[CurBounce + 1].tracerays
+            }
         }
     }
     __syncthreads();
@@ -321,13 +328,19 @@ uint32_t tt_bounce_tiles(uint32_t n) { return (n + TT_BOUNCE_TILE - 1u) / TT_BOU
 
 // counter: [0] survivor count, [1] tile ticket, then tt_bounce_tiles(n) 64-bit status words; all
 // zeroed by the caller before the launch.
+// n_dev (nullable): device-resident ray count, clamped to n (then n is the capacity the grid covers);
+// n_next_dev (nullable): receives the survivor count on the device.
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
-                            const tt_mesh_data* md, uint32_t* counter, hipStream_t st) {
-    if (n == 0) return hipSuccess;
+                            const tt_mesh_data* md, uint32_t* counter, hipStream_t st, const uint32_t* n_dev,
+                            uint32_t* n_next_dev) {
+    if (n == 0) {
+        if (n_next_dev) return hipMemsetAsync(n_next_dev, 0, 4, st);
+        return hipSuccess;
+    }
     const uint32_t tiles = tt_bounce_tiles(n);
     hipLaunchKernelGGL(tt_bounce_kernel, dim3(tiles), dim3(TT_BOUNCE_BLOCK), 0, st, rays, src_off, dst_off, n, far_plane,
                        cur_bounce, frames, max_bounce, tris, md, counter,
-                       reinterpret_cast<unsigned long long*>(counter + 4), tiles);
+                       reinterpret_cast<unsigned long long*>(counter + 4), tiles, n_dev, n_next_dev);
     return hipGetLastError();
 }

@@ -304,8 +304,9 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
 
 }  // namespace
 
-template <bool STATS, bool MATCHECK>
-__global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
+// IND: device-resident ray count (tt_trace_shadow_ex_indirect), its own kernel (tt_shadow_kernel_indirect)
+template <bool STATS, bool MATCHECK, bool IND>
+__device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
     __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
     const uint32_t gtid = blockIdx.x * TT_BLOCK + tid;
@@ -319,7 +320,8 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
     uint32_t pool_next = 0, pool_end = 0, more = 1;
     const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
     SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
-    const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
+    const uint32_t n_rays = IND ? launch_ray_count(A) : A.n_rays;
+    const uint32_t n_tiles = (n_rays + 63u) >> 6;
     const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
     const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
@@ -391,7 +393,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
             if (avail < n_idle && more) {
-                new_count = sched_reserve(A.ctl, A.n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
+                new_count = sched_reserve(A.ctl, n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
                 more = new_count > 0 ? 1u : 0u;
             }
             const uint32_t take_old = min(avail, n_idle);
@@ -564,7 +566,7 @@ __global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
 // (throughput.xyz, 1 = reached): it keeps the encoders' registers out of the traversal kernel.
 __global__ void tt_shadow_accumulate(ShadowArgs A, const float4* __restrict__ vis) {
     const uint32_t ri = blockIdx.x * TT_BLOCK + threadIdx.x;
-    if (ri >= A.n_rays) return;
+    if (ri >= launch_ray_count(A)) return;
     const float4 v = vis[ri];
     if (v.w != 1.0f) return;
     const tt_shadow_ray& R = A.rays[ri];
@@ -620,9 +622,24 @@ hipError_t tt_launch_shadow_accumulate(const ShadowArgs* a, const float4* vis, h
     return hipGetLastError();
 }
 
+template <bool STATS, bool MATCHECK>
+__global__ TT_BOUNDS void tt_shadow_kernel(ShadowArgs A) {
+    shadow_body<STATS, MATCHECK, false>(A);
+}
+template <bool MATCHECK>
+__global__ TT_BOUNDS void tt_shadow_kernel_indirect(ShadowArgs A) {
+    shadow_body<false, MATCHECK, true>(A);
+}
+
 // ------------------------------------------------------------------ launchers
 template <bool S, bool M>
 static hipError_t launch_shadow(const ShadowArgs& a, uint32_t grid, hipStream_t st) {
+    if constexpr (!S) {
+        if (a.n_rays_dev) {
+            hipLaunchKernelGGL((tt_shadow_kernel_indirect<M>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((tt_shadow_kernel<S, M>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
     return hipGetLastError();
 }

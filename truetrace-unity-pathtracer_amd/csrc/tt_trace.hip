@@ -66,8 +66,10 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
 
 
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
-template <bool STATS, bool MATCHECK, int INFO>
-__global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
+// IND: the ray count is device-resident (tt_trace_closest_indirect): instantiated as its own kernel
+// (tt_trace_kernel_indirect), so the direct launches keep exactly their code and kernel names.
+template <bool STATS, bool MATCHECK, int INFO, bool IND>
+__device__ __forceinline__ void trace_body(const TraceArgs& A) {
     __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
     zero_next_control(A.ctl_next, tid);
@@ -85,7 +87,11 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     uint32_t pool_next = 0, pool_end = 0, more = 1;
     const uint32_t wave_id = blockIdx.x * (TT_BLOCK / TT_WAVE) + (tid >> 6);
     SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
-    const uint32_t n_tiles = (A.n_rays + 63u) >> 6;
+    const uint32_t n_rays = IND ? launch_ray_count(A) : A.n_rays;
+    const uint32_t n_tiles = (n_rays + 63u) >> 6;
+    // work index -> ray index in 8x8 screen tiles: full-frame primary batches only (a device count
+    // decides at run time)
+    const bool swizzle = IND ? (A.tile_swizzle && n_rays == A.width * A.height) : (A.tile_swizzle != 0u);
     const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
     const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
@@ -148,7 +154,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
             if (avail < n_idle && more) {
-                new_count = sched_reserve(A.ctl, A.n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
+                new_count = sched_reserve(A.ctl, n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
                 more = new_count > 0 ? 1u : 0u;
             }
             const uint32_t take_old = min(avail, n_idle);
@@ -166,7 +172,7 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
             if (!active && widx != 0xffffffffu) {
                 // work index -> ray index (8x8 screen tiles for full-frame primary batches)
                 uint32_t local = widx;
-                if (A.tile_swizzle) {
+                if (swizzle) {
                     const uint32_t tw = A.width >> 3;
                     const uint32_t t = widx >> 6, l = widx & 63u;
                     const uint32_t ty = fastdiv(t, A.div_tiles), tx = t - ty * tw;
@@ -355,9 +361,24 @@ __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     }
 }
 
+template <bool STATS, bool MATCHECK, int INFO>
+__global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
+    trace_body<STATS, MATCHECK, INFO, false>(A);
+}
+template <bool MATCHECK, int INFO>
+__global__ TT_BOUNDS void tt_trace_kernel_indirect(TraceArgs A) {
+    trace_body<false, MATCHECK, INFO, true>(A);
+}
+
 // ------------------------------------------------------------------ launchers
 template <bool S, bool M, int I>
 static hipError_t launch_one(const TraceArgs& a, uint32_t grid, hipStream_t st) {
+    if constexpr (!S) {
+        if (a.n_rays_dev) {  // stats launches never take a device count (tt_api.hip refuses them)
+            hipLaunchKernelGGL((tt_trace_kernel_indirect<M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((tt_trace_kernel<S, M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
     return hipGetLastError();
 }

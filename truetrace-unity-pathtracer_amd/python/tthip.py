@@ -183,7 +183,8 @@ _HIP = None
 HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_destroy", "tt_last_error",
                "tt_scene_upload", "tt_scene_update_nodes", "tt_scene_update_meshdata", "tt_scene_bytes",
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
-               "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics",
+               "tt_enqueue_diffuse_bounce", "tt_trace_closest_indirect", "tt_enqueue_diffuse_bounce_indirect",
+               "tt_trace_shadow_ex_indirect", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics",
                "tt_selftest_rcp"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
@@ -276,6 +277,10 @@ def hip_lib():
         L.tt_trace_closest.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, C.POINTER(Stats)]
         L.tt_trace_shadow.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, C.POINTER(Stats)]
         L.tt_trace_shadow_ex.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, vp, C.POINTER(Stats)]
+        if hasattr(L, "tt_trace_closest_indirect"):  # (absent from round-2 variant libraries, tools/run_variants.py)
+            L.tt_trace_closest_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
+            L.tt_trace_shadow_ex_indirect.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, vp, vp]
+            L.tt_enqueue_diffuse_bounce_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, i32, i32, vp]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_scene_upload_texture_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
@@ -771,6 +776,18 @@ class Engine:
             self._check(st, "tt_trace_closest")
         return (s, st) if not check else s
 
+    def trace_indirect(self, rays, n_rays_dev, capacity: int, bounce: int, far_plane: float, width: int, height: int,
+                       info=None, colors=None, flags: int = 0, check: bool = True):
+        """tt_trace_closest_indirect: traces min(*n_rays_dev, capacity) rays, the count read on the device
+        (a uint32 device tensor, e.g. the n_next_dev of enqueue_bounce_indirect); device pointers, async."""
+        p = TraceParams(n_rays=capacity, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
+                        flags=flags | TT_TRACE_DEVICE_PTRS)
+        st = self.L.tt_trace_closest_indirect(self.h, C.byref(p), _ptr(n_rays_dev), _ptr(rays), _ptr(info),
+                                              _ptr(colors))
+        if check:
+            self._check(st, "tt_trace_closest_indirect")
+        return st
+
     def tlas_refit(self, n_tlas_nodes: int, mesh_aabbs, device: bool = False, asynchronous: bool = False):
         """tt_tlas_refit (AssetManager.RefitTLAS): re-quantize TLAS nodes [0, n_tlas_nodes) in HBM from
         per-mesh world AABBs (n_mesh x {BBMax, BBMin})."""
@@ -825,6 +842,17 @@ class Engine:
             self._check(st, "tt_trace_shadow" if legacy else "tt_trace_shadow_ex")
         return (s, st) if not check else s
 
+    def trace_shadow_indirect(self, shadow_rays, n_rays_dev, capacity: int, bounce: int, width: int, height: int,
+                              visibility=None, colors=None, nee_pos=None, flags: int = 0, cache=None, check: bool = True):
+        """tt_trace_shadow_ex_indirect: min(*n_rays_dev, capacity) shadow rays; device pointers, async."""
+        p = ShadowParams(n_rays=capacity, bounce=bounce, screen_width=width, screen_height=height,
+                         flags=flags | TT_TRACE_DEVICE_PTRS)
+        st = self.L.tt_trace_shadow_ex_indirect(self.h, C.byref(p), _ptr(n_rays_dev), _ptr(shadow_rays),
+                                                _ptr(visibility), _ptr(colors), _ptr(nee_pos), _ptr(cache))
+        if check:
+            self._check(st, "tt_trace_shadow_ex_indirect")
+        return st
+
     def resolve_normals(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int,
                         out=None, device: bool = False):
         p = TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
@@ -852,6 +880,18 @@ class Engine:
         self._check(self.L.tt_enqueue_diffuse_bounce(self.h, C.byref(p), _ptr(rays), frames, max_bounce,
                                                      C.byref(n)), "tt_enqueue_diffuse_bounce")
         return n.value
+
+    def enqueue_bounce_indirect(self, rays, n_rays_dev, capacity, n_next_dev, bounce, far_plane, width, height,
+                                frames=0, max_bounce=3, check: bool = True):
+        """tt_enqueue_diffuse_bounce_indirect: the traced count from n_rays_dev (None: capacity), the survivor
+        count written to the device uint32 n_next_dev; no synchronization."""
+        p = TraceParams(n_rays=capacity, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
+                        flags=TT_TRACE_DEVICE_PTRS)
+        st = self.L.tt_enqueue_diffuse_bounce_indirect(self.h, C.byref(p), _ptr(n_rays_dev), _ptr(rays), frames,
+                                                       max_bounce, _ptr(n_next_dev))
+        if check:
+            self._check(st, "tt_enqueue_diffuse_bounce_indirect")
+        return st
 
 
 def validate(s: Scene):
