@@ -47,13 +47,32 @@ def main():
     steps0 = cnt["node_visits"].astype(np.int64) + cnt["tri_tests"].astype(np.int64)
     out = {"tool": "tools/exp_lpt.py", "config": cfg, "ranks": ranks, "launches": {}}
 
-    def run(name, recs, n, bounce, steps):
+    def chunk_max(steps, n):
         nch = (n + 63) // 64
         pad = np.zeros(nch * 64, np.int64)
         pad[:n] = steps
-        cmax = pad.reshape(nch, 64).max(1)
+        return pad.reshape(nch, 64).max(1)
+
+    def seg_sorted(cm, key_sign):
+        """longest-first inside each of the kernel's 8 XCD segments (the screen bands stay per XCD)"""
+        nch = len(cm)
+        out = []
+        for k in range(8):
+            lo, hi = nch * k // 8, nch * (k + 1) // 8
+            out.append(lo + np.argsort(key_sign * cm[lo:hi], kind="stable"))
+        return np.concatenate(out)
+
+    def run(name, recs, n, bounce, steps, steps_other=None):
+        nch = (n + 63) // 64
+        cmax = chunk_max(steps, n)
+        buckets = np.minimum(np.log2(cmax + 1).astype(np.int64) * 2, 31)  # ~16 coarse cost classes
         orders = {"natural": np.arange(nch), "lpt": np.argsort(-cmax, kind="stable"),
-                  "spt": np.argsort(cmax, kind="stable")}
+                  "spt": np.argsort(cmax, kind="stable"), "lpt_seg": seg_sorted(cmax, -1),
+                  "lpt_bucket": np.argsort(-buckets, kind="stable")}
+        if steps_other is not None:  # the cost map of ANOTHER jittered frame (temporal reuse)
+            co = chunk_max(steps_other, n)
+            orders["lpt_other_frame"] = np.argsort(-co, kind="stable")
+            orders["lpt_seg_other_frame"] = seg_sorted(co, -1)
         res = {}
         for oname, o in orders.items():
             idx = (o[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)
@@ -75,7 +94,12 @@ def main():
         out["launches"][name] = res
         print(name, res, file=sys.stderr, flush=True)
 
-    run("primary", base[:n0], n0, 0, steps0)
+    r1 = O.generate(c2w, ip, W, H, T.NEAR, T.FAR, jitter=1, frames=1, max_bounce=1)
+    b1 = np.zeros(2 * WH, tthip.RAY_DTYPE)
+    b1[:n0] = r1[pix]
+    st, cnt1 = O.trace(sc, b1, n0, 0, T.FAR, W, H, counts=True, nthreads=16)
+    steps0_other = cnt1["node_visits"].astype(np.int64) + cnt1["tri_tests"].astype(np.int64)
+    run("primary", base[:n0], n0, 0, steps0, steps0_other)
     # bounce-1 rays from the oracle's own enqueue of the traced primaries
     traced = base.copy()
     O.trace(sc, traced, n0, 0, T.FAR, W, H, nthreads=16)
