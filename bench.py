@@ -145,16 +145,18 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         torch.cuda.synchronize(dev)
         return bufs, counts
 
-    def parts_layout(sc, view, W, H, nb, info, colors_t, P=2):
+    def parts_layout(sc, view, W, H, nb, info, colors_t, P=2, adaptive=False):
         """The same frame as P tile-interleaved parts, each with its own engine context on its own
         stream and its own chain of bounce launches (bench.py's metric layout): wall
-        ms per frame over all launches of all parts."""
+        ms per frame over all launches of all parts. adaptive: TT_TRACE_ADAPTIVE_ORDER on every launch,
+        the frames alternating between two jittered samples (frames_accumulated 0 / 1), so each launch's
+        order comes from the previous frame's costs, never from its own rays."""
         import ttdist
 
         WH = W * H
         c2w, ip = view.camera(W, H)
-        base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(base, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=max(nb, 1), device=True)
+        n_frames = 2 if adaptive else 1
+        flags = tthip.TT_TRACE_ADAPTIVE_ORDER if adaptive else 0
         extra_engs, streams = [], []
         try:
             for _ in range(P - 1):
@@ -162,29 +164,37 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 e1 = tthip.Engine(dev.index, stream=streams[-1].cuda_stream)
                 extra_engs.append(e1)
                 e1.upload(sc)
-            chains = []
-            for e, pix_np in zip([eng] + extra_engs, ttdist.part_pixels(W, H, 1, 0, P)):
-                cur = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-                n = int(pix_np.shape[0])
-                cur.view(2 * WH, 48)[:n] = base.view(WH, 48)[torch.from_numpy(pix_np).to(dev)]
-                torch.cuda.synchronize(dev)
-                bufs, counts = [cur.clone()], [n]
-                for b in range(nb):
-                    e.trace(cur, counts[-1], b, far, W, H, device=True)
-                    counts.append(e.enqueue_bounce(cur, counts[-1], b, far, W, H, frames=0,
-                                                   max_bounce=max(nb, 1), device=True))
-                    bufs.append(cur.clone())
-                torch.cuda.synchronize(dev)
-                chains.append((e, bufs, counts))
+            chains = [[] for _ in range(n_frames)]  # chains[f]: per part (engine, bufs, counts)
+            base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+            for f in range(n_frames):
+                eng.generate(base, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=f, max_bounce=max(nb, 1),
+                             device=True)
+                for e, pix_np in zip([eng] + extra_engs, ttdist.part_pixels(W, H, 1, 0, P)):
+                    cur = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+                    n = int(pix_np.shape[0])
+                    cur.view(2 * WH, 48)[:n] = base.view(WH, 48)[torch.from_numpy(pix_np).to(dev)]
+                    torch.cuda.synchronize(dev)
+                    bufs, counts = [cur.clone()], [n]
+                    for b in range(nb):
+                        e.trace(cur, counts[-1], b, far, W, H, device=True)
+                        counts.append(e.enqueue_bounce(cur, counts[-1], b, far, W, H, frames=f,
+                                                       max_bounce=max(nb, 1), device=True))
+                        bufs.append(cur.clone())
+                    torch.cuda.synchronize(dev)
+                    chains[f].append((e, bufs, counts))
+            del base
+            k_frame = [0]
 
             def frame():
+                ch = chains[k_frame[0] % n_frames]
+                k_frame[0] += 1
                 for b in range(nb + 1):
-                    for e, bufs, counts in chains:
+                    for e, bufs, counts in ch:
                         e.trace(bufs[b], counts[b], b, far, W, H, info=info, colors=colors_t if b > 0 else None,
-                                device=True, asynchronous=True)
+                                device=True, asynchronous=True, flags=flags)
 
-            reps = max(3, args.steps // 2)
-            for _ in range(max(1, args.warmup)):
+            reps = max(4, args.steps // 2) // n_frames * n_frames
+            for _ in range(max(2, args.warmup)):
                 frame()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -192,13 +202,29 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 frame()
             torch.cuda.synchronize(dev)
             ms = (time.perf_counter() - t0) * 1e3 / reps
-            rays = sum(sum(c) for _, _, c in chains)
+            rays = sum(sum(sum(c) for _, _, c in ch) for ch in chains) / n_frames
             return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": int(rays)}
         finally:
             for e1 in extra_engs:
                 e1.close()
 
-    def run(name, scene_fn, view, W, H, nb, extra_fn, with_parts=False):
+    def adaptive_one_launch(view, W, H, nb, info, colors_t):
+        """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch
+        ordered by the previous frame's costs); per-bounce HIP-event ms (order kernel included)."""
+        fr = [rays_with_bounces(view, W, H, nb, f) for f in range(2)]
+        launches = [(lambda bufs=bufs, counts=counts, b=b: eng.trace(
+            bufs[b], counts[b], b, far, W, H, info=info, colors=colors_t if b > 0 else None, device=True,
+            asynchronous=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER))
+            for bufs, counts in fr for b in range(nb + 1)]
+        ms = timed_launches(eng, launches, max(2, args.warmup), max(2, args.steps // 4))
+        ms = ms.reshape(-1, nb + 1)  # rows: frames
+        rays = [sum(c[b] for _, c in fr) / 2.0 for b in range(nb + 1)]
+        mean = ms.mean(0)
+        del fr
+        return {"trace_ms": [round(float(m), 4) for m in mean],
+                "mrays_s": round(float(sum(rays)) / float(mean.sum()) / 1e3, 1), "rays_mean": [int(r) for r in rays]}
+
+    def run(name, scene_fn, view, W, H, nb, extra_fn, with_parts=False, adaptive=False):
         try:
             t0 = time.time()
             sc = scene_fn()
@@ -221,6 +247,17 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                         extra[key] = parts_layout(sc, view, W, H, nb, info, colors_t, P)
                     except Exception as e:  # noqa: BLE001
                         extra[key] = {"error": f"{type(e).__name__}: {e}"}
+            if adaptive:  # TT_TRACE_ADAPTIVE_ORDER (tt_order.hip), frames alternating
+                try:
+                    ad = {"one_launch_per_bounce": adaptive_one_launch(view, W, H, nb, info, colors_t)}
+                    if with_parts:
+                        ad["two_parts_two_streams"] = parts_layout(sc, view, W, H, nb, info, colors_t, 2, True)
+                    ad["note"] = ("every launch flagged; two jittered frames (frames_accumulated 0 / 1) alternate, "
+                                  "so a launch's order comes from the previous frame's costs; order kernel inside "
+                                  "the per-launch HIP-event times")
+                    extra["adaptive_order"] = ad
+                except Exception as e:  # noqa: BLE001
+                    extra["adaptive_order"] = {"error": f"{type(e).__name__}: {e}"}
             pack(name, counts, ms, extra)
             del info, colors_t
             return sc
@@ -247,7 +284,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         sc4 = run("c4_bistro_primary_plus_1_bounce_1080p", T.c4_bistro, T.C4_VIEW, 1920, 1080, 1,
             lambda sc: {"unique_tris": int(len(sc.tris)), "instanced_tris": sc.meta["instanced_tris"],
                         "unique_blas": 600, "instances": 2400, "cwbvh_nodes": int(len(sc.nodes))},
-            with_parts=True)
+            with_parts=True, adaptive=True)
     if "dyn" in which:
         # the reference's per-frame dynamic-scene update on C4 (AssetManager.cs:1767-1826): every
         # frame rewrites all _MeshData records (MeshDataBuffer.SetData, :1825) and refits the TLAS
@@ -366,7 +403,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         log(f"aux refit: {rec}")
     if "c5" in which:
         run("c5_san_miguel_primary_4k", T.c5_san_miguel, T.C5_VIEW, 3840, 2160, 0,
-            lambda sc: {"tris": int(len(sc.tris)), "cwbvh_nodes": int(len(sc.nodes))}, with_parts=True)
+            lambda sc: {"tris": int(len(sc.tris)), "cwbvh_nodes": int(len(sc.nodes))}, with_parts=True,
+            adaptive=True)
     return out
 
 

@@ -22,6 +22,7 @@ namespace TrueTrace.Hip
         None = 0, DevicePtrs = 1u << 0, UseReSTIRGI = 1u << 1, UseASVGF = 1u << 2, Stats = 1u << 3, Async = 1u << 4,
         IgnoreGlass = 1u << 5,       // IgnoreGlassMain  (IntersectionKernels.compute:42-44)
         IgnoreBackfacing = 1u << 6,  // IgnoreBackfacing (IntersectionKernels.compute:45-47)
+        AdaptiveOrder = 1u << 7,     // dequeue the previous launch's costliest 8x8 tiles first (same results)
         RadianceCache = 1u << 7,     // tt_trace_shadow_ex: the RadianceCache define (GlobalDefines.cginc:15)
         VisibilityCheck = 1u << 8    // tt_trace_shadow_ex: VisabilityCheckCompute (CommonData.cginc:710-819)
     }

@@ -1,0 +1,109 @@
+"""TT_TRACE_ADAPTIVE_ORDER (csrc/tt_order.hip): a flagged launch records per-8x8-tile costs, the next
+flagged launch of the same bounce index dequeues its chunks longest-first. Only which lane traces
+which ray changes, so every flagged launch must be byte-identical to the unflagged one (which the
+parity suites pin against the oracle). Every record's hit fields start as a sentinel, so a ray the
+reordered dequeue skipped would show.
+
+Covered: the full-frame 8x8 tile swizzle (chunk = pixel tile) and compacted lists (chunk -> tile
+through its first record's PixelIndex); ragged counts (the partial last chunk must stay last);
+counts below one chunk per segment; a screen-size change (costs dropped); the material-check
+kernel form; _PrimaryTriangleInfo at bounce 0 and the GlobalColors-gated form at bounce 1; C2 at
+1080p (primary + its compacted bounce-1 rays)."""
+import numpy as np
+import pytest
+
+import ttconfigs as T
+import tthip
+from parity_util import FAR
+
+pytestmark = pytest.mark.gpu
+ORD = tthip.TT_TRACE_ADAPTIVE_ORDER
+
+
+def _sentinel(rays_t):
+    """uint8 device view of RayData[]: every hits field set to 0xFFFFFFFF."""
+    v = rays_t.view(-1, 48)
+    v[:, 32:48] = 255
+    return rays_t
+
+
+def _run(engine, base, n, bounce, W, H, flags, colors=None):
+    import torch
+
+    t = _sentinel(base.clone())
+    info = torch.zeros(W * H * 16, dtype=torch.uint8, device=base.device)
+    engine.trace(t, n, bounce, FAR, W, H, info=info, colors=colors, device=True, flags=flags)
+    torch.cuda.synchronize()
+    return t, info
+
+
+def _check_order_invariance(engine, base, n, bounce, W, H, extra=0, colors=None, repeats=3):
+    import torch
+
+    ref, ref_info = _run(engine, base, n, bounce, W, H, extra, colors)
+    for k in range(repeats):  # k = 0 records costs (natural order), k >= 1 dequeue in the sorted order
+        got, got_info = _run(engine, base, n, bounce, W, H, extra | ORD, colors)
+        assert torch.equal(got, ref), (n, bounce, k)
+        assert torch.equal(got_info, ref_info), (n, bounce, k)
+
+
+def _soup_frame(engine, W, H, seed=41, frames=0):
+    import torch
+
+    sc = tthip.single_object_scene(tthip.Mesh.soup(seed, 30000, 1.0, 0.1))
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 2.4), (-0.1, -0.05, -1.0), (0, 1, 0), 60.0, W, H, 0.05, FAR)
+    engine.upload(sc)
+    base = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=torch.device("cuda:0"))
+    engine.generate(base, c2w, ip, W, H, 0.05, FAR, jitter=1, frames=frames, max_bounce=2, device=True)
+    return base
+
+
+def test_adaptive_order_full_frame_and_ragged(engine):
+    W, H = 256, 160
+    WH = W * H
+    base = _soup_frame(engine, W, H)
+    # full frame (8x8 tile swizzle), then compacted-list forms: ragged, tiny, one ray
+    for n in (WH, WH - 1, 4097, 1000, 63, 1):
+        _check_order_invariance(engine, base, n, 0, W, H)
+    # the material-check kernel form (IgnoreBackfacing at bounce 0)
+    _check_order_invariance(engine, base, WH, 0, W, H, extra=tthip.TT_TRACE_IGNORE_BACKFACING)
+    _check_order_invariance(engine, base, WH - 5, 0, W, H, extra=tthip.TT_TRACE_IGNORE_BACKFACING)
+
+
+def test_adaptive_order_screen_change_and_bounce(engine):
+    import torch
+
+    # a different screen size on the same context and bounce slot: the old costs are dropped
+    for W, H in ((200, 120), (120, 96), (200, 120)):
+        base = _soup_frame(engine, W, H, seed=43)
+        _check_order_invariance(engine, base, W * H, 0, W, H, repeats=2)
+    # bounce 1 on the compacted survivors of the traced primaries (the odd-bounce half of the buffer)
+    W, H = 200, 120
+    base = _soup_frame(engine, W, H, seed=43, frames=2)
+    engine.trace(base, W * H, 0, FAR, W, H, device=True)
+    nb = engine.enqueue_bounce(base, W * H, 0, FAR, W, H, frames=2, max_bounce=2, device=True)
+    assert 0 < nb < W * H
+    colors = np.zeros(W * H, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = (np.arange(W * H) % 3) - 1.0  # every Data.w gate form
+    col_t = torch.from_numpy(colors.view(np.uint8)).to(base.device)
+    _check_order_invariance(engine, base, nb, 1, W, H, colors=col_t)
+
+
+def test_adaptive_order_c2_1080p_primary_and_bounce(engine):
+    """The bench workload: C2 at 1920x1080, the primary launch and the compacted bounce-1 launch,
+    each three times with the flag (the 2nd and 3rd in the sorted order), byte-identical."""
+    import torch
+
+    W, H = 1920, 1080
+    WH = W * H
+    sc = T.c2_sponza()
+    engine.upload(sc)
+    c2w, ip = T.C2_VIEW.camera(W, H)
+    base = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=torch.device("cuda:0"))
+    engine.generate(base, c2w, ip, W, H, T.NEAR, FAR, jitter=1, frames=0, max_bounce=1, device=True)
+    _check_order_invariance(engine, base, WH, 0, W, H)
+    engine.trace(base, WH, 0, FAR, W, H, device=True)
+    nb = engine.enqueue_bounce(base, WH, 0, FAR, W, H, frames=0, max_bounce=1, device=True)
+    colors = torch.zeros(WH * 64, dtype=torch.uint8, device=base.device)
+    colors.view(torch.float32).view(WH, 16)[:, 15] = -1.0  # Data.w = -1: info written for every ray
+    _check_order_invariance(engine, base, nb, 1, W, H, colors=colors)

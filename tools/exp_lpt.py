@@ -62,7 +62,7 @@ def main():
             out.append(lo + np.argsort(key_sign * cm[lo:hi], kind="stable"))
         return np.concatenate(out)
 
-    def run(name, recs, n, bounce, steps, steps_other=None):
+    def run(name, recs, n, bounce, steps, steps_other=None, extra=None):
         nch = (n + 63) // 64
         cmax = chunk_max(steps, n)
         buckets = np.minimum(np.log2(cmax + 1).astype(np.int64) * 2, 31)  # ~16 coarse cost classes
@@ -73,6 +73,9 @@ def main():
             co = chunk_max(steps_other, n)
             orders["lpt_other_frame"] = np.argsort(-co, kind="stable")
             orders["lpt_seg_other_frame"] = seg_sorted(co, -1)
+        for k, co in (extra or {}).items():  # chunk cost estimates from another frame, keyed by pixel tile
+            orders["lpt_" + k] = np.argsort(-co, kind="stable")
+            orders["lpt_seg_" + k] = seg_sorted(co, -1)
         res = {}
         for oname, o in orders.items():
             idx = (o[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)
@@ -99,7 +102,9 @@ def main():
     b1[:n0] = r1[pix]
     st, cnt1 = O.trace(sc, b1, n0, 0, T.FAR, W, H, counts=True, nthreads=16)
     steps0_other = cnt1["node_visits"].astype(np.int64) + cnt1["tri_tests"].astype(np.int64)
-    run("primary", base[:n0], n0, 0, steps0, steps0_other)
+    nodes0_other = cnt1["node_visits"].astype(np.int64)
+    run("primary", base[:n0], n0, 0, steps0, steps0_other,
+        {"reps_other_frame": chunk_max(nodes0_other, n0)})
     # bounce-1 rays from the oracle's own enqueue of the traced primaries
     traced = base.copy()
     O.trace(sc, traced, n0, 0, T.FAR, W, H, nthreads=16)
@@ -107,7 +112,33 @@ def main():
     brec = traced[WH: WH + nb].copy()
     st, cb = O.trace(sc, traced, nb, 1, T.FAR, W, H, counts=True, nthreads=16)
     steps1 = cb["node_visits"].astype(np.int64) + cb["tri_tests"].astype(np.int64)
-    run("bounce1", brec, nb, 1, steps1)
+    # temporal estimate for the compacted bounce list: frame 1's bounce-1 cost per 8x8 pixel tile,
+    # looked up through each chunk's PixelIndex (first record, or the max over all its records)
+    tr1 = b1.copy()
+    O.trace(sc, tr1, n0, 0, T.FAR, W, H, nthreads=16)
+    nb1 = O.enqueue_bounce(sc, tr1, n0, 0, T.FAR, W, H, frames=1)
+    st, cb1 = O.trace(sc, tr1, nb1, 1, T.FAR, W, H, counts=True, nthreads=16)
+    s1 = cb1["node_visits"].astype(np.int64) + cb1["tri_tests"].astype(np.int64)
+    r1n = cb1["node_visits"].astype(np.int64)
+    ntile = (W // 8) * (H // 8)
+
+    def tile_of(p):
+        p = p.astype(np.int64)
+        return (p // W // 8) * (W // 8) + (p % W) // 8
+
+    def tile_map(pixels, cost):
+        m = np.zeros(ntile, np.int64)
+        np.maximum.at(m, tile_of(pixels), cost)
+        return m
+
+    p1 = tr1[WH: WH + nb1]["PixelIndex"] if "PixelIndex" in tr1.dtype.names else tr1[WH: WH + nb1]["pixel_index"]
+    pb = brec["PixelIndex"] if "PixelIndex" in brec.dtype.names else brec["pixel_index"]
+    M, Mr = tile_map(p1, s1), tile_map(p1, r1n)
+    first = np.arange(0, nb, 64)
+    est = {"first_rec_other_frame": M[tile_of(pb[first])],
+           "reps_first_rec_other_frame": Mr[tile_of(pb[first])],
+           "allrec_other_frame": chunk_max(M[tile_of(pb)], nb)}
+    run("bounce1", brec, nb, 1, steps1, None, est)
     print(json.dumps(out, indent=1))
 
 

@@ -18,7 +18,7 @@
 
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
 uint32_t tt_trace_chunk_rays();
-hipError_t tt_trace_occupancy_table(int* out12);
+hipError_t tt_trace_occupancy_table(int* out18);
 hipError_t tt_launch_shadow(const ShadowArgs* a, uint32_t grid, hipStream_t st, int stats, int matcheck);
 hipError_t tt_launch_shadow_accumulate(const ShadowArgs* a, const float4* vis, hipStream_t st);
 void tt_shadow_occupancy_table(int* out4);
@@ -98,7 +98,7 @@ struct tt_ctx {
     int num_cus = 0;
     int blocks_per_cu = 0;
     uint32_t grid = 0;
-    uint32_t grid_of[12] = {};  // resident persistent grid per kernel instantiation
+    uint32_t grid_of[18] = {};  // resident persistent grid per kernel instantiation (12..17: adaptive order)
     uint32_t shadow_grid_of[4] = {};  // the same for the any-hit kernel (stats * 2 + matcheck)
     TraceControl* ctl = nullptr;  // two control blocks: a trace launch uses one and zeroes the other
     uint32_t* sticky = nullptr;   // stack overflows of every launch since the last tt_async_overflows
@@ -170,6 +170,15 @@ struct tt_ctx {
     };
     Pinned pin[2];
     uint32_t pin_cur = 0;
+    // TT_TRACE_ADAPTIVE_ORDER: per bounce index (min(bounce, 7)), the last flagged launch's per-tile
+    // costs and the order buffer the next one dequeues in (tt_order.hip)
+    struct OrderSlot {
+        DevBuf<uint32_t> cost[2];  // cost[cur]: the last launch's costs (when valid)
+        DevBuf<uint32_t> order;
+        uint32_t cur = 0, w = 0, h = 0;
+        bool valid = false;
+    };
+    OrderSlot ord[8];
 };
 
 // Per-call timing ring entries (tt_timing_read) around device work issued on the context stream.
@@ -523,7 +532,7 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
         return TT_ERR_HIP;
     }
     c->num_cus = prop.multiProcessorCount;
-    int occ[12];
+    int occ[18];
     (void)tt_trace_occupancy_table(occ);
     // Residency check beyond the occupancy API: measured on MI355X, five 32-KiB-LDS blocks were
     // not co-resident (the fifth started only when another exited), consistent with the LDS being
@@ -532,7 +541,7 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     const int lds_cap = lds_block ? 2 * (int)((80u * 1024u) / lds_block) : 8;
     int knob = 0;
     if (const char* e = std::getenv("TT_BLOCKS_PER_CU")) knob = std::atoi(e);  // tuning/diagnostic knob
-    for (int k = 0; k < 12; k++) {
+    for (int k = 0; k < 18; k++) {
         int b = std::max(1, std::min(std::min(occ[k], lds_cap), 8));
         if (knob > 0 && knob < b) b = knob;
         c->grid_of[k] = (uint32_t)(c->num_cus * b);
@@ -547,7 +556,7 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     c->blocks_per_cu = (int)(c->grid_of[1] / c->num_cus);
     c->grid = c->grid_of[1];
     uint32_t max_grid = 0;
-    for (int k = 0; k < 12; k++) max_grid = std::max(max_grid, c->grid_of[k]);
+    for (int k = 0; k < 18; k++) max_grid = std::max(max_grid, c->grid_of[k]);
     for (int k = 0; k < 4; k++) max_grid = std::max(max_grid, c->shadow_grid_of[k]);
     c->spill_threads = max_grid * tt_trace_block_size();
     // two control blocks + the sticky overflow counter behind them
@@ -1127,6 +1136,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     const bool async = dev && ((p->flags & TT_TRACE_ASYNC) || n_dev);
     const bool want_stats = (p->flags & TT_TRACE_STATS) != 0;
     const int info_mode = info ? (p->bounce == 0 ? 1 : 2) : 0;
+    const bool adaptive = (p->flags & TT_TRACE_ADAPTIVE_ORDER) && !want_stats && !n_dev;
     if (n_dev) {
         if (!dev) return fail(c, TT_ERR_INVALID_ARG, "a device-resident ray count needs TT_TRACE_DEVICE_PTRS");
         if (want_stats) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_STATS needs a host ray count");
@@ -1200,8 +1210,29 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     // rank's shard at 8 GPUs -- on ~1 wave per SIMD, 4 chunks each)
     const uint32_t waves_needed = (p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays();
     const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
-    const uint32_t grid = std::max(1u, std::min(c->grid_of[(want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode],
-                                                 blocks_needed));
+    const uint32_t grid = std::max(
+        1u, std::min(c->grid_of[(adaptive ? 12 : want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode], blocks_needed));
+    // TT_TRACE_ADAPTIVE_ORDER: this launch fills cost[cur ^ 1] (per 64-ray chunk); with the previous
+    // launch's costs in cost[cur] the order kernel (inside the timed entry) sorts this launch's chunks
+    tt_ctx::OrderSlot* os = nullptr;
+    const uint32_t n_chunks = (p->n_rays + 63u) / 64u;
+    if (adaptive) {
+        os = &c->ord[std::min(p->bounce, 7)];
+        if (os->w != p->screen_width || os->h != p->screen_height) {  // (costs outlive scene updates: a hint)
+            os->valid = false;
+            os->w = p->screen_width;
+            os->h = p->screen_height;
+        }
+        if (os->order.n < n_chunks) {  // (a fresh map pair starts from zero costs)
+            TT_HIP(c, os->order.alloc(n_chunks));
+            TT_HIP(c, os->cost[0].alloc(n_chunks));
+            TT_HIP(c, os->cost[1].alloc(n_chunks));
+            TT_HIP(c, hipMemsetAsync(os->cost[0].p, 0, sizeof(uint32_t) * n_chunks, c->stream));
+            os->valid = false;
+        }
+        if (!os->valid) TT_HIP(c, hipMemsetAsync(os->cost[os->cur ^ 1u].p, 0, sizeof(uint32_t) * n_chunks, c->stream));
+        a.chunk_cost = os->cost[os->cur ^ 1u].p;
+    }
     // Control blocks: every trace kernel zeroes the OTHER block at its start (block 0, plain stores;
     // the previous launch on the stream, which used it, has finished), so back-to-back async
     // launches need no fill kernel in between. Synchronous / stats launches, and the first launch
@@ -1214,7 +1245,22 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     c->ctl_zero[0] = c->ctl_zero[1] = false;
+    static const bool record_only = std::getenv("TT_ORDER_RECORD_ONLY") != nullptr;  // A/B knob: costs, no order
+    if (os && os->valid && !record_only) {
+        OrderArgs o;
+        o.cost = os->cost[os->cur].p;
+        o.cost_clear = os->cost[os->cur ^ 1u].p;
+        o.n_rays = p->n_rays;
+        o.n_chunks = n_chunks;
+        o.order = os->order.p;
+        TT_HIP(c, tt_launch_order(o, c->stream));
+        a.order = os->order.p;
+    }
     TT_HIP(c, tt_launch_trace(a, want_stats, matcheck, info_mode, grid, c->stream));
+    if (os) {
+        os->cur ^= 1u;
+        os->valid = true;
+    }
     c->ctl_zero[ci ^ 1u] = true;
     c->ctl_cur = ci ^ 1u;
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));

@@ -150,7 +150,20 @@ struct TraceArgs {
     TraceControl* ctl_next;      // the other control block: zeroed by this launch for the next one
     FastDiv div_width;           // n / width (pixel decode of finished rays)
     FastDiv div_tiles;           // n / (width / 8) (8x8 tile swizzle in the refill)
+    // TT_TRACE_ADAPTIVE_ORDER (tt_trace_kernel_ord only)
+    const uint32_t* order;       // nullable: work chunk -> ray chunk (64 rays), from tt_order_kernel
+    uint32_t* chunk_cost;        // per ray chunk: max Reps of its rays (atomicMax, rays with Reps >= TT_ORDER_MIN_REPS)
 };
+
+// Adaptive-order builder (tt_order.hip): one block per scheduler segment sorts the segment's
+// chunks by the previous launch's chunk costs, longest first.
+struct OrderArgs {
+    const uint32_t* cost;        // previous launch's per-chunk costs
+    uint32_t* cost_clear;        // the map this launch's trace fills: zeroed here ([0, n_chunks))
+    uint32_t n_rays, n_chunks;
+    uint32_t* order;             // out: n_chunks entries
+};
+hipError_t tt_launch_order(const OrderArgs& a, hipStream_t st);
 
 // Any-hit visibility launch (tt_shadow.hip, kernel_shadow replacement).
 struct ShadowArgs {

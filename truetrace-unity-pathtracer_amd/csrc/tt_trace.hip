@@ -62,13 +62,35 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
     reinterpret_cast<uint4*>(R)[2] = make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
     return best.t != A.far_plane;
 }
+
+// TT_TRACE_ADAPTIVE_ORDER: a finished (or Reps-exhausted) ray's cost -- its Reps count -- into its
+// ray chunk's entry of the launch's cost map (no-return atomic max; tt_order.hip sorts the next
+// launch's chunks by it). The ray chunk is the 8x8 pixel tile in the full-frame swizzle, else
+// (ray index - offset) / 64. Rays below TT_ORDER_MIN_REPS skip the atomic: chunks whose rays are all
+// cheap keep cost 0 and their natural order, and a launch issues few atomics.
+static_assert(TT_CHUNK_BIG == 64, "the adaptive order maps one dequeue (TT_CHUNK_BIG rays) to one 64-ray chunk");
+#ifndef TT_ORDER_MIN_REPS
+#define TT_ORDER_MIN_REPS 32
+#endif
+__device__ __forceinline__ void record_chunk_cost(const TraceArgs& A, bool swizzle, uint32_t ray_index, int32_t reps) {
+    if (reps < TT_ORDER_MIN_REPS) return;
+    const uint32_t local = ray_index - A.ray_offset;
+    uint32_t c = local >> 6;
+    if (swizzle) {
+        const uint32_t py = fastdiv(local, A.div_width), px = local - py * A.width;
+        c = (py >> 3) * (A.width >> 3) + (px >> 3);
+    }
+    atomicMax(A.chunk_cost + c, (uint32_t)reps);
+}
 }  // namespace
 
 
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
 // IND: the ray count is device-resident (tt_trace_closest_indirect): instantiated as its own kernel
 // (tt_trace_kernel_indirect), so the direct launches keep exactly their code and kernel names.
-template <bool STATS, bool MATCHECK, int INFO, bool IND>
+// ORD: TT_TRACE_ADAPTIVE_ORDER (tt_trace_kernel_ord): chunks are dequeued in A.order (when set) and
+// every ray's Reps count goes into the tile cost map.
+template <bool STATS, bool MATCHECK, int INFO, bool IND, bool ORD>
 __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     __shared__ uint2 s_stack[TT_LDS_STACK][TT_BLOCK];
     const uint32_t tid = threadIdx.x;
@@ -118,6 +140,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         const bool hit = write_record<INFO>(A, ray_index, pix, col_w, best, world_ray());
         if (STATS) c_hits += hit ? 1u : 0u;
         (void)hit;
+        if (ORD) record_chunk_cost(A, swizzle, ray_index, Reps);
     };
     while (true) {
         // ---------------------------------------------------------------- refill
@@ -142,10 +165,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             auto finish_wide = [&](const WideState& w) {
                 const bool hit = write_record<INFO>(A, w.ray_index, w.pix, w.col_w, w.best, w.wray);
                 if (STATS) c_hits += hit ? 1u : 0u;
+                if (ORD) record_chunk_cost(A, swizzle, w.ray_index, w.Reps);
+            };
+            auto exhaust_wide = [&](const WideState& w) {
+                if (ORD) record_chunk_cost(A, swizzle, w.ray_index, w.Reps);
             };
             wide_phase<STATS, MATCHECK, 2>(A, st, s_stack, spill, spill_stride, nodes, tris, lane,
                                            Counters{c_nodes, c_tris, c_blas, c_acc, c_hits, c_reps, c_ovf},
-                                           finish_wide);
+                                           finish_wide, exhaust_wide);
             break;
         }
 #endif
@@ -156,6 +183,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             if (avail < n_idle && more) {
                 new_count = sched_reserve(A.ctl, n_rays, n_tiles, lane, n_idle - avail, wave_id, S, new_base);
                 more = new_count > 0 ? 1u : 0u;
+                // a reservation is one whole 64-ray work chunk (TT_CHUNK_BIG, chunk-aligned segments): the
+                // adaptive order maps it to the ray chunk it dequeues (one wave-uniform load)
+                if (ORD && A.order && new_count > 0)
+                    new_base = (__builtin_amdgcn_readfirstlane(A.order[new_base >> 6]) << 6) | (new_base & 63u);
             }
             const uint32_t take_old = min(avail, n_idle);
             const uint32_t take_new = min(n_idle - take_old, new_count);
@@ -229,6 +260,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
+                if (ORD) record_chunk_cost(A, swizzle, ray_index, Reps);
             } else if (cg.y & 0xff000000u) {  // IntersectionKernels.compute:157-187
                 const uint32_t cio = firstbithigh(cg.y);
                 const uint32_t slot = (cio - 24u) ^ (oct & 0xffu);
@@ -363,11 +395,21 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 
 template <bool STATS, bool MATCHECK, int INFO>
 __global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
-    trace_body<STATS, MATCHECK, INFO, false>(A);
+    trace_body<STATS, MATCHECK, INFO, false, false>(A);
 }
 template <bool MATCHECK, int INFO>
 __global__ TT_BOUNDS void tt_trace_kernel_indirect(TraceArgs A) {
-    trace_body<false, MATCHECK, INFO, true>(A);
+    trace_body<false, MATCHECK, INFO, true, false>(A);
+}
+// (held at 5 waves per SIMD like the direct kernels: the cost record would otherwise cost INFO = 2 a
+// wave; the material-check forms keep the default bounds, which do not spill VGPRs)
+template <int INFO>
+__global__ __launch_bounds__(TT_BLOCK, 5) void tt_trace_kernel_ord(TraceArgs A) {
+    trace_body<false, false, INFO, false, true>(A);
+}
+template <int INFO>
+__global__ TT_BOUNDS void tt_trace_kernel_ord_mat(TraceArgs A) {
+    trace_body<false, true, INFO, false, true>(A);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -376,6 +418,11 @@ static hipError_t launch_one(const TraceArgs& a, uint32_t grid, hipStream_t st) 
     if constexpr (!S) {
         if (a.n_rays_dev) {  // stats launches never take a device count (tt_api.hip refuses them)
             hipLaunchKernelGGL((tt_trace_kernel_indirect<M, I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+            return hipGetLastError();
+        }
+        if (a.chunk_cost) {  // TT_TRACE_ADAPTIVE_ORDER (never with stats or a device count)
+            if (M) hipLaunchKernelGGL((tt_trace_kernel_ord_mat<I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
+            else hipLaunchKernelGGL((tt_trace_kernel_ord<I>), dim3(grid), dim3(TT_BLOCK), 0, st, a);
             return hipGetLastError();
         }
     }
@@ -397,14 +444,23 @@ hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int in
 }
 
 // Occupancy (resident blocks per CU) of every instantiation: they differ in registers, so each
-// launch sizes its persistent grid from its own entry. index = stats*6 + matcheck*3 + info.
+// launch sizes its persistent grid from its own entry.
 template <bool S, bool M, int I>
 static int occ_one() {
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_trace_kernel<S, M, I>, TT_BLOCK, 0) != hipSuccess) b = 1;
     return b;
 }
-hipError_t tt_trace_occupancy_table(int* out12) {
+template <bool M, int I>
+static int occ_ord() {
+    int b = 0;
+    const hipError_t e = M ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_trace_kernel_ord_mat<I>, TT_BLOCK, 0)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tt_trace_kernel_ord<I>, TT_BLOCK, 0);
+    return e == hipSuccess ? b : 1;
+}
+// index = stats*6 + matcheck*3 + info; 12 + matcheck*3 + info: the adaptive-order kernels
+hipError_t tt_trace_occupancy_table(int* out18) {
+    int* out12 = out18;
     out12[0] = occ_one<false, false, 0>();
     out12[1] = occ_one<false, false, 1>();
     out12[2] = occ_one<false, false, 2>();
@@ -417,6 +473,12 @@ hipError_t tt_trace_occupancy_table(int* out12) {
     out12[9] = occ_one<true, true, 0>();
     out12[10] = occ_one<true, true, 1>();
     out12[11] = occ_one<true, true, 2>();
+    out18[12] = occ_ord<false, 0>();
+    out18[13] = occ_ord<false, 1>();
+    out18[14] = occ_ord<false, 2>();
+    out18[15] = occ_ord<true, 0>();
+    out18[16] = occ_ord<true, 1>();
+    out18[17] = occ_ord<true, 2>();
     return hipGetLastError();
 }
 

@@ -176,12 +176,13 @@ __device__ __forceinline__ uint32_t node_intersect_part(const uint4 n0, const ui
 
 
 // The drain loop for groups of G lanes; regroups into 2G-lane groups when the live rays fit and
-// returns when every ray of the wave has finished. `finish(st)` writes a finished ray's records
-// (called on the group's first lane only).
-template <bool STATS, bool MATCHECK, int G, class Finish>
+// returns when every ray of the wave has finished. `finish(st)` writes a finished ray's records,
+// `exhaust(st)` sees a ray that hit the Reps bound (nothing is written for it); both are called on
+// the group's first lane only.
+template <bool STATS, bool MATCHECK, int G, class Finish, class Exhaust>
 __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[TT_BLOCK], uint2* __restrict__ spill,
                            uint32_t spill_stride, __amdgpu_buffer_rsrc_t nodes, __amdgpu_buffer_rsrc_t tris,
-                           uint32_t lane, Counters C, Finish& finish) {
+                           uint32_t lane, Counters C, Finish& finish, Exhaust& exhaust) {
     const uint32_t sub = lane & (G - 1);
     const uint32_t base = lane & ~(uint32_t)(G - 1);
     const uint32_t tid = st.scol, gtid = st.gcol;  // the stack the TT_PUSH / TT_POP macros address
@@ -193,7 +194,8 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
         if constexpr (G < 8) {
             if (n * (2 * G) <= TT_WAVE) {
                 regroup<2 * G>(st, lead, lane);
-                wide_phase<STATS, MATCHECK, 2 * G>(A, st, s_stack, spill, spill_stride, nodes, tris, lane, C, finish);
+                wide_phase<STATS, MATCHECK, 2 * G>(A, st, s_stack, spill, spill_stride, nodes, tris, lane, C, finish,
+                                                   exhaust);
                 return;
             }
         }
@@ -202,6 +204,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
             if (st.Reps >= TT_MAX_REPS) {
                 st.active = false;  // loop bound hit: the reference writes nothing
                 if (STATS && sub == 0u) C.reps++;
+                if (sub == 0u) exhaust(st);
             } else if (st.cg.y & 0xff000000u) {  // IntersectionKernels.compute:157-187
                 const uint32_t cio = firstbithigh(st.cg.y);
                 const uint32_t slot = (cio - 24u) ^ (st.oct & 0xffu);

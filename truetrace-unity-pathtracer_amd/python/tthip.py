@@ -41,6 +41,7 @@ TT_TRACE_STATS = 1 << 3
 TT_TRACE_ASYNC = 1 << 4
 TT_TRACE_IGNORE_GLASS = 1 << 5       # IgnoreGlassMain (IntersectionKernels.compute:42-44)
 TT_TRACE_IGNORE_BACKFACING = 1 << 6  # IgnoreBackfacing (IntersectionKernels.compute:45-47)
+TT_TRACE_ADAPTIVE_ORDER = 1 << 7  # dequeue the previous launch's costliest tiles first (tt_order.hip)
 TT_SHADOW_RADIANCE_CACHE = 1 << 7    # RadianceCache define (GlobalDefines.cginc:15) for tt_trace_shadow_ex
 TT_SHADOW_VISIBILITY_CHECK = 1 << 8  # VisabilityCheckCompute semantics (CommonData.cginc:710-819)
 TT_STACK_SIZE = 16
