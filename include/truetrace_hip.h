@@ -364,14 +364,16 @@ enum {
     TT_TRACE_IGNORE_GLASS = 1u << 5,
     TT_TRACE_IGNORE_BACKFACING = 1u << 6,
     /* Adaptive dequeue order (tt_trace_closest only; ignored with TT_TRACE_STATS and by
-     * tt_trace_closest_indirect). The launch records, per 8x8 pixel tile, the largest Reps count of
-     * its rays (rays map to tiles through RayData.PixelIndex), and the next flagged launch with the
-     * same bounce index and screen size on this context dequeues its 64-ray chunks longest-first
-     * within each of the scheduler's segments, a chunk's cost being that of the tile its first
-     * record's PixelIndex names. Long rays then start early instead of forming the launch's tail.
-     * Which lane traces which ray changes, what is written does not: results are identical to an
-     * unflagged launch. The reference pops rays in InterlockedAdd order
-     * (IntersectionKernels.compute:79-81), so no order is part of its contract. */
+     * tt_trace_closest_indirect). The launch records, per 64-ray chunk (the 8x8 pixel tile of a
+     * full-frame batch, else 64 consecutive records), the largest Reps count of its rays, and the
+     * next flagged launch with the same bounce index and screen size on this context dequeues its
+     * chunks longest-first within each of the scheduler's segments, so long rays start early instead
+     * of forming the launch's tail. Pays on scenes whose long rays are latency-bound chains (the
+     * Bistro-shaped C4: -18% primary launch time with the previous, differently jittered frame's
+     * costs); neutral to slightly negative on small, L2-resident scenes. Which lane traces which ray
+     * changes, what is written does not: results are identical to an unflagged launch. The
+     * reference pops rays in InterlockedAdd order (IntersectionKernels.compute:79-81), so no order
+     * is part of its contract. */
     TT_TRACE_ADAPTIVE_ORDER = 1u << 7
 };
 

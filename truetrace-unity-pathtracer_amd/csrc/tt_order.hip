@@ -4,12 +4,16 @@
 // serial chains of dependent node / triangle fetches (up to ~1 us each when they miss the L2s).
 // When such a ray is dequeued late it becomes the launch's tail: on the Bistro-shaped C4 scene a
 // 1080p primary launch spends ~0.2 ms of its ~1.06 ms finishing rays that started late
-// (profiles/r03/exp_lpt_c4_temporal.json). The flagged trace kernel records, per 8x8 pixel tile,
-// the largest Reps count of the rays it traced; before the next flagged launch of the same bounce
-// index this kernel sorts each scheduler segment's 64-ray chunks by those costs, longest first, so
-// the expensive chunks start with the launch. Frames are temporally coherent (the costs of the
-// previous, differently jittered frame order the next one nearly as well as the exact costs do:
-// C4 primary 1.06 -> 0.83 ms vs 0.82 ms with exact costs, same file).
+// (profiles/r03/exp_lpt_temporal_c4_c2.txt: longest-chunk-first with the exact costs 0.82 ms, with
+// the costs of ANOTHER jittered frame 0.83-0.85 ms -- frames are temporally coherent).
+//
+// The flagged trace kernel (tt_trace_kernel_ord) records, per 64-ray chunk (the 8x8 pixel tile in
+// the full-frame swizzle, else records [64 m, 64 m + 64) of the batch), the largest Reps count of
+// its rays that reached TT_ORDER_MIN_REPS; before the next flagged launch of the same bounce index
+// this kernel sorts each scheduler segment's chunks by those costs, longest first, and the trace
+// kernel maps each dequeue (one whole chunk) through the result. A compacted bounce list shifts
+// from frame to frame, so its chunk m is only approximately the previous frame's chunk m: a hint,
+// which is all an order needs (results never depend on it).
 //
 // One block per segment (TT_SEGS, the work ranges the trace kernel's XCD groups dequeue from, so
 // each segment keeps its screen band and its L2): a counting sort over OKEYS cost buckets in LDS.
