@@ -148,7 +148,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
     def parts_layout(sc, view, W, H, nb, info, colors_t, P=2, adaptive=False):
         """The same frame as P tile-interleaved parts, each with its own engine context on its own
         stream and its own chain of bounce launches (bench.py's metric layout): wall
-        ms per frame over all launches of all parts. adaptive: TT_TRACE_ADAPTIVE_ORDER on every launch,
+        ms per frame over all launches of all parts. adaptive: TT_TRACE_ADAPTIVE_ORDER on the primary launches,
         the frames alternating between two jittered samples (frames_accumulated 0 / 1), so each launch's
         order comes from the previous frame's costs, never from its own rays."""
         import ttdist
@@ -191,7 +191,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 for b in range(nb + 1):
                     for e, bufs, counts in ch:
                         e.trace(bufs[b], counts[b], b, far, W, H, info=info, colors=colors_t if b > 0 else None,
-                                device=True, asynchronous=True, flags=flags)
+                                device=True, asynchronous=True, flags=flags if b == 0 else 0)
 
             reps = max(4, args.steps // 2) // n_frames * n_frames
             for _ in range(max(2, args.warmup)):
@@ -210,11 +210,12 @@ def aux_configs(torch, tthip, eng, dev, args, which):
 
     def adaptive_one_launch(view, W, H, nb, info, colors_t):
         """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch
-        ordered by the previous frame's costs); per-bounce HIP-event ms (order kernel included)."""
+        ordered by the previous frame's costs; the primary launches flagged); per-bounce HIP-event ms (order
+        kernel included)."""
         fr = [rays_with_bounces(view, W, H, nb, f) for f in range(2)]
         launches = [(lambda bufs=bufs, counts=counts, b=b: eng.trace(
             bufs[b], counts[b], b, far, W, H, info=info, colors=colors_t if b > 0 else None, device=True,
-            asynchronous=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER))
+            asynchronous=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER if b == 0 else 0))
             for bufs, counts in fr for b in range(nb + 1)]
         ms = timed_launches(eng, launches, max(2, args.warmup), max(2, args.steps // 4))
         ms = ms.reshape(-1, nb + 1)  # rows: frames
@@ -252,7 +253,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                     ad = {"one_launch_per_bounce": adaptive_one_launch(view, W, H, nb, info, colors_t)}
                     if with_parts:
                         ad["two_parts_two_streams"] = parts_layout(sc, view, W, H, nb, info, colors_t, 2, True)
-                    ad["note"] = ("every launch flagged; two jittered frames (frames_accumulated 0 / 1) alternate, "
+                    ad["note"] = ("primary launches flagged (a compacted bounce list's chunks shift from frame to "
+                                  "frame, DESIGN.md 3.1); two jittered frames (frames_accumulated 0 / 1) alternate, "
                                   "so a launch's order comes from the previous frame's costs; order kernel inside "
                                   "the per-launch HIP-event times")
                     extra["adaptive_order"] = ad
@@ -1076,6 +1078,14 @@ def main():
                  "mrays_s": round((WH + rnb) / float(rmean.sum()) / 1e3, 1),
                  "primary_nodes_per_ray": round(rs.node_visits / WH, 2), "reps_exhausted": int(rs.reps_exhausted),
                  "note": "RayGenKernels.compute:47 with UseReCur: column x=W/2 has direction.z == -0.0 (NaN z slabs)"}
+        # UseReCur's camera rays are the same every frame, so TT_TRACE_ADAPTIVE_ORDER on the primary
+        # launch is ordered by exactly its previous frame's costs: the Reps-exhausting chain starts first
+        launches[0] = lambda: eng.trace(rr, WH, 0, far, W, H, info=info, device=True, asynchronous=True,
+                                        flags=tthip.TT_TRACE_ADAPTIVE_ORDER)
+        ams = timed_launches(eng, launches, max(2, args.warmup), args.steps).mean(0)
+        recur["adaptive_order"] = {"trace_ms": [round(float(m), 4) for m in ams],
+                                   "mrays_s": round((WH + rnb) / float(ams.sum()) / 1e3, 1),
+                                   "note": "primary launch flagged (identical camera rays every UseReCur frame)"}
         del rr
         log(f"recur (unjittered) primary + bounce: {recur}")
 

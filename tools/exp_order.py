@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--parts", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--ranks", type=int, default=1, help="trace rank 0's 64x64-tile shard of an N-GPU frame")
+    ap.add_argument("--primary-only", action="store_true", help="flag the primary launches only")
     args = ap.parse_args()
     import torch
     import tthip
@@ -56,7 +58,10 @@ def main():
     colors = np.zeros(WH, tthip.COL_DTYPE)
     colors["Data"][:, 3] = 1.0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
-    pix_parts = [np.arange(WH)] if P == 1 else ttdist.part_pixels(W, H, 1, 0, P)
+    if args.ranks > 1:
+        pix_parts = ttdist.part_pixels(W, H, args.ranks, 0, P)
+    else:
+        pix_parts = [np.arange(WH)] if P == 1 else ttdist.part_pixels(W, H, 1, 0, P)
     # frames[f][s] = (rays buffer, n primary, n bounce) of part s of jittered frame f
     frames = []
     full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
@@ -86,9 +91,9 @@ def main():
             for s in range(P):
                 buf, n, m = fr[s]
                 engs[s].trace(buf, m, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True,
-                              flags=flags)
+                              flags=0 if args.primary_only else flags)
 
-    out = {"tool": "tools/exp_order.py", "config": args.config, "parts": P, "width": W, "height": H,
+    out = {"tool": "tools/exp_order.py", "config": args.config, "parts": P, "ranks": args.ranks, "primary_only": args.primary_only, "width": W, "height": H,
            "rays_per_step": rays_per, "rounds": []}
     for r in range(args.rounds):
         rec = {}
