@@ -77,3 +77,17 @@ def test_null_context_selftest_is_rejected():
     L = tthip.hip_lib()
     n = C.c_uint64()
     assert L.tt_selftest_rcp(None, C.addressof(n)) == tthip.TT_ERR_INVALID_ARG
+
+
+def test_flag_constants_match_the_header():
+    """Every TT_TRACE_* / TT_SHADOW_* / TT_ERR_* constant tthip binds equals the header's enum value."""
+    src = open(os.path.join(REPO, "include", "truetrace_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    hdr = {}
+    for name, expr in re.findall(r"\b(TT_(?:TRACE|SHADOW|ERR)_[A-Z0-9_]+)\s*=\s*([^,\n}]+)", src):
+        hdr[name] = int(eval(expr.replace("u", ""), {}))  # "1u << 7" -> 1 << 7
+    bound = {k: getattr(tthip, k) for k in dir(tthip) if re.fullmatch(r"TT_(TRACE|SHADOW|ERR)_[A-Z0-9_]+", k)}
+    assert "TT_TRACE_ADAPTIVE_ORDER" in bound and "TT_TRACE_DEVICE_PTRS" in bound
+    for k, v in bound.items():
+        assert k in hdr, f"{k} is bound in tthip but not declared in truetrace_hip.h"
+        assert hdr[k] == v, (k, hdr[k], v)
