@@ -541,15 +541,18 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     const int lds_cap = lds_block ? 2 * (int)((80u * 1024u) / lds_block) : 8;
     int knob = 0;
     if (const char* e = std::getenv("TT_BLOCKS_PER_CU")) knob = std::atoi(e);  // tuning/diagnostic knob
+    // at most 32 waves per CU (8 blocks of 4 waves at the default 256-thread block)
+    const int wpb = (int)std::max(1u, tt_trace_block_size() / 64u);
+    const int block_cap = std::max(1, 32 / wpb);
     for (int k = 0; k < 18; k++) {
-        int b = std::max(1, std::min(std::min(occ[k], lds_cap), 8));
+        int b = std::max(1, std::min(std::min(occ[k], lds_cap), block_cap));
         if (knob > 0 && knob < b) b = knob;
         c->grid_of[k] = (uint32_t)(c->num_cus * b);
     }
     int socc[4];
     tt_shadow_occupancy_table(socc);
     for (int k = 0; k < 4; k++) {
-        int b = std::max(1, std::min(std::min(socc[k], lds_cap), 8));
+        int b = std::max(1, std::min(std::min(socc[k], lds_cap), block_cap));
         if (knob > 0 && knob < b) b = knob;
         c->shadow_grid_of[k] = (uint32_t)(c->num_cus * b);
     }
@@ -1209,7 +1212,8 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     // waves as it has chunks (r02: sizing this for 256-ray chunks left a 260k-ray launch -- one
     // rank's shard at 8 GPUs -- on ~1 wave per SIMD, 4 chunks each)
     const uint32_t waves_needed = (p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays();
-    const uint32_t blocks_needed = (waves_needed + 3u) / 4u;
+    const uint32_t wpb = std::max(1u, tt_trace_block_size() / 64u);  // waves per block
+    const uint32_t blocks_needed = (waves_needed + wpb - 1u) / wpb;
     const uint32_t grid = std::max(
         1u, std::min(c->grid_of[(adaptive ? 12 : want_stats ? 6 : 0) + (matcheck ? 3 : 0) + info_mode], blocks_needed));
     // TT_TRACE_ADAPTIVE_ORDER: this launch fills cost[cur ^ 1] (per 64-ray chunk); with the previous
@@ -1412,7 +1416,8 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     a.bounce = p->bounce;
     a.flags = p->flags;
     const bool matcheck = c->any_shadow_skip || c->any_cutout || c->any_atlas_shadow;
-    const uint32_t blocks_needed = ((p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays() + 3u) / 4u;
+    const uint32_t wpb = std::max(1u, tt_trace_block_size() / 64u);  // waves per block
+    const uint32_t blocks_needed = ((p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays() + wpb - 1u) / wpb;
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));
     TT_HIP(c, hipMemsetAsync(c->ctl + c->ctl_cur, 0, sizeof(TraceControl), c->stream));

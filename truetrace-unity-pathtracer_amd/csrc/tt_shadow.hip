@@ -564,8 +564,9 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
 // Indirect and PrimaryNEERay, with or without the RadianceCache define (include/truetrace_hip.h).
 // A streaming pass over the launch's rays after the traversal, driven by its visibility record
 // (throughput.xyz, 1 = reached): it keeps the encoders' registers out of the traversal kernel.
-__global__ void tt_shadow_accumulate(ShadowArgs A, const float4* __restrict__ vis) {
-    const uint32_t ri = blockIdx.x * TT_BLOCK + threadIdx.x;
+constexpr uint32_t TT_ACC_BLOCK = 256;  // streaming pass: plain 256-thread blocks
+__global__ __launch_bounds__(TT_ACC_BLOCK) void tt_shadow_accumulate(ShadowArgs A, const float4* __restrict__ vis) {
+    const uint32_t ri = blockIdx.x * TT_ACC_BLOCK + threadIdx.x;
     if (ri >= launch_ray_count(A)) return;
     const float4 v = vis[ri];
     if (v.w != 1.0f) return;
@@ -618,7 +619,8 @@ __global__ void tt_shadow_accumulate(ShadowArgs A, const float4* __restrict__ vi
 }
 
 hipError_t tt_launch_shadow_accumulate(const ShadowArgs* a, const float4* vis, hipStream_t st) {
-    hipLaunchKernelGGL(tt_shadow_accumulate, dim3((a->n_rays + TT_BLOCK - 1) / TT_BLOCK), dim3(TT_BLOCK), 0, st, *a, vis);
+    hipLaunchKernelGGL(tt_shadow_accumulate, dim3((a->n_rays + TT_ACC_BLOCK - 1) / TT_ACC_BLOCK), dim3(TT_ACC_BLOCK), 0,
+                       st, *a, vis);
     return hipGetLastError();
 }
 

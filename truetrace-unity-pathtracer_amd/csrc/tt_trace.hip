@@ -404,7 +404,7 @@ __global__ TT_BOUNDS void tt_trace_kernel_indirect(TraceArgs A) {
 // (held at 5 waves per SIMD like the direct kernels: the cost record would otherwise cost INFO = 2 a
 // wave; the material-check forms keep the default bounds, which do not spill VGPRs)
 template <int INFO>
-__global__ __launch_bounds__(TT_BLOCK, 5) void tt_trace_kernel_ord(TraceArgs A) {
+__global__ __launch_bounds__(TT_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void tt_trace_kernel_ord(TraceArgs A) {
     trace_body<false, false, INFO, false, true>(A);
 }
 template <int INFO>
