@@ -656,8 +656,9 @@ def main():
                     help="a rank's pixels (N = 1: the frame; N > 1: its tiles) are traced as this many tile-interleaved "
                          "parts, each by its own engine on its own stream (each part's bounce-1 after its own primary), "
                          "so one part's launch drain overlaps the other parts' work (tools/exp_streams.py). 1: one "
-                         "launch per bounce; 0 (default): 2, or 3 at N >= 4 (shards of <= 1/4 frame: measured "
-                         "-11%% / -4%% step time at the N = 4 / 8 shards vs 2 parts, profiles/r02/exp_streams_2v3_w*.json)")
+                         "launch per bounce; 0 (default): 2 for a full frame's worth per rank (N = 1, the spp "
+                         "headline), 3 for the strong-scaling shards at N >= 4 (<= 1/4 frame: -12%% / -2%% step time "
+                         "at the N = 4 / 8 shards vs 2 parts, profiles/r03/parts/)")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     ap.add_argument("--steady-steps", type=int, default=200,
                     help="N = 1: steps of the secondary steady-state leg after the timed region (0 = skip)")
@@ -768,8 +769,12 @@ def main():
     # a rank's pixels (the whole frame at N = 1) as P tile-interleaved parts, each traced by its own
     # engine context on its own stream: a part's launches overlap the other parts' launch drains
     # (tools/exp_streams.py); P = 1 is one full-frame launch per bounce in the kernel's own tile order
+    # parts per rank: a full frame's worth of rays (N = 1, and every rank of the spp headline) as 2 parts;
+    # the strong-scaling shards of <= 1/4 frame as 3 (one-wave blocks, profiles/r03/parts/: N = 4 shard
+    # 0.371 -> 0.327 ms, N = 8 0.236 -> 0.231 ms per step; a full frame 0.784-0.80 (2) vs 0.808-0.82 (3))
+    P_strong = max(1, args.parts) if args.parts > 0 else (3 if world >= 4 else 2)
     if args.parts <= 0:
-        args.parts = 3 if world >= 4 else 2
+        args.parts = 3 if (world >= 4 and not spp) else 2
     P = max(1, args.parts) if (tiles or world == 1) else 1
     split = tiles or P > 1
 
@@ -825,39 +830,65 @@ def main():
         # shards padded to the largest so every rank sends one equal-size message; a rank's parts back
         # to back. The gather runs on its own stream, overlapped with the bounce-1 traces (which read and
         # write only the other half of the ping-pong buffers); the step ends when both are done, so the
-        # timed step includes the collective.
+        # timed step includes the collective. On the GPU the primary traces write their hit records
+        # straight into the send buffer (tt_trace_closest_hits: no strided copy out of GlobalRays), two
+        # send buffers alternating by step, so step k + 2's primaries wait for step k's gather only. The
+        # gloo rehearsal (host-side collective) copies the records to a host buffer instead.
         g = Gather()
         n_t = torch.tensor([p.n for p in ps], dtype=torch.int64, device=red_dev)
         sz = [torch.zeros_like(n_t) for _ in range(world)]
         dist.all_gather(sz, n_t)
         g.sizes = [[int(v) for v in x.tolist()] for x in sz]
-        g.hits_buf = torch.zeros((max(sum(x) for x in g.sizes), 4), dtype=torch.int32, device=red_dev)
-        g.gather_list = [torch.empty_like(g.hits_buf) for _ in range(world)] if rank == 0 else None
+        g.stream_hits = red_dev.type == "cuda"
+        nbuf = 2 if g.stream_hits else 1
+        g.bufs = [torch.zeros((max(sum(x) for x in g.sizes), 4), dtype=torch.int32, device=red_dev)
+                  for _ in range(nbuf)]
+        g.lists = [[torch.empty_like(bf) for _ in range(world)] if rank == 0 else None for bf in g.bufs]
         g.comm = torch.cuda.Stream(dev)
+        g.done = [torch.cuda.Event() for _ in range(nbuf)]  # stream_hits: gather of buffer b finished
         g.copied = torch.cuda.Event()
+        g.k = 0
+        o = 0
+        for p in ps:
+            p.hit_slices = [bf[o:o + p.n] for bf in g.bufs]
+            o += p.n
         return g
+
+    def last_gather(g):
+        """(sizes, per-rank gathered blocks) of the most recent step's gather (rank 0)."""
+        return g.sizes, g.lists[(g.k - 1) % len(g.bufs)]
 
     def make_step(ps, g):
         def step_fn():
+            b = g.k % len(g.bufs) if g is not None else 0
             for p in ps:
-                p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True)
+                if g is not None and g.stream_hits:
+                    if g.k >= len(g.bufs):
+                        p.stream.wait_event(g.done[b])  # the gather that last read send buffer b is done
+                    p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True,
+                                hits_out=p.hit_slices[b])
+                else:
+                    p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True)
             if g is not None:
                 for p in ps:
                     g.comm.wait_stream(p.stream)  # the primary hit records are final
                 with torch.cuda.stream(g.comm):
-                    o = 0
-                    for p in ps:
-                        g.hits_buf[o:o + p.n].copy_(p.prim_hits)
-                        o += p.n
-                    g.copied.record(g.comm)
-                    dist.gather(g.hits_buf, g.gather_list, dst=0)
+                    if not g.stream_hits:
+                        for p in ps:
+                            p.hit_slices[0].copy_(p.prim_hits)
+                        g.copied.record(g.comm)
+                    dist.gather(g.bufs[b], g.lists[b], dst=0)
+                    if g.stream_hits:
+                        g.done[b].record(g.comm)
             for p in ps:
                 p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
             if g is not None:
-                for p in ps:
-                    # the next step's primary trace rewrites the records copied out above: it waits for the
-                    # copy, not for the gather (which reads hits_buf; the next copy is ordered after it on comm)
-                    p.stream.wait_event(g.copied)
+                if not g.stream_hits:
+                    for p in ps:
+                        # the next step's primary trace rewrites the records copied out above: it waits for the
+                        # copy, not for the gather (which reads the buffer; the next copy is ordered after it)
+                        p.stream.wait_event(g.copied)
+                g.k += 1
         return step_fn
 
     def timed(ps, step_fn):
@@ -899,7 +930,7 @@ def main():
         f"; parts {P}" + (f"; {world}-sample frame (spp)" if spp else ""))
 
     G = make_gather(parts) if tiles else None
-    sizes, gather_list = (G.sizes, G.gather_list) if G is not None else (None, None)
+    sizes, gather_list = None, None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
     step = make_step(parts, G)
@@ -955,6 +986,8 @@ def main():
         return one.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
 
     gather_parity = None
+    if G is not None:
+        sizes, gather_list = last_gather(G)  # the last step's gather (steady-state steps included)
     if split and rank == 0:
         if spp:
             fr = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gather_list, sizes)], W, H, world, P)
@@ -974,7 +1007,7 @@ def main():
     # round-robin (P parts per rank), the same per-step gather; frame time = the slowest rank's
     strong = None
     if spp and world > 1:
-        ps_s = build_parts([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)], fresh=True)
+        ps_s = build_parts([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P_strong)], fresh=True)
         g_s = make_gather(ps_s)
         el_s = timed(ps_s, make_step(ps_s, g_s))
         for p in ps_s:
@@ -987,11 +1020,12 @@ def main():
         dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
         par = None
         if rank == 0:
-            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(g_s.gather_list, g_s.sizes)], g_s.sizes, W, H,
-                                        world, P)
+            sz_s, gl_s = last_gather(g_s)
+            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H,
+                                        world, P_strong)
             par = bool(np.array_equal(fr1, one_gpu_frame(0)))
         strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
-                  "scaling": "strong", "ranks": world, "parts_per_rank": P,
+                  "scaling": "strong", "ranks": world, "parts_per_rank": P_strong,
                   "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4),
                   "rays_per_step_all_ranks": int(round(float(rsum.item()) / args.steps)),
                   "gather_identical_to_1gpu": par,

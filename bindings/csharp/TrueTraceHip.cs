@@ -116,6 +116,9 @@ namespace TrueTrace.Hip
             IntPtr nRaysDev, IntPtr globalRays, IntPtr primaryInfo, IntPtr globalColors);
         [DllImport(Lib)] public static extern TTStatus tt_trace_shadow_ex_indirect(IntPtr ctx, ref TTShadowParams p,
             IntPtr nRaysDev, IntPtr shadowRays, IntPtr visibility, IntPtr globalColors, IntPtr neePos, IntPtr cacheBuffer);
+        // tt_trace_closest + each ray's 16-B hit record written contiguously to hitsOut (the multi-GPU gather's input)
+        [DllImport(Lib)] public static extern TTStatus tt_trace_closest_hits(IntPtr ctx, ref TTTraceParams p,
+            IntPtr globalRays, IntPtr primaryInfo, IntPtr globalColors, IntPtr hitsOut);
         [DllImport(Lib)] public static extern TTStatus tt_async_overflows(IntPtr ctx, out ulong count);
         [DllImport(Lib)] public static extern IntPtr tt_ctx_stream(IntPtr ctx);
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.

@@ -408,6 +408,14 @@ typedef struct tt_stats {
 tt_status tt_trace_closest(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
                            uint32_t* primary_info, const tt_col_data* global_colors,
                            tt_stats* stats);
+/* tt_trace_closest that also writes each ray's 16-byte hit record contiguously: ray i of the launch
+ * (GlobalRays[offset + i]) -> hits_out[4 i .. 4 i + 3], the same bytes as its RayData.hits. The hit
+ * records of a tile-sharded frame are what the multi-GPU path gathers; written by
+ * the trace itself they need no strided copy out of GlobalRays before the collective. Requires
+ * TT_TRACE_DEVICE_PTRS; hits_out is 16-byte-aligned device memory of n_rays records. Everything
+ * else (flags, stats, synchronization) is tt_trace_closest's. */
+tt_status tt_trace_closest_hits(tt_ctx* ctx, const tt_trace_params* p, tt_ray_data* global_rays,
+                                uint32_t* primary_info, const tt_col_data* global_colors, uint32_t* hits_out);
 /* kernel_trace dispatched indirectly (the reference keeps BufferSizes[CurBounce].tracerays on the
  * GPU; TransferKernel turns it into DispatchIndirect arguments, RayTracingShader.compute:736-747,
  * RayTracingMaster.cs:964-970): the launch traces min(*n_rays_dev, p->n_rays) rays, the count read

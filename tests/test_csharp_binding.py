@@ -28,6 +28,7 @@ def test_flag_values_match_header():
     pairs = {"DevicePtrs": "TT_TRACE_DEVICE_PTRS", "UseReSTIRGI": "TT_TRACE_USE_RESTIRGI",
              "UseASVGF": "TT_TRACE_USE_ASVGF", "Stats": "TT_TRACE_STATS", "Async": "TT_TRACE_ASYNC",
              "IgnoreGlass": "TT_TRACE_IGNORE_GLASS", "IgnoreBackfacing": "TT_TRACE_IGNORE_BACKFACING",
+             "AdaptiveOrder": "TT_TRACE_ADAPTIVE_ORDER",
              "RadianceCache": "TT_SHADOW_RADIANCE_CACHE", "VisibilityCheck": "TT_SHADOW_VISIBILITY_CHECK"}
     for c, h in pairs.items():
         assert cs[c] == hdr[h], (c, h)

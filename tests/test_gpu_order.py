@@ -1,14 +1,15 @@
-"""TT_TRACE_ADAPTIVE_ORDER (csrc/tt_order.hip): a flagged launch records per-8x8-tile costs, the next
-flagged launch of the same bounce index dequeues its chunks longest-first. Only which lane traces
-which ray changes, so every flagged launch must be byte-identical to the unflagged one (which the
-parity suites pin against the oracle). Every record's hit fields start as a sentinel, so a ray the
-reordered dequeue skipped would show.
+"""Scheduling and output forms of the closest-hit launch that must not change what it computes.
 
-Covered: the full-frame 8x8 tile swizzle (chunk = pixel tile) and compacted lists (chunk -> tile
-through its first record's PixelIndex); ragged counts (the partial last chunk must stay last);
-counts below one chunk per segment; a screen-size change (costs dropped); the material-check
-kernel form; _PrimaryTriangleInfo at bounce 0 and the GlobalColors-gated form at bounce 1; C2 at
-1080p (primary + its compacted bounce-1 rays)."""
+TT_TRACE_ADAPTIVE_ORDER (csrc/tt_order.hip): a flagged launch records per-64-ray-chunk costs, the
+next flagged launch of the same bounce index dequeues its chunks longest-first. Only which lane
+traces which ray changes, so every flagged launch must be byte-identical to the unflagged one (which
+the parity suites pin against the oracle). Every record's hit fields start as a sentinel, so a ray
+the reordered dequeue skipped would show. Covered: the full-frame 8x8 tile swizzle and compacted
+lists; ragged counts (the partial last chunk must stay last); counts below one chunk per segment; a
+screen-size change (costs dropped); the material-check kernel form; _PrimaryTriangleInfo at bounce 0
+and the GlobalColors-gated form at bounce 1; C2 at 1080p (primary + its compacted bounce-1 rays).
+
+tt_trace_closest_hits: the compact hit-record stream the multi-GPU gather sends."""
 import numpy as np
 import pytest
 
@@ -107,3 +108,42 @@ def test_adaptive_order_c2_1080p_primary_and_bounce(engine):
     colors = torch.zeros(WH * 64, dtype=torch.uint8, device=base.device)
     colors.view(torch.float32).view(WH, 16)[:, 15] = -1.0  # Data.w = -1: info written for every ray
     _check_order_invariance(engine, base, nb, 1, W, H, colors=colors)
+
+
+def test_hit_stream_equals_ray_records(engine):
+    """tt_trace_closest_hits: hits_out[i] is ray i's RayData.hits (full frame, ragged compacted list, an
+    odd bounce's offset half, the adaptive-order kernel, the wide drain), and the rest of the outputs
+    equal tt_trace_closest's; refusals for host / misaligned streams."""
+    import torch
+
+    W, H = 256, 160
+    WH = W * H
+    base = _soup_frame(engine, W, H, seed=47, frames=1)
+    dev = base.device
+    cases = [(WH, 0, 0), (WH - 7, 0, 0), (4097, 0, ORD), (WH, 0, ORD)]
+    for n, bounce, flags in cases:
+        ref, ref_info = _run(engine, base, n, bounce, W, H, 0)
+        got = _sentinel(base.clone())
+        info = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+        hs = torch.full((n, 4), -1, dtype=torch.int32, device=dev)
+        for _ in range(2 if flags else 1):
+            engine.trace(got, n, bounce, FAR, W, H, info=info, device=True, flags=flags, hits_out=hs)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref) and torch.equal(info, ref_info), (n, flags)
+        assert torch.equal(hs, got.view(-1, 48)[:n, 32:48].contiguous().view(torch.int32)), (n, flags)
+    # bounce 1: the records live in the odd half (GlobalRays[W*H + i]); hits_out is indexed from 0
+    engine.trace(base, WH, 0, FAR, W, H, device=True)
+    nb = engine.enqueue_bounce(base, WH, 0, FAR, W, H, frames=1, max_bounce=2, device=True)
+    got = _sentinel(base.clone())
+    hs = torch.full((nb, 4), -1, dtype=torch.int32, device=dev)
+    engine.trace(got, nb, 1, FAR, W, H, device=True, hits_out=hs)
+    torch.cuda.synchronize()
+    assert torch.equal(hs, got.view(-1, 48)[WH:WH + nb, 32:48].contiguous().view(torch.int32))
+    # refusals: host pointers, a misaligned stream
+    host_rays = np.zeros(2 * WH, tthip.RAY_DTYPE)
+    hs = torch.zeros((WH + 1, 4), dtype=torch.int32, device=dev)
+    p = tthip.TraceParams(n_rays=WH, bounce=0, far_plane=FAR, screen_width=W, screen_height=H, flags=0)
+    assert engine.L.tt_trace_closest_hits(engine.h, tthip.C.byref(p), host_rays.ctypes.data, None, None,
+                                          hs.data_ptr()) == tthip.TT_ERR_INVALID_ARG
+    assert engine.trace(got, WH, 0, FAR, W, H, device=True, hits_out=hs.view(-1)[1:], check=False)[1] \
+        == tthip.TT_ERR_INVALID_ARG

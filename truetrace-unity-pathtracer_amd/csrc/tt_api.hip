@@ -1117,7 +1117,8 @@ void tt_ctx_set_error(tt_ctx* c, const char* msg) {                // tt_build.h
 // n_dev (nullable): the device-resident ray count (tt_trace_closest_indirect); p->n_rays is then the
 // capacity the launch covers, and the call is asynchronous with device pointers.
 static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_dev, tt_ray_data* rays,
-                                    uint32_t* info, const tt_col_data* colors, tt_stats* stats) {
+                                    uint32_t* info, const tt_col_data* colors, tt_stats* stats,
+                                    uint32_t* hits_out = nullptr) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or rays");
@@ -1144,6 +1145,11 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
         if (!dev) return fail(c, TT_ERR_INVALID_ARG, "a device-resident ray count needs TT_TRACE_DEVICE_PTRS");
         if (want_stats) return fail(c, TT_ERR_INVALID_ARG, "TT_TRACE_STATS needs a host ray count");
         if (!is_device_ptr(n_dev)) return fail(c, TT_ERR_INVALID_ARG, "the ray count pointer is not device memory");
+    }
+    if (hits_out) {
+        if (!dev) return fail(c, TT_ERR_INVALID_ARG, "a hit-record stream needs TT_TRACE_DEVICE_PTRS");
+        if (!is_device_ptr(hits_out)) return fail(c, TT_ERR_INVALID_ARG, "hits_out is not device memory");
+        if (reinterpret_cast<uintptr_t>(hits_out) % 16) return fail(c, TT_ERR_INVALID_ARG, "hits_out must be 16-byte aligned");
     }
     if (stats) std::memset(stats, 0, sizeof(*stats));
     if (p->n_rays == 0) return TT_OK;
@@ -1205,6 +1211,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
                       p->screen_height % 8 == 0) ? 1u : 0u;
     a.div_width = fastdiv_make(std::max(1u, p->screen_width));
     a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
+    a.hits_out = reinterpret_cast<uint4*>(hits_out);
     const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout ||
                           ((p->flags & TT_TRACE_IGNORE_GLASS) && c->host.any_atlas_shadow) ||
                           ((p->flags & TT_TRACE_IGNORE_BACKFACING) && p->bounce == 0);
@@ -1307,6 +1314,12 @@ extern "C" {
 tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
                            const tt_col_data* colors, tt_stats* stats) {
     return trace_closest_call(c, p, nullptr, rays, info, colors, stats);
+}
+
+tt_status tt_trace_closest_hits(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
+                                const tt_col_data* colors, uint32_t* hits_out) {
+    if (!hits_out) return c ? fail(c, TT_ERR_INVALID_ARG, "null hits_out") : TT_ERR_INVALID_ARG;
+    return trace_closest_call(c, p, nullptr, rays, info, colors, nullptr, hits_out);
 }
 
 tt_status tt_trace_closest_indirect(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_rays_dev, tt_ray_data* rays,

@@ -153,6 +153,7 @@ struct TraceArgs {
     // TT_TRACE_ADAPTIVE_ORDER (tt_trace_kernel_ord only)
     const uint32_t* order;       // nullable: work chunk -> ray chunk (64 rays), from tt_order_kernel
     uint32_t* chunk_cost;        // per ray chunk: max Reps of its rays (atomicMax, rays with Reps >= TT_ORDER_MIN_REPS)
+    uint4* hits_out;             // nullable (tt_trace_closest_hits): ray i's hit record also at hits_out[i]
 };
 
 // Adaptive-order builder (tt_order.hip): one block per scheduler segment sorts the segment's

@@ -59,7 +59,13 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
         }
     }
     const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
-    reinterpret_cast<uint4*>(R)[2] = make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+    const uint4 hit = make_uint4((uint32_t)best.mesh_id, (uint32_t)best.tri_id, __float_as_uint(best.t), uv);
+    reinterpret_cast<uint4*>(R)[2] = hit;
+    if (A.hits_out) {  // the compact record stream (multi-GPU gather): a raw buffer store, 32-bit offset
+        const u32x4 v = {hit.x, hit.y, hit.z, hit.w};
+        __builtin_amdgcn_raw_buffer_store_b128(v, buffer_rsrc(A.hits_out, 0x7fffffff), (ray_index - A.ray_offset) << 4,
+                                               0, 0);
+    }
     return best.t != A.far_plane;
 }
 

@@ -186,7 +186,7 @@ HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_des
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
                "tt_enqueue_diffuse_bounce", "tt_trace_closest_indirect", "tt_enqueue_diffuse_bounce_indirect",
                "tt_trace_shadow_ex_indirect", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics",
-               "tt_selftest_rcp"]
+               "tt_selftest_rcp", "tt_trace_closest_hits"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
@@ -282,6 +282,8 @@ def hip_lib():
             L.tt_trace_closest_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
             L.tt_trace_shadow_ex_indirect.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, vp, vp]
             L.tt_enqueue_diffuse_bounce_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, i32, i32, vp]
+        if hasattr(L, "tt_trace_closest_hits"):
+            L.tt_trace_closest_hits.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_scene_upload_texture_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
@@ -767,12 +769,15 @@ class Engine:
 
     def trace(self, rays, n_rays: int, bounce: int, far_plane: float, width: int, height: int, info=None,
               colors=None, flags: int = 0, device: bool = False, stats: bool = False, check: bool = True,
-              asynchronous: bool = False):
+              asynchronous: bool = False, hits_out=None):
         p = TraceParams(n_rays=n_rays, bounce=bounce, far_plane=far_plane, screen_width=width, screen_height=height,
                         flags=flags | (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_STATS if stats else 0)
                         | (TT_TRACE_ASYNC if asynchronous else 0))
         s = Stats()
-        st = self.L.tt_trace_closest(self.h, C.byref(p), _ptr(rays), _ptr(info), _ptr(colors), C.byref(s))
+        if hits_out is not None:  # tt_trace_closest_hits: also the compact hit-record stream (no stats)
+            st = self.L.tt_trace_closest_hits(self.h, C.byref(p), _ptr(rays), _ptr(info), _ptr(colors), _ptr(hits_out))
+        else:
+            st = self.L.tt_trace_closest(self.h, C.byref(p), _ptr(rays), _ptr(info), _ptr(colors), C.byref(s))
         if check:
             self._check(st, "tt_trace_closest")
         return (s, st) if not check else s
