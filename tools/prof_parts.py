@@ -42,7 +42,13 @@ def main():
            "step_span_ms": round((t1 - t0) / 1e6 / a.steps, 4),
            "per_stream_launch_ms": {f"stream {s} {k}": round(sum(v) / len(v), 4)
                                     for (s, k), v in sorted(per_stream.items())}}
-    single = rest[2 * a.warmup: 2 * (a.warmup + a.steps)]
+    # the single-stream leg: the launches after the last one on a part stream other than the first's
+    # (bench.py runs its steady-state steps, still in parts, in between)
+    part_streams = {r["Stream_Id"] for r in timed}
+    others = part_streams - {timed[0]["Stream_Id"]} if timed else set()
+    last_other = max((i for i, r in enumerate(rest) if r["Stream_Id"] in others), default=-1)
+    leg = rest[last_other + 1:]
+    single = leg[2 * a.warmup: 2 * (a.warmup + a.steps)]
     if single:
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in single]
         out["single_stream_avg_launch_ms"] = round(sum(d) / len(d), 4)
@@ -51,10 +57,14 @@ def main():
         b = json.loads(open(a.bench).read().strip().splitlines()[-1])
         rf = b["roofline"]
         out["bench_ms_per_step"] = b["ms_per_step"]
-        out["bench_achieved_GBs"] = rf["achieved"]
-        out["trace_achieved_GBs"] = round(rf["alg_bytes_per_step"] / (out["step_span_ms"] * 1e-3) / 1e9, 1)
+        hb = rf.get("hbm", rf)  # round 3: the algorithmic-bytes view moved to roofline.hbm
+        out["bench_achieved_alg_GBs"] = hb.get("achieved_alg_gbs", rf.get("achieved"))
+        out["trace_achieved_alg_GBs"] = round(hb["alg_bytes_per_step"] / (out["step_span_ms"] * 1e-3) / 1e9, 1)
         if rf.get("single_stream"):
             out["bench_single_stream_avg_launch_ms"] = rf["single_stream"]["avg_launch_ms"]
+        pl = rf.get("per_launch", {})
+        if pl:  # roofline.per_launch: HIP-event launch times of the single-stream leg, per kernel
+            out["bench_per_launch_ms"] = {v["kernel"]: v["launch_ms"] for v in pl.values()}
     print(json.dumps(out, indent=1))
 
 
