@@ -25,7 +25,11 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 SEED0 = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 # "variants": every case also draws the compile-time trace variants of GlobalDefines.cginc:4,11 as
 # launch flags (IgnoreGlassMain / IgnoreBackfacing, both, or neither) for its closest-hit traces
-VARIANTS = len(sys.argv) > 3 and sys.argv[3] == "variants"
+MODES = sys.argv[3].split(",") if len(sys.argv) > 3 else []
+VARIANTS = "variants" in MODES
+# "adaptive": every closest-hit launch runs twice with TT_TRACE_ADAPTIVE_ORDER (the second one dequeues
+# in the order the first one's costs give) and the second one's records are compared
+ADAPTIVE = "adaptive" in MODES
 FLAG_SETS = (0, tthip.TT_TRACE_IGNORE_GLASS, tthip.TT_TRACE_IGNORE_BACKFACING,
              tthip.TT_TRACE_IGNORE_GLASS | tthip.TT_TRACE_IGNORE_BACKFACING)
 eng = tthip.Engine(0)
@@ -36,7 +40,12 @@ def compare(sc, rays, n, bounce, W, H, info=True, flags=0):
     rg, rc = rays.copy(), rays.copy()
     ig = np.zeros((W * H, 4), np.uint32) if info else None
     ic = np.zeros((W * H, 4), np.uint32) if info else None
-    eng.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags)
+    if ADAPTIVE:
+        r0 = rays.copy()
+        eng.trace(r0, n, bounce, FAR, W, H, info=None, flags=flags | tthip.TT_TRACE_ADAPTIVE_ORDER)
+        eng.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags | tthip.TT_TRACE_ADAPTIVE_ORDER)
+    else:
+        eng.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags)
     st, _ = O.trace(sc, rc, n, bounce, FAR, W, H, info=ic, nthreads=CPU_THREADS, flags=flags)
     assert st == 0
     off = W * H if bounce % 2 else 0
