@@ -135,7 +135,13 @@ def main():
     pb = brec["PixelIndex"] if "PixelIndex" in brec.dtype.names else brec["pixel_index"]
     M, Mr = tile_map(p1, s1), tile_map(p1, r1n)
     first = np.arange(0, nb, 64)
-    est = {"first_rec_other_frame": M[tile_of(pb[first])],
+    # the SAME frame's primary costs per 8x8 tile (known before the bounce launch), through the
+    # chunk's first record / all its records
+    Mp = tile_map(base[:n0]["PixelIndex"], steps0)
+    Mpr = tile_map(base[:n0]["PixelIndex"], cnt["node_visits"].astype(np.int64))
+    est = {"prim_tile_first_rec": Mp[tile_of(pb[first])], "prim_tile_allrec": chunk_max(Mp[tile_of(pb)], nb),
+           "prim_reps_tile_first_rec": Mpr[tile_of(pb[first])],
+           "first_rec_other_frame": M[tile_of(pb[first])],
            "reps_first_rec_other_frame": Mr[tile_of(pb[first])],
            "allrec_other_frame": chunk_max(M[tile_of(pb)], nb)}
     run("bounce1", brec, nb, 1, steps1, None, est)
