@@ -1,13 +1,14 @@
 #!/bin/bash
 # Unit-utilisation PMC passes (as tools/pmc_units.sh) on one BASELINE config's traces
-# (tools/prof_config.py). Usage: tools/pmc_units_config.sh c4 <outdir>
+# (tools/prof_config.py). Usage: tools/pmc_units_config.sh c4 <outdir> [extra prof_config args, e.g. --adaptive]
 set -e
 CFG=$1
 OUT=${2:-gpurun_out/pmcu_$CFG}
+EXTRA="${@:3}"
 mkdir -p $OUT
 ROOT=${GRAFT_REPO_ROOT:-$PWD}
 cd /tmp && export TMPDIR=/tmp && cd $ROOT
-run() { name=$1; shift; timeout -k 10 400 rocprofv3 --pmc "$@" -d $OUT/$name -o $name --output-format csv -- python tools/prof_config.py $CFG --reps 1 > $OUT/$name.log 2>&1; }
+run() { name=$1; shift; timeout -k 10 400 rocprofv3 --pmc "$@" -d $OUT/$name -o $name --output-format csv -- python tools/prof_config.py $CFG --reps ${REPS:-1} $EXTRA > $OUT/$name.log 2>&1; }
 run u1 TA_TA_BUSY TA_BUSY GRBM_GUI_ACTIVE
 run u2 TD_TD_BUSY TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ
 run u3 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F SQ_INSTS_VALU_INT SQ_INSTS_VALU_ADD_F SQ_INSTS_VALU_MUL_F SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU

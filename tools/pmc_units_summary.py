@@ -41,10 +41,17 @@ def main():
     for f in sorted(glob.glob(f"{root}/*/*_counter_collection.csv")):
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):
-            if "tt_trace_kernel<false" not in r["Kernel_Name"]:
+            if "tt_trace_kernel<false" not in r["Kernel_Name"] and "tt_trace_kernel_ord<" not in r["Kernel_Name"]:
                 continue
             per[(r["Kernel_Name"].split("(")[0], r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-        for (k, _), cs in per.items():
+        # an adaptive-order kernel's first dispatch has no order yet (it only records costs): skip it
+        first_ord = {}
+        for (k, d) in per:
+            if "_ord<" in k:
+                first_ord[k] = min(first_ord.get(k, int(d)), int(d))
+        for (k, d), cs in per.items():
+            if k in first_ord and int(d) == first_ord[k] and sum(1 for kk, _ in per if kk == k) > 1:
+                continue
             for c, v in cs.items():
                 agg[k][c].append(v)
     rays = bench_rays(root)
