@@ -209,6 +209,20 @@ namespace TrueTrace.Hip
             return s;
         }
 
+        /// TraceDevice that also writes ray i's 16-byte hit record to hitsOut[i] (HIP device memory, 16-byte
+        /// aligned, nRays records): the buffer a multi-GPU host gathers (tt_trace_closest_hits).
+        public void TraceDeviceHits(IntPtr globalRays, uint nRays, int curBounce, float farPlane, int width, int height,
+                                    IntPtr hitsOut, IntPtr primaryInfo = default, IntPtr globalColors = default,
+                                    TTTraceFlags extra = TTTraceFlags.None, bool async = false)
+        {
+            var p = new TTTraceParams
+            {
+                nRays = nRays, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width, screenHeight = (uint)height,
+                flags = extra | TTTraceFlags.DevicePtrs | (async ? TTTraceFlags.Async : 0)
+            };
+            Check(Native.tt_trace_closest_hits(m_ctx, ref p, globalRays, primaryInfo, globalColors, hitsOut));
+        }
+
         /// kernel_trace as DispatchIndirect: the ray count is the uint at `nRaysDevice` (HIP device memory,
         /// written by an earlier operation on the context stream, e.g. the shading pass's BufferSizes),
         /// clamped to `capacity`; the call never waits for the GPU.
