@@ -929,6 +929,71 @@ def main():
         f"tris/ray {s_bnc.tri_tests / max(parts[0].nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}"
         f"; parts {P}" + (f"; {world}-sample frame (spp)" if spp else ""))
 
+    # The two auxiliary legs that trace the metric's own scene -- the single-stream leg (N = 1) and the
+    # sample-sharded layout (N > 1) -- run BEFORE the timed region: they are sustained GPU work, so the
+    # timed steps start with the engine clocks settled instead of ramping through the first ~30 ms
+    # (profiles/r03/warm/: the same 20-step window reads 0.805-0.816 ms per step straight after setup
+    # and 0.783-0.787 once ~40 ms of work has run; the steady-state leg after the region, 0.779).
+    # the kernel alone, one launch at a time (N = 1, P > 1): the full frame in the kernel's own tile
+    # order on the shared stream, per-launch HIP events -- the per-launch roofline and the launch
+    # times rocprofv3 reports for this command's trace kernels
+    single = None
+    frame_rays, frame_nb = (rays, nb) if (P == 1 and world == 1) else (None, None)  # a full-frame, traced ray buffer (N = 1)
+    if world == 1 and P > 1:
+        one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
+        o_prim = eng.trace(one, WH, 0, far, W, H, info=info, device=True, stats=True)
+        onb = eng.enqueue_bounce(one, WH, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+        o_bnc = eng.trace(one, onb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
+        frame_rays, frame_nb = one, onb
+        if not args.no_single:
+            launches = [lambda: eng.trace(one, WH, 0, far, W, H, info=info, device=True, asynchronous=True),
+                        lambda: eng.trace(one, onb, 1, far, W, H, info=info, colors=colors_t, device=True,
+                                          asynchronous=True)]
+            oms = timed_launches(eng, launches, args.warmup, args.steps)
+            o_avg = float(oms.mean())
+            o_ach = ((alg_bytes(o_prim, 0, WH) + alg_bytes(o_bnc, 1, onb)) / 2.0) / (o_avg * 1e-3) / 1e9
+            single = {"achieved": round(o_ach, 1), "frac": round(o_ach / HBM_PEAK_GBS, 4),
+                      "avg_launch_ms": round(o_avg, 4), "trace_ms_primary": round(float(oms[:, 0].mean()), 4),
+                      "trace_ms_bounce": round(float(oms[:, 1].mean()), 4),
+                      "mrays_s": round((WH + onb) / float(oms.sum(1).mean()) / 1e3, 2)}
+            log(f"single-stream leg (the kernel alone, one launch at a time): {single}")
+
+    # secondary N > 1 layout: every rank traces its own full-frame jittered sample (weak scaling)
+    sample_sharded = None
+    if tiles:
+        srays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(srays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
+        eng.trace(srays, WH, 0, far, W, H, device=True)
+        snb = eng.enqueue_bounce(srays, WH, 0, far, W, H, frames=rank, max_bounce=1, device=True)
+
+        def sstep():
+            eng.trace(srays, WH, 0, far, W, H, info=info, device=True, asynchronous=True)
+            eng.trace(srays, snb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
+
+        for _ in range(args.warmup):
+            sstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            sstep()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        st = torch.tensor([time.perf_counter() - ts, float((WH + snb) * args.steps)], dtype=torch.float64,
+                          device=red_dev)
+        tmax = st[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        rsum = st[1:].clone()
+        dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
+        sample_sharded = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
+                          "scaling": "weak", "ranks": world,
+                          "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4)}
+        del srays
+        log(f"sample-sharded (weak) layout: {sample_sharded}")
+
     G = make_gather(parts) if tiles else None
     sizes, gather_list = None, None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
@@ -1035,66 +1100,6 @@ def main():
         log(f"strong-scaling tile layout: {strong}")
     for e_, _ in lanes[1:]:
         e_.close()
-
-    # the kernel alone, one launch at a time (N = 1, P > 1): the full frame in the kernel's own tile
-    # order on the shared stream, per-launch HIP events -- the per-launch roofline and the launch
-    # times rocprofv3 reports for this command's trace kernels
-    single = None
-    frame_rays, frame_nb = (rays, nb) if (P == 1 and world == 1) else (None, None)  # a full-frame, traced ray buffer (N = 1)
-    if world == 1 and P > 1:
-        one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
-        o_prim = eng.trace(one, WH, 0, far, W, H, info=info, device=True, stats=True)
-        onb = eng.enqueue_bounce(one, WH, 0, far, W, H, frames=frames, max_bounce=1, device=True)
-        o_bnc = eng.trace(one, onb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
-        frame_rays, frame_nb = one, onb
-        if not args.no_single:
-            launches = [lambda: eng.trace(one, WH, 0, far, W, H, info=info, device=True, asynchronous=True),
-                        lambda: eng.trace(one, onb, 1, far, W, H, info=info, colors=colors_t, device=True,
-                                          asynchronous=True)]
-            oms = timed_launches(eng, launches, args.warmup, args.steps)
-            o_avg = float(oms.mean())
-            o_ach = ((alg_bytes(o_prim, 0, WH) + alg_bytes(o_bnc, 1, onb)) / 2.0) / (o_avg * 1e-3) / 1e9
-            single = {"achieved": round(o_ach, 1), "frac": round(o_ach / HBM_PEAK_GBS, 4),
-                      "avg_launch_ms": round(o_avg, 4), "trace_ms_primary": round(float(oms[:, 0].mean()), 4),
-                      "trace_ms_bounce": round(float(oms[:, 1].mean()), 4),
-                      "mrays_s": round((WH + onb) / float(oms.sum(1).mean()) / 1e3, 2)}
-            log(f"single-stream leg (the kernel alone, one launch at a time): {single}")
-
-    # secondary N > 1 layout: every rank traces its own full-frame jittered sample (weak scaling)
-    sample_sharded = None
-    if tiles:
-        srays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(srays, c2w, ip, W, H, 0.3, far, jitter=1, frames=rank, max_bounce=1, device=True)
-        eng.trace(srays, WH, 0, far, W, H, device=True)
-        snb = eng.enqueue_bounce(srays, WH, 0, far, W, H, frames=rank, max_bounce=1, device=True)
-
-        def sstep():
-            eng.trace(srays, WH, 0, far, W, H, info=info, device=True, asynchronous=True)
-            eng.trace(srays, snb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
-
-        for _ in range(args.warmup):
-            sstep()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        ts = time.perf_counter()
-        for _ in range(args.steps):
-            sstep()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        st = torch.tensor([time.perf_counter() - ts, float((WH + snb) * args.steps)], dtype=torch.float64,
-                          device=red_dev)
-        tmax = st[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        rsum = st[1:].clone()
-        dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
-        sample_sharded = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
-                          "scaling": "weak", "ranks": world,
-                          "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4)}
-        del srays
-        log(f"sample-sharded (weak) layout: {sample_sharded}")
 
     # ---- auxiliary: the UseReCur ray generation (no jitter), primary + bounce 1, N=1
     recur = None
