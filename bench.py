@@ -163,7 +163,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 streams.append(torch.cuda.Stream(dev))
                 e1 = tthip.Engine(dev.index, stream=streams[-1].cuda_stream)
                 extra_engs.append(e1)
-                e1.upload(sc)
+                e1.share_scene(eng)  # one scene copy for all parts (tt_ctx_share_scene)
             chains = [[] for _ in range(n_frames)]  # chains[f]: per part (engine, bufs, counts)
             base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
             for f in range(n_frames):
@@ -442,7 +442,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         s1 = torch.cuda.Stream(dev)
         e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
         try:
-            e1.upload(sc)
+            e1.share_scene(eng)
             chains = []
             for e, pp in zip((eng, e1), ttdist.part_pixels(W, H, world, rank, 2)):
                 chains.append((e, full.view(WH, 48)[torch.from_numpy(pp).to(dev)].contiguous(), int(pp.shape[0])))
@@ -788,7 +788,7 @@ def main():
         while len(lanes) <= s:
             st = torch.cuda.Stream(dev)
             e = tthip.Engine(gpu, stream=st.cuda_stream)
-            e.upload(scene)
+            e.share_scene(eng)  # the parts trace ONE scene copy (tt_ctx_share_scene): one cache footprint
             lanes.append((e, st))
         return lanes[s]
 
@@ -1274,7 +1274,7 @@ def main():
                                     else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
                    "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it"
                              + (f" (part 0 of {P}: its launches overlap the other parts')" if P > 1 else ""),
-                   "parts_per_rank": P, "samples_per_frame": world if spp else 1,
+                   "parts_per_rank": P, "parts_share_one_scene_copy": P > 1, "samples_per_frame": world if spp else 1,
                    "dist_world_size": dist_world, "dist_backend": backend if dist_world else None,
                    "launcher": ("bench.py self-launch" if os.environ.get("TT_BENCH_SELF_LAUNCHED") == "1"
                                 else "external (WORLD_SIZE set)" if env_world is not None else "none (1 rank)"),

@@ -119,6 +119,8 @@ namespace TrueTrace.Hip
         // tt_trace_closest + each ray's 16-B hit record written contiguously to hitsOut (the multi-GPU gather's input)
         [DllImport(Lib)] public static extern TTStatus tt_trace_closest_hits(IntPtr ctx, ref TTTraceParams p,
             IntPtr globalRays, IntPtr primaryInfo, IntPtr globalColors, IntPtr hitsOut);
+        // dst traces src's scene buffers (no copy) on its own stream: the parts of a frame share one scene
+        [DllImport(Lib)] public static extern TTStatus tt_ctx_share_scene(IntPtr dst, IntPtr src);
         [DllImport(Lib)] public static extern TTStatus tt_async_overflows(IntPtr ctx, out ulong count);
         [DllImport(Lib)] public static extern IntPtr tt_ctx_stream(IntPtr ctx);
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
@@ -208,6 +210,11 @@ namespace TrueTrace.Hip
             Check(Native.tt_trace_closest_dev(m_ctx, ref p, globalRays, primaryInfo, globalColors, out TTStats s));
             return s;
         }
+
+        /// Trace `lender`'s scene on this context's stream without a copy (tt_ctx_share_scene): e.g. the second
+        /// half of a frame traced concurrently on its own context. Update the scene through the lender;
+        /// dispose this context before the lender.
+        public void ShareScene(TrueTraceHip lender) { Check(Native.tt_ctx_share_scene(m_ctx, lender.m_ctx)); }
 
         /// TraceDevice that also writes ray i's 16-byte hit record to hitsOut[i] (HIP device memory, 16-byte
         /// aligned, nRays records): the buffer a multi-GPU host gathers (tt_trace_closest_hits).

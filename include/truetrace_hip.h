@@ -342,6 +342,16 @@ tt_status tt_scene_read_tris(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cud
  * Synchronizes the context stream. */
 tt_status tt_scene_read_nodes(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cwbvh_node* out);
 
+/* Makes `dst` trace `src`'s scene: no copy, the device buffers of src's last tt_scene_upload (and its
+ * atlases) are read by dst's launches on dst's own stream. For several contexts tracing one scene
+ * concurrently (e.g. a frame's tile-interleaved parts, one context and stream each): one cache
+ * footprint instead of one per context. Scene updates (tt_scene_update_*, tt_tlas_refit,
+ * tt_blas_refit) go through src and are seen by dst; ordering them against dst's launches is the
+ * caller's (streams). While borrowers exist, src refuses tt_scene_upload / the atlas uploads and
+ * tt_ctx_destroy (destroy the borrowers first); dst refuses every scene-mutating call. Same device;
+ * src must not itself borrow. Synchronizes both streams. */
+tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src);
+
 /* Bytes of HBM the scene occupies (device copies + derived traversal layouts). */
 tt_status tt_scene_bytes(const tt_ctx* ctx, uint64_t* bytes);
 

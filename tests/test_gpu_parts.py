@@ -79,3 +79,66 @@ def test_two_parts_on_two_streams_equal_one_launch():
     finally:
         for e in engines:
             e.close()
+
+
+def test_shared_scene_traces_identically_and_refuses_mutation(engine):
+    """tt_ctx_share_scene: a context tracing another's scene buffers (no copy, its own stream) writes the
+    same records as the owner (primary with info, bounce 1), sees the owner's in-place updates (a
+    _MeshData rewrite + TLAS refit), and the guards hold: no scene mutation through the borrower, no
+    re-upload or destroy of the lender while it lends, no sharing from a borrower."""
+    import torch
+
+    W, H = 320, 200
+    WH = W * H
+    dev = torch.device("cuda:0")
+    sc = tthip.single_object_scene(tthip.Mesh.soup(51, 20000, 1.0, 0.1))
+    c2w, ip = tthip.unity_camera((0.3, 0.2, 2.4), (-0.1, -0.05, -1.0), (0, 1, 0), 60.0, W, H, 0.05, FAR)
+    st_a, st_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    lender = tthip.Engine(0, stream=st_a.cuda_stream)
+    borrower = tthip.Engine(0, stream=st_b.cuda_stream)
+    try:
+        lender.upload(sc)
+        borrower.share_scene(lender)
+        base = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        lender.generate(base, c2w, ip, W, H, 0.05, FAR, jitter=1, frames=0, max_bounce=2, device=True)
+        torch.cuda.synchronize(dev)
+
+        def both(bounce, n, src):
+            outs = []
+            for e in (lender, borrower):
+                r = src.clone()
+                info = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+                e.trace(r, n, bounce, FAR, W, H, info=info if bounce == 0 else None, device=True)
+                outs.append((r, info))
+            torch.cuda.synchronize(dev)
+            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), bounce
+            return outs[0][0]
+
+        traced = both(0, WH, base)
+        nb = lender.enqueue_bounce(traced, WH, 0, FAR, W, H, frames=0, max_bounce=2, device=True)
+        both(1, nb, traced)
+        # an in-place update through the lender is what the borrower traces next
+        md = sc.meshdata.copy()
+        w2l = md["W2L"][0].astype(np.float64).reshape(4, 4).T
+        shift = np.eye(4)
+        shift[:3, 3] = [-0.05, 0.0, 0.02]
+        md["W2L"][0] = tthip.unity_colmajor(w2l @ shift)
+        lender.update_meshdata(0, md)
+        torch.cuda.synchronize(dev)
+        moved = both(0, WH, base)
+        assert not torch.equal(moved, traced)  # the update changed the hits, on both contexts alike
+        # guards
+        assert borrower.L.tt_scene_update_meshdata(borrower.h, 0, 1, md.ctypes.data) == tthip.TT_ERR_INVALID_ARG
+        assert lender.L.tt_scene_upload(lender.h, sc.nodes.ctypes.data, len(sc.nodes), sc.tris.ctypes.data,
+                                        len(sc.tris), sc.tlas.ctypes.data, len(sc.tlas), sc.meshdata.ctypes.data,
+                                        len(sc.meshdata), sc.materials.ctypes.data,
+                                        len(sc.materials)) == tthip.TT_ERR_INVALID_ARG
+        assert lender.L.tt_ctx_destroy(lender.h) == tthip.TT_ERR_INVALID_ARG  # still lending
+        third = tthip.Engine(0)
+        try:
+            assert third.L.tt_ctx_share_scene(third.h, borrower.h) == tthip.TT_ERR_INVALID_ARG  # no chains
+        finally:
+            third.close()
+    finally:
+        lender.close()  # closes its borrower first
+    assert borrower.h is None

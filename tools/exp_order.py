@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ranks", type=int, default=1, help="trace rank 0's 64x64-tile shard of an N-GPU frame")
     ap.add_argument("--primary-only", action="store_true", help="flag the primary launches only")
+    ap.add_argument("--share", action="store_true", help="parts > 0 trace part 0's scene (tt_ctx_share_scene)")
     args = ap.parse_args()
     import torch
     import tthip
@@ -50,7 +51,10 @@ def main():
     for s in range(P):
         st = main_stream if s == 0 else torch.cuda.Stream(dev)
         e = tthip.Engine(0, stream=st.cuda_stream)
-        e.upload(sc)
+        if s > 0 and args.share:
+            e.share_scene(engs[0])
+        else:
+            e.upload(sc)
         engs.append(e)
         streams.append(st)
     c2w, ip = view.camera(W, H)
@@ -93,7 +97,7 @@ def main():
                 engs[s].trace(buf, m, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True,
                               flags=0 if args.primary_only else flags)
 
-    out = {"tool": "tools/exp_order.py", "config": args.config, "parts": P, "ranks": args.ranks, "primary_only": args.primary_only, "width": W, "height": H,
+    out = {"tool": "tools/exp_order.py", "config": args.config, "parts": P, "ranks": args.ranks, "primary_only": args.primary_only, "share": args.share, "width": W, "height": H,
            "rays_per_step": rays_per, "rounds": []}
     for r in range(args.rounds):
         rec = {}
@@ -119,7 +123,7 @@ def main():
             rec[mode] = d
         out["rounds"].append(rec)
         print(r, json.dumps(rec), file=sys.stderr, flush=True)
-    for e in engs:
+    for e in reversed(engs):
         e.close()
     print(json.dumps(out, indent=1))
 

@@ -54,10 +54,18 @@ struct DevBuf {
         n = count;
         return hipSuccess;
     }
+    bool own = true;  // false: borrowed from another context's scene (tt_ctx_share_scene), never freed here
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && own) (void)hipFree(p);
         p = nullptr;
         n = 0;
+        own = true;
+    }
+    void borrow(const DevBuf& o) {
+        release();
+        p = o.p;
+        n = o.n;
+        own = false;
     }
 };
 
@@ -179,7 +187,21 @@ struct tt_ctx {
         bool valid = false;
     };
     OrderSlot ord[8];
+    // tt_ctx_share_scene: a borrower traces its lender's scene buffers (read-only) on its own stream
+    tt_ctx* lender = nullptr;  // set on a borrower
+    int borrowers = 0;         // on a lender: contexts currently tracing its scene
 };
+
+// Scene-mutating calls are refused on a borrower (update the lender), and reallocating ones on a
+// lender that has borrowers (their pointers would dangle).
+#define TT_REFUSE_BORROWER(c)                                                                              \
+    do {                                                                                                   \
+        if ((c)->lender) return fail((c), TT_ERR_INVALID_ARG, "this context traces a shared scene: update the context it shares from"); \
+    } while (0)
+#define TT_REFUSE_LENDER(c)                                                                                \
+    do {                                                                                                   \
+        if ((c)->borrowers > 0) return fail((c), TT_ERR_INVALID_ARG, "other contexts share this scene: destroy them (or re-share) first"); \
+    } while (0)
 
 // Per-call timing ring entries (tt_timing_read) around device work issued on the context stream.
 static hipError_t ring_open(tt_ctx* c, uint32_t& slot) {
@@ -597,8 +619,10 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
 
 tt_status tt_ctx_destroy(tt_ctx* c) {
     if (!c) return TT_ERR_INVALID_ARG;
+    if (c->borrowers > 0) return fail(c, TT_ERR_INVALID_ARG, "other contexts share this scene: destroy them first");
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->lender) c->lender->borrowers--;
     c->nodes.release();
     c->tris_raw.release();
     c->tris.release();
@@ -717,6 +741,8 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
                           uint32_t n_tris, const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md,
                           uint32_t n_mesh, const tt_material* mats, uint32_t n_mat) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
+    TT_REFUSE_LENDER(c);
     if (!nodes || !n_nodes || !tris || !n_tris || !tlas || !n_tlas || !md || !n_mesh || (n_mat && !mats))
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_upload: null or empty buffer");
     TT_HIP(c, hipSetDevice(c->device));
@@ -779,6 +805,8 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
 
 tt_status tt_scene_upload_alpha_atlas(tt_ctx* c, const uint8_t* texels, uint32_t width, uint32_t height) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
+    TT_REFUSE_LENDER(c);
     if (!texels || width == 0 || height == 0 || (uint64_t)width * height > 0x7fffffffull)
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_upload_alpha_atlas: empty or oversized atlas");
     TT_HIP(c, hipSetDevice(c->device));
@@ -793,6 +821,8 @@ tt_status tt_scene_upload_alpha_atlas(tt_ctx* c, const uint8_t* texels, uint32_t
 
 tt_status tt_scene_upload_texture_atlas(tt_ctx* c, const uint16_t* rgba_half, uint32_t width, uint32_t height) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
+    TT_REFUSE_LENDER(c);
     if (!rgba_half || width == 0 || height == 0 || (uint64_t)width * height > 0x7fffffffull / 8u)
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_upload_texture_atlas: empty or oversized atlas");
     TT_HIP(c, hipSetDevice(c->device));
@@ -805,8 +835,51 @@ tt_status tt_scene_upload_texture_atlas(tt_ctx* c, const uint16_t* rgba_half, ui
     return TT_OK;
 }
 
+// Traces on `dst` read `src`'s scene buffers (nodes, triangles, TLAS, mesh and leaf records, materials,
+// atlases) instead of a copy: two contexts tracing concurrently (the two-part layout) then share one
+// cache footprint. The borrowed buffers are read-only for `dst`.
+tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
+    if (!dst || !src) return TT_ERR_INVALID_ARG;
+    if (dst == src) return fail(dst, TT_ERR_INVALID_ARG, "a context cannot share its own scene");
+    if (!src->has_scene) return fail(dst, TT_ERR_NO_SCENE, "the source context has no scene");
+    if (src->lender) return fail(dst, TT_ERR_INVALID_ARG, "the source context shares another context's scene");
+    if (dst->borrowers > 0) return fail(dst, TT_ERR_INVALID_ARG, "other contexts share this context's scene");
+    if (dst->device != src->device) return fail(dst, TT_ERR_INVALID_ARG, "the contexts are on different devices");
+    TT_HIP(dst, hipSetDevice(dst->device));
+    TT_HIP(dst, hipStreamSynchronize(dst->stream));  // nothing of dst's still reads its old scene
+    TT_HIP(dst, hipStreamSynchronize(src->stream));  // src's upload has landed
+    if (dst->lender) dst->lender->borrowers--;
+    dst->nodes.borrow(src->nodes);
+    dst->tris_raw.borrow(src->tris_raw);
+    dst->tris.borrow(src->tris);
+    dst->tlas.borrow(src->tlas);
+    dst->mesh_raw.borrow(src->mesh_raw);
+    dst->mesh.borrow(src->mesh);
+    dst->leaf.borrow(src->leaf);
+    dst->mat_tag.borrow(src->mat_tag);
+    dst->mat_cut.borrow(src->mat_cut);
+    dst->mat_glass.borrow(src->mat_glass);
+    dst->tex.borrow(src->tex);
+    dst->atlas.borrow(src->atlas);
+    dst->tex_w = src->tex_w;
+    dst->tex_h = src->tex_h;
+    dst->atlas_w = src->atlas_w;
+    dst->atlas_h = src->atlas_h;
+    dst->host = src->host;
+    dst->any_invisible = src->any_invisible;
+    dst->any_shadow_skip = src->any_shadow_skip;
+    dst->any_atlas_shadow = src->any_atlas_shadow;
+    dst->any_cutout = src->any_cutout;
+    dst->has_scene = true;
+    dst->scene_gen++;
+    dst->lender = src;
+    src->borrowers++;
+    return TT_OK;
+}
+
 tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh, uint32_t flags) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!mesh_aabbs || n_tlas_nodes == 0 || n_tlas_nodes > c->host.nodes.size())
         return fail(c, TT_ERR_INVALID_ARG, "tt_tlas_refit: null boxes or n_tlas_nodes out of range");
@@ -841,6 +914,7 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
 tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* vertices, const int32_t* indices,
                         const int32_t* leaf_of_triangle) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !vertices || !indices || !leaf_of_triangle || !p->n_tris || !p->n_vertices || p->vertex_stride < 6)
         return fail(c, TT_ERR_INVALID_ARG, "tt_blas_refit: null array, empty mesh or vertex_stride < 6");
@@ -998,6 +1072,7 @@ tt_status refresh_leaves(tt_ctx* c) {
 
 tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!nodes || (uint64_t)first + count > c->host.nodes.size())
         return fail(c, TT_ERR_INVALID_ARG, "node update range out of bounds");
@@ -1034,6 +1109,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
 
 tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, const tt_mesh_data* md) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_BORROWER(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!md || (uint64_t)first + count > c->host.mesh.size())
         return fail(c, TT_ERR_INVALID_ARG, "meshdata update range out of bounds");

@@ -186,7 +186,7 @@ HIP_SYMBOLS = ["tt_abi_version", "tt_device_count", "tt_ctx_create", "tt_ctx_des
                "tt_trace_closest", "tt_sync", "tt_ctx_stream", "tt_resolve_normals", "tt_generate_primary",
                "tt_enqueue_diffuse_bounce", "tt_trace_closest_indirect", "tt_enqueue_diffuse_bounce_indirect",
                "tt_trace_shadow_ex_indirect", "tt_timing_reset", "tt_timing_read", "tt_scene_validate", "tt_trace_diagnostics",
-               "tt_selftest_rcp", "tt_trace_closest_hits"]
+               "tt_selftest_rcp", "tt_trace_closest_hits", "tt_ctx_share_scene"]
 SCENE_SYMBOLS = ["tt_blas_build", "tt_blas_get_info", "tt_blas_copy", "tt_blas_free", "tt_scene_assemble",
                  "tt_scene_build_get_info", "tt_scene_build_copy", "tt_scene_build_free", "tt_pack_octahedral",
                  "tt_bvh2_build", "tt_dotnet_sort_by_key", "tt_synth_cornell", "tt_synth_soup", "tt_synth_sponza",
@@ -282,6 +282,8 @@ def hip_lib():
             L.tt_trace_closest_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
             L.tt_trace_shadow_ex_indirect.argtypes = [vp, C.POINTER(ShadowParams), vp, vp, vp, vp, vp, vp]
             L.tt_enqueue_diffuse_bounce_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, i32, i32, vp]
+        if hasattr(L, "tt_ctx_share_scene"):
+            L.tt_ctx_share_scene.argtypes = [vp, vp]
         if hasattr(L, "tt_trace_closest_hits"):
             L.tt_trace_closest_hits.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
@@ -689,8 +691,23 @@ class Engine:
 
     def close(self):
         if getattr(self, "h", None):
+            for b in list(getattr(self, "_borrowers", [])):  # contexts tracing this one's scene go first
+                e = b()
+                if e is not None:
+                    e.close()
             self.L.tt_ctx_destroy(self.h)
             self.h = None
+            self._lender = None
+
+    def share_scene(self, src: "Engine"):
+        """tt_ctx_share_scene: trace `src`'s scene (its device buffers, no copy) on this context's stream."""
+        import weakref
+
+        self._check(self.L.tt_ctx_share_scene(self.h, src.h), "tt_ctx_share_scene")
+        self._lender = src  # keeps the lender alive while this context reads its buffers
+        if not hasattr(src, "_borrowers"):
+            src._borrowers = []
+        src._borrowers.append(weakref.ref(self))
 
     __del__ = close
 
