@@ -25,10 +25,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--bench", default="")
+    ap.add_argument("--single-last", action="store_true",
+                    help="round-2 bench order (the single-stream leg after the timed region)")
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace))
             if r["Kernel_Name"].split("(")[0].replace(" ", "") in TIMED]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    lead = []
+    if not a.single_last:  # round 3: bench.py runs the single-stream leg BEFORE the timed parts
+        lead, rows = rows[:2 * (a.warmup + a.steps)], rows[2 * (a.warmup + a.steps):]
     n_parts = 2 * a.parts * (a.warmup + a.steps)
     parts, rest = rows[:n_parts], rows[n_parts:]
     timed = parts[2 * a.parts * a.warmup:]
@@ -42,12 +47,15 @@ def main():
            "step_span_ms": round((t1 - t0) / 1e6 / a.steps, 4),
            "per_stream_launch_ms": {f"stream {s} {k}": round(sum(v) / len(v), 4)
                                     for (s, k), v in sorted(per_stream.items())}}
-    # the single-stream leg: the launches after the last one on a part stream other than the first's
-    # (bench.py runs its steady-state steps, still in parts, in between)
-    part_streams = {r["Stream_Id"] for r in timed}
-    others = part_streams - {timed[0]["Stream_Id"]} if timed else set()
-    last_other = max((i for i, r in enumerate(rest) if r["Stream_Id"] in others), default=-1)
-    leg = rest[last_other + 1:]
+    if a.single_last:
+        # the single-stream leg: the launches after the last one on a part stream other than the first's
+        # (bench.py runs its steady-state steps, still in parts, in between)
+        part_streams = {r["Stream_Id"] for r in timed}
+        others = part_streams - {timed[0]["Stream_Id"]} if timed else set()
+        last_other = max((i for i, r in enumerate(rest) if r["Stream_Id"] in others), default=-1)
+        leg = rest[last_other + 1:]
+    else:
+        leg = lead
     single = leg[2 * a.warmup: 2 * (a.warmup + a.steps)]
     if single:
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in single]
