@@ -420,7 +420,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     import ttconfigs as T
     import ttdist
 
-    rec, ok, ms, ms_parts = {}, 1, 0.0, 0.0
+    rec, ok, ms, ms_parts, ms_parts_ad = {}, 1, 0.0, 0.0, 0.0
     W, H, far = 3840, 2160, T.FAR
     WH = W * H
     try:
@@ -462,6 +462,28 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
             torch.cuda.synchronize(dev)
             ms_parts = (time.perf_counter() - tp) * 1e3 / reps
             hits_parts = torch.cat([buf.view(m, 48)[:, 32:48] for _, buf, m in chains]).contiguous()
+            # the same layout with the adaptive dequeue order: two jittered frames
+            # alternate, so every launch is ordered by the previous frame's costs
+            full1 = torch.zeros_like(full)
+            eng.generate(full1, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=1, max_bounce=1, device=True)
+            chains1 = [(e, full1.view(WH, 48)[torch.from_numpy(pp).to(dev)].contiguous(), int(pp.shape[0]))
+                       for e, pp in zip((eng, e1), ttdist.part_pixels(W, H, world, rank, 2))]
+            torch.cuda.synchronize(dev)
+
+            def frame_ad(k):
+                for e, buf, m in (chains if k % 2 == 0 else chains1):
+                    e.trace(buf, m, 0, far, W, H, device=True, asynchronous=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER)
+
+            for k in range(max(2, args.warmup)):
+                frame_ad(k)
+            torch.cuda.synchronize(dev)
+            reps_ad = max(4, args.steps // 2) // 2 * 2
+            tp = time.perf_counter()
+            for k in range(reps_ad):
+                frame_ad(k)
+            torch.cuda.synchronize(dev)
+            ms_parts_ad = (time.perf_counter() - tp) * 1e3 / reps_ad
+            del full1, chains1
         finally:
             e1.close()
     except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
@@ -474,7 +496,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     if flags[0].item() < 1.0:
         return rec if rank == 0 else None
-    tp_max = torch.tensor([ms_parts], dtype=torch.float64, device=red_dev)
+    tp_max = torch.tensor([ms_parts, ms_parts_ad], dtype=torch.float64, device=red_dev)
     dist.all_reduce(tp_max, op=dist.ReduceOp.MAX)
     hits = mine.view(n, 48)[:, 32:48].contiguous().view(torch.int32).to(red_dev)
     torch.cuda.synchronize(dev)
@@ -493,14 +515,17 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     eng.trace(full, WH, 0, far, W, H, device=True)
     ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
     frame_ms = float(t_max.item())
-    frame_ms_parts = float(tp_max.item())
+    frame_ms_parts, frame_ms_parts_ad = float(tp_max[0].item()), float(tp_max[1].item())
     rec.update(config="c5_san_miguel_4k_tiles", ranks=world, tile=64, frame_rays=WH,
                trace_ms_slowest_rank=round(frame_ms, 4), trace_ms_rank0=round(ms, 4),
                mrays_s_frame=round(WH / frame_ms / 1e3, 1), gather_ms=round(gather_ms, 3),
                identical_to_1gpu=bool(np.array_equal(frame, ref)),
                two_parts=dict(ms_per_frame_slowest_rank=round(frame_ms_parts, 4),
                               mrays_s_frame=round(WH / frame_ms_parts / 1e3, 1),
-                              identical_to_1gpu=bool(np.array_equal(frame2, ref))))
+                              identical_to_1gpu=bool(np.array_equal(frame2, ref))),
+               two_parts_adaptive_order=dict(ms_per_frame_slowest_rank=round(frame_ms_parts_ad, 4),
+                                             mrays_s_frame=round(WH / frame_ms_parts_ad / 1e3, 1),
+                                             note="frames_accumulated 0 / 1 alternating; results order-independent"))
     log(f"c5 tiles: {rec}")
     return rec
 
