@@ -655,6 +655,11 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->cam.release();
     c->counter.release();
     c->spill.release();
+    for (auto& os : c->ord) {  // TT_TRACE_ADAPTIVE_ORDER state
+        os.cost[0].release();
+        os.cost[1].release();
+        os.order.release();
+    }
     if (c->ctl) (void)hipFree(c->ctl);
     for (uint32_t i = 0; i < TT_RING; i++) {
         if (c->ring0[i]) (void)hipEventDestroy(c->ring0[i]);
