@@ -1266,6 +1266,20 @@ def main():
     dom = max(valu.values(), key=lambda v: v["launch_ms"]) if valu else None
 
     ms_per_step = elapsed * 1e3 / args.steps
+    # the whole step (all parts' launches, overlapped) against the time its VALU work takes with VALU
+    # issue 100% busy at 2.4 GHz: rank 0's primary and bounce-1 rays x their issue cycles per ray
+    step_valu = None
+    cyc1 = units_k.get("1", {}).get("valu_issue_cycles_per_ray")
+    cyc2 = units_k.get("2", {}).get("valu_issue_cycles_per_ray")
+    if cyc1 and cyc2:
+        rays1, rays2 = int(sum(p.n for p in parts)), int(sum(p.nb for p in parts))
+        ceil_ms = (rays1 * cyc1 + rays2 * cyc2) / (1024 * 2.4e9) * 1e3
+        step_valu = {"ceiling_ms": round(ceil_ms, 4), "ms_per_step": round(ms_per_step, 4),
+                     "frac": round(ceil_ms / ms_per_step, 4), "rays": [rays1, rays2],
+                     "note": "rank 0's step (all its parts' primary + bounce-1 launches, overlapped on their streams) "
+                             "against the time the same rays' VALU work takes at 100% VALU issue on 1024 SIMDs at "
+                             "2.4 GHz (issue cycles per ray from the PMC pass); includes launch gaps and drains"
+                             + ("" if world == 1 else " and the gather")}
     result = {
         "metric": METRIC,
         "value": round(total_rays / elapsed / 1e6, 2),
@@ -1334,7 +1348,7 @@ def main():
                                      "from L2 / MALL: traffic = fabric bytes per launch from " + (traffic_src or "no PMC pass")
                                      + " (2 x FETCH_SIZE + WRITE_SIZE, includes Infinity-Cache hits), so HBM does not "
                                      "bind this loop"},
-                     "units_busy": units, "single_stream": single,
+                     "units_busy": units, "single_stream": single, "step": step_valu,
                      "note": "bound = VALU issue (DESIGN.md §3.1): achieved = rays/s of the dominant launch (one launch "
                              "at a time, HIP events on its stream), peak = the same launch's VALU-issue ceiling = 1024 "
                              "SIMDs x 2.4 GHz / VALU issue cycles per ray from the PMC pass " + (units_src or "(none)")
