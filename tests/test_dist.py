@@ -100,7 +100,7 @@ def test_spp_units_partition_every_sample_and_balance_ranks():
     cover every (sample, pixel) exactly once and give every rank one frame's worth of tiles."""
     W, H = 1920, 1080
     T = ttdist.n_tiles(W, H)
-    for world, parts in ((1, 2), (2, 2), (3, 2), (4, 3), (8, 3)):
+    for world, parts in ((1, 2), (2, 2), (3, 2), (4, 3), (8, 2), (8, 3)):
         seen = np.zeros((world, W * H), np.int32)
         for r in range(world):
             units = ttdist.spp_part_pixels(W, H, world, r, parts)
@@ -122,7 +122,7 @@ def test_spp_units_partition_every_sample_and_balance_ranks():
 
 def test_spp_assemble_reorders_gathered_blocks():
     W, H = 200, 130
-    for world, parts in ((2, 2), (3, 1), (4, 3)):
+    for world, parts in ((2, 2), (3, 1), (4, 3), (8, 2)):
         frames = np.zeros((world, W * H, 4), np.uint32)
         frames[:, :, 0] = np.arange(W * H, dtype=np.uint32)[None, :]
         frames[:, :, 1] = np.arange(world, dtype=np.uint32)[:, None]
@@ -171,14 +171,25 @@ def _spp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_two_rank_spp_shard_and_gather():
+def _run_spp_ranks(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_spp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_spp_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=180)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) is True
+
+
+def test_gloo_two_rank_spp_shard_and_gather():
+    _run_spp_ranks(2)
+
+
+def test_gloo_eight_rank_spp_shard_and_gather():
+    """The largest --gpus the driver runs (N = 8), rehearsed on the CPU: 8 gloo ranks, each traces its
+    (sample, tile) units of an 8-sample frame with the oracle, one gather to rank 0, every sample
+    reassembled identical to a whole-frame trace."""
+    _run_spp_ranks(8)
