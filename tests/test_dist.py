@@ -82,7 +82,7 @@ def test_part_split_partitions_each_rank_and_reassembles():
     streams; the parts cover the rank's pixels exactly and the per-rank blocks (parts back to back)
     reassemble into the screen."""
     W, H = 1920, 1080
-    for world, parts in ((2, 2), (8, 2), (4, 3), (1, 2)):
+    for world, parts in ((2, 2), (8, 2), (4, 3), (8, 3), (1, 2)):
         frame = np.zeros((W * H, 4), np.uint32)
         frame[:, 0] = np.arange(W * H, dtype=np.uint32)  # every pixel's record names its pixel
         blocks, sizes = [], []
