@@ -9,7 +9,8 @@
       1920x1080: full-frame primary and bounce-1 parity, BLAS-entry counts equal.
   C5  San-Miguel-shaped 10M tris at 3840x2160: determinism, full-frame oracle parity, and
       the 8-GPU 64x64 round-robin tile sharding reassembled byte-identical to
-      the single-launch frame (hit records and _PrimaryTriangleInfo).
+      the single-launch frame (hit records and _PrimaryTriangleInfo); the bench's C5 frame
+      (MaxBounce 1, frames 0), whose one direction.x == +0 ray is the launch's longest chain.
 """
 import numpy as np
 import pytest
@@ -80,8 +81,13 @@ def test_c4_bistro_1080p_full_parity(engine, c4):
     assert s2.node_visits == int(cnt2["node_visits"].sum())
 
 
-def test_c5_san_miguel_4k_full_parity_and_tile_sharded(engine):
-    sc = T.c5_san_miguel()
+@pytest.fixture(scope="module")
+def c5():
+    return T.c5_san_miguel()
+
+
+def test_c5_san_miguel_4k_full_parity_and_tile_sharded(engine, c5):
+    sc = c5
     assert len(sc.tris) == T.C5_TRIS
     W, H = T.C5_VIEW.width, T.C5_VIEW.height
     WH = W * H
@@ -116,3 +122,30 @@ def test_c5_san_miguel_4k_full_parity_and_tile_sharded(engine):
     full = ttdist.assemble_tiles(parts, W, H, world)
     assert np.array_equal(full, a["hits"][:WH])
     assert np.array_equal(info_t, info_a)
+
+
+def test_c5_bench_frame_degenerate_ray(engine, c5):
+    """bench.py's C5 frame (Generate with MaxBounce 1, frames 0) holds exactly one ray with an
+    exactly-zero direction component (pixel 5,652,973: direction.x == +0, inf / NaN x slabs, 529
+    node visits and 1,134 triangle tests -- profiles/r03/c5_tail/). That ray, every other ray within
+    1e-6 of an axis, and a strided sample of the frame: traced on the GPU as one compacted list and by
+    the oracle, byte-identical records and equal per-ray work."""
+    W, H = T.C5_VIEW.width, T.C5_VIEW.height
+    WH = W * H
+    c2w, ip = T.C5_VIEW.camera()
+    engine.upload(c5)
+    rays = np.zeros(2 * WH, tthip.RAY_DTYPE)
+    engine.generate(rays, c2w, ip, W, H, T.NEAR, FAR, jitter=1, frames=0, max_bounce=1)
+    d = rays["direction"][:WH]
+    zero = np.where((d == 0).any(axis=1))[0]
+    assert zero.tolist() == [5652973] and d[5652973, 0] == 0 and not np.signbit(d[5652973, 0])
+    near_axis = np.where((np.abs(d) < 1e-6).any(axis=1))[0]
+    pick = np.unique(np.concatenate([near_axis, np.arange(0, WH, 101)]))
+    n = len(pick)
+    sub = np.zeros(2 * n, tthip.RAY_DTYPE)
+    sub[:n] = rays[pick]
+    rg, rc, ig, ic, s, cnt = trace_both(engine, c5, sub, n, 0, n, 1, info=False, upload=False)
+    assert_same(rg, rc, ig, ic, 0, n)
+    assert s.node_visits == int(cnt["node_visits"].sum()) and s.tri_tests == int(cnt["tri_tests"].sum())
+    k = int(np.searchsorted(pick, 5652973))
+    assert cnt["node_visits"][k] == 529 and cnt["tri_tests"][k] == 1134
