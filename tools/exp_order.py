@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ranks", type=int, default=1, help="trace rank 0's 64x64-tile shard of an N-GPU frame")
     ap.add_argument("--primary-only", action="store_true", help="flag the primary launches only")
+    ap.add_argument("--tile", type=int, default=64, help="part split tile edge (ttdist's default 64)")
     ap.add_argument("--share", action="store_true", help="parts > 0 trace part 0's scene (tt_ctx_share_scene)")
     args = ap.parse_args()
     import torch
@@ -63,9 +64,9 @@ def main():
     colors["Data"][:, 3] = 1.0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
     if args.ranks > 1:
-        pix_parts = ttdist.part_pixels(W, H, args.ranks, 0, P)
+        pix_parts = ttdist.part_pixels(W, H, args.ranks, 0, P, tile=args.tile)
     else:
-        pix_parts = [np.arange(WH)] if P == 1 else ttdist.part_pixels(W, H, 1, 0, P)
+        pix_parts = [np.arange(WH)] if P == 1 else ttdist.part_pixels(W, H, 1, 0, P, tile=args.tile)
     # frames[f][s] = (rays buffer, n primary, n bounce) of part s of jittered frame f
     frames = []
     full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
