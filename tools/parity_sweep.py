@@ -30,6 +30,10 @@ VARIANTS = "variants" in MODES
 # "adaptive": every closest-hit launch runs twice with TT_TRACE_ADAPTIVE_ORDER (the second one dequeues
 # in the order the first one's costs give) and the second one's records are compared
 ADAPTIVE = "adaptive" in MODES
+# "axis": degenerate directions -- every third case looks exactly down an axis (whole rows / columns of
+# rays with a zero component), and 3% of every case's primary rays get one or two components replaced by
+# +0.0 or -0.0 (inf / NaN slabs in the node test: the C5 bench frame's longest ray is one of these)
+AXIS = "axis" in MODES
 FLAG_SETS = (0, tthip.TT_TRACE_IGNORE_GLASS, tthip.TT_TRACE_IGNORE_BACKFACING,
              tthip.TT_TRACE_IGNORE_GLASS | tthip.TT_TRACE_IGNORE_BACKFACING)
 eng = tthip.Engine(0)
@@ -92,8 +96,18 @@ for k in range(N):
         pos = np.array([0.3, 0.2, 3.0]) + rng.normal(0, 0.3, 3)
         look = np.array([0.0, 0.0, -1.0]) + rng.normal(0, 0.1, 3)
     W, H = int(rng.integers(40, 256)), int(rng.integers(24, 160))
+    if AXIS and k % 3 == 1:
+        look = np.zeros(3)
+        look[int(rng.integers(0, 3))] = float(rng.choice([-1.0, 1.0]))
+        if abs(look[1]) == 1.0:  # not parallel to the camera's up vector
+            look = np.array([0.0, 0.0, -1.0])
     c2w, ip = tthip.unity_camera(pos, look, (0, 1, 0), float(rng.uniform(30, 90)), W, H, 0.05, FAR)
     rays = O.generate(c2w, ip, W, H, 0.05, FAR)
+    if AXIS:
+        pick = np.nonzero(rng.random(W * H) < 0.03)[0]
+        for i in pick:
+            for ax in rng.choice(3, size=int(rng.integers(1, 3)), replace=False):
+                rays["direction"][i, ax] = np.float32(-0.0) if rng.random() < 0.5 else np.float32(0.0)
     eng.upload(sc)
     b0, rg = compare(sc, rays, W * H, 0, W, H, flags=flags)
     # bounce 1 from the GPU's primary hits (identical to the oracle's when b0 == 0)
