@@ -346,8 +346,12 @@ tt_status tt_scene_read_nodes(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cw
  * atlases) are read by dst's launches on dst's own stream. For several contexts tracing one scene
  * concurrently (e.g. a frame's tile-interleaved parts, one context and stream each): one cache
  * footprint instead of one per context. Scene updates (tt_scene_update_*, tt_tlas_refit,
- * tt_blas_refit) go through src and are seen by dst; ordering them against dst's launches is the
- * caller's (streams). While borrowers exist, src refuses tt_scene_upload / the atlas uploads and
+ * tt_blas_refit) go through src and are seen by dst, ordered by the library in call order across
+ * the two streams, with no host synchronization: a dst launch (trace, shadow, resolve, enqueue,
+ * scene read) waits on the GPU for every src mutation called before it, and a src mutation waits
+ * for every dst launch called before it (HIP events; the reference's per-frame "rewrite the TLAS
+ * and _MeshData, then dispatch", AssetManager.cs:1821-1825, needs no caller-side ordering). While
+ * borrowers exist, src refuses tt_scene_upload / the atlas uploads and
  * tt_ctx_destroy (destroy the borrowers first); dst refuses every scene-mutating call. Same device;
  * src must not itself borrow. Synchronizes both streams. */
 tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src);

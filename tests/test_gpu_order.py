@@ -147,3 +147,43 @@ def test_hit_stream_equals_ray_records(engine):
                                           hs.data_ptr()) == tthip.TT_ERR_INVALID_ARG
     assert engine.trace(got, WH, 0, FAR, W, H, device=True, hits_out=hs.view(-1)[1:], check=False)[1] \
         == tthip.TT_ERR_INVALID_ARG
+
+
+def test_hit_stream_keeps_the_records_of_rays_without_one(engine):
+    """A ray that ends without a record -- the Reps < 1000 bound (IntersectionKernels.compute:155) or a
+    stack overflow -- leaves RayData.hits as it was, and its hits_out entry is that same unchanged word
+    (not whatever the stream buffer held: the stream starts as a sentinel unlike RayData.hits).
+    Reps: the C2 1080p frame with UseReCur's unjittered camera, whose column x = W/2 has direction.z ==
+    -0.0 and one Reps-exhausting ray (bench.py aux_recur_unjittered); overflow: the 17-level KAT."""
+    import torch
+
+    import kat_cases as K
+
+    dev = torch.device("cuda:0")
+    W, H = 1920, 1080
+    WH = W * H
+    engine.upload(T.c2_sponza())
+    c2w, ip = T.C2_VIEW.camera(W, H)
+    base = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+    engine.generate(base, c2w, ip, W, H, T.NEAR, FAR, jitter=0, frames=0, max_bounce=1, device=True)
+    st = engine.trace(base.clone(), WH, 0, FAR, W, H, device=True, stats=True)
+    assert st.reps_exhausted >= 1
+    for flags in (0, ORD, ORD):  # natural order; adaptive (records costs), adaptive (sorted order)
+        got = base.clone()
+        hs = torch.full((WH, 4), 0x5A5A5A5A, dtype=torch.int32, device=dev)
+        engine.trace(got, WH, 0, FAR, W, H, device=True, flags=flags, hits_out=hs)
+        torch.cuda.synchronize()
+        assert torch.equal(hs, got.view(-1, 48)[:WH, 32:48].contiguous().view(torch.int32)), flags
+    # the exhausted ray's record is the one Generate wrote (the miss record), in both outputs
+    unchanged = (got.view(-1, 48)[:WH, 32:48] == base.view(-1, 48)[:WH, 32:48]).all(1)
+    assert int(unchanged.sum()) >= 1
+    # stack overflow: one ray, 17 nested levels
+    sc, rays = K.stack_overflow_scene(17)
+    engine.upload(sc)
+    r = torch.from_numpy(rays.view(np.uint8).copy()).to(dev)
+    hs = torch.full((1, 4), 0x5A5A5A5A, dtype=torch.int32, device=dev)
+    _, code = engine.trace(r, 1, 0, FAR, 1, 1, device=True, hits_out=hs, check=False)
+    torch.cuda.synchronize()
+    assert code == tthip.TT_ERR_STACK_OVERFLOW
+    assert torch.equal(hs, r.view(-1, 48)[:1, 32:48].contiguous().view(torch.int32))
+    assert torch.equal(r, torch.from_numpy(rays.view(np.uint8).copy()).to(dev))  # RayData untouched

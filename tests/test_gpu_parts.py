@@ -142,3 +142,90 @@ def test_shared_scene_traces_identically_and_refuses_mutation(engine):
     finally:
         lender.close()  # closes its borrower first
     assert borrower.h is None
+
+
+def test_shared_scene_mutations_are_ordered_without_host_sync():
+    """The per-frame pattern of the reference (AssetManager.cs:1821-1825: rewrite _MeshData, refit the
+    TLAS, then dispatch the traces) across a lender and a borrower on two streams, with NO host
+    synchronization between the calls, each stream kept busy by a queue of full-frame traces so an
+    unordered call would overtake:
+      * lender update_meshdata + tlas_refit, then a borrower trace -> the records of the moved scene;
+      * a borrower trace, then lender update_meshdata + tlas_refit -> the records of the scene as it was
+        when the trace was called.
+    Expected records come from one synchronous context tracing both poses."""
+    import torch
+
+    from test_gpu_parity import refit_scene
+
+    rng = np.random.default_rng(7)
+    a = refit_scene(33)
+    b = refit_scene(33, offsets=rng.normal(0, 1.5, (120, 3)))
+    dev = torch.device("cuda:0")
+    W, H = 160, 90
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    BW, BH = 1920, 1080  # the busy work: full-frame traces of the same scene
+    bc2w, bip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, BW, BH, 0.3, FAR)
+    boxes = {k: torch.from_numpy(np.ascontiguousarray(s.meta["mesh_aabbs"], np.float32)).to(dev)
+             for k, s in (("a", a), ("b", b))}
+    md = {"a": a.meshdata, "b": b.meshdata}
+
+    ref = tthip.Engine(0)
+    try:
+        ref.upload(a)
+        rays0 = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
+        big = torch.zeros(2 * BW * BH * 48, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        ref.generate(rays0, c2w, ip, W, H, 0.3, FAR, jitter=1, frames=0, max_bounce=1, device=True)
+        ref.generate(big, bc2w, bip, BW, BH, 0.3, FAR, jitter=1, frames=0, max_bounce=1, device=True)
+        exp = {}
+        for k in ("a", "b"):
+            ref.update_meshdata(0, md[k])
+            ref.tlas_refit(a.tlas_nodes, boxes[k], device=True)
+            r = rays0.clone()
+            torch.cuda.synchronize(dev)
+            ref.trace(r, W * H, 0, FAR, W, H, device=True)
+            exp[k] = r.view(-1, 48)[: W * H, 32:48].clone()
+        assert not torch.equal(exp["a"], exp["b"])  # the move changes the hits
+    finally:
+        ref.close()
+
+    st_a, st_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    lender = tthip.Engine(0, stream=st_a.cuda_stream)
+    borrower = tthip.Engine(0, stream=st_b.cuda_stream)
+
+    def busy(e, k=12):
+        for _ in range(k):
+            e.trace(big, BW * BH, 0, FAR, BW, BH, device=True, asynchronous=True)
+
+    def pose(k, asynchronous):
+        lender.update_meshdata(0, md[k])
+        lender.tlas_refit(a.tlas_nodes, boxes[k], device=True, asynchronous=asynchronous)
+
+    try:
+        lender.upload(a)
+        borrower.share_scene(lender)
+        for rep in range(2):
+            # lender mutates (behind its busy queue), then the borrower traces at once
+            pose("a", False)
+            r = rays0.clone()
+            torch.cuda.synchronize(dev)
+            busy(lender)
+            pose("b", True)
+            borrower.trace(r, W * H, 0, FAR, W, H, device=True, asynchronous=True)
+            torch.cuda.synchronize(dev)
+            assert torch.equal(r.view(-1, 48)[: W * H, 32:48], exp["b"]), ("lender -> borrower", rep)
+            # the borrower traces (behind its busy queue), then the lender mutates at once
+            r2 = rays0.clone()
+            torch.cuda.synchronize(dev)
+            busy(borrower)
+            borrower.trace(r2, W * H, 0, FAR, W, H, device=True, asynchronous=True)
+            pose("a", True)
+            torch.cuda.synchronize(dev)
+            assert torch.equal(r2.view(-1, 48)[: W * H, 32:48], exp["b"]), ("borrower -> lender", rep)
+            r3 = rays0.clone()
+            torch.cuda.synchronize(dev)
+            borrower.trace(r3, W * H, 0, FAR, W, H, device=True)
+            assert torch.equal(r3.view(-1, 48)[: W * H, 32:48], exp["a"]), ("after both", rep)
+    finally:
+        lender.close()
+    assert borrower.h is None

@@ -95,6 +95,7 @@ struct SceneHost {
     std::vector<BlasKey> blas_ok;       // sorted: (root, NodeOffset, TriOffset) triples walked and valid
     std::vector<uint8_t> is_tlas_node;  // node reached by the TLAS-level walk
     std::vector<uint32_t> tlas_nodes;   // the same, as a list
+    std::vector<uint8_t> is_blas_node;  // node reached by a validated BLAS walk (never TLAS-only updated)
 };
 
 }  // namespace
@@ -190,6 +191,16 @@ struct tt_ctx {
     // tt_ctx_share_scene: a borrower traces its lender's scene buffers (read-only) on its own stream
     tt_ctx* lender = nullptr;  // set on a borrower
     int borrowers = 0;         // on a lender: contexts currently tracing its scene
+    // Cross-stream order of a shared scene (the reference rewrites the TLAS and _MeshData every frame,
+    // then dispatches, AssetManager.cs:1821-1825): a lender mutation waits for the borrowers' launches
+    // already enqueued, and a borrower launch waits for the lender's mutations already enqueued.
+    std::vector<tt_ctx*> borrower_list;  // lender: the contexts tracing its scene
+    hipEvent_t ev_scene = nullptr;       // lender: after its last scene mutation (recorded while borrowed)
+    uint64_t scene_mut = 0;              // lender: mutations recorded in ev_scene so far
+    hipEvent_t ev_read = nullptr;        // borrower: after its last launch that reads the shared scene
+    uint64_t read_seq = 0;               // borrower: reads recorded in ev_read so far
+    uint64_t read_waited = 0;            // borrower: reads the lender's stream already waits for
+    uint64_t mut_waited = 0;             // borrower: lender mutations this stream already waits for
 };
 
 // Scene-mutating calls are refused on a borrower (update the lender), and reallocating ones on a
@@ -214,6 +225,51 @@ static hipError_t ring_close(tt_ctx* c, uint32_t slot) {
     c->ev0 = c->ring0[slot];
     c->ev1 = c->ring1[slot];
     return e;
+}
+
+// Shared-scene ordering (tt_ctx_share_scene). A borrower's launch that reads the lender's scene
+// buffers is bracketed by scene_read_begin / _end, a lender's scene mutation by scene_write_begin /
+// _end. Events are only waited on when something new was recorded since the last wait, so a borrower
+// of a static scene adds one event record per launch and no waits.
+static hipError_t lazy_event(hipEvent_t& ev) {
+    return ev ? hipSuccess : hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+}
+static hipError_t scene_read_begin(tt_ctx* c) {
+    const tt_ctx* L = c->lender;
+    if (!L || L->scene_mut == c->mut_waited) return hipSuccess;
+    const hipError_t e = hipStreamWaitEvent(c->stream, L->ev_scene, 0);
+    if (e == hipSuccess) c->mut_waited = L->scene_mut;
+    return e;
+}
+static hipError_t scene_read_end(tt_ctx* c) {
+    if (!c->lender) return hipSuccess;
+    hipError_t e = lazy_event(c->ev_read);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_read, c->stream);
+    if (e == hipSuccess) c->read_seq++;
+    return e;
+}
+static hipError_t scene_write_begin(tt_ctx* c) {
+    for (tt_ctx* b : c->borrower_list) {
+        if (b->read_seq == b->read_waited) continue;
+        const hipError_t e = hipStreamWaitEvent(c->stream, b->ev_read, 0);
+        if (e != hipSuccess) return e;
+        b->read_waited = b->read_seq;
+    }
+    return hipSuccess;
+}
+static hipError_t scene_write_end(tt_ctx* c) {
+    if (c->borrower_list.empty()) return hipSuccess;  // a later borrower syncs the stream when it shares
+    hipError_t e = lazy_event(c->ev_scene);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_scene, c->stream);
+    if (e == hipSuccess) c->scene_mut++;
+    return e;
+}
+static void unlink_borrower(tt_ctx* b) {
+    tt_ctx* L = b->lender;
+    if (!L) return;
+    L->borrowers--;
+    L->borrower_list.erase(std::remove(L->borrower_list.begin(), L->borrower_list.end(), b), L->borrower_list.end());
+    b->lender = nullptr;
 }
 
 namespace {
@@ -252,6 +308,7 @@ struct Validator {
 
     uint32_t max_matdat = 0;
     std::vector<uint32_t> tlas_visit;  // nodes reached by the last TLAS-level walk
+    std::vector<uint32_t> blas_visit;  // nodes reached by the BLAS-level walks of this validator
     std::vector<SceneHost::BlasKey> keys;  // BLAS (root, NodeOffset, TriOffset) walked by run()
     bool walk(uint32_t root, uint32_t node_offset, uint32_t tri_offset, bool tlas_level) {
         epoch++;
@@ -268,6 +325,7 @@ struct Validator {
             if (epoch_of[ni] == epoch) continue;
             epoch_of[ni] = epoch;
             if (tlas_level) tlas_visit.push_back(ni);
+            else blas_visit.push_back(ni);
             const tt_cwbvh_node& n = s.nodes[ni];
             const uint32_t imask = n.e_imask >> 24;
             for (int k = 0; k < 8; k++) {
@@ -371,6 +429,8 @@ void remember_validation(SceneHost& h, const Validator& v) {
     h.is_tlas_node.assign(h.nodes.size(), 0u);
     h.tlas_nodes = v.tlas_visit;
     for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
+    h.is_blas_node.assign(h.nodes.size(), 0u);
+    for (uint32_t n : v.blas_visit) h.is_blas_node[n] = 1u;
 }
 
 tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris, uint32_t n_tris,
@@ -622,7 +682,9 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     if (c->borrowers > 0) return fail(c, TT_ERR_INVALID_ARG, "other contexts share this scene: destroy them first");
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->lender) c->lender->borrowers--;
+    unlink_borrower(c);
+    if (c->ev_scene) (void)hipEventDestroy(c->ev_scene);
+    if (c->ev_read) (void)hipEventDestroy(c->ev_read);
     c->nodes.release();
     c->tris_raw.release();
     c->tris.release();
@@ -853,7 +915,7 @@ tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
     TT_HIP(dst, hipSetDevice(dst->device));
     TT_HIP(dst, hipStreamSynchronize(dst->stream));  // nothing of dst's still reads its old scene
     TT_HIP(dst, hipStreamSynchronize(src->stream));  // src's upload has landed
-    if (dst->lender) dst->lender->borrowers--;
+    unlink_borrower(dst);
     dst->nodes.borrow(src->nodes);
     dst->tris_raw.borrow(src->tris_raw);
     dst->tris.borrow(src->tris);
@@ -879,6 +941,9 @@ tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
     dst->scene_gen++;
     dst->lender = src;
     src->borrowers++;
+    src->borrower_list.push_back(dst);
+    dst->mut_waited = src->scene_mut;  // everything src enqueued so far has landed (synchronized above)
+    dst->read_waited = dst->read_seq;
     return TT_OK;
 }
 
@@ -909,9 +974,11 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
         d_boxes = c->st_boxes.p;
     }
     uint32_t slot;
+    TT_HIP(c, scene_write_begin(c));
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
     TT_HIP(c, ring_close(c, slot));
+    TT_HIP(c, scene_write_end(c));
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -983,10 +1050,12 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     a.tris88 = c->tris_raw.p + tri_base;
     a.tripos = c->tris.p + tri_base;
     uint32_t slot;
+    TT_HIP(c, scene_write_begin(c));
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_blas_construct(a, c->stream));
     TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
     TT_HIP(c, ring_close(c, slot));
+    TT_HIP(c, scene_write_end(c));
     if (!(p->flags & TT_TRACE_ASYNC) || !dev) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -997,6 +1066,7 @@ tt_status tt_scene_read_tris(tt_ctx* c, uint32_t first, uint32_t count, tt_cuda_
     if (!out || (uint64_t)first + count > c->host.n_tris)
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_tris: range out of bounds");
     TT_HIP(c, hipSetDevice(c->device));
+    TT_HIP(c, scene_read_begin(c));
     TT_HIP(c, hipMemcpyAsync(out, c->tris_raw.p + first, sizeof(tt_cuda_triangle) * count, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
@@ -1008,6 +1078,7 @@ tt_status tt_scene_read_nodes(tt_ctx* c, uint32_t first, uint32_t count, tt_cwbv
     if (!out || (uint64_t)first + count > c->host.nodes.size())
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_nodes: range out of bounds");
     TT_HIP(c, hipSetDevice(c->device));
+    TT_HIP(c, scene_read_begin(c));
     TT_HIP(c, hipMemcpyAsync(out, c->nodes.p + first, sizeof(tt_cwbvh_node) * count, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
@@ -1088,8 +1159,11 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     // A rewrite of TLAS-level nodes only (the per-frame case: BVH8AggregatedBuffer.SetData of the
     // TLAS region) re-walks the TLAS level; the BLASes were validated at upload and are unchanged.
     // Any other rewrite re-validates the whole scene.
+    // (a node that a validated BLAS also reaches -- a TLAS rewrite may have re-pointed a child into one
+    // -- takes the full check: its triangle indices matter at BLAS level)
     bool tlas_only = true;
-    for (uint32_t i = first; i < first + count && tlas_only; i++) tlas_only = h.is_tlas_node[i] != 0;
+    for (uint32_t i = first; i < first + count && tlas_only; i++)
+        tlas_only = h.is_tlas_node[i] != 0 && h.is_blas_node[i] == 0;
     Validator v(h);
     const bool ok = tlas_only ? v.walk(0, 0, 0, true) : v.run();
     if (!ok) {
@@ -1106,8 +1180,10 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, hipSetDevice(c->device));
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, nodes, sizeof(tt_cwbvh_node) * count, pinned));
+    TT_HIP(c, scene_write_begin(c));
     TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, pinned, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
+    TT_HIP(c, scene_write_end(c));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
     return TT_OK;
 }
@@ -1141,6 +1217,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
         if (!v.walk_mesh(r))
             return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: %s", v.why.c_str());
         added.push_back(k);
+        for (uint32_t n : v.blas_visit) h.is_blas_node[n] = 1u;  // (kept even if a later record fails: conservative)
     }
     if (!added.empty()) {
         h.blas_ok.insert(h.blas_ok.end(), added.begin(), added.end());
@@ -1152,6 +1229,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     // (MeshGpu) and patches the TLAS leaf records that name an updated mesh, on the stream
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, md, sizeof(tt_mesh_data) * count, pinned));
+    TT_HIP(c, scene_write_begin(c));
     TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, pinned, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
     const uint32_t n_tlas = (uint32_t)h.tlas.size();
@@ -1159,6 +1237,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream, c->mesh_raw.p, c->mesh.p,
                        c->leaf.p, c->tlas.p, n_tlas, first, count);
     TT_HIP(c, hipGetLastError());
+    TT_HIP(c, scene_write_end(c));
     return TT_OK;
 }
 
@@ -1231,6 +1310,8 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
         if (!dev) return fail(c, TT_ERR_INVALID_ARG, "a hit-record stream needs TT_TRACE_DEVICE_PTRS");
         if (!is_device_ptr(hits_out)) return fail(c, TT_ERR_INVALID_ARG, "hits_out is not device memory");
         if (reinterpret_cast<uintptr_t>(hits_out) % 16) return fail(c, TT_ERR_INVALID_ARG, "hits_out must be 16-byte aligned");
+        // the kernel stores record i at the 32-bit byte offset 16 i of a 2 GiB buffer descriptor
+        if (p->n_rays > (1u << 27)) return fail(c, TT_ERR_INVALID_ARG, "a hit-record stream holds at most 2^27 rays per call");
     }
     if (stats) std::memset(stats, 0, sizeof(*stats));
     if (p->n_rays == 0) return TT_OK;
@@ -1334,10 +1415,13 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     static const bool always_reset = std::getenv("TT_CTL_ALWAYS_RESET") != nullptr;  // A/B knob
     if (!async || want_stats || !c->ctl_zero[ci] || always_reset)
         TT_HIP(c, hipMemsetAsync(c->ctl + ci, 0, sizeof(TraceControl), c->stream));
+    TT_HIP(c, scene_read_begin(c));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     c->ctl_zero[0] = c->ctl_zero[1] = false;
     static const bool record_only = std::getenv("TT_ORDER_RECORD_ONLY") != nullptr;  // A/B knob: costs, no order
+    if (os && os->valid && record_only)  // the order kernel (which clears the map this launch fills) is skipped
+        TT_HIP(c, hipMemsetAsync(os->cost[os->cur ^ 1u].p, 0, sizeof(uint32_t) * n_chunks, c->stream));
     if (os && os->valid && !record_only) {
         OrderArgs o;
         o.cost = os->cost[os->cur].p;
@@ -1356,6 +1440,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     c->ctl_zero[ci ^ 1u] = true;
     c->ctl_cur = ci ^ 1u;
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
+    TT_HIP(c, scene_read_end(c));
     c->ring_n++;
     c->ev0 = c->ring0[slot];
     c->ev1 = c->ring1[slot];
@@ -1515,12 +1600,14 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));
     TT_HIP(c, hipMemsetAsync(c->ctl + c->ctl_cur, 0, sizeof(TraceControl), c->stream));
+    TT_HIP(c, scene_read_begin(c));
     const uint32_t slot = c->ring_n % TT_RING;
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     c->ctl_zero[0] = c->ctl_zero[1] = false;  // the any-hit kernel zeroes nothing
     TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     if (accumulate) TT_HIP(c, tt_launch_shadow_accumulate(&a, d_vis, c->stream));
+    TT_HIP(c, scene_read_end(c));
     c->ring_n++;
     c->ev0 = c->ring0[slot];
     c->ev1 = c->ring1[slot];
@@ -1596,8 +1683,10 @@ tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_d
         if (c->st_normals.n < (size_t)6 * p->n_rays) TT_HIP(c, c->st_normals.alloc((size_t)6 * p->n_rays));
         d_out = c->st_normals.p;
     }
+    TT_HIP(c, scene_read_begin(c));
     TT_HIP(c, tt_launch_resolve(d_rays, off, p->n_rays, p->far_plane, c->tris_raw.p, (uint32_t)c->tris_raw.n,
                                 c->mesh_raw.p, (uint32_t)c->mesh_raw.n, d_out, c->stream));
+    TT_HIP(c, scene_read_end(c));
     if (!dev) TT_HIP(c, hipMemcpyAsync(normals6, d_out, sizeof(float) * 6 * p->n_rays, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
@@ -1665,11 +1754,13 @@ static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_
         TT_HIP(c, hipMemcpyAsync(d + src, rays + src, sizeof(tt_ray_data) * p->n_rays, hipMemcpyHostToDevice, c->stream));
     }
     uint32_t slot;
+    TT_HIP(c, scene_read_begin(c));
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 4 * ctl_words, c->stream));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
                                c->mesh_raw.p, c->counter.p, c->stream, n_dev, n_next_dev));
     TT_HIP(c, ring_close(c, slot));
+    TT_HIP(c, scene_read_end(c));
     if (n_next_dev) {  // BufferSizes[CurBounce + 1].tracerays stays on the GPU: no host round trip
         if (n_next) *n_next = 0;
         return TT_OK;

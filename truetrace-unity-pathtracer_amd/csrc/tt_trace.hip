@@ -69,6 +69,18 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
     return best.t != A.far_plane;
 }
 
+// A ray that ends without a record (the Reps bound, IntersectionKernels.compute:155, or a stack
+// overflow) leaves RayData.hits as it was; the compact stream (tt_trace_closest_hits) promises the
+// same bytes as RayData.hits, so it gets the unchanged word (a rare path: one 16-B load).
+__device__ __forceinline__ void keep_record(const TraceArgs& A, uint32_t ray_index) {
+    if (A.hits_out) {
+        const uint4 h = reinterpret_cast<const uint4*>(A.rays + ray_index)[2];
+        const u32x4 v = {h.x, h.y, h.z, h.w};
+        __builtin_amdgcn_raw_buffer_store_b128(v, buffer_rsrc(A.hits_out, 0x7fffffff), (ray_index - A.ray_offset) << 4,
+                                               0, 0);
+    }
+}
+
 // TT_TRACE_ADAPTIVE_ORDER: a finished (or Reps-exhausted) ray's cost -- its Reps count -- into its
 // ray chunk's entry of the launch's cost map (no-return atomic max; tt_order.hip sorts the next
 // launch's chunks by it). The ray chunk is the 8x8 pixel tile in the full-frame swizzle, else
@@ -174,6 +186,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 if (ORD) record_chunk_cost(A, swizzle, w.ray_index, w.Reps);
             };
             auto exhaust_wide = [&](const WideState& w) {
+                keep_record(A, w.ray_index);
                 if (ORD) record_chunk_cost(A, swizzle, w.ray_index, w.Reps);
             };
             wide_phase<STATS, MATCHECK, 2>(A, st, s_stack, spill, spill_stride, nodes, tris, lane,
@@ -266,6 +279,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
+                keep_record(A, ray_index);
                 if (ORD) record_chunk_cost(A, swizzle, ray_index, Reps);
             } else if (cg.y & 0xff000000u) {  // IntersectionKernels.compute:157-187
                 const uint32_t cio = firstbithigh(cg.y);
@@ -297,6 +311,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                     active = false;
                     if (STATS) c_ovf++;
                     TT_REPORT_OVERFLOW(A);
+                    keep_record(A, ray_index);
                 }
             } else {  // :188-191
                 tg = cg;
@@ -336,6 +351,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                     active = false;
                     if (STATS) c_ovf++;
                     TT_REPORT_OVERFLOW(A);
+                    keep_record(A, ray_index);
                 }
                 tg.y = 0u;
             }

@@ -177,8 +177,8 @@ __device__ __forceinline__ uint32_t node_intersect_part(const uint4 n0, const ui
 
 // The drain loop for groups of G lanes; regroups into 2G-lane groups when the live rays fit and
 // returns when every ray of the wave has finished. `finish(st)` writes a finished ray's records,
-// `exhaust(st)` sees a ray that hit the Reps bound (nothing is written for it); both are called on
-// the group's first lane only.
+// `exhaust(st)` sees a ray that ends without a record (the Reps bound or a stack overflow: the
+// reference writes nothing for it); both are called on the group's first lane only.
 template <bool STATS, bool MATCHECK, int G, class Finish, class Exhaust>
 __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[TT_BLOCK], uint2* __restrict__ spill,
                            uint32_t spill_stride, __amdgpu_buffer_rsrc_t nodes, __amdgpu_buffer_rsrc_t tris,
@@ -231,6 +231,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
                     if (sub == 0u) {
                         if (STATS) C.ovf++;
                         TT_REPORT_OVERFLOW(A);
+                        exhaust(st);
                     }
                 }
             } else {  // :188-191
@@ -272,6 +273,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
                     if (sub == 0u) {
                         if (STATS) C.ovf++;
                         TT_REPORT_OVERFLOW(A);
+                        exhaust(st);
                     }
                 }
                 st.tg.y = 0u;

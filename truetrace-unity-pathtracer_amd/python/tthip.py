@@ -689,21 +689,30 @@ class Engine:
         if st != TT_OK:
             raise TTError(st, f"{what}: {self.L.tt_last_error(self.h).decode()}")
 
+    def _unlink_lender(self):
+        """Drops this engine from its lender's borrower list (re-share or close)."""
+        lender = getattr(self, "_lender", None)
+        if lender is not None:
+            lender._borrowers = [r for r in getattr(lender, "_borrowers", []) if r() is not None and r() is not self]
+        self._lender = None
+
     def close(self):
         if getattr(self, "h", None):
             for b in list(getattr(self, "_borrowers", [])):  # contexts tracing this one's scene go first
                 e = b()
                 if e is not None:
                     e.close()
+            self._borrowers = []
+            self._unlink_lender()
             self.L.tt_ctx_destroy(self.h)
             self.h = None
-            self._lender = None
 
     def share_scene(self, src: "Engine"):
         """tt_ctx_share_scene: trace `src`'s scene (its device buffers, no copy) on this context's stream."""
         import weakref
 
         self._check(self.L.tt_ctx_share_scene(self.h, src.h), "tt_ctx_share_scene")
+        self._unlink_lender()  # a re-share leaves the previous lender's list
         self._lender = src  # keeps the lender alive while this context reads its buffers
         if not hasattr(src, "_borrowers"):
             src._borrowers = []
