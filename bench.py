@@ -413,119 +413,104 @@ def aux_configs(torch, tthip, eng, dev, args, which):
 def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     """BASELINE configs[4] as the north star lays it out, run after the metric when
     N > 1: the San-Miguel-shaped scene (10 M tris) replicated on every rank, the 3840x2160 frame's
-    64x64 tiles dealt round-robin, each rank tracing its primary rays (HIP events, median of the
-    timed launches), then one gather of the 16-B hit records to rank 0, which reassembles the frame
-    and compares it with one GPU tracing the whole frame. Strong scaling: frame time = slowest rank.
+    64x64 tiles dealt round-robin, each rank tracing its tiles' primary rays as P parts x F frame slots
+    (ttlayout.FrameLayout: frame k + 1 overlaps frame k's drain), one RCCL gather of the frame's 16-B hit
+    records to rank 0 per frame, which reassembles the frame and compares it with one GPU tracing the
+    whole frame. Strong scaling: frame time = slowest rank; efficiency against the N = 1 frame (the whole
+    4K frame, 2 parts, the same slots) traced on every rank's own GPU at once in the same run (fastest).
     Failures are agreed on collectively before the gather, so one rank's error cannot hang the rest."""
     import ttconfigs as T
     import ttdist
+    import ttlayout
 
-    rec, ok, ms, ms_parts, ms_parts_ad = {}, 1, 0.0, 0.0, 0.0
+    rec, ok = {}, 1
     W, H, far = 3840, 2160, T.FAR
     WH = W * H
+    F = max(1, args.strong_slots)
+    P = max(1, args.parts) if args.parts > 0 else (3 if world >= 4 else 2)
+    el1 = el_n = 0.0
+    lay = None
     try:
         t0 = time.time()
         sc = T.c5_san_miguel()
         build_s = time.time() - t0
         eng.upload(sc)
         c2w, ip = T.C5_VIEW.camera(W, H)
-        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=1, device=True)
-        pix = torch.from_numpy(ttdist.tile_pixels(W, H, world, rank)).to(dev)
-        n = int(pix.shape[0])
-        mine = full.view(WH, 48)[pix].contiguous()
-        launch = [lambda: eng.trace(mine, n, 0, far, W, H, device=True, asynchronous=True)]
-        ms = float(np.median(timed_launches(eng, launch, max(1, args.warmup), max(3, args.steps // 2))))
-        rec.update(rays_this_rank=n, build_s=round(build_s, 1))
-        # the metric's layout: the rank's tiles as 2 tile-interleaved parts, each on its own engine
-        # context and stream, frames back to back (a part's launch drain overlaps the other's work)
-        s1 = torch.cuda.Stream(dev)
-        e1 = tthip.Engine(dev.index, stream=s1.cuda_stream)
-        try:
-            e1.share_scene(eng)
-            chains = []
-            for e, pp in zip((eng, e1), ttdist.part_pixels(W, H, world, rank, 2)):
-                chains.append((e, full.view(WH, 48)[torch.from_numpy(pp).to(dev)].contiguous(), int(pp.shape[0])))
-            torch.cuda.synchronize(dev)
+        make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, far)
 
-            def frame():
-                for e, buf, m in chains:
-                    e.trace(buf, m, 0, far, W, H, device=True, asynchronous=True)
-
-            for _ in range(max(1, args.warmup)):
-                frame()
+        def timed_layout(plan):
+            lay_ = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=F, bounce=False,
+                                        info=False)
+            for _ in range(max(2, args.warmup)):
+                lay_.step()
             torch.cuda.synchronize(dev)
-            reps = max(3, args.steps // 2)
+            lay_.timing_reset()
+            reps = max(4, args.steps // 2)
             tp = time.perf_counter()
             for _ in range(reps):
-                frame()
+                lay_.step()
             torch.cuda.synchronize(dev)
-            ms_parts = (time.perf_counter() - tp) * 1e3 / reps
-            hits_parts = torch.cat([buf.view(m, 48)[:, 32:48] for _, buf, m in chains]).contiguous()
-            # the same layout with the adaptive dequeue order (DESIGN.md §3.1): two jittered frames
-            # alternate, so every launch is ordered by the previous frame's costs
-            full1 = torch.zeros_like(full)
-            eng.generate(full1, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=1, max_bounce=1, device=True)
-            chains1 = [(e, full1.view(WH, 48)[torch.from_numpy(pp).to(dev)].contiguous(), int(pp.shape[0]))
-                       for e, pp in zip((eng, e1), ttdist.part_pixels(W, H, world, rank, 2))]
-            torch.cuda.synchronize(dev)
+            el = (time.perf_counter() - tp) * 1e3 / reps
+            lay_.launch_ms()
+            return lay_, el
 
-            def frame_ad(k):
-                for e, buf, m in (chains if k % 2 == 0 else chains1):
-                    e.trace(buf, m, 0, far, W, H, device=True, asynchronous=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER)
-
-            for k in range(max(2, args.warmup)):
-                frame_ad(k)
-            torch.cuda.synchronize(dev)
-            reps_ad = max(4, args.steps // 2) // 2 * 2
-            tp = time.perf_counter()
-            for k in range(reps_ad):
-                frame_ad(k)
-            torch.cuda.synchronize(dev)
-            ms_parts_ad = (time.perf_counter() - tp) * 1e3 / reps_ad
-            del full1, chains1
-        finally:
-            e1.close()
+        # the N = 1 frame on every rank's GPU at once (no collective inside)
+        solo, el1 = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)])
+        solo.close()
+        del solo
+        lay, el_n = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)])
+        rec.update(rays_this_rank=lay.n_prim(), build_s=round(build_s, 1))
     except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
         ok = 0
         rec["error"] = f"rank {rank}: {type(e).__name__}: {e}"
         log(f"c5 tiles failed: {rec['error']}")
-    flags = torch.tensor([float(ok), ms], dtype=torch.float64, device=red_dev)
-    dist.all_reduce(flags[:1], op=dist.ReduceOp.MIN)
-    t_max = torch.tensor([ms], dtype=torch.float64, device=red_dev)
-    dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    flags = torch.tensor([float(ok)], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     if flags[0].item() < 1.0:
+        if lay is not None:
+            lay.close()
         return rec if rank == 0 else None
-    tp_max = torch.tensor([ms_parts, ms_parts_ad], dtype=torch.float64, device=red_dev)
-    dist.all_reduce(tp_max, op=dist.ReduceOp.MAX)
-    hits = mine.view(n, 48)[:, 32:48].contiguous().view(torch.int32).to(red_dev)
+    t1 = torch.tensor([el1], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(t1, op=dist.ReduceOp.MIN)
+    tn = torch.tensor([el_n], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(tn, op=dist.ReduceOp.MAX)
+    # the frame again, with the per-frame gather inside the timed frames (on the comm stream)
+    lay.attach_gather(dist, world, rank, red_dev)
+    for _ in range(max(2, args.warmup)):
+        lay.step()
     torch.cuda.synchronize(dev)
     dist.barrier()
-    tg = time.perf_counter()
-    parts = ttdist.gather_hits(hits, world, rank)
     torch.cuda.synchronize(dev)
-    gather_ms = (time.perf_counter() - tg) * 1e3
-    # the two-part records, one gather too (each rank's parts back to back)
-    parts2 = ttdist.gather_hits(hits_parts.view(torch.int32).to(red_dev), world, rank)
+    reps = max(4, args.steps // 2)
+    tg = time.perf_counter()
+    for _ in range(reps):
+        lay.step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    el_g = (time.perf_counter() - tg) * 1e3 / reps
+    lay.launch_ms()
+    tgm = torch.tensor([el_g], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(tgm, op=dist.ReduceOp.MAX)
+    sizes, gl = lay.last_gathered() if rank == 0 else (None, None)
+    lay.close()
     if rank != 0:
         return None
-    frame = ttdist.assemble_tiles(parts, W, H, world)
-    sizes2 = [[int(pp.shape[0]) for pp in ttdist.part_pixels(W, H, world, r, 2)] for r in range(world)]
-    frame2 = ttdist.assemble_parts(parts2, sizes2, W, H, world, 2)
+    frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl, sizes)], sizes, W, H, world, P)
+    full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+    eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=1, device=True)
     eng.trace(full, WH, 0, far, W, H, device=True)
     ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
-    frame_ms = float(t_max.item())
-    frame_ms_parts, frame_ms_parts_ad = float(tp_max[0].item()), float(tp_max[1].item())
-    rec.update(config="c5_san_miguel_4k_tiles", ranks=world, tile=64, frame_rays=WH,
-               trace_ms_slowest_rank=round(frame_ms, 4), trace_ms_rank0=round(ms, 4),
-               mrays_s_frame=round(WH / frame_ms / 1e3, 1), gather_ms=round(gather_ms, 3),
+    ms1, msn, msg = float(t1.item()), float(tn.item()), float(tgm.item())
+    rec.update(config="c5_san_miguel_4k_tiles", ranks=world, tile=64, parts_per_rank=P, frame_slots=F,
+               frame_rays=WH, n1_ms_per_frame=round(ms1, 4), ms_per_frame_slowest_rank=round(msn, 4),
+               efficiency=round(ms1 / (world * msn), 4), mrays_s_frame=round(WH / msn / 1e3, 1),
+               with_gather=dict(ms_per_frame_slowest_rank=round(msg, 4), efficiency=round(ms1 / (world * msg), 4),
+                                mrays_s_frame=round(WH / msg / 1e3, 1)),
                identical_to_1gpu=bool(np.array_equal(frame, ref)),
-               two_parts=dict(ms_per_frame_slowest_rank=round(frame_ms_parts, 4),
-                              mrays_s_frame=round(WH / frame_ms_parts / 1e3, 1),
-                              identical_to_1gpu=bool(np.array_equal(frame2, ref))),
-               two_parts_adaptive_order=dict(ms_per_frame_slowest_rank=round(frame_ms_parts_ad, 4),
-                                             mrays_s_frame=round(WH / frame_ms_parts_ad / 1e3, 1),
-                                             note="frames_accumulated 0 / 1 alternating; results order-independent"))
+               note="efficiency = t(N = 1: the whole 4K frame, 2 parts, same slots, on every rank's GPU at once, "
+                    "fastest) / (N x t(N), slowest rank); with_gather: the per-frame RCCL gather of the hit records to "
+                    "rank 0 inside the timed frames")
     log(f"c5 tiles: {rec}")
     return rec
 
@@ -684,6 +669,16 @@ def main():
                          "launch per bounce; 0 (default): 2 for a full frame's worth per rank (N = 1, the spp "
                          "headline), 3 for the strong-scaling shards at N >= 4 (<= 1/4 frame: -12%% / -2%% step time "
                          "at the N = 4 / 8 shards vs 2 parts, profiles/r03/parts/)")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="frame slots F of the headline layout (ttlayout.FrameLayout): frame k runs on slot k %% F with "
+                         "its own buffers and streams, so frame k + 1's primary launches overlap frame k's bounce-1 "
+                         "launches. 0 (default): 1 for a full frame's worth per rank, --strong-slots for the "
+                         "strong-scaling shards (--shard tiles)")
+    ap.add_argument("--strong-slots", type=int, default=2,
+                    help="frame slots of the strong-scaling tile layouts (N > 1: aux_strong_tiles, aux_c5_tiles) and of "
+                         "their N = 1 reference frames")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N > 1: skip the strong-scaling 1080p tile layout and its N = 1 reference frame")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
     ap.add_argument("--steady-steps", type=int, default=200,
                     help="N = 1: steps of the secondary steady-state leg after the timed region (0 = skip)")
@@ -729,6 +724,7 @@ def main():
     import torch.distributed as dist
     import tthip
     import ttdist
+    import ttlayout
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the HIP engine has no CPU fallback)")
@@ -779,7 +775,6 @@ def main():
     tthip.set_build_engine(eng, min_tris=100_000)
 
     # ------------------------------------------------------------------ resident rays
-    rays = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
     info = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
     colors = np.zeros(WH, tthip.COL_DTYPE)
     colors["Data"][:, 3] = 1.0  # shade set Data.w = CurBounce + 1 = 1 at bounce 0
@@ -791,144 +786,38 @@ def main():
     # its screen column x = W/2 has direction.z == -0.0 exactly, whose NaN z slabs make ~1,000 rays
     # walk ~900 nodes each (tools/long_rays.py). The sample layout jitters with frames = rank.
     jitter, frames = 1, (rank if (world > 1 and not tiles) else 0)
-    # a rank's pixels (the whole frame at N = 1) as P tile-interleaved parts, each traced by its own
-    # engine context on its own stream: a part's launches overlap the other parts' launch drains
-    # (tools/exp_streams.py); P = 1 is one full-frame launch per bounce in the kernel's own tile order
-    # parts per rank: a full frame's worth of rays (N = 1, and every rank of the spp headline) as 2 parts;
-    # the strong-scaling shards of <= 1/4 frame as 3 (one-wave blocks, profiles/r03/parts/: N = 4 shard
-    # 0.371 -> 0.327 ms, N = 8 0.236 -> 0.231 ms per step; a full frame 0.784-0.80 (2) vs 0.808-0.82 (3))
+    # a rank's pixels (the whole frame at N = 1) as P tile-interleaved parts x F frame slots, each part of
+    # each slot traced by its own engine context on its own stream (ttlayout.FrameLayout): a part's launches
+    # overlap the other parts' launch drains, and with F >= 2 frame k + 1's primaries overlap frame k's
+    # bounce-1 launches. Parts per rank: a full frame's worth of rays (N = 1, and every rank of the spp
+    # headline) as 2 parts; the strong-scaling shards of <= 1/4 frame as 3 (one-wave blocks,
+    # profiles/r03/parts/: N = 4 shard 0.371 -> 0.327 ms, N = 8 0.236 -> 0.231 ms per step; a full frame
+    # 0.784-0.80 (2) vs 0.808-0.82 (3)).
     P_strong = max(1, args.parts) if args.parts > 0 else (3 if world >= 4 else 2)
+    F_strong = max(1, args.strong_slots)
     if args.parts <= 0:
         args.parts = 3 if (world >= 4 and not spp) else 2
     P = max(1, args.parts) if (tiles or world == 1) else 1
+    F = max(1, args.slots if args.slots > 0 else (F_strong if (tiles and not spp) else 1))
     split = tiles or P > 1
+    make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, 0.3, far, jitter=jitter)
 
-    class Part:  # one launch stream of this rank: its engine, stream, rays and counts
-        pass
+    def layout_of(plan, slots):
+        return ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots,
+                                    bounce=True, info=True, colors=colors_t, frames=frames)
 
-    # part s always runs on the same engine context and stream (part 0: the shared main stream)
-    lanes = [(eng, stream)]
-
-    def lane(s):
-        while len(lanes) <= s:
-            st = torch.cuda.Stream(dev)
-            e = tthip.Engine(gpu, stream=st.cuda_stream)
-            e.share_scene(eng)  # the parts trace ONE scene copy (tt_ctx_share_scene): one cache footprint
-            lanes.append((e, st))
-        return lanes[s]
-
-    def build_parts(plan, fresh=False):
-        """plan: per part, [(sample k, pixel indices)]: the rays of sample k (Generate with
-        frames_accumulated = k) at those pixels, compacted back to back into the part's ping-pong
-        buffer (part 0: the main buffer `rays` unless fresh); then one stats trace of each bounce and
-        the bounce-1 enqueue (setup, untimed)."""
-        ps = []
-        for s_, lst in enumerate(plan):
-            p = Part()
-            p.eng, p.stream = lane(s_)
-            p.rays = rays if (s_ == 0 and not fresh) else torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-            p.n = int(sum(len(pix) for _, pix in lst))
-            ps.append(p)
-        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-        for k in sorted({k for lst in plan for k, _ in lst}):
-            eng.generate(full, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=k, max_bounce=1, device=True)
-            for p, lst in zip(ps, plan):
-                o = 0
-                for kk, pix in lst:
-                    if kk == k and len(pix):
-                        p.rays.view(2 * WH, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
-                    o += len(pix)
-        del full
-        torch.cuda.synchronize(dev)  # the other parts' engines run on their own streams
-        for p in ps:
-            p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, stats=True)
-            p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=frames, max_bounce=1, device=True)
-            p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, stats=True)
-            p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
-        torch.cuda.synchronize(dev)
-        return ps
-
-    class Gather:  # the per-step RCCL gather of the primary hit records to rank 0
-        pass
-
-    def make_gather(ps):
-        # shards padded to the largest so every rank sends one equal-size message; a rank's parts back
-        # to back. The gather runs on its own stream, overlapped with the bounce-1 traces (which read and
-        # write only the other half of the ping-pong buffers); the step ends when both are done, so the
-        # timed step includes the collective. On the GPU the primary traces write their hit records
-        # straight into the send buffer (tt_trace_closest_hits: no strided copy out of GlobalRays), two
-        # send buffers alternating by step, so step k + 2's primaries wait for step k's gather only. The
-        # gloo rehearsal (host-side collective) copies the records to a host buffer instead.
-        g = Gather()
-        n_t = torch.tensor([p.n for p in ps], dtype=torch.int64, device=red_dev)
-        sz = [torch.zeros_like(n_t) for _ in range(world)]
-        dist.all_gather(sz, n_t)
-        g.sizes = [[int(v) for v in x.tolist()] for x in sz]
-        g.stream_hits = red_dev.type == "cuda"
-        nbuf = 2 if g.stream_hits else 1
-        g.bufs = [torch.zeros((max(sum(x) for x in g.sizes), 4), dtype=torch.int32, device=red_dev)
-                  for _ in range(nbuf)]
-        g.lists = [[torch.empty_like(bf) for _ in range(world)] if rank == 0 else None for bf in g.bufs]
-        g.comm = torch.cuda.Stream(dev)
-        g.done = [torch.cuda.Event() for _ in range(nbuf)]  # stream_hits: gather of buffer b finished
-        g.copied = torch.cuda.Event()
-        g.k = 0
-        o = 0
-        for p in ps:
-            p.hit_slices = [bf[o:o + p.n] for bf in g.bufs]
-            o += p.n
-        return g
-
-    def last_gather(g):
-        """(sizes, per-rank gathered blocks) of the most recent step's gather (rank 0)."""
-        return g.sizes, g.lists[(g.k - 1) % len(g.bufs)]
-
-    def make_step(ps, g):
-        def step_fn():
-            b = g.k % len(g.bufs) if g is not None else 0
-            for p in ps:
-                if g is not None and g.stream_hits:
-                    if g.k >= len(g.bufs):
-                        p.stream.wait_event(g.done[b])  # the gather that last read send buffer b is done
-                    p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True,
-                                hits_out=p.hit_slices[b])
-                else:
-                    p.eng.trace(p.rays, p.n, 0, far, W, H, info=info, device=True, asynchronous=True)
-            if g is not None:
-                for p in ps:
-                    g.comm.wait_stream(p.stream)  # the primary hit records are final
-                with torch.cuda.stream(g.comm):
-                    if not g.stream_hits:
-                        for p in ps:
-                            p.hit_slices[0].copy_(p.prim_hits)
-                        g.copied.record(g.comm)
-                    dist.gather(g.bufs[b], g.lists[b], dst=0)
-                    if g.stream_hits:
-                        g.done[b].record(g.comm)
-            for p in ps:
-                p.eng.trace(p.rays, p.nb, 1, far, W, H, info=info, colors=colors_t, device=True, asynchronous=True)
-            if g is not None:
-                if not g.stream_hits:
-                    for p in ps:
-                        # the next step's primary trace rewrites the records copied out above: it waits for the
-                        # copy, not for the gather (which reads the buffer; the next copy is ordered after it)
-                        p.stream.wait_event(g.copied)
-                g.k += 1
-        return step_fn
-
-    def timed(ps, step_fn):
+    def timed(lay):
         """W untimed steps, then exactly K steps between barrier + synchronize pairs: this rank's seconds."""
         for _ in range(args.warmup):
-            step_fn()
+            lay.step()
         torch.cuda.synchronize(dev)
-        for p in ps:
-            p.eng.timing_reset()
+        lay.timing_reset()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0_ = time.perf_counter()
         for _ in range(args.steps):
-            step_fn()
+            lay.step()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -941,8 +830,9 @@ def main():
         plan = [[(frames, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)]
     else:  # the whole frame, one launch per bounce in the kernel's own tile order
         plan = [[(frames, np.arange(WH, dtype=np.int64))]]
-    parts = build_parts(plan)
-    n_prim, nb = sum(p.n for p in parts), sum(p.nb for p in parts)
+    layout = layout_of(plan, F)
+    parts = layout.parts
+    n_prim, nb = layout.n_prim(), layout.n_bounce()
     rays_per_step = n_prim + nb
     s_prim, s_bnc = parts[0].s_prim, parts[0].s_bnc
     B_prim = alg_bytes(s_prim, 0, parts[0].n)  # part 0's launches (the engine ring below)
@@ -952,7 +842,7 @@ def main():
         f"tris/ray {s_prim.tri_tests / max(parts[0].n, 1):.2f} "
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(parts[0].nb, 1):.2f} "
         f"tris/ray {s_bnc.tri_tests / max(parts[0].nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}"
-        f"; parts {P}" + (f"; {world}-sample frame (spp)" if spp else ""))
+        f"; parts {P}, frame slots {F}" + (f"; {world}-sample frame (spp)" if spp else ""))
 
     # The two auxiliary legs that trace the metric's own scene -- the single-stream leg (N = 1) and the
     # sample-sharded layout (N > 1) -- run BEFORE the timed region: they are sustained GPU work, so the
@@ -963,8 +853,8 @@ def main():
     # order on the shared stream, per-launch HIP events -- the per-launch roofline and the launch
     # times rocprofv3 reports for this command's trace kernels
     single = None
-    frame_rays, frame_nb = (rays, nb) if (P == 1 and world == 1) else (None, None)  # a full-frame, traced ray buffer (N = 1)
-    if world == 1 and P > 1:
+    frame_rays, frame_nb = (parts[0].rays, nb) if (P == 1 and world == 1) else (None, None)
+    if world == 1 and (P > 1 or F > 1):
         one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         o_prim = eng.trace(one, WH, 0, far, W, H, info=info, device=True, stats=True)
@@ -1019,15 +909,28 @@ def main():
         del srays
         log(f"sample-sharded (weak) layout: {sample_sharded}")
 
-    G = make_gather(parts) if tiles else None
-    sizes, gather_list = None, None
+    # N > 1: the N = 1 frame (the whole 1080p frame in the single-GPU layout: 2 parts, F_strong slots) on
+    # every rank's own GPU at once, no collective -- the T(1) of the strong-scaling efficiency below,
+    # measured in the same run on the same kind of GPU (the fastest rank's, conservative)
+    solo_ms = None
+    if world > 1 and not args.no_strong:
+        solo = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], F_strong)
+        el_solo = timed(solo)
+        solo.launch_ms()
+        solo.close()
+        t = torch.tensor([el_solo], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        solo_ms = float(t.item()) * 1e3 / args.steps
+        solo_rays = solo.rays_per_frame()
+        del solo
+        log(f"N = 1 frame on each rank's GPU (2 parts, {F_strong} slots): {solo_ms:.4f} ms (fastest rank)")
+
+    G = layout.attach_gather(dist, world, rank, red_dev) if tiles else None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
-    step = make_step(parts, G)
-    elapsed = timed(parts, step)
-    launch_ms = ring_tail(eng, 2, args.steps).reshape(-1)  # part 0's launches, the last <= 128 steps
-    for p in parts[1:]:
-        ring_tail(p.eng, 2, args.steps)
+    elapsed = timed(layout)
+    lm = layout.launch_ms()  # part 0's launches, the last <= 128 frames of its slot
+    launch_ms = lm.reshape(-1)
     total_rays = float(rays_per_step * args.steps)
     trace_ms_rank = float(np.sum(launch_ms)) / (len(launch_ms) // 2)  # part 0's two launches per step
     if world > 1:
@@ -1046,9 +949,9 @@ def main():
     prim_ms = launch_ms[0::2]
     bnc_ms = launch_ms[1::2]
     avg_ms = float(np.mean(launch_ms))
-    if P == 1:  # GB/s per launch, averaged over both launches
+    if P == 1 and F == 1:  # GB/s per launch, averaged over both launches
         achieved = ((B_prim + B_bnc) / 2.0) / (avg_ms * 1e-3) / 1e9
-    else:  # the P parts' launches overlap: all of a step's algorithmic bytes over the step's wall time
+    else:  # the parts' launches overlap: all of a step's algorithmic bytes over the step's wall time
         achieved = B_step / (elapsed / args.steps) / 1e9
 
     # the same step for longer, right after the timed region (N = 1): the rate once clocks and caches
@@ -1059,13 +962,14 @@ def main():
         torch.cuda.synchronize(dev)
         ts = time.perf_counter()
         for _ in range(args.steady_steps):
-            step()
+            layout.step()
         torch.cuda.synchronize(dev)
         es = time.perf_counter() - ts
         steady = {"steps": args.steady_steps, "ms_per_step": round(es * 1e3 / args.steady_steps, 4),
                   "mrays_s": round(rays_per_step * args.steady_steps / es / 1e6, 2),
                   "note": "untimed-for-value: the same step repeated after the timed region"}
         log(f"steady state: {steady}")
+    layout.timing_reset()  # drain the rings of the steady steps
 
     # SURVEY 8(e) parity -- the gathered (N > 1) or the parts' (N = 1) frame(s) must equal one launch
     # tracing each whole frame
@@ -1077,7 +981,7 @@ def main():
 
     gather_parity = None
     if G is not None:
-        sizes, gather_list = last_gather(G)  # the last step's gather (steady-state steps included)
+        sizes, gather_list = layout.last_gathered()  # the last step's gather (steady-state steps included)
     if split and rank == 0:
         if spp:
             fr = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gather_list, sizes)], W, H, world, P)
@@ -1087,44 +991,52 @@ def main():
             if tiles:
                 frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
             else:
-                own = torch.cat([p.prim_hits for p in parts]).cpu()
+                own = torch.cat([p.prim_hits for p in layout.slots[(layout.k - 1) % F]]).cpu()
                 frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
             gather_parity = bool(np.array_equal(frame, one_gpu_frame(frames)))
         log(f"gathered frame(s): {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels in sample 0, "
             f"{world if spp else 1} sample(s) identical to single-GPU traces: {gather_parity}")
 
-    # N > 1 with the spp headline: the strong-scaling layout beside it -- ONE 1-sample frame's tiles dealt
-    # round-robin (P parts per rank), the same per-step gather; frame time = the slowest rank's
+    # N > 1: the strong-scaling layout -- ONE 1-sample frame's tiles dealt round-robin (P_strong parts x
+    # F_strong frame slots per rank), the same per-frame gather; frame time = the slowest rank's; its
+    # efficiency against the N = 1 frame measured above on every rank's GPU
     strong = None
-    if spp and world > 1:
-        ps_s = build_parts([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P_strong)], fresh=True)
-        g_s = make_gather(ps_s)
-        el_s = timed(ps_s, make_step(ps_s, g_s))
-        for p in ps_s:
-            ring_tail(p.eng, 2, args.steps)
-        st_ = torch.tensor([el_s, float(sum(p.n + p.nb for p in ps_s) * args.steps)], dtype=torch.float64,
-                           device=red_dev)
+    if world > 1 and not args.no_strong:
+        if spp:
+            lay_s = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P_strong)], F_strong)
+            lay_s.attach_gather(dist, world, rank, red_dev)
+        else:
+            lay_s = layout  # the headline already is the strong-scaling layout
+        el_s = timed(lay_s) if lay_s is not layout else elapsed
+        if lay_s is not layout:
+            lay_s.launch_ms()
+        st_ = torch.tensor([el_s, float(lay_s.rays_per_frame() * args.steps)], dtype=torch.float64, device=red_dev)
         tmax = st_[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         rsum = st_[1:].clone()
         dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
         par = None
         if rank == 0:
-            sz_s, gl_s = last_gather(g_s)
-            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H,
-                                        world, P_strong)
+            sz_s, gl_s = lay_s.last_gathered()
+            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H, world, lay_s.P)
             par = bool(np.array_equal(fr1, one_gpu_frame(0)))
+        ms_n = float(tmax.item()) * 1e3 / args.steps
         strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
-                  "scaling": "strong", "ranks": world, "parts_per_rank": P_strong,
-                  "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4),
-                  "rays_per_step_all_ranks": int(round(float(rsum.item()) / args.steps)),
+                  "scaling": "strong", "ranks": world, "parts_per_rank": lay_s.P, "frame_slots": lay_s.F,
+                  "ms_per_frame": round(ms_n, 4),
+                  "rays_per_frame_all_ranks": int(round(float(rsum.item()) / args.steps)),
+                  "n1_ms_per_frame": round(solo_ms, 4), "n1_rays_per_frame": int(solo_rays),
+                  "efficiency": round(solo_ms / (world * ms_n), 4),
                   "gather_identical_to_1gpu": par,
-                  "layout": "one 1080p frame (1 sample): 64x64 tiles round-robin over the ranks + one RCCL gather "
-                            "of its primary hit records per step"}
-        del ps_s, g_s
+                  "layout": "one 1080p frame (1 sample): 64x64 tiles round-robin over the ranks, each rank's tiles "
+                            f"as {lay_s.P} parts x {lay_s.F} frame slots, + one RCCL gather of the frame's primary "
+                            "hit records per frame; efficiency = t(N = 1 frame, 2 parts, same slots, every rank's "
+                            "GPU at once, fastest) / (N x t(N))"}
+        if lay_s is not layout:
+            lay_s.close()
+            del lay_s
         log(f"strong-scaling tile layout: {strong}")
-    for e_, _ in lanes[1:]:
-        e_.close()
+    layout.close()  # the borrowing contexts go before any aux leg re-uploads `eng`'s scene
 
     # ---- auxiliary: the UseReCur ray generation (no jitter), primary + bounce 1, N=1
     recur = None
@@ -1160,7 +1072,7 @@ def main():
     if not args.no_shadow:
         # the frame's primary hits at N = 1, part 0's at N > 1
         sr = (nee_rays(torch, frame_rays, WH, far, light=(0.0, 9.0, 0.5)) if frame_rays is not None else
-              nee_rays(torch, rays, parts[0].n, far, light=(0.0, 9.0, 0.5)))
+              nee_rays(torch, parts[0].rays, parts[0].n, far, light=(0.0, 9.0, 0.5)))
         ns = int(sr.shape[0]) // 48
         work = torch.empty_like(sr)
         work.copy_(sr)
@@ -1232,6 +1144,10 @@ def main():
             tj = json.load(f)
         traffic = round(float(tj["mean_bytes_per_launch"]))
         traffic_src = "profiles/traffic_latest.json <- " + tj.get("source", "?").split(" ")[0]
+        traffic_k = {k.rstrip(">").split(",")[-1].strip(): v["bytes"] for k, v in tj.get("per_kernel", {}).items()
+                     if k.startswith("void tt_trace_kernel<false, false,")}
+    else:
+        traffic_k = {}
 
     # unit utilisation of the same kernels from the round's separate PMC passes (tools/pmc_units.sh
     # -> profiles/units_latest.json): the binding units, since the scene is cache-resident
@@ -1248,7 +1164,7 @@ def main():
     # clock (valu_ceiling_grays_s, from the PMC pass's VALU issue cycles per ray). One launch at a
     # time (P = 1: the metric's launches; P > 1: the single-stream leg), so a launch's duration is
     # the kernel's. The dominant kernel is the longer launch.
-    if P == 1:
+    if P == 1 and F == 1:
         per_launch = {"1": (n_prim, float(np.mean(prim_ms))), "2": (nb, float(np.mean(bnc_ms)))}
     elif single is not None:
         per_launch = {"1": (WH, single["trace_ms_primary"]), "2": (frame_nb, single["trace_ms_bounce"])}
@@ -1264,6 +1180,15 @@ def main():
                       "valu_issue_cycles_per_ray": u.get("valu_issue_cycles_per_ray"),
                       "frac": round(rate / ceil, 4) if ceil else None}
     dom = max(valu.values(), key=lambda v: v["launch_ms"]) if valu else None
+    # the DRAM-side fraction (SURVEY §8(d) consistency warning): the PMC pass's fabric bytes of each launch
+    # (2 x FETCH_SIZE + WRITE_SIZE, per the gfx950 correction) over the same launch's HIP-event duration
+    dram = {}
+    for k, v in valu.items():
+        if k in traffic_k:
+            gbs = traffic_k[k] / (v["launch_ms"] * 1e-3) / 1e9
+            dram[k] = {"kernel": v["kernel"], "traffic_bytes": round(traffic_k[k]), "launch_ms": v["launch_ms"],
+                       "gbs": round(gbs, 1), "frac_dram": round(gbs / HBM_PEAK_GBS, 4)}
+    dom_dram = dram.get(max(valu, key=lambda k: valu[k]["launch_ms"])) if valu and dram else None
 
     ms_per_step = elapsed * 1e3 / args.steps
     # the whole step (all parts' launches, overlapped) against the time its VALU work takes with VALU
@@ -1300,20 +1225,23 @@ def main():
                    "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "jitter": jitter,
                    "seed": hex(args.seed),
                    "parallelism": ((f"single GPU, full frame as {P} tile-interleaved parts on {P} streams"
-                                    if P > 1 else "single GPU, full frame") if world == 1 else
+                                    if P > 1 else "single GPU, full frame")
+                                   + (f", {F} frame slots (frame k + 1's primaries overlap frame k's bounce-1 "
+                                      "launches)" if F > 1 else "") if world == 1 else
                                    ((f"{world}-sample 1080p frame (sample k = Generate with frames_accumulated = k), "
                                      f"its (sample, 64x64 tile) units round-robin over {world} ranks (one frame's "
                                      f"worth each: weak scaling), " if spp else
                                      f"one 1080p frame's 64x64 screen tiles round-robin over {world} ranks, ")
                                     + f"each rank's tiles as {P} "
-                                    f"tile-interleaved parts on {P} streams, + one RCCL gather of the "
+                                    f"tile-interleaved parts x {F} frame slots on {P * F} streams, + one RCCL gather of the "
                                     f"primary hit records to rank 0 per step (inside the timed step"
                                     + (", overlapped with the bounce-1 trace on a second stream)" if gather_overlapped
                                        else ")") if tiles
                                     else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
                    "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it"
                              + (f" (part 0 of {P}: its launches overlap the other parts')" if P > 1 else ""),
-                   "parts_per_rank": P, "parts_share_one_scene_copy": P > 1, "samples_per_frame": world if spp else 1,
+                   "parts_per_rank": P, "frame_slots": F, "parts_share_one_scene_copy": P * F > 1,
+                   "samples_per_frame": world if spp else 1,
                    "dist_world_size": dist_world, "dist_backend": backend if dist_world else None,
                    "launcher": ("bench.py self-launch" if os.environ.get("TT_BENCH_SELF_LAUNCHED") == "1"
                                 else "external (WORLD_SIZE set)" if env_world is not None else "none (1 rank)"),
@@ -1339,6 +1267,8 @@ def main():
                      "hbm": {"achieved_alg_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
                              "frac_alg": round(achieved / HBM_PEAK_GBS, 4),
                              "traffic_bytes_per_launch": traffic,
+                             "frac_dram": dom_dram["frac_dram"] if dom_dram else None,
+                             "dram_per_launch": dram or None,
                              "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0) if P == 1 else round(B_step / (2 * P)),
                              "alg_bytes_per_step": round(B_step),
                              "note": ("achieved_alg_gbs = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean "

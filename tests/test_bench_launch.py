@@ -85,7 +85,7 @@ def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
     whole frame, and the strong-scaling tile layout beside it (one frame, same gather) identical too."""
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
                         "--no-shadow", "--no-c5-tiles", "--steady-steps", "0"],
-                       env=_env(TT_BENCH_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=115)
+                       env=_env(TT_BENCH_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-3000:]
     (d,) = _json_lines(r.stdout)
     assert d["n_gpus"] == 2
@@ -96,4 +96,7 @@ def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
     assert c["rays_per_step_all_ranks"] > 8_000_000  # two 1080p samples, primary + bounce 1
     st = c["aux_strong_tiles"]
     assert st["scaling"] == "strong" and st["gather_identical_to_1gpu"] is True
-    assert 4_000_000 < st["rays_per_step_all_ranks"] < 4_200_000
+    assert 4_000_000 < st["rays_per_frame_all_ranks"] < 4_200_000
+    assert st["frame_slots"] == 2 and 4_000_000 < st["n1_rays_per_frame"] < 4_200_000
+    assert 0.0 < st["efficiency"]
+    assert abs(st["efficiency"] - st["n1_ms_per_frame"] / (2 * st["ms_per_frame"])) < 0.01

@@ -1,0 +1,68 @@
+#!/bin/bash
+# One parameterised GPU job for gpurun (replaces the per-experiment r0x_*.sh scripts of rounds 1-3):
+#   bash tools/gpu/job.sh TAG STAGE [STAGE ...]
+# Stages run in order, each under its own time limit, outputs in gpurun_out/TAG/; the job stops at
+# the first failing stage (no GPU step runs after a failure). Stages:
+#   tests      pytest -m gpu (the parity suite)
+#   bench      the driver's command: python bench.py --gpus 1 --steps 20 --warmup 5
+#   quick      bench without aux configs / CPU baseline (layout and headline only)
+#   slots2     quick with 2 frame slots (frame k + 1's primaries overlap frame k's bounce-1 launches)
+#   newtests   the GPU tests of the layouts, shared scenes and hit streams only
+#   prof       rocprofv3 --kernel-trace --stats of the bench + the FETCH_SIZE / WRITE_SIZE passes
+#              (tools/profile_round.sh -> traffic JSON; profiles/traffic_latest.json is fed from it)
+#   pmcu       the PMC unit passes behind roofline (tools/pmc_units.sh -> profiles/units_latest.json)
+#   diag       per-block execution counts (TT_DIAG_BLOCKS build, tools/diag_blocks.py)
+#   replay     strong-scaling replay of every rank's N-GPU shard on this GPU (tools/strong_replay.py)
+#   gloo2      the 2-rank bench rehearsal on this GPU (gloo collectives, C5 tiles included)
+#   sweep      randomized parity sweep (tools/parity_sweep.py), 300 plain + 300 variants/adaptive
+#   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
+#   ab         the bench headline per variant: AB_LIBS="product n128 ..." (lib/variants/libtruetrace_hip_NAME.so),
+#              AB_ARGS extra bench.py flags
+#   abcfg      one-launch C4 and C5 per variant (tools/run_variants.py; AB_LIBS names lib/variants entries)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$PWD}"
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() {  # run NAME SECONDS CMD...: one GPU step, its own limit, output to $OUT/NAME.{out,err}
+    local name=$1 secs=$2
+    shift 2
+    echo "[job] $name: $*" >&2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+    local rc=$?
+    echo "[job] $name rc=$rc" >&2
+    tail -c 400 "$OUT/$name.out" >&2
+    return $rc
+}
+for stage in "$@"; do
+    case $stage in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit $? ;;
+    bench) run bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
+    quick) run quick 300 python -u bench.py --steps 20 --warmup 5 --aux "" --cpu-seconds 2 || exit $? ;;
+    slots2) run slots2 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --slots 2 || exit $? ;;
+    newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parts.py \
+                  tests/test_gpu_order.py tests/test_bench_launch.py -m gpu || exit $? ;;
+    prof) run prof 900 bash tools/profile_round.sh "$TAG" || exit $? ;;
+    pmcu) run pmcu 900 bash tools/pmc_units.sh "$OUT/pmcu" || exit $? ;;
+    diag) run diag 200 env TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_diag.so \
+              python -u tools/diag_blocks.py c2 || exit $? ;;
+    replay) run replay 600 python -u tools/strong_replay.py --configs c2,c5 || exit $? ;;
+    gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
+               --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
+    sweep) run sweep_plain 600 python -u tools/parity_sweep.py 300 40000 || exit $?
+           run sweep_var 600 python -u tools/parity_sweep.py 300 41000 variants,adaptive || exit $? ;;
+    variants) run variants 900 python -u tools/run_variants.py || exit $? ;;
+    ab) for v in ${AB_LIBS:-product}; do  # the bench headline (no aux legs) per library variant, in turn
+            lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so
+            [ "$v" = product ] && lib=truetrace-unity-pathtracer_amd/lib/libtruetrace_hip.so
+            run "ab_$v" 300 env TT_HIP_LIB=$lib python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline \
+                --no-recur --no-shadow ${AB_ARGS:-} || exit $?
+        done ;;
+    abcfg) for v in ${AB_LIBS:-product}; do  # one-launch C4 / C5 per variant (tools/run_variants.py)
+            for cfg in c4 c5; do run "abcfg_${v}_$cfg" 400 env RV_CFG=$cfg python -u tools/run_variants.py "$v" || exit $?; done
+        done ;;
+    *) echo "unknown stage $stage" >&2; exit 2 ;;
+    esac
+done
+echo "[job] $TAG done" >&2

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Strong-scaling prediction on ONE GPU (VERDICT r3 "Next 1"): replays, one rank at a
+time, exactly the launches every rank of an N-GPU strong-scaling run issues -- its 64x64 round-robin
+tiles as P tile-interleaved parts x F frame slots (ttlayout.FrameLayout, the layout bench.py runs for
+aux_strong_tiles / aux_c5_tiles) -- and predicts
+
+    t(N)   = max over ranks r of rank r's frame time (ms per frame, frames back to back)
+    eff(N) = t(1) / (N * t(N)),   t(1) = the whole frame in the N = 1 layout (2 parts, same F)
+
+The per-frame RCCL gather of the hit records is not replayed (it runs on its own stream beside the
+traces; bench.py measures it on a real node). Configs: C2 (Sponza-shaped 1080p, primary + bounce 1)
+and C5 (San-Miguel-shaped 4K, primary only). Output: one JSON document on stdout (commit it under
+profiles/). Usage: tools/strong_replay.py [--configs c2,c5] [--slots 2] [--parts-small 3] [--steps 30]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c2,c5")
+    ap.add_argument("--slots", type=int, default=2)
+    ap.add_argument("--parts-small", type=int, default=3, help="parts per rank at N >= 4 (bench.py's default)")
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to replay per N")
+    args = ap.parse_args()
+    import torch
+    import tthip
+    import ttconfigs as T
+    import ttdist
+    import ttlayout
+
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    eng = tthip.Engine(0, stream=stream.cuda_stream)
+    tthip.set_build_engine(eng, min_tris=100_000)
+    out = {"tool": "tools/strong_replay.py", "device": torch.cuda.get_device_name(0), "slots": args.slots,
+           "steps": args.steps, "configs": {}}
+
+    def frame_ms(lay):
+        for _ in range(args.warmup):
+            lay.step()
+        torch.cuda.synchronize(dev)
+        lay.timing_reset()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lay.step()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        lay.launch_ms()
+        return ms
+
+    def run(name, scene, view, W, H, bounce):
+        eng.upload(scene)
+        c2w, ip = view.camera(W, H)
+        make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, T.FAR)
+        colors = None
+        if bounce:
+            import numpy as np
+
+            col = np.zeros(W * H, tthip.COL_DTYPE)
+            col["Data"][:, 3] = 1.0
+            colors = torch.from_numpy(col.view(np.uint8)).to(dev)
+        rows = []
+        t1 = None
+        for n in [int(x) for x in args.ns.split(",")]:
+            P = 2 if n < 4 else args.parts_small
+            ranks = range(n) if args.ranks == "all" else [int(r) for r in args.ranks.split(",") if int(r) < n]
+            per = []
+            for r in ranks:
+                lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR,
+                                           [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P)], make_full,
+                                           slots=args.slots, bounce=bounce, info=True, colors=colors)
+                ms = frame_ms(lay)
+                per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
+                lay.close()
+                del lay
+                print(f"[replay] {name} N={n} rank {r}: {per[-1]}", file=sys.stderr, flush=True)
+            t_n = max(p["ms_per_frame"] for p in per)
+            if n == 1:
+                t1 = t_n
+            rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": args.slots, "ranks": per,
+                         "t_frame_ms_slowest_rank": t_n,
+                         "predicted_efficiency": round(t1 / (n * t_n), 3) if t1 else None,
+                         "predicted_frame_mrays_s": round(sum(p["rays"] for p in per) / t_n / 1e3, 1)
+                         if args.ranks == "all" else None})
+        out["configs"][name] = {"width": W, "height": H, "tris": int(len(scene.tris)), "rows": rows}
+
+    which = set(args.configs.split(","))
+    if "c2" in which:
+        run("c2_sponza_1080p_primary_plus_bounce1", T.c2_sponza(), T.C2_VIEW, 1920, 1080, True)
+    if "c5" in which:
+        t0 = time.time()
+        sc = T.c5_san_miguel()
+        print(f"[replay] c5 build {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+        run("c5_san_miguel_4k_primary", sc, T.C5_VIEW, 3840, 2160, False)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

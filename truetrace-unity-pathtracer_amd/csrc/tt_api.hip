@@ -125,6 +125,7 @@ struct tt_ctx {
     bool any_cutout = false;       // some material is Cutout (needs the alpha atlas)
     SceneHost host;
     DevBuf<tt_cwbvh_node> nodes;
+    DevBuf<uint8_t> nodes_k;    // TT_NODE_STRIDE != 80: the kernels' strided copy of `nodes`
     DevBuf<tt_cuda_triangle> tris_raw;
     DevBuf<TriPos> tris;
     DevBuf<int32_t> tlas;
@@ -146,6 +147,7 @@ struct tt_ctx {
     // BLAS refit (f4, deforming / skinned meshes): one prepared plan + triangle boxes per mesh
     struct BlasRefit {
         RefitDev dev;
+        uint32_t n_nodes = 0;  // nodes the plan covers, from the mesh's first node
         uint64_t gen = ~0ull;
         uint32_t node_base = ~0u;  // the mesh's NodeOffset the plan was built for
         DevBuf<float> boxes;
@@ -263,6 +265,16 @@ static hipError_t scene_write_end(tt_ctx* c) {
     if (e == hipSuccess) e = hipEventRecord(c->ev_scene, c->stream);
     if (e == hipSuccess) c->scene_mut++;
     return e;
+}
+// The node array the kernels read: the reference's (80-B stride) or its strided copy, refreshed on the
+// context stream after every write to `nodes` (nodes [first, first + count)).
+static const uint4* kernel_nodes(const tt_ctx* c) {
+    return TT_NODE_STRIDE == 80 ? reinterpret_cast<const uint4*>(c->nodes.p) : reinterpret_cast<const uint4*>(c->nodes_k.p);
+}
+static hipError_t refresh_node_copy(tt_ctx* c, uint32_t first, uint32_t count) {
+    if (TT_NODE_STRIDE == 80 || count == 0) return hipSuccess;
+    return hipMemcpy2DAsync(c->nodes_k.p + (size_t)first * TT_NODE_STRIDE, TT_NODE_STRIDE, c->nodes.p + first,
+                            sizeof(tt_cwbvh_node), sizeof(tt_cwbvh_node), count, hipMemcpyDeviceToDevice, c->stream);
 }
 static void unlink_borrower(tt_ctx* b) {
     tt_ctx* L = b->lender;
@@ -441,7 +453,8 @@ tt_status check_scene(const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cud
         why = "null or empty buffer";
         return TT_ERR_INVALID_ARG;
     }
-    if ((uint64_t)n_nodes * sizeof(tt_cwbvh_node) >= (1ull << 32) || (uint64_t)n_tris * 48u >= (1ull << 32)) {
+    if ((uint64_t)n_nodes * std::max<uint64_t>(sizeof(tt_cwbvh_node), TT_NODE_STRIDE) >= (1ull << 32) ||
+        (uint64_t)n_tris * 48u >= (1ull << 32)) {
         why = "node or triangle array of 4 GiB or more (the trace kernel addresses them with 32-bit offsets)";
         return TT_ERR_INVALID_ARG;
     }
@@ -686,6 +699,7 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     if (c->ev_scene) (void)hipEventDestroy(c->ev_scene);
     if (c->ev_read) (void)hipEventDestroy(c->ev_read);
     c->nodes.release();
+    c->nodes_k.release();
     c->tris_raw.release();
     c->tris.release();
     c->tlas.release();
@@ -841,6 +855,13 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
         (e = c->mat_tag.alloc(tags.size())) != hipSuccess)
         return hip_fail(c, e, "scene allocation");
     TT_HIP(c, hipMemcpy(c->nodes.p, nodes, sizeof(tt_cwbvh_node) * n_nodes, hipMemcpyHostToDevice));
+    if (TT_NODE_STRIDE != 80) {
+        c->nodes_k.release();
+        if ((e = c->nodes_k.alloc((size_t)n_nodes * TT_NODE_STRIDE)) != hipSuccess) return hip_fail(c, e, "node copy");
+        TT_HIP(c, hipMemsetAsync(c->nodes_k.p, 0, (size_t)n_nodes * TT_NODE_STRIDE, c->stream));
+        TT_HIP(c, refresh_node_copy(c, 0, n_nodes));
+        TT_HIP(c, hipStreamSynchronize(c->stream));
+    }
     TT_HIP(c, hipMemcpy(c->tris_raw.p, tris, sizeof(tt_cuda_triangle) * n_tris, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->tris.p, tp.data(), sizeof(TriPos) * n_tris, hipMemcpyHostToDevice));
     TT_HIP(c, hipMemcpy(c->tlas.p, tlas, sizeof(int32_t) * n_tlas, hipMemcpyHostToDevice));
@@ -917,6 +938,7 @@ tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
     TT_HIP(dst, hipStreamSynchronize(src->stream));  // src's upload has landed
     unlink_borrower(dst);
     dst->nodes.borrow(src->nodes);
+    dst->nodes_k.borrow(src->nodes_k);
     dst->tris_raw.borrow(src->tris_raw);
     dst->tris.borrow(src->tris);
     dst->tlas.borrow(src->tlas);
@@ -977,6 +999,7 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
     TT_HIP(c, scene_write_begin(c));
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
+    TT_HIP(c, refresh_node_copy(c, 0, n_tlas_nodes));
     TT_HIP(c, ring_close(c, slot));
     TT_HIP(c, scene_write_end(c));
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
@@ -1022,6 +1045,7 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
         for (int32_t b : plan.pair_bvh) n_used = std::max(n_used, (uint32_t)b + 1u);
         TT_HIP(c, hipStreamSynchronize(c->stream));  // the old plan's buffers may be in use
         TT_HIP(c, tt_refit_prepare(plan, base, n_used, R.dev));
+        R.n_nodes = n_used;
         if (R.boxes.n < (size_t)6 * p->n_tris) TT_HIP(c, R.boxes.alloc((size_t)6 * p->n_tris));
         R.gen = c->scene_gen;
         R.node_base = node_base;
@@ -1054,6 +1078,7 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_blas_construct(a, c->stream));
     TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
+    TT_HIP(c, refresh_node_copy(c, node_base, R.n_nodes));
     TT_HIP(c, ring_close(c, slot));
     TT_HIP(c, scene_write_end(c));
     if (!(p->flags & TT_TRACE_ASYNC) || !dev) TT_HIP(c, hipStreamSynchronize(c->stream));
@@ -1183,6 +1208,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, scene_write_begin(c));
     TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, pinned, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
+    TT_HIP(c, refresh_node_copy(c, first, count));
     TT_HIP(c, scene_write_end(c));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
     return TT_OK;
@@ -1243,7 +1269,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
 
 tt_status tt_scene_bytes(const tt_ctx* c, uint64_t* bytes) {
     if (!c || !bytes) return TT_ERR_INVALID_ARG;
-    *bytes = c->nodes.n * sizeof(tt_cwbvh_node) + c->tris_raw.n * sizeof(tt_cuda_triangle) + c->tris.n * sizeof(TriPos) +
+    *bytes = c->nodes.n * sizeof(tt_cwbvh_node) + c->nodes_k.n + c->tris_raw.n * sizeof(tt_cuda_triangle) + c->tris.n * sizeof(TriPos) +
              c->tlas.n * 4 + c->mesh_raw.n * sizeof(tt_mesh_data) + c->mesh.n * sizeof(MeshGpu) + c->mat_tag.n * 4;
     return TT_OK;
 }
@@ -1342,7 +1368,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     }
     TraceArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
+    a.nodes = kernel_nodes(c);
     a.n_nodes = (uint32_t)c->host.nodes.size();
     a.tris = c->tris.p;
     a.n_tris = c->host.n_tris;
@@ -1365,6 +1391,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     a.ray_offset = off;
     a.width = p->screen_width;
     a.height = p->screen_height;
+    a.n_pixels = (uint32_t)wh;
     a.far_plane = p->far_plane;
     a.bounce = p->bounce;
     a.flags = p->flags;
@@ -1374,6 +1401,10 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     a.div_width = fastdiv_make(std::max(1u, p->screen_width));
     a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
     a.hits_out = reinterpret_cast<uint4*>(hits_out);
+#ifdef TT_DIAG_BLOCKS  // diagnostic builds only: the block counters' device buffer (tools/diag_blocks.py)
+    if (const char* dp = std::getenv("TT_DIAG_PTR"))
+        a.diag_times = reinterpret_cast<unsigned long long*>(std::strtoull(dp, nullptr, 0));
+#endif
     const bool matcheck = (c->any_invisible && p->bounce == 0) || c->any_cutout ||
                           ((p->flags & TT_TRACE_IGNORE_GLASS) && c->host.any_atlas_shadow) ||
                           ((p->flags & TT_TRACE_IGNORE_BACKFACING) && p->bounce == 0);
@@ -1570,7 +1601,7 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     }
     ShadowArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.nodes = reinterpret_cast<const uint4*>(c->nodes.p);
+    a.nodes = kernel_nodes(c);
     a.n_nodes = (uint32_t)c->host.nodes.size();
     a.tris = c->tris.p;
     a.n_tris = c->host.n_tris;

@@ -26,6 +26,12 @@ __device__ __forceinline__ float rcp_rn(float a) {
     return 1.0f / a;
 }
 
+// Byte stride of the node array the kernels read (tt_traverse.h node_offset): 80 = the reference's
+// cwbvh_nodes as uploaded; 128 = a derived copy, one node per 128-B line (tt_api.hip keeps it in step).
+#ifndef TT_NODE_STRIDE
+#define TT_NODE_STRIDE 80
+#endif
+
 // Traversal-layout triangle, 48 B: the 36 B of positions the Moller-Trumbore test reads
 // (CudaTriangle pos0/posedge1/posedge2, CommonData.cginc:63-66) + MatDat, padded so one
 // triangle is three 16-B loads. Built from AggTris at upload; AggTris itself also stays in
@@ -143,6 +149,7 @@ struct TraceArgs {
                                  // traced = min(*n_rays_dev, n_rays) -- the reference's DispatchIndirect
     uint32_t ray_offset;         // W*H on odd bounces
     uint32_t width, height;
+    uint32_t n_pixels;           // width * height (< 2^31, checked by the API)
     float far_plane;
     int32_t bounce;
     uint32_t flags;              // TT_TRACE_*

@@ -322,7 +322,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
     SegState S{blockIdx.x % TT_SEGS, 0u, 0u};
     const uint32_t n_rays = IND ? launch_ray_count(A) : A.n_rays;
     const uint32_t n_tiles = (n_rays + 63u) >> 6;
-    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
+    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * (uint32_t)TT_NODE_STRIDE);
     const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
     bool active = false;

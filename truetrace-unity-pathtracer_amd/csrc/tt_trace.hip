@@ -24,8 +24,8 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
                                              const Best& best, const LaneRay& wr) {
     tt_ray_data* R = A.rays + ray_index;
     if (INFO != 0) {
-        const uint32_t ty = fastdiv(pix, A.div_width), tx = pix - ty * A.width;
-        if (ty < A.height) {
+        // (pix % W, pix / W) with pix / W < H is the texel at index pix: no division needed
+        if (pix < A.n_pixels) {
             uint4 o;
             bool write = false;
             if (INFO == 1) {
@@ -55,7 +55,7 @@ __device__ __forceinline__ bool write_record(const TraceArgs& A, uint32_t ray_in
                     o.w = miss ? 1u : 0u;
                 }
             }
-            if (write) reinterpret_cast<uint4*>(A.info)[(size_t)ty * A.width + tx] = o;
+            if (write) reinterpret_cast<uint4*>(A.info)[pix] = o;
         }
     }
     const uint32_t uv = (uint32_t)(best.u * 65535.0f) | ((uint32_t)(best.v * 65535.0f) << 16);
@@ -120,6 +120,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     (void)spill_stride;
     (void)spill;
     const uint32_t lane = tid & (TT_WAVE - 1);
+#ifdef TT_DIAG_BLOCKS
+    if (tid < TT_DB_N) tt_db[tid] = 0ull;
+    __syncthreads();
+#endif
 
     // wave-uniform scheduler state: a private pool [pool_next, pool_end) of work indices, refilled
     // from segment `seg` (segments = contiguous 1/TT_SEGS slices of the work range, dealt to XCD
@@ -131,8 +135,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     const uint32_t n_tiles = (n_rays + 63u) >> 6;
     // work index -> ray index in 8x8 screen tiles: full-frame primary batches only (a device count
     // decides at run time)
-    const bool swizzle = IND ? (A.tile_swizzle && n_rays == A.width * A.height) : (A.tile_swizzle != 0u);
-    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * 80u);
+    const bool swizzle = IND ? (A.tile_swizzle && n_rays == A.n_pixels) : (A.tile_swizzle != 0u);
+    const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * (uint32_t)TT_NODE_STRIDE);
     const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
     // lane traversal state (IntersectionKernels.compute:62-77)
@@ -161,6 +165,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         if (ORD) record_chunk_cost(A, swizzle, ray_index, Reps);
     };
     while (true) {
+        TT_DB(0);
         // ---------------------------------------------------------------- refill
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
@@ -170,6 +175,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         // finished rays write their records in batches, right before their lanes are refilled
         if ((n_idle == TT_WAVE && pool_dry) || (n_idle >= TT_REFILL_MIN && !pool_dry) || to_wide) {
             if (pending) {
+                TT_DB(1);
                 finish_ray();
                 pending = false;
             }
@@ -177,6 +183,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         if (n_idle == TT_WAVE && pool_dry) break;
 #if TT_WIDE
         if (to_wide) {
+            TT_DB(13);
             WideState st{ray, wray, best, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset,
                          mesh_id, Reps, ray_index, pix, col_w, tid, gtid, active};
             regroup<2>(st, __ballot(active), lane);
@@ -196,6 +203,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         }
 #endif
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
+            TT_DB(2);
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
@@ -219,7 +227,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             } else {
                 pool_next += take_old;
             }
+#if TT_UNIFORM_POOL  // keep the wave-uniform scheduler state in SGPRs (the loop head's tests become SALU)
+            pool_next = __builtin_amdgcn_readfirstlane(pool_next);
+            pool_end = __builtin_amdgcn_readfirstlane(pool_end);
+            more = __builtin_amdgcn_readfirstlane(more);
+#endif
             if (!active && widx != 0xffffffffu) {
+                TT_DB(4);
+                TT_DL(19, true);
                 // work index -> ray index (8x8 screen tiles for full-frame primary batches)
                 uint32_t local = widx;
                 if (swizzle) {
@@ -232,7 +247,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
                 const uint4 r0 = rp[0], r1 = rp[1];
                 pix = r0.w;
-                if (INFO == 2) col_w = (pix < A.width * A.height) ? A.colors[pix].Data[3] : 0.0f;
+                if (INFO == 2) col_w = (pix < A.n_pixels) ? A.colors[pix].Data[3] : 0.0f;
                 ray.ox = __uint_as_float(r0.x);
                 ray.oy = __uint_as_float(r0.y);
                 ray.oz = __uint_as_float(r0.z);
@@ -276,6 +291,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         }
         // A lane is at the top of the reference's loop exactly when no leaf triangles are pending.
         if (active && tg.y == 0u) {
+            TT_DB(5);
             if (Reps >= TT_MAX_REPS) {
                 active = false;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
@@ -288,8 +304,13 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 const uint32_t child = cg.x + rel;
                 cg.y &= ~(1u << cio);
                 bool ok = true;
-                if (cg.y & 0xff000000u) TT_PUSH(cg, ok);
+                if (cg.y & 0xff000000u) {
+                    TT_DB(7);
+                    TT_PUSH(cg, ok);
+                }
                 if (ok) {
+                    TT_DB(6);
+                    TT_DL(17, true);
                     if (STATS) {  // how many node-phase lanes visit the same node as the first one
                         const uint32_t lead = __builtin_amdgcn_readfirstlane(child);
                         const uint64_t same = __ballot(child == lead), all = __ballot(true);
@@ -318,6 +339,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 cg = make_uint2(0u, 0u);
             }
             if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
+                TT_DB(8);
                 const uint32_t mo = firstbithigh(tg.y);
                 tg.y &= ~(1u << mo);
                 const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
@@ -366,6 +388,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         }
         // --------------------------------------------------------- triangle phase
         if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
+            TT_DB(9);
+            TT_DL(18, true);
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool acc = intersect_triangle<MATCHECK>(tris, A.mat, A.bounce == 0, A.flags, (int32_t)(tg.x + ti),
@@ -380,8 +404,11 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         // One place for every lane whose group is used up, whether it came from a node step or
         // from its last triangle this pass (equivalent order: the reference pops right after).
         if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+            TT_DB(10);
             if (stack_size != 0) {
+                TT_DB(11);
                 if (stack_size == tlas_ss) {
+                    TT_DB(12);
                     NodeOffset = 0;
                     TriOffset = 0;
                     tlas_ss = -1;
@@ -396,6 +423,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         }
     }
 
+#ifdef TT_DIAG_BLOCKS
+    __syncthreads();
+    if (tid < TT_DB_N && A.diag_times && tt_db[tid]) atomicAdd(A.diag_times + tid, tt_db[tid]);
+#endif
     if (STATS) {
         const uint32_t v[8] = {wave_sum(c_rays), wave_sum(c_nodes), wave_sum(c_tris), wave_sum(c_blas),
                                wave_sum(c_hits), wave_sum(c_reps), wave_sum(c_ovf), wave_sum(c_acc)};

@@ -23,6 +23,9 @@
 #ifndef TT_REFILL_MIN
 #define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
 #endif
+#ifndef TT_UNIFORM_POOL
+#define TT_UNIFORM_POOL 0  // 1: readfirstlane the scheduler's pool state after each refill (A/B option)
+#endif
 #ifndef TT_LDS_STACK
 #define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
 #endif
@@ -33,6 +36,32 @@
 #define TT_BOUNDS __launch_bounds__(TT_BLOCK, TT_WAVES_PER_EU)
 #else
 #define TT_BOUNDS __launch_bounds__(TT_BLOCK)
+#endif
+
+// TT_DIAG_BLOCKS builds (tools/diag_blocks.py; never the product): per-block execution counters of
+// the closest-hit loop in LDS, flushed to TraceArgs::diag_times at the end of the launch. TT_DB(k): one
+// wave execution of block k (counted by the first active lane); TT_DL(k, pred): lanes with pred.
+#ifdef TT_DIAG_BLOCKS
+#define TT_DB_N 32
+__shared__ unsigned long long tt_db[TT_DB_N];
+#define TT_DB(k)                                                                               \
+    do {                                                                                       \
+        const uint64_t m_ = __ballot(1);                                                       \
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m_)) atomicAdd(&tt_db[k], 1ull); \
+    } while (0)
+#define TT_DL(k, pred)                                                                         \
+    do {                                                                                       \
+        const uint64_t p_ = __ballot(pred), m_ = __ballot(1);                                  \
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m_))                              \
+            atomicAdd(&tt_db[k], (unsigned long long)__popcll(p_));                            \
+    } while (0)
+#else
+#define TT_DB(k) \
+    do {         \
+    } while (0)
+#define TT_DL(k, pred) \
+    do {               \
+    } while (0)
 #endif
 
 namespace {
@@ -72,8 +101,12 @@ __device__ __forceinline__ uint32_t buffer_load4(__amdgpu_buffer_rsrc_t r, uint3
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
 // i * 80 and i * 48 as shift-adds: written plainly, LLVM folds them back into v_mul_lo_u32, a
-// quarter-rate instruction on the traversal's critical path
+// quarter-rate instruction on the traversal's critical path. TT_NODE_STRIDE 128: the kernels read a
+// derived copy of the node array with every 80-B node at the start of its own 128-B line (tt_api.hip
+// keeps it in step with the reference array), so a node visit touches one cache line instead of 1.5.
+static_assert(TT_NODE_STRIDE == 80 || TT_NODE_STRIDE == 128, "node stride: 80 (the reference array) or 128");
 __device__ __forceinline__ uint32_t node_offset(uint32_t i) {
+    if (TT_NODE_STRIDE == 128) return i << 7;
     uint32_t r;
     asm("v_lshl_add_u32 %0, %1, 2, %1\n\tv_lshlrev_b32 %0, 4, %0" : "=&v"(r) : "v"(i));
     return r;
@@ -362,6 +395,7 @@ __device__ __forceinline__ uint32_t sched_reserve(TraceControl* ctl, uint32_t n_
         const uint32_t len = hi > lo ? hi - lo : 0u;
         const uint32_t want = max(need, (uint32_t)TT_CHUNK_BIG);
         uint32_t off = 0;
+        TT_DB(3);
         if (lane == 0) off = atomicAdd(&ctl->seg_ticket[S.seg * 32u], want);
         off = __builtin_amdgcn_readfirstlane(off);
         if (off < len) {

@@ -191,6 +191,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
         const uint64_t lead = __ballot(st.active && sub == 0u);
         const uint32_t n = (uint32_t)__popcll(lead);
         if (n == 0u) return;
+        TT_DB(G == 2 ? 14 : G == 4 ? 15 : 16);
         if constexpr (G < 8) {
             if (n * (2 * G) <= TT_WAVE) {
                 regroup<2 * G>(st, lead, lane);
@@ -214,6 +215,8 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
                 bool ok = true;
                 if (st.cg.y & 0xff000000u) TT_PUSH(st.cg, ok);
                 if (ok) {
+                    TT_DB(G == 2 ? 20 : G == 4 ? 21 : 22);
+                    TT_DL(23, sub == 0u);
                     const uint32_t no = node_offset(child);
                     const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
                                 n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
@@ -283,6 +286,8 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
         // --------------------------------------------------------- triangle phase
         // :220-226 visits the leaf's triangles highest bit first; lane `sub` takes the sub-th of them
         if (st.active && st.tg.y != 0u) {
+            TT_DB(G == 2 ? 24 : G == 4 ? 25 : 26);
+            TT_DL(27, sub == 0u);
             uint32_t m = st.tg.y;
 #pragma unroll
             for (uint32_t k = 0; k + 1 < (uint32_t)G; k++)

@@ -1,0 +1,248 @@
+"""ttlayout — how one rank issues its share of a frame's trace launches (bench.py, tools/strong_replay.py).
+
+The reference dispatches kernel_trace once per bounce over the whole screen
+(RayTracingMaster.cs:954-1007). A rank here traces its pixels (the whole frame at N = 1, its 64x64
+tiles under tile sharding) as
+
+  * P tile-interleaved **parts** (ttdist.part_pixels), each traced by its own engine context on its
+    own HIP stream, so one part's launch drain overlaps the other parts' work; and
+  * F **frame slots**: frame k runs on slot k % F. Each slot has its own ray, _PrimaryTriangleInfo
+    and hit-record buffers and its own streams, so frame k + 1's primary launches (which depend on
+    nothing of frame k) run while frame k's bounce-1 launches drain. Inside a frame the order is the
+    reference's: a part's bounce-1 launch follows its primary launch on the same stream.
+
+All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). A step is one
+frame: every part's primary launch (writing its 16-B hit records straight into the gather's send
+buffer when there is one, tt_trace_closest_hits), the optional gather of those records to rank 0 on a
+communication stream, then every part's bounce-1 launch. Bounce-1 rays are the primary hits'
+diffuse continuations (tt_enqueue_diffuse_bounce), built once at setup -- the enqueue is the
+caller's kernel, not the trace -- and re-traced every frame (the kernel resets every ray's state).
+_PrimaryTriangleInfo is written at bounce 0; the bounce-1 form goes to a second buffer (the
+reference rebinds the texture to GIWorldPosA at bounce > 0, RayTracingMaster.cs:884).
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import numpy as np
+
+
+class Part:
+    """One launch stream of a rank: engine context, stream, its compacted rays and counts."""
+
+    eng = None
+    stream = None
+    rays = None
+    n = 0
+    nb = 0
+    s_prim = None
+    s_bnc = None
+    prim_hits = None
+    hit_slices: List = []
+
+
+class FrameLayout:
+    """A rank's frame as ``len(plan)`` parts x ``slots`` frame slots (module docstring).
+
+    plan: per part, [(sample k, pixel indices)] -- the rays of sample k (``make_full(k)``: a W*H
+    RayData buffer of that sample's Generate) at those pixels, back to back in the part's buffer.
+    bounce: trace bounce 1 too (False: primary only, the C5 config).
+    lend: the engine whose scene every context traces (slot 0 / part 0 reuses it)."""
+
+    def __init__(self, torch, tthip, lend, dev, W: int, H: int, far: float, plan, make_full: Callable,
+                 slots: int = 1, bounce: bool = True, info: bool = True, colors=None, frames: int = 0):
+        self.torch, self.tthip, self.dev = torch, tthip, dev
+        self.W, self.H, self.far = W, H, far
+        self.P, self.F = len(plan), max(1, int(slots))
+        self.bounce, self.colors, self.frames = bounce, colors, frames
+        WH = W * H
+        self.engines = []  # (engine, stream) per context, lend's first; contexts created here are closed by close()
+        self.own = []
+        self.slots: List[List[Part]] = []
+        base_stream = torch.cuda.current_stream(dev)
+        self.info0 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if info else None for _ in range(self.F)]
+        self.info1 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if (info and bounce) else None
+                      for _ in range(self.F)]
+        for f in range(self.F):
+            row = []
+            for s, lst in enumerate(plan):
+                p = Part()
+                if f == 0 and s == 0:
+                    p.eng, p.stream = lend, base_stream
+                else:
+                    st = torch.cuda.Stream(dev)
+                    e = tthip.Engine(dev.index, stream=st.cuda_stream)
+                    e.share_scene(lend)  # ONE scene copy: one cache footprint for all contexts
+                    self.own.append(e)
+                    p.eng, p.stream = e, st
+                p.n = int(sum(len(pix) for _, pix in lst))
+                # GlobalRays ping-pong: bounce-1 rays live at [W*H, W*H + nb) (odd bounces, the API's offset)
+                p.rays = torch.zeros(((WH + p.n) if bounce else max(p.n, 1)) * 48, dtype=torch.uint8, device=dev)
+                row.append(p)
+            self.slots.append(row)
+        # fill the parts' primary rays, sample by sample
+        for k in sorted({k for lst in plan for k, _ in lst}):
+            full = make_full(k)
+            for row in self.slots:
+                for p, lst in zip(row, plan):
+                    o = 0
+                    for kk, pix in lst:
+                        if kk == k and len(pix):
+                            p.rays.view(-1, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
+                        o += len(pix)
+            del full
+        torch.cuda.synchronize(dev)
+        # setup: one stats trace per bounce (part counters) and the bounce-1 enqueue, on every slot
+        for f, row in enumerate(self.slots):
+            for p in row:
+                p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, stats=True)
+                if bounce:
+                    p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+                    p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=self.info1[f], colors=colors,
+                                          device=True, stats=True)
+                p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
+                p.hit_slices = []
+        torch.cuda.synchronize(dev)
+        self.gather = None
+        self.k = 0
+        self.k_reset = 0
+
+    # ---------------------------------------------------------------- sizes
+    @property
+    def parts(self) -> List[Part]:
+        """Slot 0's parts (every slot traces the same rays)."""
+        return self.slots[0]
+
+    def rays_per_frame(self) -> int:
+        return int(sum(p.n + p.nb for p in self.parts))
+
+    def n_prim(self) -> int:
+        return int(sum(p.n for p in self.parts))
+
+    def n_bounce(self) -> int:
+        return int(sum(p.nb for p in self.parts))
+
+    # ---------------------------------------------------------------- gather
+    def attach_gather(self, dist, world: int, rank: int, red_dev):
+        """The per-frame gather of the primary hit records to rank 0 (RCCL on the GPU, gloo rehearsals on
+        the host). Shards are padded to the largest so every rank sends one equal-size message; a rank's
+        parts back to back. On the GPU the primary traces write their records straight into the slot's
+        send buffer (tt_trace_closest_hits); two send buffers per slot alternate, so a slot's next frame
+        waits only for the gather two frames back. The gloo form copies the records to a host buffer."""
+        torch = self.torch
+        g = _Gather()
+        n_t = torch.tensor([p.n for p in self.parts], dtype=torch.int64, device=red_dev)
+        sz = [torch.zeros_like(n_t) for _ in range(world)]
+        dist.all_gather(sz, n_t)
+        g.dist, g.world, g.rank = dist, world, rank
+        g.sizes = [[int(v) for v in x.tolist()] for x in sz]
+        g.stream_hits = red_dev.type == "cuda"
+        g.nbuf = 2 * self.F if g.stream_hits else 1
+        m = max(sum(x) for x in g.sizes)
+        g.bufs = [torch.zeros((m, 4), dtype=torch.int32, device=red_dev) for _ in range(g.nbuf)]
+        g.lists = [[torch.empty_like(bf) for _ in range(world)] if rank == 0 else None for bf in g.bufs]
+        g.comm = torch.cuda.Stream(self.dev)
+        g.done = [torch.cuda.Event() for _ in range(g.nbuf)]
+        g.used = [False] * g.nbuf
+        g.copied = torch.cuda.Event()
+        g.last = None
+        o = 0
+        for s in range(self.P):
+            n = self.parts[s].n
+            for row in self.slots:
+                row[s].hit_slices = [bf[o:o + n] for bf in g.bufs]
+            o += n
+        self.gather = g
+        return g
+
+    def last_gathered(self):
+        """(sizes, per-rank gathered blocks) of the most recent frame's gather (rank 0)."""
+        g = self.gather
+        return g.sizes, g.lists[g.last]
+
+    # ---------------------------------------------------------------- one frame
+    def step(self):
+        k = self.k
+        self.k += 1
+        f = k % self.F
+        row = self.slots[f]
+        g = self.gather
+        W, H, far = self.W, self.H, self.far
+        b = (f + self.F * ((k // self.F) % 2)) % g.nbuf if g is not None else 0
+        for p in row:
+            if g is not None and g.stream_hits:
+                if g.used[b]:
+                    p.stream.wait_event(g.done[b])  # the gather that last read send buffer b is done
+                p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, asynchronous=True,
+                            hits_out=p.hit_slices[b])
+            else:
+                p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, asynchronous=True)
+        if g is not None:
+            torch = self.torch
+            for p in row:
+                g.comm.wait_stream(p.stream)  # this frame's primary hit records are final
+            with torch.cuda.stream(g.comm):
+                if not g.stream_hits:
+                    for p in row:
+                        p.hit_slices[0].copy_(p.prim_hits)
+                    g.copied.record(g.comm)
+                g.dist.gather(g.bufs[b], g.lists[b], dst=0)
+                if g.stream_hits:
+                    g.done[b].record(g.comm)
+                    g.used[b] = True
+            g.last = b
+        if self.bounce:
+            for p in row:
+                p.eng.trace(p.rays, p.nb, 1, far, W, H, info=self.info1[f], colors=self.colors, device=True,
+                            asynchronous=True)
+        if g is not None and not g.stream_hits:
+            for p in row:
+                # the next primary trace rewrites the records copied out above: it waits for the copy
+                p.stream.wait_event(g.copied)
+
+    def streams(self):
+        return [p.stream for row in self.slots for p in row]
+
+    def timing_reset(self):
+        for row in self.slots:
+            for p in row:
+                p.eng.timing_reset()
+        self.k_reset = self.k
+
+    def launch_ms(self, ring: int = 256) -> Optional[np.ndarray]:
+        """Part 0's per-launch HIP-event times of the last frames its slot traced since timing_reset
+        (rows: frames, columns: primary[, bounce-1]) -- slot 0's, or the first slot that traced one;
+        every context's ring is drained."""
+        per = 2 if self.bounce else 1
+        out = None
+        for f, row in enumerate(self.slots):
+            mine = sum(1 for k in range(self.k_reset, self.k) if k % self.F == f)
+            for s, p in enumerate(row):
+                ms = np.asarray(p.eng.timing_read(), np.float64)
+                rows = min(mine, ring // per)
+                assert len(ms) == rows * per, (len(ms), rows, per)
+                if s == 0 and out is None and rows > 0:
+                    out = ms.reshape(rows, per)
+        return out
+
+    def close(self):
+        for e in self.own:
+            e.close()
+        self.own = []
+
+
+class _Gather:
+    pass
+
+
+def full_frame_maker(torch, eng, dev, W: int, H: int, c2w, ip, near: float, far: float, jitter: int = 1,
+                     max_bounce: int = 1):
+    """make_full for FrameLayout: sample k's primary rays (the reference's Generate with
+    frames_accumulated = k) in a fresh W*H RayData buffer."""
+
+    def make(k: int):
+        full = torch.zeros(W * H * 48, dtype=torch.uint8, device=dev)
+        eng.generate(full, c2w, ip, W, H, near, far, jitter=jitter, frames=k, max_bounce=max_bounce, device=True)
+        return full
+
+    return make
