@@ -417,7 +417,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     (ttlayout.FrameLayout: frame k + 1 overlaps frame k's drain), one RCCL gather of the frame's 16-B hit
     records to rank 0 per frame, which reassembles the frame and compares it with one GPU tracing the
     whole frame. Strong scaling: frame time = slowest rank; efficiency against the N = 1 frame (the whole
-    4K frame, 2 parts, the same slots) traced on every rank's own GPU at once in the same run (fastest).
+    4K frame, 2 parts, 1 slot) traced on every rank's own GPU at once in the same run (fastest).
     Failures are agreed on collectively before the gather, so one rank's error cannot hang the rest."""
     import ttconfigs as T
     import ttdist
@@ -438,8 +438,8 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         c2w, ip = T.C5_VIEW.camera(W, H)
         make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, far)
 
-        def timed_layout(plan):
-            lay_ = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=F, bounce=False,
+        def timed_layout(plan, slots=F):
+            lay_ = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots, bounce=False,
                                         info=False)
             for _ in range(max(2, args.warmup)):
                 lay_.step()
@@ -454,8 +454,8 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
             lay_.launch_ms()
             return lay_, el
 
-        # the N = 1 frame on every rank's GPU at once (no collective inside)
-        solo, el1 = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)])
+        # the N = 1 frame (2 parts, 1 slot: the single-GPU layout) on every rank's GPU at once (no collective)
+        solo, el1 = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], slots=1)
         solo.close()
         del solo
         lay, el_n = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)])
@@ -508,7 +508,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
                with_gather=dict(ms_per_frame_slowest_rank=round(msg, 4), efficiency=round(ms1 / (world * msg), 4),
                                 mrays_s_frame=round(WH / msg / 1e3, 1)),
                identical_to_1gpu=bool(np.array_equal(frame, ref)),
-               note="efficiency = t(N = 1: the whole 4K frame, 2 parts, same slots, on every rank's GPU at once, "
+               note="efficiency = t(N = 1: the whole 4K frame, 2 parts, 1 slot, on every rank's GPU at once, "
                     "fastest) / (N x t(N), slowest rank); with_gather: the per-frame RCCL gather of the hit records to "
                     "rank 0 inside the timed frames")
     log(f"c5 tiles: {rec}")
@@ -674,7 +674,7 @@ def main():
                          "its own buffers and streams, so frame k + 1's primary launches overlap frame k's bounce-1 "
                          "launches. 0 (default): 1 for a full frame's worth per rank, --strong-slots for the "
                          "strong-scaling shards (--shard tiles)")
-    ap.add_argument("--strong-slots", type=int, default=2,
+    ap.add_argument("--strong-slots", type=int, default=1,
                     help="frame slots of the strong-scaling tile layouts (N > 1: aux_strong_tiles, aux_c5_tiles) and of "
                          "their N = 1 reference frames")
     ap.add_argument("--no-strong", action="store_true",
@@ -909,12 +909,12 @@ def main():
         del srays
         log(f"sample-sharded (weak) layout: {sample_sharded}")
 
-    # N > 1: the N = 1 frame (the whole 1080p frame in the single-GPU layout: 2 parts, F_strong slots) on
+    # N > 1: the N = 1 frame (the whole 1080p frame in the single-GPU headline layout: 2 parts, 1 slot) on
     # every rank's own GPU at once, no collective -- the T(1) of the strong-scaling efficiency below,
     # measured in the same run on the same kind of GPU (the fastest rank's, conservative)
     solo_ms = None
     if world > 1 and not args.no_strong:
-        solo = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], F_strong)
+        solo = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], 1)
         el_solo = timed(solo)
         solo.launch_ms()
         solo.close()
@@ -923,7 +923,7 @@ def main():
         solo_ms = float(t.item()) * 1e3 / args.steps
         solo_rays = solo.rays_per_frame()
         del solo
-        log(f"N = 1 frame on each rank's GPU (2 parts, {F_strong} slots): {solo_ms:.4f} ms (fastest rank)")
+        log(f"N = 1 frame on each rank's GPU (2 parts, 1 slot): {solo_ms:.4f} ms (fastest rank)")
 
     G = layout.attach_gather(dist, world, rank, red_dev) if tiles else None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
@@ -1030,7 +1030,7 @@ def main():
                   "gather_identical_to_1gpu": par,
                   "layout": "one 1080p frame (1 sample): 64x64 tiles round-robin over the ranks, each rank's tiles "
                             f"as {lay_s.P} parts x {lay_s.F} frame slots, + one RCCL gather of the frame's primary "
-                            "hit records per frame; efficiency = t(N = 1 frame, 2 parts, same slots, every rank's "
+                            "hit records per frame; efficiency = t(N = 1 frame, 2 parts, 1 slot, every rank's "
                             "GPU at once, fastest) / (N x t(N))"}
         if lay_s is not layout:
             lay_s.close()

@@ -47,7 +47,7 @@ for stage in "$@"; do
     pmcu) run pmcu 900 bash tools/pmc_units.sh "$OUT/pmcu" || exit $? ;;
     diag) run diag 200 env TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_diag.so \
               python -u tools/diag_blocks.py c2 || exit $? ;;
-    replay) run replay 600 python -u tools/strong_replay.py --configs c2,c5 || exit $? ;;
+    replay) run replay 900 python -u tools/strong_replay.py --configs c2,c5 ${REPLAY_ARGS:-} || exit $? ;;
     gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
     sweep) run sweep_plain 600 python -u tools/parity_sweep.py 300 40000 || exit $?

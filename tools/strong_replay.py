@@ -5,7 +5,7 @@ tiles as P tile-interleaved parts x F frame slots (ttlayout.FrameLayout, the lay
 aux_strong_tiles / aux_c5_tiles) -- and predicts
 
     t(N)   = max over ranks r of rank r's frame time (ms per frame, frames back to back)
-    eff(N) = t(1) / (N * t(N)),   t(1) = the whole frame in the N = 1 layout (2 parts, same F)
+    eff(N) = t(1) / (N * t(N)),   t(1) = the whole frame in the N = 1 layout (2 parts, 1 slot)
 
 The per-frame RCCL gather of the hit records is not replayed (it runs on its own stream beside the
 traces; bench.py measures it on a real node). Configs: C2 (Sponza-shaped 1080p, primary + bounce 1)
@@ -27,8 +27,10 @@ sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c2,c5")
-    ap.add_argument("--slots", type=int, default=2)
+    ap.add_argument("--slots", type=int, default=1, help="frame slots per rank (bench.py --strong-slots)")
     ap.add_argument("--parts-small", type=int, default=3, help="parts per rank at N >= 4 (bench.py's default)")
+    ap.add_argument("--layouts", default=None,
+                    help="comma list of PxF layouts to replay at every N > 1 instead of (parts, --slots), e.g. 3x1,1x3")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ns", default="1,2,4,8")
@@ -75,26 +77,32 @@ def main():
         rows = []
         t1 = None
         for n in [int(x) for x in args.ns.split(",")]:
-            P = 2 if n < 4 else args.parts_small
+            if n == 1:  # the reference: the single-GPU headline layout (2 parts, one slot)
+                layouts = [(2, 1)]
+            elif args.layouts:
+                layouts = [tuple(int(v) for v in l.split("x")) for l in args.layouts.split(",")]
+            else:
+                layouts = [(2 if n < 4 else args.parts_small, args.slots)]
             ranks = range(n) if args.ranks == "all" else [int(r) for r in args.ranks.split(",") if int(r) < n]
-            per = []
-            for r in ranks:
-                lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR,
-                                           [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P)], make_full,
-                                           slots=args.slots, bounce=bounce, info=True, colors=colors)
-                ms = frame_ms(lay)
-                per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
-                lay.close()
-                del lay
-                print(f"[replay] {name} N={n} rank {r}: {per[-1]}", file=sys.stderr, flush=True)
-            t_n = max(p["ms_per_frame"] for p in per)
-            if n == 1:
-                t1 = t_n
-            rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": args.slots, "ranks": per,
-                         "t_frame_ms_slowest_rank": t_n,
-                         "predicted_efficiency": round(t1 / (n * t_n), 3) if t1 else None,
-                         "predicted_frame_mrays_s": round(sum(p["rays"] for p in per) / t_n / 1e3, 1)
-                         if args.ranks == "all" else None})
+            for P, F in layouts:
+                per = []
+                for r in ranks:
+                    lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR,
+                                               [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P)], make_full,
+                                               slots=F, bounce=bounce, info=True, colors=colors)
+                    ms = frame_ms(lay)
+                    per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
+                    lay.close()
+                    del lay
+                    print(f"[replay] {name} N={n} {P}x{F} rank {r}: {per[-1]}", file=sys.stderr, flush=True)
+                t_n = max(p["ms_per_frame"] for p in per)
+                if n == 1:
+                    t1 = t_n
+                rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": F, "ranks": per,
+                             "t_frame_ms_slowest_rank": t_n,
+                             "predicted_efficiency": round(t1 / (n * t_n), 3) if t1 else None,
+                             "predicted_frame_mrays_s": round(sum(p["rays"] for p in per) / t_n / 1e3, 1)
+                             if args.ranks == "all" else None})
         out["configs"][name] = {"width": W, "height": H, "tris": int(len(scene.tris)), "rows": rows}
 
     which = set(args.configs.split(","))

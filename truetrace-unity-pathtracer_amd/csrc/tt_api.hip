@@ -139,6 +139,9 @@ struct tt_ctx {
     uint32_t tex_w = 0, tex_h = 0;
     DevBuf<uint8_t> atlas;      // _AlphaAtlas (R8)
     uint32_t atlas_w = 0, atlas_h = 0;
+    // TT_ROOT_LEAF: node 0 as the device holds it is known on the host (upload, node updates); a device
+    // refit of the TLAS rewrites it without a read-back, so the fast root step is off until the next update
+    bool root_known = false;
     // TLAS refit (f4): plan valid for (scene generation, n_tlas_nodes)
     RefitDev refit;
     uint64_t scene_gen = 0, refit_gen = ~0ull;
@@ -877,6 +880,7 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
         TT_HIP(c, hipMemcpy(c->mat_glass.p, h.glass.data(), sizeof(GlassMat) * h.glass.size(), hipMemcpyHostToDevice));
     }
     c->host = std::move(h);
+    c->root_known = true;
     c->any_invisible = any_invisible;
     c->scene_gen++;
     c->any_shadow_skip = c->host.any_shadow_skip;
@@ -1000,6 +1004,7 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
     TT_HIP(c, refresh_node_copy(c, 0, n_tlas_nodes));
+    c->root_known = false;  // node 0 was rewritten on the device
     TT_HIP(c, ring_close(c, slot));
     TT_HIP(c, scene_write_end(c));
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
@@ -1211,6 +1216,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, refresh_node_copy(c, first, count));
     TT_HIP(c, scene_write_end(c));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
+    if (first == 0) c->root_known = true;  // node 0 is the host's again
     return TT_OK;
 }
 
@@ -1401,6 +1407,11 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     a.div_width = fastdiv_make(std::max(1u, p->screen_width));
     a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
     a.hits_out = reinterpret_cast<uint4*>(hits_out);
+    {  // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root, when the host knows the device's node 0
+        const tt_ctx* owner = c->lender ? c->lender : c;
+        if (owner->root_known && !owner->host.nodes.empty())
+            a.root = root_leaf_of(reinterpret_cast<const uint32_t*>(owner->host.nodes.data()));
+    }
 #ifdef TT_DIAG_BLOCKS  // diagnostic builds only: the block counters' device buffer (tools/diag_blocks.py)
     if (const char* dp = std::getenv("TT_DIAG_PTR"))
         a.diag_times = reinterpret_cast<unsigned long long*>(std::strtoull(dp, nullptr, 0));

@@ -126,6 +126,52 @@ struct MatView {
         if ((A).sticky_overflow) atomicAdd((A).sticky_overflow, 1u); \
     } while (0)
 
+// TT_ROOT_LEAF: the TLAS root (node 0) of a one-leaf TLAS -- no internal child and exactly one
+// non-empty child slot, a leaf: the TLAS the reference builds for a scene of one ParentObject instance,
+// such as an imported OBJ (C2, C3, C5). Its node step (IntersectionKernels.compute:157-187, the first of
+// every ray, at t_max = FarPlane) is then that one child's slab test (tt_trace.hip root_leaf_hit, the
+// node test's arithmetic for that child), so hits, Reps and stats are unchanged. Derived on the host
+// from the node-0 bytes the device holds (tt_api.hip: known after an upload or a node update; a device
+// refit of the TLAS turns it off until the next update), passed as a kernel argument (SGPRs).
+#ifndef TT_ROOT_LEAF
+#define TT_ROOT_LEAF 0
+#endif
+struct RootLeaf {
+    uint32_t ok;                          // node 0 qualifies
+    uint32_t qlo, qhi;                    // the child's quantized planes: bytes 0-2 = x, y, z
+    uint32_t e;                           // node 0's exponent bytes (x, y, z) = node_0w & 0xffffff
+    float px, py, pz;                     // node origin
+    uint32_t base_child, base_tri, bits;  // node 0's base indices; the leaf's hit bits (child_bits << low5)
+};
+__host__ __device__ inline uint32_t rl_byte(uint32_t w, uint32_t k) { return (w >> (k * 8u)) & 0xffu; }
+// w: node 0's 20 words (the 80-B layout)
+__host__ __device__ inline RootLeaf root_leaf_of(const uint32_t* w) {
+    RootLeaf R{};
+    uint32_t count = 0, slot = 0, inner = 0;
+    for (uint32_t j = 0; j < 8u; j++) {
+        const uint32_t meta = rl_byte(w[6 + (j >> 2)], j & 3u);
+        if (meta >> 5) {
+            count++;
+            slot = j;
+            inner |= (meta & (meta << 1) & 0x10u) ? 1u : 0u;  // node_intersect's inner-child test
+        }
+    }
+    const uint32_t h = slot >> 2, k = slot & 3u;
+    R.ok = (w[3] >> 24) == 0u && count == 1u && inner == 0u;
+    R.qlo = rl_byte(w[8 + h], k) | rl_byte(w[12 + h], k) << 8 | rl_byte(w[16 + h], k) << 16;
+    R.qhi = rl_byte(w[10 + h], k) | rl_byte(w[14 + h], k) << 8 | rl_byte(w[18 + h], k) << 16;
+    R.e = w[3] & 0xffffffu;
+    uint32_t p[3] = {w[0], w[1], w[2]};
+    R.px = __builtin_bit_cast(float, p[0]);
+    R.py = __builtin_bit_cast(float, p[1]);
+    R.pz = __builtin_bit_cast(float, p[2]);
+    R.base_child = w[4];
+    R.base_tri = w[5];
+    const uint32_t meta = rl_byte(w[6 + h], k);
+    R.bits = (meta >> 5) << (meta & 0x1fu);
+    return R;
+}
+
 struct TraceArgs {
     const uint4* nodes;          // 80 B nodes as 5 x uint4
     uint32_t n_nodes;
@@ -161,6 +207,7 @@ struct TraceArgs {
     const uint32_t* order;       // nullable: work chunk -> ray chunk (64 rays), from tt_order_kernel
     uint32_t* chunk_cost;        // per ray chunk: max Reps of its rays (atomicMax, rays with Reps >= TT_ORDER_MIN_REPS)
     uint4* hits_out;             // nullable (tt_trace_closest_hits): ray i's hit record also at hits_out[i]
+    RootLeaf root;               // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root (root.ok = 0: the generic path)
 };
 
 // Adaptive-order builder (tt_order.hip): one block per scheduler segment sorts the segment's

@@ -103,6 +103,36 @@ __device__ __forceinline__ void record_chunk_cost(const TraceArgs& A, bool swizz
 }  // namespace
 
 
+// TT_ROOT_LEAF (TraceArgs::root, tt_device.h): the root of a one-leaf TLAS is stepped when a ray starts
+// and the TLAS leaf -> BLAS switch follows before the loop's node step, so the ray's first node step in
+// the loop is already its BLAS root (one loop iteration less per ray).
+namespace {
+// node_intersect (tt_traverse.h) for the root's one child: the same operations in the same order
+__device__ __forceinline__ bool root_leaf_hit(const RootLeaf& R, const LaneRay& r, float max_distance) {
+    const float adjx = __uint_as_float(rl_byte(R.e, 0) << 23) * r.ix;
+    const float adjy = __uint_as_float(rl_byte(R.e, 1) << 23) * r.iy;
+    const float adjz = __uint_as_float(rl_byte(R.e, 2) << 23) * r.iz;
+    const float orgx = r.ix * (R.px - r.ox);
+    const float orgy = r.iy * (R.py - r.oy);
+    const float orgz = r.iz * (R.pz - r.oz);
+    const bool nx = r.dx < 0.0f, ny = r.dy < 0.0f, nz = r.dz < 0.0f;
+    const uint32_t x_min = rl_byte(nx ? R.qhi : R.qlo, 0), x_max = rl_byte(nx ? R.qlo : R.qhi, 0);
+    const uint32_t y_min = rl_byte(ny ? R.qhi : R.qlo, 1), y_max = rl_byte(ny ? R.qlo : R.qhi, 1);
+    const uint32_t z_min = rl_byte(nz ? R.qhi : R.qlo, 2), z_max = rl_byte(nz ? R.qlo : R.qhi, 2);
+    const float tminx = fma_((float)x_min, adjx, orgx);
+    const float tminy = fma_((float)y_min, adjy, orgy);
+    const float tminz = fma_((float)z_min, adjz, orgz);
+    const float tmaxx = fma_((float)x_max, adjx, orgx);
+    const float tmaxy = fma_((float)y_max, adjy, orgy);
+    const float tmaxz = fma_((float)z_max, adjz, orgz);
+    const float tmin = fmaxf(fmaxf(tminx, tminy), fmaxf(tminz, 1e-8f));
+    float tmaxz_c;
+    asm("v_min_f32 %0, %1, %2" : "=v"(tmaxz_c) : "v"(tmaxz), "v"(max_distance));
+    const float tmax = fminf(fminf(tmaxx, tmaxy), tmaxz_c);
+    return tmin < tmax;
+}
+}  // namespace
+
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
 // IND: the ray count is device-resident (tt_trace_closest_indirect): instantiated as its own kernel
 // (tt_trace_kernel_indirect), so the direct launches keep exactly their code and kernel names.
@@ -157,6 +187,49 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     // the world-space ray (ray2, IntersectionKernels.compute:151), kept in registers
     auto world_ray = [&]() -> LaneRay { return wray; };
 
+#if TT_ROOT_LEAF
+    const bool rl_ok = A.root.ok != 0u;  // a kernel argument: wave-uniform
+#endif
+    // :194-219 TLAS leaf -> BLAS (the lane is at TLAS level with pending leaf bits in tg)
+    auto enter_blas = [&]() {
+            TT_DB(8);
+            const uint32_t mo = firstbithigh(tg.y);
+            tg.y &= ~(1u << mo);
+            const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
+            const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
+            const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
+            const int4 mo5 = reinterpret_cast<const int4*>(mp)[4];
+            mesh_id = mo5.x;
+            NodeOffset = mo4.y;
+            TriOffset = mo4.x;
+            bool ok = true;
+            if (tg.y != 0u) TT_PUSH(tg, ok);
+            if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
+            if (ok) {
+                tlas_ss = stack_size;
+                MatOffset = mo4.z;
+                LaneRay nr;
+                nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
+                nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
+                nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
+                nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
+                nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
+                nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
+                nr.ix = rcp_rn(nr.dx);
+                nr.iy = rcp_rn(nr.dy);
+                nr.iz = rcp_rn(nr.dz);
+                ray = nr;
+                oct = octant_inv4(ray);
+                cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+                if (STATS) c_blas++;
+            } else {
+                active = false;
+                if (STATS) c_ovf++;
+                TT_REPORT_OVERFLOW(A);
+                keep_record(A, ray_index);
+            }
+            tg.y = 0u;
+    };
     // :229-241: the finished ray's hit record and _PrimaryTriangleInfo
     auto finish_ray = [&]() {
         const bool hit = write_record<INFO>(A, ray_index, pix, col_w, best, world_ray());
@@ -275,8 +348,23 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 Reps = 0;
                 active = true;
                 if (STATS) c_rays++;
+#if TT_ROOT_LEAF
+                if (rl_ok) {  // the root's node step, then the TLAS leaf -> BLAS switch
+                    const RootLeaf& RL = A.root;
+                    const bool hit = root_leaf_hit(RL, ray, best.t);
+                    cg = make_uint2(RL.base_child, 0u);  // (hitmask & 0xff000000) | imask: both 0
+                    tg = make_uint2(RL.base_tri, hit ? RL.bits : 0u);
+                    Reps = 1;
+                    if (STATS) c_nodes++;
+                }
+#endif
             }
         }
+#if TT_ROOT_LEAF
+        // the started rays that hit the root's leaf switch to their BLAS before this iteration's node
+        // step (a TLAS-level lane has no pending leaf bits at the loop top otherwise)
+        if (rl_ok && active && tg.y != 0u && tlas_ss == -1) enter_blas();
+#endif
 
         // ------------------------------------------------------------- node phase
         if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)
@@ -338,45 +426,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 tg = cg;
                 cg = make_uint2(0u, 0u);
             }
-            if (active && tg.y != 0u && tlas_ss == -1) {  // :194-219 TLAS leaf -> BLAS
-                TT_DB(8);
-                const uint32_t mo = firstbithigh(tg.y);
-                tg.y &= ~(1u << mo);
-                const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
-                const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
-                const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
-                const int4 mo5 = reinterpret_cast<const int4*>(mp)[4];
-                mesh_id = mo5.x;
-                NodeOffset = mo4.y;
-                TriOffset = mo4.x;
-                bool ok = true;
-                if (tg.y != 0u) TT_PUSH(tg, ok);
-                if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
-                if (ok) {
-                    tlas_ss = stack_size;
-                    MatOffset = mo4.z;
-                    LaneRay nr;
-                    nr.dx = fma_(m0.z, ray.dz, fma_(m0.y, ray.dy, m0.x * ray.dx));
-                    nr.dy = fma_(m1.z, ray.dz, fma_(m1.y, ray.dy, m1.x * ray.dx));
-                    nr.dz = fma_(m2.z, ray.dz, fma_(m2.y, ray.dy, m2.x * ray.dx));
-                    nr.ox = fma_(m0.z, ray.oz, fma_(m0.y, ray.oy, m0.x * ray.ox)) + m0.w;
-                    nr.oy = fma_(m1.z, ray.oz, fma_(m1.y, ray.oy, m1.x * ray.ox)) + m1.w;
-                    nr.oz = fma_(m2.z, ray.oz, fma_(m2.y, ray.oy, m2.x * ray.ox)) + m2.w;
-                    nr.ix = rcp_rn(nr.dx);
-                    nr.iy = rcp_rn(nr.dy);
-                    nr.iz = rcp_rn(nr.dz);
-                    ray = nr;
-                    oct = octant_inv4(ray);
-                    cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
-                    if (STATS) c_blas++;
-                } else {
-                    active = false;
-                    if (STATS) c_ovf++;
-                    TT_REPORT_OVERFLOW(A);
-                    keep_record(A, ray_index);
-                }
-                tg.y = 0u;
-            }
+            if (active && tg.y != 0u && tlas_ss == -1) enter_blas();  // :194-219 TLAS leaf -> BLAS
         }
 
         if (STATS) {

@@ -23,8 +23,11 @@
 #ifndef TT_REFILL_MIN
 #define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
 #endif
+#ifndef TT_PUSH_FAST
+#define TT_PUSH_FAST 0  // 1: the stack push tests only "an LDS entry is free" on its common path (A/B option)
+#endif
 #ifndef TT_UNIFORM_POOL
-#define TT_UNIFORM_POOL 0  // 1: readfirstlane the scheduler's pool state after each refill (A/B option)
+#define TT_UNIFORM_POOL 1  // readfirstlane the scheduler's pool state after each refill (0: A/B; +1.2% bench, profiles/r04/ab)
 #endif
 #ifndef TT_LDS_STACK
 #define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
@@ -443,6 +446,24 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // Traversal stack: entries [0, TT_LDS_STACK) in LDS s_stack[entry][thread] (64 distinct banks per
 // wave access), deeper entries in a global spill area [entry][grid thread]. Expect in scope:
 // s_stack, spill, spill_stride, gtid, tid, stack_size.
+#if TT_PUSH_FAST  // one compare on the common path (an LDS entry is free); overflow / spill only beyond it
+#define TT_PUSH(val, ok)                                                            \
+    do {                                                                            \
+        if (TT_LDS_STACK >= TT_STACK_SIZE || stack_size < TT_LDS_STACK) {           \
+            if (TT_LDS_STACK >= TT_STACK_SIZE && stack_size == TT_STACK_SIZE) {     \
+                ok = false;                                                         \
+            } else {                                                                \
+                s_stack[stack_size][tid] = (val);                                   \
+                stack_size++;                                                       \
+            }                                                                       \
+        } else if (stack_size == TT_STACK_SIZE) {                                   \
+            ok = false;                                                             \
+        } else {                                                                    \
+            spill[(size_t)(stack_size - TT_LDS_STACK) * spill_stride + gtid] = (val); \
+            stack_size++;                                                           \
+        }                                                                           \
+    } while (0)
+#else
 #define TT_PUSH(val, ok)                                                            \
     do {                                                                            \
         if (stack_size == TT_STACK_SIZE) {                                          \
@@ -455,6 +476,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
             stack_size++;                                                           \
         }                                                                           \
     } while (0)
+#endif
 #define TT_POP(dst)                                                                 \
     do {                                                                            \
         --stack_size;                                                               \
