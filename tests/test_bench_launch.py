@@ -97,6 +97,6 @@ def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
     st = c["aux_strong_tiles"]
     assert st["scaling"] == "strong" and st["gather_identical_to_1gpu"] is True
     assert 4_000_000 < st["rays_per_frame_all_ranks"] < 4_200_000
-    assert st["frame_slots"] == 2 and 4_000_000 < st["n1_rays_per_frame"] < 4_200_000
+    assert st["frame_slots"] >= 1 and 4_000_000 < st["n1_rays_per_frame"] < 4_200_000
     assert 0.0 < st["efficiency"]
     assert abs(st["efficiency"] - st["n1_ms_per_frame"] / (2 * st["ms_per_frame"])) < 0.01

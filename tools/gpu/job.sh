@@ -14,6 +14,9 @@
 #   diag       per-block execution counts (TT_DIAG_BLOCKS build, tools/diag_blocks.py)
 #   replay     strong-scaling replay of every rank's N-GPU shard on this GPU (tools/strong_replay.py)
 #   gloo2      the 2-rank bench rehearsal on this GPU (gloo collectives, C5 tiles included)
+#   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
+#   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
+#   order      tools/exp_order.py per TT_ORDER_HOT threshold (ORDER_HOT, ORDER_CFGS, ORDER_ARGS)
 #   sweep      randomized parity sweep (tools/parity_sweep.py), 300 plain + 300 variants/adaptive
 #   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
 #   ab         the bench headline per variant: AB_LIBS="product n128 ..." (lib/variants/libtruetrace_hip_NAME.so),
@@ -48,6 +51,23 @@ for stage in "$@"; do
     diag) run diag 200 env TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_diag.so \
               python -u tools/diag_blocks.py c2 || exit $? ;;
     replay) run replay 900 python -u tools/strong_replay.py --configs c2,c5 ${REPLAY_ARGS:-} || exit $? ;;
+    longray) run longray 300 python -u tools/long_ray_chain.py || exit $? ;;
+    c4loc) export TMPDIR=/tmp
+           for v in ${AB_LIBS:-cur n128}; do  # C4 one-launch time + L2 hit / miss and fabric reads per variant
+               run "c4loc_time_$v" 400 env RV_CFG=c4 python -u tools/run_variants.py "$v" || exit $?
+               export TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so
+               run "c4loc_tcc_$v" 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/c4loc_tcc_$v" -o tcc \
+                   --output-format csv -- python tools/prof_config.py c4 --reps 2 || exit $?
+               run "c4loc_fetch_$v" 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c4loc_fetch_$v" -o fetch \
+                   --output-format csv -- python tools/prof_config.py c4 --reps 2 || exit $?
+               unset TT_HIP_LIB
+           done ;;
+    order) for h in ${ORDER_HOT:-0 128}; do  # adaptive order, hoisting only chunks costing >= h node steps (0: full sort)
+               for cfg in ${ORDER_CFGS:-c4 c5}; do
+                   run "order_${cfg}_hot$h" 400 env TT_ORDER_HOT=$h python -u tools/exp_order.py --config $cfg \
+                       --primary-only ${ORDER_ARGS:-} || exit $?
+               done
+           done ;;
     gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
     sweep) run sweep_plain 600 python -u tools/parity_sweep.py 300 40000 || exit $?

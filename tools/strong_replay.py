@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to replay per N")
+    ap.add_argument("--tile", type=int, default=64, help="screen tile edge of the round-robin sharding")
     args = ap.parse_args()
     import torch
     import tthip
@@ -48,7 +49,7 @@ def main():
     eng = tthip.Engine(0, stream=stream.cuda_stream)
     tthip.set_build_engine(eng, min_tris=100_000)
     out = {"tool": "tools/strong_replay.py", "device": torch.cuda.get_device_name(0), "slots": args.slots,
-           "steps": args.steps, "configs": {}}
+           "tile": args.tile, "steps": args.steps, "configs": {}}
 
     def frame_ms(lay):
         for _ in range(args.warmup):
@@ -88,7 +89,8 @@ def main():
                 per = []
                 for r in ranks:
                     lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR,
-                                               [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P)], make_full,
+                                               [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile)],
+                                               make_full,
                                                slots=F, bounce=bounce, info=True, colors=colors)
                     ms = frame_ms(lay)
                     per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})

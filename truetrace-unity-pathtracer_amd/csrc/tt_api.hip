@@ -1470,6 +1470,11 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
         o.cost_clear = os->cost[os->cur ^ 1u].p;
         o.n_rays = p->n_rays;
         o.n_chunks = n_chunks;
+        static const uint32_t hot = [] {  // A/B knob: hoist only the chunks of long rays
+            const char* e = std::getenv("TT_ORDER_HOT");
+            return e ? (uint32_t)std::atoi(e) : 0u;
+        }();
+        o.hot = hot;
         o.order = os->order.p;
         TT_HIP(c, tt_launch_order(o, c->stream));
         a.order = os->order.p;

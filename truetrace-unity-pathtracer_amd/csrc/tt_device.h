@@ -216,6 +216,7 @@ struct OrderArgs {
     const uint32_t* cost;        // previous launch's per-chunk costs
     uint32_t* cost_clear;        // the map this launch's trace fills: zeroed here ([0, n_chunks))
     uint32_t n_rays, n_chunks;
+    uint32_t hot;                // chunks costing less than this keep their natural order (0: sort all)
     uint32_t* order;             // out: n_chunks entries
 };
 hipError_t tt_launch_order(const OrderArgs& a, hipStream_t st);

@@ -28,7 +28,10 @@ constexpr uint32_t OB = 256;      // threads per block: small, so the kernel fit
 constexpr uint32_t OKEYS = 1024;  // cost buckets (Reps <= TT_MAX_REPS = 1000 fits)
 constexpr uint32_t OITEMS = 8;    // chunks per thread per batch: their key loads are in flight together
 
-__device__ __forceinline__ uint32_t chunk_key(const OrderArgs& A, uint32_t m) { return min(A.cost[m], OKEYS - 1u); }
+__device__ __forceinline__ uint32_t chunk_key(const OrderArgs& A, uint32_t m) {
+    const uint32_t c = A.cost[m];
+    return c < A.hot ? 0u : min(c, OKEYS - 1u);  // below `hot`: one bucket, sorted last, natural order
+}
 
 __global__ __launch_bounds__(OB) void tt_order_kernel(OrderArgs A) {
     __shared__ uint32_t s_off[OKEYS];
