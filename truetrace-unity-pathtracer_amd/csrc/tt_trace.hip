@@ -243,6 +243,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         const uint64_t idle = __ballot(!active);
         const uint32_t n_idle = (uint32_t)__popcll(idle);
         const bool pool_dry = !more && pool_next >= pool_end;
+#if TT_DRAIN_PRIO
+        // a draining wave issues ahead of the waves of launches still in their bulk (other parts / frames)
+        if (pool_dry) __builtin_amdgcn_s_setprio(TT_DRAIN_PRIO);
+#endif
         // the queue is dry and the live rays fit in 2-lane groups: cooperative drain (tt_wide.h)
         const bool to_wide = TT_WIDE && pool_dry && n_idle < TT_WAVE && TT_WAVE - n_idle <= TT_WIDE_ENTER;
         // finished rays write their records in batches, right before their lanes are refilled

@@ -26,6 +26,9 @@
 #ifndef TT_PUSH_FAST
 #define TT_PUSH_FAST 0  // 1: the stack push tests only "an LDS entry is free" on its common path (A/B option)
 #endif
+#ifndef TT_DRAIN_PRIO
+#define TT_DRAIN_PRIO 0  // s_setprio level a wave takes once its launch's queue is dry (0: off; A/B option)
+#endif
 #ifndef TT_UNIFORM_POOL
 #define TT_UNIFORM_POOL 1  // readfirstlane the scheduler's pool state after each refill (0: A/B; +1.2% bench, profiles/r04/ab)
 #endif
