@@ -134,7 +134,7 @@ struct MatView {
 // from the node-0 bytes the device holds (tt_api.hip: known after an upload or a node update; a device
 // refit of the TLAS turns it off until the next update), passed as a kernel argument (SGPRs).
 #ifndef TT_ROOT_LEAF
-#define TT_ROOT_LEAF 0
+#define TT_ROOT_LEAF 1
 #endif
 struct RootLeaf {
     uint32_t ok;                          // node 0 qualifies

@@ -21,10 +21,10 @@
 #define TT_CHUNK_BIG 64   // rays per dequeue (the surplus waits in the wave's pool)
 #endif
 #ifndef TT_REFILL_MIN
-#define TT_REFILL_MIN 16  // refill idle lanes once at least this many are idle
+#define TT_REFILL_MIN 20  // refill idle lanes once at least this many are idle (16 -> 20: profiles/r04/ab)
 #endif
 #ifndef TT_PUSH_FAST
-#define TT_PUSH_FAST 0  // 1: the stack push tests only "an LDS entry is free" on its common path (A/B option)
+#define TT_PUSH_FAST 1  // the stack push tests only "an LDS entry is free" on its common path (0: A/B; profiles/r04/ab)
 #endif
 #ifndef TT_DRAIN_PRIO
 #define TT_DRAIN_PRIO 0  // s_setprio level a wave takes once its launch's queue is dry (0: off; A/B option)
