@@ -160,8 +160,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         extra_engs, streams = [], []
         try:
             for _ in range(P - 1):
-                streams.append(torch.cuda.Stream(dev))
-                e1 = tthip.Engine(dev.index, stream=streams[-1].cuda_stream)
+                streams.append(tthip.DedicatedStream(torch, dev))  # a HW queue of its own (ttlayout docstring)
+                e1 = tthip.Engine(dev.index, stream=streams[-1].stream.cuda_stream)
                 extra_engs.append(e1)
                 e1.share_scene(eng)  # one scene copy for all parts (tt_ctx_share_scene)
             chains = [[] for _ in range(n_frames)]  # chains[f]: per part (engine, bufs, counts)
@@ -207,6 +207,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         finally:
             for e1 in extra_engs:
                 e1.close()
+            for st in streams:
+                st.close()
 
     def adaptive_one_launch(view, W, H, nb, info, colors_t):
         """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch

@@ -211,6 +211,18 @@ int32_t tt_abi_version(void);
 /* Number of visible HIP devices (0 on a machine without a GPU). */
 int32_t tt_device_count(void);
 
+/* A non-blocking hipStream_t on a hardware queue of its own, for the concurrent launch streams of
+ * one frame (parts / frame slots / the hit-record gather). Plain hipStreamCreate streams share a
+ * process's few HW queues round-robin: two persistent trace grids whose streams land on one queue
+ * run back to back instead of overlapping each other's drain (measured: a 2-part step then takes
+ * the time of both launches, 0.45 vs 0.25 ms at an 8-GPU shard; profiles/r04/streams/). The stream is
+ * made with hipExtStreamCreateWithCUMask and every CU enabled, which gives it a dedicated queue.
+ * The reference has no equivalent (Unity issues one command buffer); a host that records its
+ * dispatches on several queues (RayTracingMaster.cs:954-1007 per camera) would use one per queue.
+ * Destroy with tt_stream_destroy (it synchronises the stream first). */
+tt_status tt_stream_create(int32_t device, void** stream);
+tt_status tt_stream_destroy(void* stream);
+
 /* ---------------------------------------------------------- scene */
 /* Replaces AssetManager.SetMeshTraceBuffers (AssetManager.cs:75-88): copies the
  * aggregated buffers into HBM (the host keeps ownership of its arrays). Any previous

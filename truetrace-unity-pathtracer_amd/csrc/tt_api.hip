@@ -597,6 +597,37 @@ int32_t tt_device_count(void) {
 
 const char* tt_last_error(const tt_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+tt_status tt_stream_create(int32_t device, void** stream) {
+    if (!stream) return TT_ERR_INVALID_ARG;
+    *stream = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        return TT_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= ndev) return TT_ERR_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return TT_ERR_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TT_ERR_HIP;
+    // every CU enabled: the mask only exists to get a HW queue that no other stream shares
+    std::vector<uint32_t> mask(((uint32_t)prop.multiProcessorCount + 31u) / 32u, 0xffffffffu);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        return TT_ERR_HIP;
+    }
+    *stream = s;
+    return TT_OK;
+}
+
+tt_status tt_stream_destroy(void* stream) {
+    if (!stream) return TT_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const hipError_t a = hipStreamSynchronize(s);
+    const hipError_t b = hipStreamDestroy(s);
+    return (a == hipSuccess && b == hipSuccess) ? TT_OK : TT_ERR_HIP;
+}
+
 tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     if (!cfg || !out) return TT_ERR_INVALID_ARG;
     *out = nullptr;

@@ -325,12 +325,14 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
     const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * (uint32_t)TT_NODE_STRIDE);
     const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
-    bool active = false;
+    // a lane without a ray holds tg.y == TT_IDLE (as in tt_trace.hip: a live ray's pending-leaf word never
+    // has bit 31 set), so each phase test is one compare of tg.y
+    constexpr uint32_t TT_IDLE = 0x80000000u;
     uint32_t ray_index = 0;
     LaneRay ray{}, wray{};
     float max_distance = 0.0f;
     float3 thr = make_float3(1.0f, 1.0f, 1.0f);  // throughput (:361), scaled by glass tints
-    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
+    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, TT_IDLE);
     uint32_t oct = 0;
     int32_t stack_size = 0, tlas_ss = -1;
     int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, Reps = 0;
@@ -370,16 +372,17 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
 
     while (true) {
         // ---------------------------------------------------------------- refill
-        const uint64_t idle = __ballot(!active);
-        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        const uint64_t idle = __ballot((int32_t)tg.y < 0);
+        // (two 32-bit SALU counts: a 64-bit count is tested with VALU v_cmp_*_u64)
+        const uint32_t n_idle = (uint32_t)__builtin_popcount((uint32_t)idle) + (uint32_t)__builtin_popcount((uint32_t)(idle >> 32));
         const bool pool_dry = !more && pool_next >= pool_end;
         if (n_idle == TT_WAVE && pool_dry) break;
 #if TT_WIDE
         // the queue is dry and the live rays fit in 2-lane groups: cooperative drain (tt_wide.h)
         if (pool_dry && TT_WAVE - n_idle <= TT_WIDE_ENTER) {
             ShadowWide st{ray, wray, max_distance, thr, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset,
-                          MatOffset, Reps, ray_index, tid, gtid, active};
-            regroup_shadow<2>(st, __ballot(active), lane);
+                          MatOffset, Reps, ray_index, tid, gtid, (int32_t)tg.y >= 0};
+            regroup_shadow<2>(st, __ballot((int32_t)tg.y >= 0), lane);
             auto occ_w = [&](const ShadowWide& w) { do_occlude(w.ray_index); };
             auto reach_w = [&](const ShadowWide& w) { do_reach(w.ray_index, w.wray, w.thr); };
             auto exh_w = [&](const ShadowWide& w) { do_exhaust(w.ray_index); };
@@ -408,7 +411,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
             } else {
                 pool_next += take_old;
             }
-            if (!active && widx != 0xffffffffu) {  // :355-371
+            if ((int32_t)tg.y < 0 && widx != 0xffffffffu) {  // :355-371
                 ray_index = widx;
                 const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
                 const uint4 r0 = rp[0], r1 = rp[1];
@@ -436,15 +439,14 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                 TriOffset = 0;
                 MatOffset = 0;
                 Reps = 0;
-                active = true;
                 if (STATS) c_rays++;
             }
         }
 
         // ------------------------------------------------------------- node phase
-        if (active && tg.y == 0u) {
+        if (tg.y == 0u) {
             if (Reps >= TT_MAX_REPS) {  // :373 loop bound: nothing is written
-                active = false;
+                tg.y = TT_IDLE;
                 if (STATS) c_reps++;
                 do_exhaust(ray_index);
             } else if (cg.y & 0xff000000u) {  // :374-403
@@ -468,7 +470,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                     Reps++;
                     if (STATS) c_nodes++;
                 } else {
-                    active = false;
+                    tg.y = TT_IDLE;
                     if (STATS) c_ovf++;
                     TT_REPORT_OVERFLOW(A);
                 }
@@ -476,7 +478,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                 tg = cg;
                 cg = make_uint2(0u, 0u);
             }
-            if (active && tg.y != 0u && tlas_ss == -1) {  // :411-435 TLAS leaf -> BLAS
+            if ((int32_t)tg.y > 0 && tlas_ss == -1) {  // :411-435 TLAS leaf -> BLAS
                 const uint32_t mo = firstbithigh(tg.y);
                 tg.y &= ~(1u << mo);
                 const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
@@ -487,6 +489,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                 bool ok = true;
                 if (tg.y != 0u) TT_PUSH(tg, ok);
                 if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
+                tg.y = 0u;
                 if (ok) {
                     tlas_ss = stack_size;
                     MatOffset = mo4.z;
@@ -505,16 +508,15 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                     cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
                     if (STATS) c_blas++;
                 } else {
-                    active = false;
+                    tg.y = TT_IDLE;
                     if (STATS) c_ovf++;
                     TT_REPORT_OVERFLOW(A);
                 }
-                tg.y = 0u;
             }
         }
 
         // --------------------------------------------------------- triangle phase
-        if (active && tg.y != 0u) {  // :436-446, highest bit first, until the first occluder
+        if ((int32_t)tg.y > 0) {  // :436-446, highest bit first, until the first occluder
             const uint32_t ti = firstbithigh(tg.y);
             tg.y &= ~(1u << ti);
             const bool occ =
@@ -522,13 +524,13 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
             if (STATS) c_tris++;
             if (occ) {  // :449-454
                 do_occlude(ray_index);
-                active = false;
+                tg.y = TT_IDLE;
                 if (STATS) c_occ++;
             }
         }
 
         // ----------------------------------------- advance: pop / finish (:456-494)
-        if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+        if (tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
             if (stack_size != 0) {
                 if (stack_size == tlas_ss) {
                     NodeOffset = 0;
@@ -540,7 +542,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                 TT_POP(cg);
             } else {  // reached the light (TerrainExists false): :457-485
                 do_reach(ray_index, wray, thr);
-                active = false;
+                tg.y = TT_IDLE;
                 if (STATS) c_vis++;
             }
         }

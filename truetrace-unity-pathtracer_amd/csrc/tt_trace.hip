@@ -169,15 +169,18 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     const __amdgpu_buffer_rsrc_t nodes = buffer_rsrc(A.nodes, A.n_nodes * (uint32_t)TT_NODE_STRIDE);
     const __amdgpu_buffer_rsrc_t tris = buffer_rsrc(A.tris, A.n_tris * (uint32_t)sizeof(TriPos));
 
-    // lane traversal state (IntersectionKernels.compute:62-77)
-    bool active = false;
+    // lane traversal state (IntersectionKernels.compute:62-77). A lane without a ray (idle, finished or
+    // ended) holds tg.y == TT_IDLE: the pending-leaf word of a live ray never has bit 31 set (hit bits
+    // 0-23 only), so "active" needs no register of its own and every phase test of the loop is one
+    // compare of tg.y: at the loop top (tg.y == 0), leaf triangles pending ((int)tg.y > 0), idle (< 0).
+    constexpr uint32_t TT_IDLE = 0x80000000u;
     uint32_t ray_index = 0;
     uint32_t pix = 0;    // RayData.PixelIndex, kept from the ray load
     float col_w = 0.0f;  // GlobalColors[pix].Data.w (INFO == 2), loaded when the ray starts
     bool pending = false;  // finished, record not yet written (TT_DEFER_FINISH)
     LaneRay ray{}, wray{};
     Best best{};
-    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, 0u);
+    uint2 cg = make_uint2(0u, 0u), tg = make_uint2(0u, TT_IDLE);
     uint32_t oct = 0;
     int32_t stack_size = 0, tlas_ss = -1;
     int32_t NodeOffset = 0, TriOffset = 0, MatOffset = 0, mesh_id = -1, Reps = 0;
@@ -205,6 +208,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             bool ok = true;
             if (tg.y != 0u) TT_PUSH(tg, ok);
             if (ok && (cg.y & 0xff000000u)) TT_PUSH(cg, ok);
+            tg.y = 0u;
             if (ok) {
                 tlas_ss = stack_size;
                 MatOffset = mo4.z;
@@ -223,12 +227,11 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
                 if (STATS) c_blas++;
             } else {
-                active = false;
+                tg.y = TT_IDLE;
                 if (STATS) c_ovf++;
                 TT_REPORT_OVERFLOW(A);
                 keep_record(A, ray_index);
             }
-            tg.y = 0u;
     };
     // :229-241: the finished ray's hit record and _PrimaryTriangleInfo
     auto finish_ray = [&]() {
@@ -240,8 +243,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     while (true) {
         TT_DB(0);
         // ---------------------------------------------------------------- refill
-        const uint64_t idle = __ballot(!active);
-        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        const uint64_t idle = __ballot((int32_t)tg.y < 0);
+        // (two 32-bit counts: written as __popcll, the compiler keeps the count 64-bit and tests it with two
+        // VALU v_cmp_*_u64 per iteration)
+        const uint32_t n_idle = (uint32_t)__builtin_popcount((uint32_t)idle) + (uint32_t)__builtin_popcount((uint32_t)(idle >> 32));
         const bool pool_dry = !more && pool_next >= pool_end;
 #if TT_DRAIN_PRIO
         // a draining wave issues ahead of the waves of launches still in their bulk (other parts / frames)
@@ -262,8 +267,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         if (to_wide) {
             TT_DB(13);
             WideState st{ray, wray, best, cg, tg, oct, stack_size, tlas_ss, NodeOffset, TriOffset, MatOffset,
-                         mesh_id, Reps, ray_index, pix, col_w, tid, gtid, active};
-            regroup<2>(st, __ballot(active), lane);
+                         mesh_id, Reps, ray_index, pix, col_w, tid, gtid, (int32_t)tg.y >= 0};
+            regroup<2>(st, __ballot((int32_t)tg.y >= 0), lane);
             auto finish_wide = [&](const WideState& w) {
                 const bool hit = write_record<INFO>(A, w.ray_index, w.pix, w.col_w, w.best, w.wray);
                 if (STATS) c_hits += hit ? 1u : 0u;
@@ -309,7 +314,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             pool_end = __builtin_amdgcn_readfirstlane(pool_end);
             more = __builtin_amdgcn_readfirstlane(more);
 #endif
-            if (!active && widx != 0xffffffffu) {
+            if ((int32_t)tg.y < 0 && widx != 0xffffffffu) {
                 TT_DB(4);
                 TT_DL(19, true);
                 // work index -> ray index (8x8 screen tiles for full-frame primary batches)
@@ -350,7 +355,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 MatOffset = 0;
                 mesh_id = -1;
                 Reps = 0;
-                active = true;
                 if (STATS) c_rays++;
 #if TT_ROOT_LEAF
                 if (rl_ok) {  // the root's node step, then the TLAS leaf -> BLAS switch
@@ -367,13 +371,13 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 #if TT_ROOT_LEAF
         // the started rays that hit the root's leaf switch to their BLAS before this iteration's node
         // step (a TLAS-level lane has no pending leaf bits at the loop top otherwise)
-        if (rl_ok && active && tg.y != 0u && tlas_ss == -1) enter_blas();
+        if (rl_ok && (int32_t)tg.y > 0 && tlas_ss == -1) enter_blas();
 #endif
 
         // ------------------------------------------------------------- node phase
         if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)
-            const uint64_t nm = __ballot(active && tg.y == 0u && Reps < TT_MAX_REPS && (cg.y & 0xff000000u));
-            const uint64_t am = __ballot(active);  // outside the lane-0 branch: a ballot there sees lane 0 only
+            const uint64_t nm = __ballot(tg.y == 0u && Reps < TT_MAX_REPS && (cg.y & 0xff000000u));
+            const uint64_t am = __ballot((int32_t)tg.y >= 0);  // outside the lane-0 branch: a ballot there sees lane 0 only
             if (lane == 0) {
                 d_iter++;
                 d_node_lanes += (uint32_t)__popcll(nm);
@@ -382,10 +386,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             }
         }
         // A lane is at the top of the reference's loop exactly when no leaf triangles are pending.
-        if (active && tg.y == 0u) {
+        if (tg.y == 0u) {
             TT_DB(5);
             if (Reps >= TT_MAX_REPS) {
-                active = false;  // loop bound hit: the reference writes nothing
+                tg.y = TT_IDLE;  // loop bound hit: the reference writes nothing
                 if (STATS) c_reps++;
                 keep_record(A, ray_index);
                 if (ORD) record_chunk_cost(A, swizzle, ray_index, Reps);
@@ -421,7 +425,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                     Reps++;
                     if (STATS) c_nodes++;
                 } else {
-                    active = false;
+                    tg.y = TT_IDLE;
                     if (STATS) c_ovf++;
                     TT_REPORT_OVERFLOW(A);
                     keep_record(A, ray_index);
@@ -430,18 +434,18 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 tg = cg;
                 cg = make_uint2(0u, 0u);
             }
-            if (active && tg.y != 0u && tlas_ss == -1) enter_blas();  // :194-219 TLAS leaf -> BLAS
+            if ((int32_t)tg.y > 0 && tlas_ss == -1) enter_blas();  // :194-219 TLAS leaf -> BLAS
         }
 
         if (STATS) {
-            const uint64_t tm = __ballot(active && tg.y != 0u);
+            const uint64_t tm = __ballot((int32_t)tg.y > 0);
             if (lane == 0) {
                 d_tri_lanes += (uint32_t)__popcll(tm);
                 d_tri_iters += tm ? 1u : 0u;
             }
         }
         // --------------------------------------------------------- triangle phase
-        if (active && tg.y != 0u) {  // :220-226, highest bit first, one triangle per pass
+        if ((int32_t)tg.y > 0) {  // :220-226, highest bit first, one triangle per pass
             TT_DB(9);
             TT_DL(18, true);
             const uint32_t ti = firstbithigh(tg.y);
@@ -457,7 +461,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         // ----------------------------------------- advance: pop / finish (:228-251)
         // One place for every lane whose group is used up, whether it came from a node step or
         // from its last triangle this pass (equivalent order: the reference pops right after).
-        if (active && tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
+        if (tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
             TT_DB(10);
             if (stack_size != 0) {
                 TT_DB(11);
@@ -472,7 +476,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 TT_POP(cg);
             } else {
                 pending = true;  // written at the next refill (or when the wave drains)
-                active = false;
+                tg.y = TT_IDLE;
             }
         }
     }

@@ -296,6 +296,11 @@ def hip_lib():
         L.tt_blas_build_device.argtypes = [vp, vp, u32, vp, vp, u32, C.POINTER(u32), vp, C.POINTER(u32)]
         L.tt_bvh2_presort_device.argtypes = [vp, vp, u32, vp]
         L.tt_sync.argtypes = [vp]
+        if hasattr(L, "tt_stream_create"):
+            L.tt_stream_create.argtypes = [i32, C.POINTER(vp)]
+            L.tt_stream_create.restype = i32
+            L.tt_stream_destroy.argtypes = [vp]
+            L.tt_stream_destroy.restype = i32
         L.tt_async_overflows.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
@@ -924,6 +929,28 @@ class Engine:
         if check:
             self._check(st, "tt_enqueue_diffuse_bounce_indirect")
         return st
+
+
+class DedicatedStream:
+    """A HIP stream on a hardware queue of its own (tt_stream_create) wrapped as a torch ExternalStream.
+
+    Concurrent trace launches (the parts / frame slots of ttlayout.FrameLayout, the gather stream) need
+    streams that do not share a HW queue: a process's plain streams are dealt round-robin over a few
+    queues, and two persistent grids on one queue run back to back instead of overlapping each other's
+    drain (profiles/r04/streams/). ``close()`` synchronises and destroys it."""
+
+    def __init__(self, torch, dev):
+        L = hip_lib()
+        h = C.c_void_p()
+        _check(L.tt_stream_create(int(dev.index or 0), C.byref(h)), "tt_stream_create")
+        self.handle = h.value
+        self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
+
+    def close(self):
+        if self.handle:
+            _check(hip_lib().tt_stream_destroy(C.c_void_p(self.handle)), "tt_stream_destroy")
+            self.handle = None
+            self.stream = None
 
 
 def validate(s: Scene):

@@ -11,7 +11,12 @@ tiles under tile sharding) as
     nothing of frame k) run while frame k's bounce-1 launches drain. Inside a frame the order is the
     reference's: a part's bounce-1 launch follows its primary launch on the same stream.
 
-All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). A step is one
+All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). Every stream the
+layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.DedicatedStream,
+tt_stream_create): plain torch streams are dealt round-robin over a process's few HW queues, and two
+persistent trace grids on one queue run back to back -- measured on the strong-scaling replay, the
+ranks whose second part landed on the base stream's queue took 0.45 instead of 0.25 ms per frame
+(profiles/r04/streams/queue_map.txt). TT_LAYOUT_POOL_STREAMS=1 restores torch pool streams (A/B). A step is one
 frame: every part's primary launch (writing its 16-B hit records straight into the gather's send
 buffer when there is one, tt_trace_closest_hits), the optional gather of those records to rank 0 on a
 communication stream, then every part's bounce-1 launch. Bounce-1 rays are the primary hits'
@@ -22,6 +27,7 @@ reference rebinds the texture to GIWorldPosA at bounce > 0, RayTracingMaster.cs:
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional
 
 import numpy as np
@@ -58,6 +64,8 @@ class FrameLayout:
         WH = W * H
         self.engines = []  # (engine, stream) per context, lend's first; contexts created here are closed by close()
         self.own = []
+        self.own_streams = []  # tthip.DedicatedStream objects, destroyed by close() after the contexts
+        self.pool_streams = os.environ.get("TT_LAYOUT_POOL_STREAMS", "0") == "1"
         self.slots: List[List[Part]] = []
         base_stream = torch.cuda.current_stream(dev)
         self.info0 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if info else None for _ in range(self.F)]
@@ -70,7 +78,7 @@ class FrameLayout:
                 if f == 0 and s == 0:
                     p.eng, p.stream = lend, base_stream
                 else:
-                    st = torch.cuda.Stream(dev)
+                    st = self.new_stream()
                     e = tthip.Engine(dev.index, stream=st.cuda_stream)
                     e.share_scene(lend)  # ONE scene copy: one cache footprint for all contexts
                     self.own.append(e)
@@ -107,6 +115,14 @@ class FrameLayout:
         self.k = 0
         self.k_reset = 0
 
+    def new_stream(self):
+        """A launch stream on its own HW queue (module docstring); a torch pool stream under the A/B knob."""
+        if self.pool_streams:
+            return self.torch.cuda.Stream(self.dev)
+        d = self.tthip.DedicatedStream(self.torch, self.dev)
+        self.own_streams.append(d)
+        return d.stream
+
     # ---------------------------------------------------------------- sizes
     @property
     def parts(self) -> List[Part]:
@@ -141,7 +157,7 @@ class FrameLayout:
         m = max(sum(x) for x in g.sizes)
         g.bufs = [torch.zeros((m, 4), dtype=torch.int32, device=red_dev) for _ in range(g.nbuf)]
         g.lists = [[torch.empty_like(bf) for _ in range(world)] if rank == 0 else None for bf in g.bufs]
-        g.comm = torch.cuda.Stream(self.dev)
+        g.comm = self.new_stream()
         g.done = [torch.cuda.Event() for _ in range(g.nbuf)]
         g.used = [False] * g.nbuf
         g.copied = torch.cuda.Event()
@@ -229,6 +245,11 @@ class FrameLayout:
         for e in self.own:
             e.close()
         self.own = []
+        if self.gather is not None:
+            self.gather.comm = None
+        for d in self.own_streams:
+            d.close()
+        self.own_streams = []
 
 
 class _Gather:
