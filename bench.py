@@ -429,7 +429,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     W, H, far = 3840, 2160, T.FAR
     WH = W * H
     F = max(1, args.strong_slots)
-    P = max(1, args.parts) if args.parts > 0 else (3 if world >= 4 else 2)
+    P = max(1, args.strong_parts)
     el1 = el_n = 0.0
     lay = None
     try:
@@ -669,16 +669,20 @@ def main():
                          "parts, each by its own engine on its own stream (each part's bounce-1 after its own primary), "
                          "so one part's launch drain overlaps the other parts' work (tools/exp_streams.py). 1: one "
                          "launch per bounce; 0 (default): 2 for a full frame's worth per rank (N = 1, the spp "
-                         "headline), 3 for the strong-scaling shards at N >= 4 (<= 1/4 frame: -12%% / -2%% step time "
-                         "at the N = 4 / 8 shards vs 2 parts, profiles/r03/parts/)")
+                         "headline); the strong-scaling shards use --strong-parts")
     ap.add_argument("--slots", type=int, default=0,
                     help="frame slots F of the headline layout (ttlayout.FrameLayout): frame k runs on slot k %% F with "
                          "its own buffers and streams, so frame k + 1's primary launches overlap frame k's bounce-1 "
                          "launches. 0 (default): 1 for a full frame's worth per rank, --strong-slots for the "
                          "strong-scaling shards (--shard tiles)")
-    ap.add_argument("--strong-slots", type=int, default=1,
-                    help="frame slots of the strong-scaling tile layouts (N > 1: aux_strong_tiles, aux_c5_tiles) and of "
-                         "their N = 1 reference frames")
+    ap.add_argument("--strong-slots", type=int, default=3,
+                    help="frame slots of the strong-scaling tile layouts (N > 1: aux_strong_tiles, aux_c5_tiles, "
+                         "--shard tiles): frames k, k + 1, k + 2 of a rank in flight at once, each slot on its own HW "
+                         "queue. 1 part x 3 slots is the best layout measured for the <= 1/2-frame shards "
+                         "(tools/strong_replay.py, profiles/r04/replay/r04g_dedicated_queues.json: C2 N = 8 0.150 "
+                         "ms per frame vs 0.223-0.271 for 2x2 / 2x1 / 3x1)")
+    ap.add_argument("--strong-parts", type=int, default=1,
+                    help="tile-interleaved parts per rank of the strong-scaling tile layouts (see --strong-slots)")
     ap.add_argument("--no-strong", action="store_true",
                     help="N > 1: skip the strong-scaling 1080p tile layout and its N = 1 reference frame")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
@@ -792,15 +796,14 @@ def main():
     # each slot traced by its own engine context on its own stream (ttlayout.FrameLayout): a part's launches
     # overlap the other parts' launch drains, and with F >= 2 frame k + 1's primaries overlap frame k's
     # bounce-1 launches. Parts per rank: a full frame's worth of rays (N = 1, and every rank of the spp
-    # headline) as 2 parts; the strong-scaling shards of <= 1/4 frame as 3 (one-wave blocks,
-    # profiles/r03/parts/: N = 4 shard 0.371 -> 0.327 ms, N = 8 0.236 -> 0.231 ms per step; a full frame
-    # 0.784-0.80 (2) vs 0.808-0.82 (3)).
-    P_strong = max(1, args.parts) if args.parts > 0 else (3 if world >= 4 else 2)
+    # headline) as 2 parts; the strong-scaling shards (one frame's tiles over N ranks) as --strong-parts x
+    # --strong-slots, default 1 x 3 (profiles/r04/replay/r04g_dedicated_queues.json).
+    P_strong = max(1, args.strong_parts)
     F_strong = max(1, args.strong_slots)
     if args.parts <= 0:
-        args.parts = 3 if (world >= 4 and not spp) else 2
+        args.parts = P_strong if (world > 1 and tiles and not spp) else 2
     P = max(1, args.parts) if (tiles or world == 1) else 1
-    F = max(1, args.slots if args.slots > 0 else (F_strong if (tiles and not spp) else 1))
+    F = max(1, args.slots if args.slots > 0 else (F_strong if (world > 1 and tiles and not spp) else 1))
     split = tiles or P > 1
     make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, 0.3, far, jitter=jitter)
 

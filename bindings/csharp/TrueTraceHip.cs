@@ -86,6 +86,8 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern TTStatus tt_ctx_destroy(IntPtr ctx);
         [DllImport(Lib)] public static extern IntPtr tt_last_error(IntPtr ctx);
         [DllImport(Lib)] public static extern int tt_device_count();
+        [DllImport(Lib)] public static extern TTStatus tt_stream_create(int device, out IntPtr stream);
+        [DllImport(Lib)] public static extern TTStatus tt_stream_destroy(IntPtr stream);
         // Element types are the reference's own host structs: BVHNode8DataCompressed (80 B),
         // CudaTriangle (88 B), int, MyMeshDataCompacted (88 B), MaterialData (252 B).
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload(IntPtr ctx,
@@ -215,6 +217,16 @@ namespace TrueTrace.Hip
         /// half of a frame traced concurrently on its own context. Update the scene through the lender;
         /// dispose this context before the lender.
         public void ShareScene(TrueTraceHip lender) { Check(Native.tt_ctx_share_scene(m_ctx, lender.m_ctx)); }
+
+        /// A hipStream_t on a hardware queue of its own (tt_stream_create) for a concurrently traced half of
+        /// the frame: pass it as TTConfig.stream of that half's context; StreamDestroy after disposing it.
+        public static IntPtr StreamCreate(int device)
+        {
+            var st = Native.tt_stream_create(device, out IntPtr s);
+            if (st != TTStatus.Ok) throw new InvalidOperationException($"tt_stream_create: {st}");
+            return s;
+        }
+        public static void StreamDestroy(IntPtr stream) { Native.tt_stream_destroy(stream); }
 
         /// TraceDevice that also writes ray i's 16-byte hit record to hitsOut[i] (HIP device memory, 16-byte
         /// aligned, nRays records): the buffer a multi-GPU host gathers (tt_trace_closest_hits).
