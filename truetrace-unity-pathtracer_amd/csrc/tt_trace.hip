@@ -286,6 +286,13 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 #endif
         if (n_idle >= TT_REFILL_MIN && !pool_dry) {
             TT_DB(2);
+#if TT_LONG_PRIO
+            // a wave carrying a long ray (>= TT_LONG_PRIO node steps so far) issues ahead of the others until
+            // its next refill without one: the long ray's dependent chain, not the wave's share of issue,
+            // is what sets a small launch's length (the degenerate-direction rays)
+            if (__ballot((int32_t)tg.y >= 0 && Reps >= TT_LONG_PRIO) != 0ull) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+#endif
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest
             const uint32_t avail = pool_end - pool_next;
             uint32_t new_base = 0, new_count = 0;
@@ -364,15 +371,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                     tg = make_uint2(RL.base_tri, hit ? RL.bits : 0u);
                     Reps = 1;
                     if (STATS) c_nodes++;
+                    // a ray that hits the root's leaf switches to its BLAS before this iteration's node step
+                    // (here, with the started lanes only: a TLAS-level lane has no pending leaf bits at the
+                    // loop top otherwise, so no per-iteration test is needed)
+                    if (hit) enter_blas();
                 }
 #endif
             }
         }
-#if TT_ROOT_LEAF
-        // the started rays that hit the root's leaf switch to their BLAS before this iteration's node
-        // step (a TLAS-level lane has no pending leaf bits at the loop top otherwise)
-        if (rl_ok && (int32_t)tg.y > 0 && tlas_ss == -1) enter_blas();
-#endif
 
         // ------------------------------------------------------------- node phase
         if (STATS) {  // SIMD-efficiency diagnostics (wave-uniform; lane 0 accumulates)

@@ -29,6 +29,9 @@
 #ifndef TT_DRAIN_PRIO
 #define TT_DRAIN_PRIO 0  // s_setprio level a wave takes once its launch's queue is dry (0: off; A/B option)
 #endif
+#ifndef TT_LONG_PRIO
+#define TT_LONG_PRIO 0  // s_setprio 2 for a wave with a ray past this many node steps, set at refills (0: off; A/B)
+#endif
 #ifndef TT_UNIFORM_POOL
 #define TT_UNIFORM_POOL 1  // readfirstlane the scheduler's pool state after each refill (0: A/B; +1.2% bench, profiles/r04/ab)
 #endif
