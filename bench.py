@@ -675,12 +675,13 @@ def main():
                          "its own buffers and streams, so frame k + 1's primary launches overlap frame k's bounce-1 "
                          "launches. 0 (default): 1 for a full frame's worth per rank, --strong-slots for the "
                          "strong-scaling shards (--shard tiles)")
-    ap.add_argument("--strong-slots", type=int, default=3,
+    ap.add_argument("--strong-slots", type=int, default=6,
                     help="frame slots of the strong-scaling tile layouts (N > 1: aux_strong_tiles, aux_c5_tiles, "
-                         "--shard tiles): frames k, k + 1, k + 2 of a rank in flight at once, each slot on its own HW "
-                         "queue. 1 part x 3 slots is the best layout measured for the <= 1/2-frame shards "
-                         "(tools/strong_replay.py, profiles/r04/replay/r04g_dedicated_queues.json: C2 N = 8 0.150 "
-                         "ms per frame vs 0.223-0.271 for 2x2 / 2x1 / 3x1)")
+                         "--shard tiles): frames k .. k + 5 of a rank in flight at once, each slot on its own HW "
+                         "queue. 1 part x 6 slots is the best layout measured for the <= 1/2-frame shards "
+                         "(tools/strong_replay.py, profiles/r04/replay/: C2 N = 8 0.135 ms per frame vs 0.155 / "
+                         "0.150 with 4 / 3 slots and 0.223-0.271 with 2x2 / 2x1 / 3x1; C5 4K N = 8 0.241 vs 0.270 / "
+                         "0.312)")
     ap.add_argument("--strong-parts", type=int, default=1,
                     help="tile-interleaved parts per rank of the strong-scaling tile layouts (see --strong-slots)")
     ap.add_argument("--no-strong", action="store_true",
@@ -797,7 +798,7 @@ def main():
     # overlap the other parts' launch drains, and with F >= 2 frame k + 1's primaries overlap frame k's
     # bounce-1 launches. Parts per rank: a full frame's worth of rays (N = 1, and every rank of the spp
     # headline) as 2 parts; the strong-scaling shards (one frame's tiles over N ranks) as --strong-parts x
-    # --strong-slots, default 1 x 3 (profiles/r04/replay/r04g_dedicated_queues.json).
+    # --strong-slots, default 1 x 6 (profiles/r04/replay/r04j_slots46.json).
     P_strong = max(1, args.strong_parts)
     F_strong = max(1, args.strong_slots)
     if args.parts <= 0:

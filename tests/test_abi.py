@@ -54,6 +54,16 @@ def test_no_device_is_loud():
     assert e.value.status == tthip.TT_ERR_NO_DEVICE
 
 
+@pytest.mark.skipif(tthip.device_count() > 0, reason="checks the no-GPU behaviour")
+def test_stream_create_without_device_is_loud():
+    L = tthip.hip_lib()
+    h = C.c_void_p()
+    assert L.tt_stream_create(0, C.byref(h)) == tthip.TT_ERR_NO_DEVICE
+    assert h.value is None
+    assert L.tt_stream_create(0, None) == tthip.TT_ERR_INVALID_ARG
+    assert L.tt_stream_destroy(None) == tthip.TT_ERR_INVALID_ARG
+
+
 def test_null_context_is_rejected():
     L = tthip.hip_lib()
     p = tthip.TraceParams(n_rays=1, bounce=0, far_plane=1.0, screen_width=1, screen_height=1, flags=0)

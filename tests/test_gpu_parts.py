@@ -14,7 +14,9 @@ from parity_util import FAR
 pytestmark = pytest.mark.gpu
 
 
-def test_two_parts_on_two_streams_equal_one_launch():
+@pytest.mark.parametrize("kind", ["pool", "dedicated"])
+def test_two_parts_on_two_streams_equal_one_launch(kind):
+    """kind: torch pool streams, or streams on HW queues of their own (tt_stream_create, the layouts' kind)."""
     import torch
 
     W, H = 1920, 1080
@@ -22,7 +24,8 @@ def test_two_parts_on_two_streams_equal_one_launch():
     dev = torch.device("cuda:0")
     scene = T.c2_sponza()
     c2w, ip = T.C2_VIEW.camera(W, H)
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    owned = [tthip.DedicatedStream(torch, dev) for _ in range(2)] if kind == "dedicated" else []
+    streams = [d.stream for d in owned] if owned else [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     engines = [tthip.Engine(0, stream=s.cuda_stream) for s in streams]
     try:
         for e in engines:
@@ -79,6 +82,9 @@ def test_two_parts_on_two_streams_equal_one_launch():
     finally:
         for e in engines:
             e.close()
+        for d in owned:
+            d.close()
+            assert d.handle is None
 
 
 def test_shared_scene_traces_identically_and_refuses_mutation(engine):

@@ -10,7 +10,7 @@ aux_strong_tiles / aux_c5_tiles) -- and predicts
 The per-frame RCCL gather of the hit records is not replayed (it runs on its own stream beside the
 traces; bench.py measures it on a real node). Configs: C2 (Sponza-shaped 1080p, primary + bounce 1)
 and C5 (San-Miguel-shaped 4K, primary only). Output: one JSON document on stdout (commit it under
-profiles/). Usage: tools/strong_replay.py [--configs c2,c5] [--parts 1] [--slots 3] [--layouts PxF,...] [--steps 30]
+profiles/). Usage: tools/strong_replay.py [--configs c2,c5] [--parts 1] [--slots 6] [--layouts PxF,...] [--steps 30]
 """
 from __future__ import annotations
 
@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c2,c5")
-    ap.add_argument("--slots", type=int, default=3, help="frame slots per rank (bench.py --strong-slots)")
+    ap.add_argument("--slots", type=int, default=6, help="frame slots per rank (bench.py --strong-slots)")
     ap.add_argument("--parts", type=int, default=1, help="parts per rank at N > 1 (bench.py --strong-parts)")
     ap.add_argument("--layouts", default=None,
                     help="comma list of PxF layouts to replay at every N > 1 instead of (parts, --slots), e.g. 3x1,1x3")
