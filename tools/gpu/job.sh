@@ -7,6 +7,8 @@
 #   bench      the driver's command: python bench.py --gpus 1 --steps 20 --warmup 5
 #   quick      bench without aux configs / CPU baseline (layout and headline only)
 #   slots2     quick with 2 frame slots (frame k + 1's primaries overlap frame k's bounce-1 launches)
+#   layouts    the N = 1 headline per parts x slots layout: LAYOUTS="2x1 2x2 1x3", REPS=2 (profiles/r04/ab/r04k_*)
+#   testlib    the GPU suite with a variant library: LIB=name (lib/variants/libtruetrace_hip_NAME.so)
 #   newtests   the GPU tests of the layouts, shared scenes and hit streams only
 #   prof       rocprofv3 --kernel-trace --stats of the bench + the FETCH_SIZE / WRITE_SIZE passes
 #              (tools/profile_round.sh -> traffic JSON; profiles/traffic_latest.json is fed from it)
@@ -20,7 +22,7 @@
 #   sweep      randomized parity sweep (tools/parity_sweep.py), 300 plain + 300 variants/adaptive
 #   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
 #   ab         the bench headline per variant: AB_LIBS="product n128 ..." (lib/variants/libtruetrace_hip_NAME.so),
-#              AB_ARGS extra bench.py flags
+#              AB_ARGS extra bench.py flags, REPS rounds of the list in turn
 #   abcfg      one-launch C4 and C5 per variant (tools/run_variants.py; AB_LIBS names lib/variants entries)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$PWD}"
@@ -44,6 +46,13 @@ for stage in "$@"; do
     bench) run bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     quick) run quick 300 python -u bench.py --steps 20 --warmup 5 --aux "" --cpu-seconds 2 || exit $? ;;
     slots2) run slots2 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --slots 2 || exit $? ;;
+    layouts) for i in $(seq ${REPS:-2}); do for l in ${LAYOUTS:-2x1 2x2 1x3}; do  # N = 1 headline per parts x slots
+                 run "n1_${l}_$i" 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --no-recur \
+                     --no-shadow --parts ${l%x*} --slots ${l#*x} || exit $?
+             done; done ;;
+    testlib) lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_${LIB:?set LIB=variant name}.so
+             run "tests_$LIB" 600 env TT_HIP_LIB=$lib python -u -m pytest tests -m gpu -x -q --timeout 300 \
+                 --timeout-method thread || exit $? ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parts.py \
                   tests/test_gpu_order.py tests/test_bench_launch.py -m gpu || exit $? ;;
     prof) run prof 900 bash tools/profile_round.sh "$TAG" || exit $? ;;
@@ -73,12 +82,12 @@ for stage in "$@"; do
     sweep) run sweep_plain 600 python -u tools/parity_sweep.py 300 40000 || exit $?
            run sweep_var 600 python -u tools/parity_sweep.py 300 41000 variants,adaptive || exit $? ;;
     variants) run variants 900 python -u tools/run_variants.py || exit $? ;;
-    ab) for v in ${AB_LIBS:-product}; do  # the bench headline (no aux legs) per library variant, in turn
+    ab) for i in $(seq ${REPS:-1}); do for v in ${AB_LIBS:-product}; do  # the bench headline per library variant, in turn
             lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so
             [ "$v" = product ] && lib=truetrace-unity-pathtracer_amd/lib/libtruetrace_hip.so
-            run "ab_$v" 300 env TT_HIP_LIB=$lib python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline \
+            run "ab_${v}_$i" 300 env TT_HIP_LIB=$lib python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline \
                 --no-recur --no-shadow ${AB_ARGS:-} || exit $?
-        done ;;
+        done; done ;;
     abcfg) for v in ${AB_LIBS:-product}; do  # one-launch C4 / C5 per variant (tools/run_variants.py)
             for cfg in c4 c5; do run "abcfg_${v}_$cfg" 400 env RV_CFG=$cfg python -u tools/run_variants.py "$v" || exit $?; done
         done ;;
