@@ -159,9 +159,9 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         flags = tthip.TT_TRACE_ADAPTIVE_ORDER if adaptive else 0
         extra_engs, streams = [], []
         try:
-            for _ in range(P - 1):
-                streams.append(tthip.DedicatedStream(torch, dev))  # a HW queue of its own (ttlayout docstring)
-                e1 = tthip.Engine(dev.index, stream=streams[-1].stream.cuda_stream)
+            for k in range(P - 1):
+                streams.append(tthip.dedicated_stream(torch, dev, k))  # a HW queue of its own (ttlayout docstring)
+                e1 = tthip.Engine(dev.index, stream=streams[-1].cuda_stream)
                 extra_engs.append(e1)
                 e1.share_scene(eng)  # one scene copy for all parts (tt_ctx_share_scene)
             chains = [[] for _ in range(n_frames)]  # chains[f]: per part (engine, bufs, counts)
@@ -207,8 +207,6 @@ def aux_configs(torch, tthip, eng, dev, args, which):
         finally:
             for e1 in extra_engs:
                 e1.close()
-            for st in streams:
-                st.close()
 
     def adaptive_one_launch(view, W, H, nb, info, colors_t):
         """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch
@@ -745,7 +743,9 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     # ONE stream for torch and the engine, current before anything is allocated or launched
-    stream = torch.cuda.Stream(dev)
+    # the base stream (part 0 / slot 0 of every layout, the aux legs, the N = 1 reference) gets a HW queue of
+    # its own too: a pool stream can share its queue with any other stream of the process (RCCL's included)
+    stream = tthip.dedicated_stream(torch, dev, -1)
     torch.cuda.set_stream(stream)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
     # TT_BENCH_RCCL_WORLD1=1 (rehearsal, not a bench mode): one rank runs the N > 1 tile path with a

@@ -44,7 +44,7 @@ def main():
     import ttlayout
 
     dev = torch.device("cuda", 0)
-    stream = torch.cuda.Stream(dev)
+    stream = tthip.dedicated_stream(torch, dev, -1)  # the base stream: a HW queue of its own, as bench.py's
     torch.cuda.set_stream(stream)
     eng = tthip.Engine(0, stream=stream.cuda_stream)
     tthip.set_build_engine(eng, min_tris=100_000)

@@ -953,6 +953,23 @@ class DedicatedStream:
             self.stream = None
 
 
+_DEDICATED = {}
+
+
+def dedicated_stream(torch, dev, i: int):
+    """The i-th process-wide stream with a HW queue of its own (a DedicatedStream made on first use and
+    kept for the process's lifetime), as a torch ExternalStream. Layouts take streams 0, 1, ... in turn,
+    so a process holds as many dedicated queues as its widest layout needs however many layouts it
+    builds (tools/strong_replay.py builds one per rank), and a stream outlives every tensor, event and
+    collective that was ever ordered on it."""
+    key = (int(dev.index or 0), int(i))
+    d = _DEDICATED.get(key)
+    if d is None:
+        d = DedicatedStream(torch, dev)
+        _DEDICATED[key] = d
+    return d.stream
+
+
 def validate(s: Scene):
     """tt_scene_validate: (status, message) of the structural check tt_scene_upload runs."""
     buf = C.create_string_buffer(512)

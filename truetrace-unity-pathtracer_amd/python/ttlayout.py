@@ -12,8 +12,8 @@ tiles under tile sharding) as
     reference's: a part's bounce-1 launch follows its primary launch on the same stream.
 
 All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). Every stream the
-layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.DedicatedStream,
-tt_stream_create): plain torch streams are dealt round-robin over a process's few HW queues, and two
+layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.dedicated_stream:
+process-wide streams made with tt_stream_create, reused by every later layout): plain torch streams are dealt round-robin over a process's few HW queues, and two
 persistent trace grids on one queue run back to back -- measured on the strong-scaling replay, the
 ranks whose second part landed on the base stream's queue took 0.45 instead of 0.25 ms per frame
 (profiles/r04/streams/queue_map.txt). TT_LAYOUT_POOL_STREAMS=1 restores torch pool streams (A/B). A step is one
@@ -64,7 +64,7 @@ class FrameLayout:
         WH = W * H
         self.engines = []  # (engine, stream) per context, lend's first; contexts created here are closed by close()
         self.own = []
-        self.own_streams = []  # tthip.DedicatedStream objects, destroyed by close() after the contexts
+        self.n_streams = 0  # process-wide dedicated streams taken so far (tthip.dedicated_stream)
         self.pool_streams = os.environ.get("TT_LAYOUT_POOL_STREAMS", "0") == "1"
         self.slots: List[List[Part]] = []
         base_stream = torch.cuda.current_stream(dev)
@@ -119,9 +119,9 @@ class FrameLayout:
         """A launch stream on its own HW queue (module docstring); a torch pool stream under the A/B knob."""
         if self.pool_streams:
             return self.torch.cuda.Stream(self.dev)
-        d = self.tthip.DedicatedStream(self.torch, self.dev)
-        self.own_streams.append(d)
-        return d.stream
+        st = self.tthip.dedicated_stream(self.torch, self.dev, self.n_streams)
+        self.n_streams += 1
+        return st
 
     # ---------------------------------------------------------------- sizes
     @property
@@ -247,9 +247,6 @@ class FrameLayout:
         self.own = []
         if self.gather is not None:
             self.gather.comm = None
-        for d in self.own_streams:
-            d.close()
-        self.own_streams = []
 
 
 class _Gather:
