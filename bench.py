@@ -988,7 +988,7 @@ def main():
     gather_parity = None
     if G is not None:
         sizes, gather_list = layout.last_gathered()  # the last step's gather (steady-state steps included)
-    if split and rank == 0:
+    if (split or F > 1) and rank == 0:
         if spp:
             fr = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gather_list, sizes)], W, H, world, P)
             gather_parity = all(bool(np.array_equal(fr[k], one_gpu_frame(k))) for k in range(world))
@@ -996,9 +996,11 @@ def main():
         else:
             if tiles:
                 frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
-            else:
+            elif split:
                 own = torch.cat([p.prim_hits for p in layout.slots[(layout.k - 1) % F]]).cpu()
                 frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
+            else:  # one part per slot in the kernel's own order: the last frame's records are in screen order
+                frame = layout.slots[(layout.k - 1) % F][0].prim_hits.contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
             gather_parity = bool(np.array_equal(frame, one_gpu_frame(frames)))
         log(f"gathered frame(s): {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels in sample 0, "
             f"{world if spp else 1} sample(s) identical to single-GPU traces: {gather_parity}")
