@@ -1209,10 +1209,25 @@ def main():
         ceil_ms = (rays1 * cyc1 + rays2 * cyc2) / (1024 * 2.4e9) * 1e3
         step_valu = {"ceiling_ms": round(ceil_ms, 4), "ms_per_step": round(ms_per_step, 4),
                      "frac": round(ceil_ms / ms_per_step, 4), "rays": [rays1, rays2],
-                     "note": "rank 0's step (all its parts' primary + bounce-1 launches, overlapped on their streams) "
+                     "note": "rank 0's step (all its parts' / frame slots' launches, overlapped on their streams) "
                              "against the time the same rays' VALU work takes at 100% VALU issue on 1024 SIMDs at "
-                             "2.4 GHz (issue cycles per ray from the PMC pass); includes launch gaps and drains"
-                             + ("" if world == 1 else " and the gather")}
+                             "2.4 GHz with every VALU instruction priced at one quad-cycle (4 x SQ_ACTIVE_INST_VALU "
+                             "per ray from the PMC pass); includes launch gaps and drains"
+                             + ("" if world == 1 else " and the gather")
+                             + ". The quad-cycle price is a model, not a hard ceiling: plain FP32 / integer ops issue "
+                             "in 2 cycles on the SIMD's 32-lane path, so with frames overlapped the step can pass it "
+                             "(frac > 1); issue_bound_2cyc is the hard bound"}
+        i1 = units_k.get("1", {}).get("valu_instr_per_ray")
+        i2 = units_k.get("2", {}).get("valu_instr_per_ray")
+        if i1 and i2:
+            instr = rays1 * i1 + rays2 * i2  # wave64 VALU instructions of the step (SQ_INSTS_VALU per ray)
+            cpi = 2.4e9 * ms_per_step * 1e-3 * 1024 / instr
+            hard_ms = instr * 2.0 / (1024 * 2.4e9) * 1e3
+            step_valu["valu_instr_per_step"] = round(instr)
+            step_valu["achieved_cycles_per_valu_instr"] = round(cpi, 3)
+            step_valu["issue_bound_2cyc"] = {"ms": round(hard_ms, 4), "frac": round(hard_ms / ms_per_step, 4),
+                                             "note": "every VALU instruction at the wave64 issue minimum, 2 cycles "
+                                                     "per SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz"}
     result = {
         "metric": METRIC,
         "value": round(total_rays / elapsed / 1e6, 2),
