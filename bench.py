@@ -45,6 +45,11 @@ METRIC = "Mrays/sec (primary+1-bounce) on Sponza CWBVH at 1080p; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+# frame slots of the N = 1 headline: the whole 1080p frame, one launch per bounce, 3 frames in flight
+# (profiles/r04/ab/r04k_* / r04l_*: 1 part x 3 slots 6,259-6,273 Mrays/s vs 2 parts x 1 slot 5,538-5,550)
+N1_SLOTS = 3
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -454,10 +459,15 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
             lay_.launch_ms()
             return lay_, el
 
-        # the N = 1 frame (2 parts, 1 slot: the single-GPU layout) on every rank's GPU at once (no collective)
-        solo, el1 = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], slots=1)
+        # the N = 1 frame on every rank's GPU at once (no collective), in both single-GPU layouts (2 parts x 1
+        # slot; one launch in the kernel's own order with N1_SLOTS frames in flight); t(1) = the faster
+        solo, el1a = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], slots=1)
+        solo.close()
+        solo, el1b = timed_layout([[(0, np.arange(WH, dtype=np.int64))]], slots=N1_SLOTS)
         solo.close()
         del solo
+        el1 = min(el1a, el1b)
+        rec["n1_ms_per_frame_by_layout_rank"] = {"2x1": round(el1a, 4), f"1x{N1_SLOTS}": round(el1b, 4)}
         lay, el_n = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)])
         rec.update(rays_this_rank=lay.n_prim(), build_s=round(build_s, 1))
     except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
@@ -508,9 +518,9 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
                with_gather=dict(ms_per_frame_slowest_rank=round(msg, 4), efficiency=round(ms1 / (world * msg), 4),
                                 mrays_s_frame=round(WH / msg / 1e3, 1)),
                identical_to_1gpu=bool(np.array_equal(frame, ref)),
-               note="efficiency = t(N = 1: the whole 4K frame, 2 parts, 1 slot, on every rank's GPU at once, "
-                    "fastest) / (N x t(N), slowest rank); with_gather: the per-frame RCCL gather of the hit records to "
-                    "rank 0 inside the timed frames")
+               note="efficiency = t(N = 1: the whole 4K frame in the faster single-GPU layout, on every rank's GPU "
+                    "at once, fastest) / (N x t(N), slowest rank); with_gather: the per-frame RCCL gather of the hit "
+                    "records to rank 0 inside the timed frames")
     log(f"c5 tiles: {rec}")
     return rec
 
@@ -670,8 +680,9 @@ def main():
                          "headline); the strong-scaling shards use --strong-parts")
     ap.add_argument("--slots", type=int, default=0,
                     help="frame slots F of the headline layout (ttlayout.FrameLayout): frame k runs on slot k %% F with "
-                         "its own buffers and streams, so frame k + 1's primary launches overlap frame k's bounce-1 "
-                         "launches. 0 (default): 1 for a full frame's worth per rank, --strong-slots for the "
+                         "its own buffers and streams on HW queues of their own, so frames k + 1 .. k + F - 1 run while "
+                         "frame k drains. 0 (default): N = 1 the whole frame as one launch per bounce with "
+                         f"{N1_SLOTS} slots; 1 for the spp headline's frame's worth per rank; --strong-slots for the "
                          "strong-scaling shards (--shard tiles)")
     ap.add_argument("--strong-slots", type=int, default=6,
                     help="frame slots of the strong-scaling tile layouts (N > 1: aux_strong_tiles, aux_c5_tiles, "
@@ -802,9 +813,12 @@ def main():
     P_strong = max(1, args.strong_parts)
     F_strong = max(1, args.strong_slots)
     if args.parts <= 0:
-        args.parts = P_strong if (world > 1 and tiles and not spp) else 2
+        # N = 1: the whole frame as ONE launch per bounce in the kernel's own tile order, N1_SLOTS frames in
+        # flight; the spp headline (a frame's worth of tile units per rank): 2 parts
+        args.parts = P_strong if (world > 1 and tiles and not spp) else (1 if world == 1 and not rccl1 else 2)
     P = max(1, args.parts) if (tiles or world == 1) else 1
-    F = max(1, args.slots if args.slots > 0 else (F_strong if (world > 1 and tiles and not spp) else 1))
+    F = max(1, args.slots if args.slots > 0 else (F_strong if (world > 1 and tiles and not spp) else
+                                                  (N1_SLOTS if world == 1 and not rccl1 and P == 1 else 1)))
     split = tiles or P > 1
     make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, 0.3, far, jitter=jitter)
 
@@ -919,17 +933,23 @@ def main():
     # every rank's own GPU at once, no collective -- the T(1) of the strong-scaling efficiency below,
     # measured in the same run on the same kind of GPU (the fastest rank's, conservative)
     solo_ms = None
+    solo_layouts = {}
     if world > 1 and not args.no_strong:
-        solo = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], 1)
-        el_solo = timed(solo)
-        solo.launch_ms()
-        solo.close()
-        t = torch.tensor([el_solo], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        solo_ms = float(t.item()) * 1e3 / args.steps
-        solo_rays = solo.rays_per_frame()
-        del solo
-        log(f"N = 1 frame on each rank's GPU (2 parts, 1 slot): {solo_ms:.4f} ms (fastest rank)")
+        # both single-GPU layouts (the whole frame as 2 parts x 1 slot, and as one launch per bounce in the
+        # kernel's own order with N1_SLOTS frames in flight -- the N = 1 headline's); t(1) = the faster
+        for name, plan_1, slots_1 in (("2x1", [[(0, pix)] for pix in ttdist.part_pixels(W, H, 1, 0, 2)], 1),
+                                      (f"1x{N1_SLOTS}", [[(0, np.arange(WH, dtype=np.int64))]], N1_SLOTS)):
+            solo = layout_of(plan_1, slots_1)
+            el_solo = timed(solo)
+            solo.launch_ms()
+            solo.close()
+            t = torch.tensor([el_solo], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            solo_layouts[name] = round(float(t.item()) * 1e3 / args.steps, 4)
+            solo_rays = solo.rays_per_frame()
+            del solo
+        solo_ms = min(solo_layouts.values())
+        log(f"N = 1 frame on each rank's GPU: {solo_layouts} ms per frame (fastest rank)")
 
     G = layout.attach_gather(dist, world, rank, red_dev) if tiles else None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
@@ -1034,12 +1054,13 @@ def main():
                   "ms_per_frame": round(ms_n, 4),
                   "rays_per_frame_all_ranks": int(round(float(rsum.item()) / args.steps)),
                   "n1_ms_per_frame": round(solo_ms, 4), "n1_rays_per_frame": int(solo_rays),
+                  "n1_ms_per_frame_by_layout": solo_layouts,
                   "efficiency": round(solo_ms / (world * ms_n), 4),
                   "gather_identical_to_1gpu": par,
                   "layout": "one 1080p frame (1 sample): 64x64 tiles round-robin over the ranks, each rank's tiles "
                             f"as {lay_s.P} parts x {lay_s.F} frame slots, + one RCCL gather of the frame's primary "
-                            "hit records per frame; efficiency = t(N = 1 frame, 2 parts, 1 slot, every rank's "
-                            "GPU at once, fastest) / (N x t(N))"}
+                            "hit records per frame; efficiency = t(N = 1 frame in the faster single-GPU layout, "
+                            "every rank's GPU at once, fastest) / (N x t(N))"}
         if lay_s is not layout:
             lay_s.close()
             del lay_s
@@ -1248,9 +1269,11 @@ def main():
                    "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "jitter": jitter,
                    "seed": hex(args.seed),
                    "parallelism": ((f"single GPU, full frame as {P} tile-interleaved parts on {P} streams"
-                                    if P > 1 else "single GPU, full frame")
-                                   + (f", {F} frame slots (frame k + 1's primaries overlap frame k's bounce-1 "
-                                      "launches)" if F > 1 else "") if world == 1 else
+                                    if P > 1 else "single GPU, full frame as one launch per bounce in the kernel's "
+                                    "own 8x8 tile order")
+                                   + (f", {F} frame slots (frames k .. k + {F - 1} in flight on streams with HW queues "
+                                      "of their own: each launch's drain overlaps the next frames' launches)"
+                                      if F > 1 else "") if world == 1 else
                                    ((f"{world}-sample 1080p frame (sample k = Generate with frames_accumulated = k), "
                                      f"its (sample, 64x64 tile) units round-robin over {world} ranks (one frame's "
                                      f"worth each: weak scaling), " if spp else
@@ -1261,8 +1284,10 @@ def main():
                                     + (", overlapped with the bounce-1 trace on a second stream)" if gather_overlapped
                                        else ")") if tiles
                                     else f"sample-sharded x{world} (frames_accumulated=rank), no collective")),
-                   "stream": "torch and engine share one torch.cuda.Stream; per-launch times are HIP events on it"
-                             + (f" (part 0 of {P}: its launches overlap the other parts')" if P > 1 else ""),
+                   "stream": "torch and engine share one stream (a torch ExternalStream on a HW queue of its own); "
+                             "per-launch times are HIP events on it"
+                             + (f" (part 0 / slot 0 of {P} x {F}: its launches overlap the others')"
+                                if P * F > 1 else ""),
                    "parts_per_rank": P, "frame_slots": F, "parts_share_one_scene_copy": P * F > 1,
                    "samples_per_frame": world if spp else 1,
                    "dist_world_size": dist_world, "dist_backend": backend if dist_world else None,

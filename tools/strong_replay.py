@@ -20,6 +20,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "truetrace-unity-pathtracer_amd", "python"))
 
@@ -36,6 +38,7 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to replay per N")
     ap.add_argument("--tile", type=int, default=64, help="screen tile edge of the round-robin sharding")
+    ap.add_argument("--n1-slots", type=int, default=3, help="frame slots of the N = 1 one-launch reference")
     args = ap.parse_args()
     import torch
     import tthip
@@ -78,8 +81,9 @@ def main():
         rows = []
         t1 = None
         for n in [int(x) for x in args.ns.split(",")]:
-            if n == 1:  # the reference: the single-GPU headline layout (2 parts, one slot)
-                layouts = [(2, 1)]
+            if n == 1:  # the reference: both single-GPU layouts (2 parts x 1 slot; the whole frame as one launch in
+                # the kernel's own order with --n1-slots frames in flight, bench.py's N = 1 headline); t(1) = the faster
+                layouts = [(2, 1), (0, args.n1_slots)]
             elif args.layouts:
                 layouts = [tuple(int(v) for v in l.split("x")) for l in args.layouts.split(",")]
             else:
@@ -88,9 +92,9 @@ def main():
             for P, F in layouts:
                 per = []
                 for r in ranks:
-                    lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR,
-                                               [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile)],
-                                               make_full,
+                    plan = ([[(0, np.arange(W * H, dtype=np.int64))]] if P == 0 else  # P = 0: native whole frame
+                            [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile)])
+                    lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR, plan, make_full,
                                                slots=F, bounce=bounce, info=True, colors=colors)
                     ms = frame_ms(lay)
                     per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
@@ -99,7 +103,7 @@ def main():
                     print(f"[replay] {name} N={n} {P}x{F} rank {r}: {per[-1]}", file=sys.stderr, flush=True)
                 t_n = max(p["ms_per_frame"] for p in per)
                 if n == 1:
-                    t1 = t_n
+                    t1 = t_n if t1 is None else min(t1, t_n)
                 rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": F, "ranks": per,
                              "t_frame_ms_slowest_rank": t_n,
                              "predicted_efficiency": round(t1 / (n * t_n), 3) if t1 else None,
