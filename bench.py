@@ -213,6 +213,33 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             for e1 in extra_engs:
                 e1.close()
 
+    def slots_layout(view, W, H, nb, colors_t):
+        """The whole frame as one launch per bounce (kernel order), N1_SLOTS frames in flight on their own
+        contexts and dedicated-queue streams (ttlayout.FrameLayout, bench.py's N = 1 layout): wall ms per
+        frame, frames back to back."""
+        import ttlayout
+
+        c2w, ip = view.camera(W, H)
+        make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, far, max_bounce=max(nb, 1))
+        lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, [[(0, np.arange(W * H, dtype=np.int64))]],
+                                   make_full, slots=N1_SLOTS, bounce=nb >= 1, info=True,
+                                   colors=colors_t if nb >= 1 else None)
+        try:
+            for _ in range(max(2, args.warmup)):
+                lay.step()
+            torch.cuda.synchronize(dev)
+            reps = max(4, args.steps // 2)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                lay.step()
+            torch.cuda.synchronize(dev)
+            ms = (time.perf_counter() - t0) * 1e3 / reps
+            lay.timing_reset()
+            rays = lay.rays_per_frame()
+            return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": int(rays)}
+        finally:
+            lay.close()
+
     def adaptive_one_launch(view, W, H, nb, info, colors_t):
         """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch
         ordered by the previous frame's costs; the primary launches flagged); per-bounce HIP-event ms (order
@@ -253,6 +280,11 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                         extra[key] = parts_layout(sc, view, W, H, nb, info, colors_t, P)
                     except Exception as e:  # noqa: BLE001
                         extra[key] = {"error": f"{type(e).__name__}: {e}"}
+            if with_parts and nb <= 1:  # the N = 1 headline's layout: one launch per bounce, N1_SLOTS frames in flight
+                try:
+                    extra[f"one_launch_{N1_SLOTS}_frame_slots"] = slots_layout(view, W, H, nb, colors_t)
+                except Exception as e:  # noqa: BLE001
+                    extra[f"one_launch_{N1_SLOTS}_frame_slots"] = {"error": f"{type(e).__name__}: {e}"}
             if adaptive:  # TT_TRACE_ADAPTIVE_ORDER (tt_order.hip), frames alternating
                 try:
                     ad = {"one_launch_per_bounce": adaptive_one_launch(view, W, H, nb, info, colors_t)}
