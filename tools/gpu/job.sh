@@ -19,7 +19,8 @@
 #   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
 #   order      tools/exp_order.py per TT_ORDER_HOT threshold (ORDER_HOT, ORDER_CFGS, ORDER_ARGS)
-#   sweep      randomized parity sweep (tools/parity_sweep.py), 300 plain + 300 variants/adaptive
+#   sweep      randomized parity sweep (tools/parity_sweep.py): SWEEP_N plain + SWEEP_N variants/adaptive + SWEEP_N
+#              degenerate-direction cases from seed SWEEP_SEED
 #   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
 #   ab         the bench headline per variant: AB_LIBS="product n128 ..." (lib/variants/libtruetrace_hip_NAME.so),
 #              AB_ARGS extra bench.py flags, REPS rounds of the list in turn
@@ -79,8 +80,10 @@ for stage in "$@"; do
            done ;;
     gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
-    sweep) run sweep_plain 600 python -u tools/parity_sweep.py 300 40000 || exit $?
-           run sweep_var 600 python -u tools/parity_sweep.py 300 41000 variants,adaptive || exit $? ;;
+    sweep) n=${SWEEP_N:-300}; s0=${SWEEP_SEED:-40000}  # plain; trace variants + adaptive order; + degenerate directions
+           run sweep_plain 900 python -u tools/parity_sweep.py $n $s0 || exit $?
+           run sweep_var 900 python -u tools/parity_sweep.py $n $((s0 + 1000)) variants,adaptive || exit $?
+           run sweep_axis 900 python -u tools/parity_sweep.py $n $((s0 + 2000)) axis,variants,adaptive || exit $? ;;
     variants) run variants 900 python -u tools/run_variants.py || exit $? ;;
     ab) for i in $(seq ${REPS:-1}); do for v in ${AB_LIBS:-product}; do  # the bench headline per library variant, in turn
             lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so
