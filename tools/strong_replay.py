@@ -73,8 +73,6 @@ def main():
         make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, T.FAR)
         colors = None
         if bounce:
-            import numpy as np
-
             col = np.zeros(W * H, tthip.COL_DTYPE)
             col["Data"][:, 3] = 1.0
             colors = torch.from_numpy(col.view(np.uint8)).to(dev)
