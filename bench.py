@@ -846,11 +846,12 @@ def main():
     F_strong = max(1, args.strong_slots)
     if args.parts <= 0:
         # N = 1: the whole frame as ONE launch per bounce in the kernel's own tile order, N1_SLOTS frames in
-        # flight; the spp headline (a frame's worth of tile units per rank): 2 parts
-        args.parts = P_strong if (world > 1 and tiles and not spp) else (1 if world == 1 and not rccl1 else 2)
+        # flight; the spp headline at N > 1 (a frame's worth of tile units per rank) the same way, so its
+        # per-rank work runs in the N = 1 layout and the driver's 1 -> N curve compares like with like
+        args.parts = P_strong if (world > 1 and tiles and not spp) else 1
     P = max(1, args.parts) if (tiles or world == 1) else 1
     F = max(1, args.slots if args.slots > 0 else (F_strong if (world > 1 and tiles and not spp) else
-                                                  (N1_SLOTS if world == 1 and not rccl1 and P == 1 else 1)))
+                                                  (N1_SLOTS if P == 1 else 1)))
     split = tiles or P > 1
     make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, 0.3, far, jitter=jitter)
 
