@@ -290,7 +290,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             // a wave carrying a long ray (>= TT_LONG_PRIO node steps so far) issues ahead of the others until
             // its next refill without one: the long ray's dependent chain, not the wave's share of issue,
             // is what sets a small launch's length (the degenerate-direction rays)
-            if (__ballot((int32_t)tg.y >= 0 && Reps >= TT_LONG_PRIO) != 0ull) __builtin_amdgcn_s_setprio(2);
+            if (__ballot((int32_t)tg.y >= 0 && Reps >= TT_LONG_PRIO) != 0ull) __builtin_amdgcn_s_setprio(TT_LONG_PRIO_LEVEL);
             else __builtin_amdgcn_s_setprio(0);
 #endif
             // wave-uniform: take from the wave's pool first, then one dequeue for the rest

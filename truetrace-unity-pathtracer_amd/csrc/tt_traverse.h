@@ -27,10 +27,13 @@
 #define TT_PUSH_FAST 1  // the stack push tests only "an LDS entry is free" on its common path (0: A/B; profiles/r04/ab)
 #endif
 #ifndef TT_DRAIN_PRIO
-#define TT_DRAIN_PRIO 0  // s_setprio level a wave takes once its launch's queue is dry (0: off; A/B option)
+#define TT_DRAIN_PRIO 2  // s_setprio level a wave takes once its launch's queue is dry (0: off; with TT_LONG_PRIO +0.8%, profiles/r04/ab/r04h_*)
 #endif
 #ifndef TT_LONG_PRIO
-#define TT_LONG_PRIO 0  // s_setprio 2 for a wave with a ray past this many node steps, set at refills (0: off; A/B)
+#define TT_LONG_PRIO 64  // s_setprio 2 for a wave with a ray past this many node steps, set at refills (0: off)
+#endif
+#ifndef TT_LONG_PRIO_LEVEL
+#define TT_LONG_PRIO_LEVEL 2  // the s_setprio level of TT_LONG_PRIO (A/B: 3 ranks it above draining waves)
 #endif
 #ifndef TT_UNIFORM_POOL
 #define TT_UNIFORM_POOL 1  // readfirstlane the scheduler's pool state after each refill (0: A/B; +1.2% bench, profiles/r04/ab)

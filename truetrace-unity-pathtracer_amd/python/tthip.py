@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -689,6 +690,7 @@ class Engine:
         if st != TT_OK:
             raise TTError(st, "tt_ctx_create (no GPU visible?)")
         self.L, self.h = L, h.value
+        _ENGINES.add(self)
 
     def _check(self, st, what):
         if st != TT_OK:
@@ -954,6 +956,35 @@ class DedicatedStream:
 
 
 _DEDICATED = {}
+_ENGINES = weakref.WeakSet()  # live contexts: closed before the dedicated streams they may issue on
+
+
+def release_dedicated_streams():
+    """Synchronises and destroys every process-wide dedicated stream (registered with atexit on the first
+    one): a queue made with a CU mask that is still alive when the HIP runtime tears down takes the process
+    down with it under rocprofv3 (exit status 139 in __cxa_finalize, gpurun_out/r04o). Torch's current
+    stream is reset to the default stream first, so nothing issues on a destroyed handle."""
+    if not _DEDICATED:
+        return
+    try:
+        import torch
+
+        for dev_i in {k[0] for k in _DEDICATED}:
+            torch.cuda.synchronize(dev_i)
+            torch.cuda.set_stream(torch.cuda.default_stream(dev_i))
+    except Exception:  # noqa: BLE001 -- teardown: the streams go regardless
+        pass
+    for e in list(_ENGINES):  # a context synchronises its stream when destroyed: destroy it first
+        try:
+            e.close()
+        except Exception:  # noqa: BLE001
+            pass
+    for d in list(_DEDICATED.values()):
+        try:
+            d.close()
+        except Exception:  # noqa: BLE001
+            pass
+    _DEDICATED.clear()
 
 
 def dedicated_stream(torch, dev, i: int):
@@ -965,6 +996,10 @@ def dedicated_stream(torch, dev, i: int):
     key = (int(dev.index or 0), int(i))
     d = _DEDICATED.get(key)
     if d is None:
+        if not _DEDICATED:
+            import atexit
+
+            atexit.register(release_dedicated_streams)
         d = DedicatedStream(torch, dev)
         _DEDICATED[key] = d
     return d.stream
