@@ -214,31 +214,46 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 e1.close()
 
     def slots_layout(view, W, H, nb, colors_t):
-        """The whole frame as one launch per bounce (kernel order), N1_SLOTS frames in flight on their own
-        contexts and dedicated-queue streams (ttlayout.FrameLayout, bench.py's N = 1 layout): wall ms per
-        frame, frames back to back."""
-        import ttlayout
-
-        c2w, ip = view.camera(W, H)
-        make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, far, max_bounce=max(nb, 1))
-        lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, [[(0, np.arange(W * H, dtype=np.int64))]],
-                                   make_full, slots=N1_SLOTS, bounce=nb >= 1, info=True,
-                                   colors=colors_t if nb >= 1 else None)
+        """The whole frame as one launch per bounce in the kernel's own order, N1_SLOTS frames in flight
+        (bench.py's N = 1 layout): slot f has its own context (borrowing the scene), its own stream with a
+        HW queue of its own, its own copies of the bounce chain's ray buffers and its own
+        _PrimaryTriangleInfo; frame k runs its bounce chain on slot k mod N1_SLOTS. Wall ms per frame,
+        frames back to back."""
+        bufs, counts = rays_with_bounces(view, W, H, nb, 0)
+        engs, chains = [eng], []
         try:
-            for _ in range(max(2, args.warmup)):
-                lay.step()
+            for f in range(1, N1_SLOTS):
+                e1 = tthip.Engine(dev.index, stream=tthip.dedicated_stream(torch, dev, f - 1).cuda_stream)
+                e1.share_scene(eng)
+                engs.append(e1)
+            for f, e in enumerate(engs):
+                chains.append((e, [b.clone() for b in bufs] if f else bufs,
+                               torch.zeros(W * H * 16, dtype=torch.uint8, device=dev)))
             torch.cuda.synchronize(dev)
-            reps = max(4, args.steps // 2)
+            k_frame = [0]
+
+            def frame():
+                e, bf, inf = chains[k_frame[0] % N1_SLOTS]
+                k_frame[0] += 1
+                for b in range(nb + 1):
+                    e.trace(bf[b], counts[b], b, far, W, H, info=inf, colors=colors_t if b > 0 else None,
+                            device=True, asynchronous=True)
+
+            for _ in range(max(2, args.warmup) * N1_SLOTS):
+                frame()
+            torch.cuda.synchronize(dev)
+            reps = max(4, args.steps // 2) * N1_SLOTS
             t0 = time.perf_counter()
             for _ in range(reps):
-                lay.step()
+                frame()
             torch.cuda.synchronize(dev)
             ms = (time.perf_counter() - t0) * 1e3 / reps
-            lay.timing_reset()
-            rays = lay.rays_per_frame()
-            return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": int(rays)}
+            rays = int(sum(counts))
+            return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": rays}
         finally:
-            lay.close()
+            for e1 in engs[1:]:
+                e1.close()
+            del chains
 
     def adaptive_one_launch(view, W, H, nb, info, colors_t):
         """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch
@@ -280,7 +295,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                         extra[key] = parts_layout(sc, view, W, H, nb, info, colors_t, P)
                     except Exception as e:  # noqa: BLE001
                         extra[key] = {"error": f"{type(e).__name__}: {e}"}
-            if with_parts and nb <= 1:  # the N = 1 headline's layout: one launch per bounce, N1_SLOTS frames in flight
+            if with_parts:  # the N = 1 headline's layout: one launch per bounce, N1_SLOTS frames in flight
                 try:
                     extra[f"one_launch_{N1_SLOTS}_frame_slots"] = slots_layout(view, W, H, nb, colors_t)
                 except Exception as e:  # noqa: BLE001
