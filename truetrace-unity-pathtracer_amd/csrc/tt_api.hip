@@ -606,18 +606,24 @@ tt_status tt_stream_create(int32_t device, void** stream) {
         return TT_ERR_NO_DEVICE;
     }
     if (device < 0 || device >= ndev) return TT_ERR_INVALID_ARG;
-    if (hipSetDevice(device) != hipSuccess) return TT_ERR_HIP;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return TT_ERR_HIP;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TT_ERR_HIP;
-    // every CU enabled: the mask only exists to get a HW queue that no other stream shares
-    std::vector<uint32_t> mask(((uint32_t)prop.multiProcessorCount + 31u) / 32u, 0xffffffffu);
     hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
-        (void)hipGetLastError();
-        return TT_ERR_HIP;
+    tt_status st = TT_OK;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        st = TT_ERR_HIP;
+    } else {
+        // every CU enabled: the mask only exists to get a HW queue that no other stream shares
+        std::vector<uint32_t> mask(((uint32_t)prop.multiProcessorCount + 31u) / 32u, 0xffffffffu);
+        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            st = TT_ERR_HIP;
+        }
     }
-    *stream = s;
-    return TT_OK;
+    (void)hipSetDevice(prev);  // the caller's current device is left as it was
+    if (st == TT_OK) *stream = s;
+    return st;
 }
 
 tt_status tt_stream_destroy(void* stream) {
