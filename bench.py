@@ -213,13 +213,17 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             for e1 in extra_engs:
                 e1.close()
 
-    def slots_layout(view, W, H, nb, colors_t):
+    def slots_layout(view, W, H, nb, colors_t, adaptive=False):
         """The whole frame as one launch per bounce in the kernel's own order, N1_SLOTS frames in flight
         (bench.py's N = 1 layout): slot f has its own context (borrowing the scene), its own stream with a
         HW queue of its own, its own copies of the bounce chain's ray buffers and its own
         _PrimaryTriangleInfo; frame k runs its bounce chain on slot k mod N1_SLOTS. Wall ms per frame,
-        frames back to back."""
-        bufs, counts = rays_with_bounces(view, W, H, nb, 0)
+        frames back to back. adaptive: TT_TRACE_ADAPTIVE_ORDER on the primary launches, each slot's
+        frames alternating between two jittered samples (frames_accumulated 0 / 1), so a launch's order
+        comes from its context's previous frame, never from its own rays."""
+        n_var = 2 if adaptive else 1
+        flags = tthip.TT_TRACE_ADAPTIVE_ORDER if adaptive else 0
+        fr = [rays_with_bounces(view, W, H, nb, v) for v in range(n_var)]
         engs, chains = [eng], []
         try:
             for f in range(1, N1_SLOTS):
@@ -227,33 +231,35 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 e1.share_scene(eng)
                 engs.append(e1)
             for f, e in enumerate(engs):
-                chains.append((e, [b.clone() for b in bufs] if f else bufs,
+                chains.append((e, [([b.clone() for b in bufs] if f else bufs, counts) for bufs, counts in fr],
                                torch.zeros(W * H * 16, dtype=torch.uint8, device=dev)))
             torch.cuda.synchronize(dev)
             k_frame = [0]
 
             def frame():
-                e, bf, inf = chains[k_frame[0] % N1_SLOTS]
+                k = k_frame[0]
+                e, var, inf = chains[k % N1_SLOTS]
+                bf, counts = var[(k // N1_SLOTS) % n_var]
                 k_frame[0] += 1
                 for b in range(nb + 1):
                     e.trace(bf[b], counts[b], b, far, W, H, info=inf, colors=colors_t if b > 0 else None,
-                            device=True, asynchronous=True)
+                            device=True, asynchronous=True, flags=flags if b == 0 else 0)
 
-            for _ in range(max(2, args.warmup) * N1_SLOTS):
+            for _ in range(max(2, args.warmup) * N1_SLOTS * n_var):
                 frame()
             torch.cuda.synchronize(dev)
-            reps = max(4, args.steps // 2) * N1_SLOTS
+            reps = max(4, args.steps // 2) * N1_SLOTS * n_var
             t0 = time.perf_counter()
             for _ in range(reps):
                 frame()
             torch.cuda.synchronize(dev)
             ms = (time.perf_counter() - t0) * 1e3 / reps
-            rays = int(sum(counts))
+            rays = int(round(sum(sum(c) for _, c in fr) / n_var))
             return {"ms_per_frame": round(ms, 4), "mrays_s": round(rays / ms / 1e3, 1), "rays": rays}
         finally:
             for e1 in engs[1:]:
                 e1.close()
-            del chains
+            del chains, fr
 
     def adaptive_one_launch(view, W, H, nb, info, colors_t):
         """TT_TRACE_ADAPTIVE_ORDER with one launch per bounce: two jittered frames alternate (each launch
@@ -305,6 +311,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                     ad = {"one_launch_per_bounce": adaptive_one_launch(view, W, H, nb, info, colors_t)}
                     if with_parts:
                         ad["two_parts_two_streams"] = parts_layout(sc, view, W, H, nb, info, colors_t, 2, True)
+                        ad[f"one_launch_{N1_SLOTS}_frame_slots"] = slots_layout(view, W, H, nb, colors_t, True)
                     ad["note"] = ("primary launches flagged (a compacted bounce list's chunks shift from frame to "
                                   "frame, DESIGN.md 3.1); two jittered frames (frames_accumulated 0 / 1) alternate, "
                                   "so a launch's order comes from the previous frame's costs; order kernel inside "
