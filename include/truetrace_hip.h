@@ -219,7 +219,8 @@ int32_t tt_device_count(void);
  * made with hipExtStreamCreateWithCUMask and every CU enabled, which gives it a dedicated queue.
  * The reference has no equivalent (Unity issues one command buffer); a host that records its
  * dispatches on several queues (RayTracingMaster.cs:954-1007 per camera) would use one per queue.
- * Destroy with tt_stream_destroy (it synchronises the stream first). */
+ * The calling thread's current device is left unchanged. Destroy with tt_stream_destroy (it
+ * synchronises the stream first). */
 tt_status tt_stream_create(int32_t device, void** stream);
 tt_status tt_stream_destroy(void* stream);
 
