@@ -35,9 +35,10 @@ run() {  # run NAME SECONDS CMD...: one GPU step, its own limit, output to $OUT/
     local name=$1 secs=$2
     shift 2
     echo "[job] $name: $*" >&2
+    local t0=$SECONDS
     timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
     local rc=$?
-    echo "[job] $name rc=$rc" >&2
+    echo "[job] $name rc=$rc ($((SECONDS - t0)) s)" >&2
     tail -c 400 "$OUT/$name.out" >&2
     return $rc
 }
