@@ -1313,7 +1313,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak" if (world > 1 and (spp or not tiles)) else "strong",
+        # the job's scaling mode, the same at every N: spp / sample keep per-GPU work fixed as N grows
+        "scaling": "strong" if args.shard == "tiles" else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded Sponza-shaped hall, tools: tt_synth_sponza); primary rays from the reference's "
