@@ -5,6 +5,7 @@
 # the first failing stage (no GPU step runs after a failure). Stages:
 #   tests      pytest -m gpu (the parity suite)
 #   bench      the driver's command: python bench.py --gpus 1 --steps 20 --warmup 5
+#   smoke      __graft_entry__.smoke() (the driver runs it before the bench)
 #   quick      bench without aux configs / CPU baseline (layout and headline only)
 #   slots2     quick with 2 frame slots (frame k + 1's primaries overlap frame k's bounce-1 launches)
 #   layouts    the N = 1 headline per parts x slots layout: LAYOUTS="2x1 2x2 1x3", REPS=2 (profiles/r04/ab/r04k_*)
@@ -45,6 +46,7 @@ run() {  # run NAME SECONDS CMD...: one GPU step, its own limit, output to $OUT/
 for stage in "$@"; do
     case $stage in
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit $? ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     quick) run quick 300 python -u bench.py --steps 20 --warmup 5 --aux "" --cpu-seconds 2 || exit $? ;;
     slots2) run slots2 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --slots 2 || exit $? ;;
