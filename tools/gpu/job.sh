@@ -6,6 +6,7 @@
 #   tests      pytest -m gpu (the parity suite)
 #   bench      the driver's command: python bench.py --gpus 1 --steps 20 --warmup 5
 #   smoke      __graft_entry__.smoke() (the driver runs it before the bench)
+#   blocks     the headline per persistent-grid size: BLOCKS="20 16 12" blocks per CU (TT_BLOCKS_PER_CU), REPS
 #   quick      bench without aux configs / CPU baseline (layout and headline only)
 #   slots2     quick with 2 frame slots (frame k + 1's primaries overlap frame k's bounce-1 launches)
 #   layouts    the N = 1 headline per parts x slots layout: LAYOUTS="2x1 2x2 1x3", REPS=2 (profiles/r04/ab/r04k_*)
@@ -46,6 +47,10 @@ run() {  # run NAME SECONDS CMD...: one GPU step, its own limit, output to $OUT/
 for stage in "$@"; do
     case $stage in
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit $? ;;
+    blocks) for i in $(seq ${REPS:-1}); do for b in ${BLOCKS:-20 16}; do  # persistent grid blocks per CU (env knob)
+                run "blocks_${b}_$i" 300 env TT_BLOCKS_PER_CU=$b python -u bench.py --steps 20 --warmup 5 --aux "" \
+                    --no-cpu-baseline --no-recur --no-shadow || exit $?
+            done; done ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     quick) run quick 300 python -u bench.py --steps 20 --warmup 5 --aux "" --cpu-seconds 2 || exit $? ;;
