@@ -414,6 +414,11 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 eng.tlas_refit(sc4.tlas_nodes, boxes[k & 1], device=True, asynchronous=True)
             refit_ms = ring_tail(eng, 1, reps)[:, 0]
             eng.upload(sc4)  # leave the scene as built
+            try:
+                slots_rec = dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H)
+            except Exception as e:  # noqa: BLE001
+                slots_rec = {"error": f"{type(e).__name__}: {e}"}
+            eng.upload(sc4)
             rays_f = W * H + float(np.mean(nbs))
             rec = {"instances_updated": n_md, "tlas_nodes": int(sc4.tlas_nodes), "frames": reps,
                    "ms_per_frame": round(ms, 4), "mrays_s": round(rays_f / ms / 1e3, 1),
@@ -422,7 +427,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                    "tlas_refit_host_ms_median": round(float(np.median(host_refit)) * 1e3, 4),
                    "tlas_refit_gpu_ms_median": round(float(np.median(refit_ms)), 4),
                    "note": "frame = update_meshdata (all records, host array, async) + tlas_refit (device boxes) + "
-                           "Generate + primary trace + enqueue (returns the count: one sync) + bounce-1 trace"}
+                           "Generate + primary trace + enqueue (returns the count: one sync) + bounce-1 trace",
+                   f"frame_slots_{N1_SLOTS}": slots_rec}
         except Exception as e:  # auxiliary: record, never lose the metric line
             rec["error"] = f"{type(e).__name__}: {e}"
         out["c4_dynamic_frame"] = rec
@@ -469,6 +475,110 @@ def aux_configs(torch, tthip, eng, dev, args, which):
     return out
 
 
+def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
+    """The reference's dynamic frame (AssetManager.cs:1767-1826: every _MeshData record rewritten and the TLAS
+    refit, then the traces) with N1_SLOTS frames in flight: slot f is a context with a TLAS, TLASBVH8Indices and
+    _MeshData of its own over `eng`'s BLASes and triangles (tt_ctx_share_blas; slot 0 is `eng` itself), on a
+    stream with a HW queue of its own. Frame k runs on slot k % N1_SLOTS: update_meshdata (pose k & 1, all
+    records) + tlas_refit + Generate (frames_accumulated = k) + primary trace + the diffuse enqueue with a
+    device-resident count + the indirect bounce-1 trace, every call asynchronous -- no host synchronization and
+    no wait on another slot. Afterwards each slot's last frame (hit records of both bounces, both
+    _PrimaryTriangleInfo forms) is compared byte for byte with one context issuing the same frame serially."""
+    import ttconfigs as T
+
+    WH = W * H
+    far = T.FAR
+    T_ = int(sc4.tlas_nodes)
+    c2w, ip = T.C4_VIEW.camera(W, H)
+    colors = np.zeros(WH, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = 1.0
+    colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+    S = N1_SLOTS
+    engs, streams = [eng], [torch.cuda.ExternalStream(eng.stream, device=dev)]
+    for f in range(1, S):
+        st = tthip.dedicated_stream(torch, dev, f - 1)
+        e = tthip.Engine(dev.index, stream=st.cuda_stream)
+        e.share_blas(eng, T_)
+        engs.append(e)
+        streams.append(st)
+    bufs = [dict(rays=torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev),
+                 i0=torch.zeros(WH * 16, dtype=torch.uint8, device=dev),
+                 i1=torch.zeros(WH * 16, dtype=torch.uint8, device=dev),
+                 cnt=torch.zeros(1, dtype=torch.int32, device=dev)) for _ in range(S)]
+    n_frames = max(2, args.warmup) * S + max(6, args.steps // 2) * S
+    counts = torch.zeros(n_frames, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    host_ms = []
+
+    def frame(k):
+        f = k % S
+        e, b = engs[f], bufs[f]
+        t0 = time.perf_counter()
+        e.update_meshdata(0, mds[k & 1])
+        e.tlas_refit(T_, boxes[k & 1], device=True, asynchronous=True)
+        e.generate(b["rays"], c2w, ip, W, H, T.NEAR, far, jitter=1, frames=k, max_bounce=1, device=True,
+                   asynchronous=True)
+        e.trace(b["rays"], WH, 0, far, W, H, info=b["i0"], device=True, asynchronous=True)
+        e.enqueue_bounce_indirect(b["rays"], None, WH, b["cnt"], 0, far, W, H, frames=k, max_bounce=1)
+        e.trace_indirect(b["rays"], b["cnt"], WH, 1, far, W, H, info=b["i1"], colors=colors_t)
+        with torch.cuda.stream(streams[f]):
+            counts[k].copy_(b["cnt"][0])
+        host_ms.append((time.perf_counter() - t0) * 1e3)
+
+    k = 0
+    try:
+        for _ in range(max(2, args.warmup) * S):
+            frame(k)
+            k += 1
+        torch.cuda.synchronize(dev)
+        k0 = k
+        reps = max(6, args.steps // 2) * S
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            frame(k)
+            k += 1
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) * 1e3 / reps
+        nb = counts[k0:k].cpu().numpy().astype(np.int64)
+        rays = reps * WH + int(nb.sum())
+        got = [{key: bufs[f][key].cpu().numpy() for key in ("rays", "i0", "i1")} | {"k": kk, "nb": int(counts[kk].item())}
+               for f, kk in ((kk % S, kk) for kk in range(k - S, k))]
+    finally:
+        for e in engs[1:]:
+            e.close()
+    # the serial reference: one context, the same calls for each slot's last frame, synchronously
+    ref = tthip.Engine(dev.index)
+    same = True
+    try:
+        ref.upload(sc4)
+        rr = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        r0 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+        r1 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+        for g in got:
+            kk = g["k"]
+            ref.update_meshdata(0, mds[kk & 1])
+            ref.tlas_refit(T_, boxes[kk & 1], device=True)
+            ref.generate(rr, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=kk, max_bounce=1, device=True)
+            ref.trace(rr, WH, 0, far, W, H, info=r0, device=True)
+            nb_ref = ref.enqueue_bounce(rr, WH, 0, far, W, H, frames=kk, max_bounce=1, device=True)
+            ref.trace(rr, nb_ref, 1, far, W, H, info=r1, colors=colors_t, device=True)
+            torch.cuda.synchronize(dev)
+            a = rr.view(-1, 48).cpu().numpy()
+            gv = g["rays"].reshape(-1, 48)
+            same = same and nb_ref == g["nb"] and np.array_equal(a[:WH], gv[:WH]) \
+                and np.array_equal(a[WH:WH + nb_ref], gv[WH:WH + nb_ref]) \
+                and np.array_equal(r0.cpu().numpy(), g["i0"]) and np.array_equal(r1.cpu().numpy(), g["i1"])
+    finally:
+        ref.close()
+    return {"slots": S, "frames": reps, "ms_per_frame": round(ms, 4), "mrays_s": round(rays / reps / ms / 1e3, 1),
+            "rays_per_frame_mean": int(round(rays / reps)), "host_ms_per_frame_median": round(float(np.median(host_ms)), 4),
+            "identical_to_serial": bool(same),
+            "note": f"frame k on slot k % {S}, each slot a context with its own TLAS / _MeshData over the shared BLASes "
+                    "(tt_ctx_share_blas): update_meshdata (all records) + tlas_refit + Generate (frames_accumulated = k) + "
+                    "primary + enqueue (device count) + indirect bounce-1, all asynchronous; each slot's last frame "
+                    "compared with one context issuing the same calls serially"}
+
+
 def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     """BASELINE configs[4] as the north star lays it out, run after the metric when
     N > 1: the San-Miguel-shaped scene (10 M tris) replicated on every rank, the 3840x2160 frame's
@@ -499,7 +609,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
 
         def timed_layout(plan, slots=F):
             lay_ = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots, bounce=False,
-                                        info=False)
+                                        info=False, slot_stride=1)  # every frame slot its own jittered sample
             for _ in range(max(2, args.warmup)):
                 lay_.step()
             torch.cuda.synchronize(dev)
@@ -557,12 +667,13 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     tgm = torch.tensor([el_g], dtype=torch.float64, device=red_dev)
     dist.all_reduce(tgm, op=dist.ReduceOp.MAX)
     sizes, gl = lay.last_gathered() if rank == 0 else (None, None)
+    last_sample = lay.sample_of(lay.last_slot(), 0)
     lay.close()
     if rank != 0:
         return None
     frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl, sizes)], sizes, W, H, world, P)
     full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-    eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=0, max_bounce=1, device=True)
+    eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=last_sample, max_bounce=1, device=True)
     eng.trace(full, WH, 0, far, W, H, device=True)
     ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
     ms1, msn, msg = float(t1.item()), float(tn.item()), float(tgm.item())
@@ -577,6 +688,51 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
                     "records to rank 0 inside the timed frames")
     log(f"c5 tiles: {rec}")
     return rec
+
+
+def oracle_records_check(scene, layout, pre, post, colors, far, W, H):
+    """The records the bench's timed launches wrote, against the oracle (oracle/tt_oracle.c through
+    tests/oracle_ctypes.py -- the checker, never the measured path). `pre`: every slot's host state after
+    FrameLayout.poison_records() (hit records and _PrimaryTriangleInfo filled with a poison byte); `post`:
+    the same buffers after the timed steps. The oracle traces each slot's primary rays (bounce 0, with
+    _PrimaryTriangleInfo) and bounce-1 rays (the GlobalColors-gated form) in place on `pre`; every 48-B
+    RayData record and every 16-B _PrimaryTriangleInfo texel must then equal `post` byte for byte (a record
+    neither side writes -- the Reps bound -- keeps the poison on both)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ctypes as O
+
+    t0 = time.perf_counter()
+    hw, aff, quota = cpu_share()
+    nthreads = max(1, min(aff, 64))
+    WH = W * H
+    bad_rec = bad_info0 = bad_info1 = 0
+    rays = 0
+    samples = []
+    for f, row in enumerate(layout.slots):
+        samples.append(sorted({layout.sample_of(f, k) for lst in layout.plan for k, _ in lst}))
+        for s_, p in enumerate(row):
+            r = pre[f]["rays"][s_]
+            O.trace(scene, r, p.n, 0, far, W, H, info=pre[f]["info0"], nthreads=nthreads)
+            if layout.bounce and p.nb:
+                O.trace(scene, r, p.nb, 1, far, W, H, info=pre[f]["info1"], colors=colors, nthreads=nthreads)
+            rays += p.n + p.nb
+            bad_rec += int(np.any(r.reshape(-1, 48) != post[f]["rays"][s_].reshape(-1, 48), axis=1).sum())
+        for key in ("info0", "info1"):
+            if pre[f][key] is not None:
+                n_bad = int(np.any(pre[f][key].reshape(-1, 16) != post[f][key].reshape(-1, 16), axis=1).sum())
+                if key == "info0":
+                    bad_info0 += n_bad
+                else:
+                    bad_info1 += n_bad
+    unwritten = sum(int(np.all(post[f]["rays"][s_].reshape(-1, 48)[:p.n, 32:48] == layout.POISON, axis=1).sum())
+                    for f, row in enumerate(layout.slots) for s_, p in enumerate(row))
+    return {"identical": bad_rec == 0 and bad_info0 == 0 and bad_info1 == 0,
+            "mismatching_ray_records": bad_rec, "mismatching_info_bounce0": bad_info0,
+            "mismatching_info_bounce1": bad_info1, "rays_checked": rays, "slots": layout.F,
+            "samples_per_slot": samples, "primary_records_left_unwritten": unwritten,
+            "kernels": "tt_trace_kernel<false,false,1> (primary) and <false,false,2> (bounce 1): the timed launches",
+            "oracle": f"oracle/tt_oracle.c ({os.path.basename(O.lib()._path)}), {nthreads} threads",
+            "seconds": round(time.perf_counter() - t0, 2)}
 
 
 def cpu_share():
@@ -718,14 +874,16 @@ def main():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x53504F4E)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", choices=["spp", "tiles", "sample"], default="spp",
-                    help="N > 1 layout. spp (default, weak scaling): the job at N ranks is an N-sample 1080p frame "
-                         "whose (sample, 64x64 tile) units are dealt round-robin to the ranks (ttdist.spp_part_pixels): "
-                         "every rank traces one frame's worth of screen tiles and their bounce-1 rays, and the primary "
-                         "hit records of all N samples are RCCL-gathered to rank 0 inside every timed step. tiles "
-                         "(strong scaling, also reported as config.aux_strong_tiles): ONE 1-sample frame's tiles dealt "
-                         "round-robin, same gather. sample: every rank traces its own full-frame sample, no collective "
-                         "(weak scaling)")
+    ap.add_argument("--no-oracle-check", action="store_true",
+                    help="N = 1: skip the oracle check of the records the timed launches wrote (oracle_check)")
+    ap.add_argument("--shard", choices=["spp", "tiles", "sample"], default="tiles",
+                    help="N > 1 layout. tiles (default, strong scaling: the north star's layout, SURVEY.md §8(e)): ONE "
+                         "1080p frame's 64x64 screen tiles dealt round-robin to the ranks, each rank tracing its tiles' "
+                         "primary and bounce-1 rays, and the frame's primary hit records RCCL-gathered to rank 0 inside "
+                         "every timed step; its efficiency against the N = 1 frame is in config.aux_strong_tiles. spp "
+                         "(weak scaling, also reported as config.aux_spp_weak): the job at N ranks is an N-sample frame "
+                         "whose (sample, tile) units are dealt round-robin (ttdist.spp_part_pixels), same gather. "
+                         "sample: every rank traces its own full-frame sample, no collective (weak scaling)")
     ap.add_argument("--parts", type=int, default=0,
                     help="a rank's pixels (N = 1: the frame; N > 1: its tiles) are traced as this many tile-interleaved "
                          "parts, each by its own engine on its own stream (each part's bounce-1 after its own primary), "
@@ -747,6 +905,8 @@ def main():
                          "0.312)")
     ap.add_argument("--strong-parts", type=int, default=1,
                     help="tile-interleaved parts per rank of the strong-scaling tile layouts (see --strong-slots)")
+    ap.add_argument("--no-spp-aux", action="store_true",
+                    help="N > 1, --shard tiles: skip the weak-scaling spp layout beside the headline (aux_spp_weak)")
     ap.add_argument("--no-strong", action="store_true",
                     help="N > 1: skip the strong-scaling 1080p tile layout and its N = 1 reference frame")
     ap.add_argument("--no-shadow", action="store_true", help="skip the auxiliary any-hit NEE measurement")
@@ -878,8 +1038,11 @@ def main():
     make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, 0.3, far, jitter=jitter)
 
     def layout_of(plan, slots):
+        # every frame slot traces its own jittered sample (slot f: sample k + f * S where the plan names
+        # sample k, S = the plan's samples), as a renderer's frames in flight do (RayGenKernels.compute:45-46)
+        n_samples = 1 + max(k for lst in plan for k, _ in lst)
         return ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots,
-                                    bounce=True, info=True, colors=colors_t, frames=frames)
+                                    bounce=True, info=True, colors=colors_t, frames=frames, slot_stride=n_samples)
 
     def timed(lay):
         """W untimed steps, then exactly K steps between barrier + synchronize pairs: this rank's seconds."""
@@ -890,6 +1053,7 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
+        k0 = lay.k
         t0_ = time.perf_counter()
         for _ in range(args.steps):
             lay.step()
@@ -897,7 +1061,9 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        return time.perf_counter() - t0_
+        el_ = time.perf_counter() - t0_
+        lay.timed_rays = lay.rays_in_frames(k0, lay.k)  # the K frames' rays (slots differ with their jitter)
+        return el_
 
     if spp:  # this rank's (sample, tile) units of the N-sample frame (ttdist.spp_part_pixels)
         plan = ttdist.spp_part_pixels(W, H, world, rank, P)
@@ -912,7 +1078,9 @@ def main():
     s_prim, s_bnc = parts[0].s_prim, parts[0].s_bnc
     B_prim = alg_bytes(s_prim, 0, parts[0].n)  # part 0's launches (the engine ring below)
     B_bnc = alg_bytes(s_bnc, 1, parts[0].nb)
-    B_step = sum(alg_bytes(p.s_prim, 0, p.n) + alg_bytes(p.s_bnc, 1, p.nb) for p in parts)  # all parts
+    # all parts' launches of a step, averaged over the frame slots (each traces its own jittered sample)
+    B_step = sum(alg_bytes(p.s_prim, 0, p.n) + alg_bytes(p.s_bnc, 1, p.nb) for row in layout.slots
+                 for p in row) / layout.F
     log(f"rank {rank}: primary {n_prim} rays nodes/ray {s_prim.node_visits / max(parts[0].n, 1):.2f} "
         f"tris/ray {s_prim.tri_tests / max(parts[0].n, 1):.2f} "
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(parts[0].nb, 1):.2f} "
@@ -1009,10 +1177,14 @@ def main():
     G = layout.attach_gather(dist, world, rank, red_dev) if tiles else None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
+    # N = 1: the records the timed launches write are checked against the oracle afterwards (oracle_check):
+    # poison every slot's hit records and _PrimaryTriangleInfo first, keep the host state as the oracle's input
+    pre_state = layout.poison_records() if (world == 1 and not args.no_oracle_check) else None
     elapsed = timed(layout)
     lm = layout.launch_ms()  # part 0's launches, the last <= 128 frames of its slot
     launch_ms = lm.reshape(-1)
-    total_rays = float(rays_per_step * args.steps)
+    total_rays = float(layout.timed_rays)
+    rays_per_step = layout.timed_rays / args.steps  # mean over the slots' frames
     trace_ms_rank = float(np.sum(launch_ms)) / (len(launch_ms) // 2)  # part 0's two launches per step
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
@@ -1041,13 +1213,14 @@ def main():
     steady = None
     if world == 1 and args.steady_steps > 0:
         torch.cuda.synchronize(dev)
+        ks = layout.k
         ts = time.perf_counter()
         for _ in range(args.steady_steps):
             layout.step()
         torch.cuda.synchronize(dev)
         es = time.perf_counter() - ts
         steady = {"steps": args.steady_steps, "ms_per_step": round(es * 1e3 / args.steady_steps, 4),
-                  "mrays_s": round(rays_per_step * args.steady_steps / es / 1e6, 2),
+                  "mrays_s": round(layout.rays_in_frames(ks, layout.k) / es / 1e6, 2),
                   "note": "untimed-for-value: the same step repeated after the timed region"}
         log(f"steady state: {steady}")
     layout.timing_reset()  # drain the rings of the steady steps
@@ -1064,9 +1237,11 @@ def main():
     if G is not None:
         sizes, gather_list = layout.last_gathered()  # the last step's gather (steady-state steps included)
     if (split or F > 1) and rank == 0:
+        last = layout.last_slot()  # the last frame's slot: its samples are sample_of(last, k)
         if spp:
             fr = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gather_list, sizes)], W, H, world, P)
-            gather_parity = all(bool(np.array_equal(fr[k], one_gpu_frame(k))) for k in range(world))
+            gather_parity = all(bool(np.array_equal(fr[k], one_gpu_frame(layout.sample_of(last, k))))
+                                for k in range(world))
             frame = fr[0]
         else:
             if tiles:
@@ -1076,9 +1251,19 @@ def main():
                 frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
             else:  # one part per slot in the kernel's own order: the last frame's records are in screen order
                 frame = layout.slots[(layout.k - 1) % F][0].prim_hits.contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
-            gather_parity = bool(np.array_equal(frame, one_gpu_frame(frames)))
+            gather_parity = bool(np.array_equal(frame, one_gpu_frame(layout.sample_of(last, frames))))
         log(f"gathered frame(s): {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels in sample 0, "
             f"{world if spp else 1} sample(s) identical to single-GPU traces: {gather_parity}")
+
+    # N = 1: every slot's records as the timed (and steady-state) launches left them -- the non-stats
+    # tt_trace_kernel<false,false,1|2> instantiations on each slot's own jittered frame -- against the oracle
+    # traced from the same poisoned pre-state (tests/oracle_ctypes.py: checker only, never the measured path)
+    oracle_check = None
+    if pre_state is not None:
+        post_state = layout.snapshot()
+        oracle_check = oracle_records_check(scene, layout, pre_state, post_state, colors, far, W, H)
+        del pre_state, post_state
+        log(f"oracle check of the timed records: {oracle_check}")
 
     # N > 1: the strong-scaling layout -- ONE 1-sample frame's tiles dealt round-robin (P_strong parts x
     # F_strong frame slots per rank), the same per-frame gather; frame time = the slowest rank's; its
@@ -1093,7 +1278,7 @@ def main():
         el_s = timed(lay_s) if lay_s is not layout else elapsed
         if lay_s is not layout:
             lay_s.launch_ms()
-        st_ = torch.tensor([el_s, float(lay_s.rays_per_frame() * args.steps)], dtype=torch.float64, device=red_dev)
+        st_ = torch.tensor([el_s, float(lay_s.timed_rays)], dtype=torch.float64, device=red_dev)
         tmax = st_[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         rsum = st_[1:].clone()
@@ -1102,7 +1287,7 @@ def main():
         if rank == 0:
             sz_s, gl_s = lay_s.last_gathered()
             fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H, world, lay_s.P)
-            par = bool(np.array_equal(fr1, one_gpu_frame(0)))
+            par = bool(np.array_equal(fr1, one_gpu_frame(lay_s.sample_of(lay_s.last_slot(), 0))))
         ms_n = float(tmax.item()) * 1e3 / args.steps
         strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
                   "scaling": "strong", "ranks": world, "parts_per_rank": lay_s.P, "frame_slots": lay_s.F,
@@ -1121,6 +1306,38 @@ def main():
             del lay_s
         log(f"strong-scaling tile layout: {strong}")
     layout.close()  # the borrowing contexts go before any aux leg re-uploads `eng`'s scene
+
+    # N > 1 with the strong-scaling headline: the weak-scaling spp layout beside it (an N-sample frame's
+    # (sample, tile) units round-robin, a frame's worth per rank in the N = 1 layout: 1 part x N1_SLOTS
+    # slots, the same per-frame gather); value = all ranks' rays / the slowest rank's time
+    spp_aux = None
+    if world > 1 and tiles and not spp and not args.no_spp_aux:
+        lay_w = layout_of(ttdist.spp_part_pixels(W, H, world, rank, 1), N1_SLOTS)
+        lay_w.attach_gather(dist, world, rank, red_dev)
+        el_w = timed(lay_w)
+        lay_w.launch_ms()
+        st_w = torch.tensor([el_w, float(lay_w.timed_rays)], dtype=torch.float64, device=red_dev)
+        tmax = st_w[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        rsum = st_w[1:].clone()
+        dist.all_reduce(rsum, op=dist.ReduceOp.SUM)
+        par_w = None
+        if rank == 0:
+            sz_w, gl_w = lay_w.last_gathered()
+            fr_w = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gl_w, sz_w)], W, H, world, 1)
+            lw = lay_w.last_slot()
+            par_w = all(bool(np.array_equal(fr_w[k], one_gpu_frame(lay_w.sample_of(lw, k)))) for k in range(world))
+        spp_aux = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
+                   "scaling": "weak", "ranks": world, "parts_per_rank": lay_w.P, "frame_slots": lay_w.F,
+                   "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4),
+                   "samples_per_frame": world, "gather_identical_to_1gpu": par_w,
+                   "layout": f"{world}-sample 1080p frame (sample k = Generate with frames_accumulated = k), its "
+                             f"(sample, 64x64 tile) units round-robin over {world} ranks (a frame's worth each), each "
+                             f"rank's units as 1 part x {lay_w.F} frame slots, + one RCCL gather of the primary hit "
+                             "records per step"}
+        lay_w.close()
+        del lay_w
+        log(f"spp (weak-scaling) layout: {spp_aux}")
 
     # ---- auxiliary: the UseReCur ray generation (no jitter), primary + bounce 1, N=1
     recur = None
@@ -1243,26 +1460,49 @@ def main():
         units, units_src = uj.get("mean"), uj.get("source")
         units_k = {k.rstrip(">").split(",")[-1].strip(): v for k, v in uj.get("per_kernel", {}).items()}
 
-    # the binding unit is VALU issue: per launch, rays/s against the rate the same
-    # instruction stream reaches with VALU issue 100% busy on all 1,024 SIMDs at the 2.4 GHz peak
-    # clock (valu_ceiling_grays_s, from the PMC pass's VALU issue cycles per ray). One launch at a
-    # time (P = 1: the metric's launches; P > 1: the single-stream leg), so a launch's duration is
-    # the kernel's. The dominant kernel is the longer launch.
+    # roofline: the dominant launch (the longer of the primary / bounce-1 launches, one launch at
+    # a time: P = F = 1, or the single-stream leg) against the HARD VALU issue bound: every wave64 VALU
+    # instruction at its 2-cycle minimum (MI355X_MICROARCH.md, per-instruction constants) on 1024 SIMDs at the
+    # 2.4 GHz peak clock, i.e. 1024 x 2.4e9 / (2 x VALU instructions per ray) rays/s -- frac <= 1 by
+    # construction. VALU instructions per ray and the unit busy fractions come from the round's PMC passes of
+    # the same kernels (tools/pmc_units.sh -> profiles/units_latest.json). Two labelled models sit beside it:
+    # the instruction-mix model (each instruction priced at its measured class cost, tools/valu_mix.py) and the
+    # quad-cycle model of rounds 1-4 (every instruction at 4 cycles); neither is a bound.
     if P == 1 and F == 1:
         per_launch = {"1": (n_prim, float(np.mean(prim_ms))), "2": (nb, float(np.mean(bnc_ms)))}
     elif single is not None:
         per_launch = {"1": (WH, single["trace_ms_primary"]), "2": (frame_nb, single["trace_ms_bounce"])}
     else:
         per_launch = {}
+    CLK, SIMDS = 2.4e9, 1024
     valu = {}
     for info, (n, ms) in per_launch.items():
         u = units_k.get(info, {})
         rate = n / (ms * 1e-3) / 1e9
-        ceil = u.get("valu_ceiling_grays_s")
+        ipr = u.get("valu_instr_per_ray")
+        hard = SIMDS * CLK / (2.0 * ipr) / 1e9 if ipr else None
+        mix_cpi = u.get("mix_cycles_per_instr")
+        mix = SIMDS * CLK / (mix_cpi * ipr) / 1e9 if (ipr and mix_cpi) else None
+        quad = u.get("valu_ceiling_grays_s")
+        # the PMC run's busy fractions of the same kernel: VALU against the 2-cycle issue bound (instructions x 2
+        # cycles over 1024 SIMDs x the run's GPU cycles), the texture-data return path (TD) and address path (TA)
+        hard_busy = (ipr * u["rays"] * 2.0 / (SIMDS * u["cycles"])) if (ipr and u.get("rays") and u.get("cycles")) else None
+        busy = {"valu_2cyc_issue": None if hard_busy is None else round(hard_busy, 3),
+                "td": u.get("td_busy"), "ta": u.get("ta_busy"), "valu_quad_cycle_model": u.get("valu_issue_busy")}
+        names = {"valu_2cyc_issue": "VALU issue (2-cycle bound)", "td": "TD (texture-data return path)",
+                 "ta": "TA (texture-address path)"}
+        cand = {k: v for k, v in busy.items() if k in names and v is not None}
+        bind = max(cand, key=cand.get) if cand else None
         valu[info] = {"kernel": f"tt_trace_kernel<false,false,{info}>", "rays": int(n), "launch_ms": round(ms, 4),
-                      "grays_s": round(rate, 4), "valu_ceiling_grays_s": ceil,
-                      "valu_issue_cycles_per_ray": u.get("valu_issue_cycles_per_ray"),
-                      "frac": round(rate / ceil, 4) if ceil else None}
+                      "grays_s": round(rate, 4), "valu_instr_per_ray": ipr,
+                      "issue_bound_2cyc_grays_s": None if hard is None else round(hard, 4),
+                      "frac": round(rate / hard, 4) if hard else None,
+                      "mix_model_grays_s": None if mix is None else round(mix, 4),
+                      "frac_mix_model": round(rate / mix, 4) if mix else None,
+                      "mix_cycles_per_instr": mix_cpi,
+                      "quad_cycle_model_grays_s": quad, "frac_quad_cycle_model": round(rate / quad, 4) if quad else None,
+                      "units_busy_pmc": busy,
+                      "binding_unit": None if bind is None else {"unit": names[bind], "busy": cand[bind]}}
     dom = max(valu.values(), key=lambda v: v["launch_ms"]) if valu else None
     # the DRAM-side fraction (SURVEY §8(d) consistency warning): the PMC pass's fabric bytes of each launch
     # (2 x FETCH_SIZE + WRITE_SIZE, per the gfx950 correction) over the same launch's HIP-event duration
@@ -1275,35 +1515,30 @@ def main():
     dom_dram = dram.get(max(valu, key=lambda k: valu[k]["launch_ms"])) if valu and dram else None
 
     ms_per_step = elapsed * 1e3 / args.steps
-    # the whole step (all parts' launches, overlapped) against the time its VALU work takes with VALU
-    # issue 100% busy at 2.4 GHz: rank 0's primary and bounce-1 rays x their issue cycles per ray
+    # the whole step (all parts' / frame slots' launches, overlapped) against the same hard bound: the step's
+    # wave64 VALU instructions (rank 0's rays x SQ_INSTS_VALU per ray) at 2 cycles on 1024 SIMDs at 2.4 GHz
     step_valu = None
-    cyc1 = units_k.get("1", {}).get("valu_issue_cycles_per_ray")
-    cyc2 = units_k.get("2", {}).get("valu_issue_cycles_per_ray")
-    if cyc1 and cyc2:
-        rays1, rays2 = int(sum(p.n for p in parts)), int(sum(p.nb for p in parts))
-        ceil_ms = (rays1 * cyc1 + rays2 * cyc2) / (1024 * 2.4e9) * 1e3
-        step_valu = {"ceiling_ms": round(ceil_ms, 4), "ms_per_step": round(ms_per_step, 4),
-                     "frac": round(ceil_ms / ms_per_step, 4), "rays": [rays1, rays2],
-                     "note": "rank 0's step (all its parts' / frame slots' launches, overlapped on their streams) "
-                             "against the time the same rays' VALU work takes at 100% VALU issue on 1024 SIMDs at "
-                             "2.4 GHz with every VALU instruction priced at one quad-cycle (4 x SQ_ACTIVE_INST_VALU "
-                             "per ray from the PMC pass); includes launch gaps and drains"
-                             + ("" if world == 1 else " and the gather")
-                             + ". The quad-cycle price is a model, not a hard ceiling: plain FP32 / integer ops issue "
-                             "in 2 cycles on the SIMD's 32-lane path, so with frames overlapped the step can pass it "
-                             "(frac > 1); issue_bound_2cyc is the hard bound"}
-        i1 = units_k.get("1", {}).get("valu_instr_per_ray")
-        i2 = units_k.get("2", {}).get("valu_instr_per_ray")
-        if i1 and i2:
-            instr = rays1 * i1 + rays2 * i2  # wave64 VALU instructions of the step (SQ_INSTS_VALU per ray)
-            cpi = 2.4e9 * ms_per_step * 1e-3 * 1024 / instr
-            hard_ms = instr * 2.0 / (1024 * 2.4e9) * 1e3
-            step_valu["valu_instr_per_step"] = round(instr)
-            step_valu["achieved_cycles_per_valu_instr"] = round(cpi, 3)
-            step_valu["issue_bound_2cyc"] = {"ms": round(hard_ms, 4), "frac": round(hard_ms / ms_per_step, 4),
-                                             "note": "every VALU instruction at the wave64 issue minimum, 2 cycles "
-                                                     "per SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz"}
+    i1 = units_k.get("1", {}).get("valu_instr_per_ray")
+    i2 = units_k.get("2", {}).get("valu_instr_per_ray")
+    if i1 and i2:
+        rays1 = sum(p.n for row in layout.slots for p in row) / layout.F
+        rays2 = sum(p.nb for row in layout.slots for p in row) / layout.F
+        instr = rays1 * i1 + rays2 * i2
+        hard_ms = instr * 2.0 / (SIMDS * CLK) * 1e3
+        step_valu = {"issue_bound_2cyc_ms": round(hard_ms, 4), "ms_per_step": round(ms_per_step, 4),
+                     "frac": round(hard_ms / ms_per_step, 4), "rays": [round(rays1), round(rays2)],
+                     "valu_instr_per_step": round(instr),
+                     "achieved_cycles_per_valu_instr": round(CLK * ms_per_step * 1e-3 * SIMDS / instr, 3),
+                     "note": "rank 0's step against the hard VALU issue bound (every wave64 VALU instruction at 2 "
+                             "cycles, 1024 SIMDs, 2.4 GHz); includes launch gaps and drains"
+                             + ("" if world == 1 else " and the gather")}
+        m1 = units_k.get("1", {}).get("mix_cycles_per_instr")
+        m2 = units_k.get("2", {}).get("mix_cycles_per_instr")
+        if m1 and m2:
+            mix_ms = (rays1 * i1 * m1 + rays2 * i2 * m2) / (SIMDS * CLK) * 1e3
+            step_valu["mix_model"] = {"ms": round(mix_ms, 4), "frac": round(mix_ms / ms_per_step, 4),
+                                      "note": "a model, not a bound: each VALU instruction at its class's measured "
+                                              "cost (tools/valu_mix.py)"}
     result = {
         "metric": METRIC,
         "value": round(total_rays / elapsed / 1e6, 2),
@@ -1357,17 +1592,27 @@ def main():
                    "kernel_mrays_s_trace_only": round((parts[0].n + parts[0].nb) / trace_ms_rank / 1e3, 2),
                    "gather_identical_to_1gpu": gather_parity,
                    "steady_state": steady,
-                   "aux_strong_tiles": strong,
+                   "aux_strong_tiles": strong, "aux_spp_weak": spp_aux,
                    "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
                    "aux_c5_tiles": c5t},
         "roofline": {"bound": "valu_issue", "unit": "Grays/s",
                      "achieved": dom["grays_s"] if dom else None,
-                     "peak": dom["valu_ceiling_grays_s"] if dom else None,
+                     "peak": dom["issue_bound_2cyc_grays_s"] if dom else None,
                      "frac": dom["frac"] if dom else None,
                      "kernel": dom["kernel"] if dom else None,
+                     "binding_unit": dom["binding_unit"] if dom else None,
+                     "units_busy_pmc": dom["units_busy_pmc"] if dom else None,
                      "traffic": traffic,
                      "per_launch": valu,
+                     "models": {"mix_grays_s": dom["mix_model_grays_s"] if dom else None,
+                                "frac_mix": dom["frac_mix_model"] if dom else None,
+                                "quad_cycle_grays_s": dom["quad_cycle_model_grays_s"] if dom else None,
+                                "frac_quad_cycle": dom["frac_quad_cycle_model"] if dom else None,
+                                "note": "models, not bounds: mix = every VALU instruction at its class's measured cost "
+                                        "(tools/valu_mix.py: the kernel's ISA x per-block execution counts x "
+                                        "profiles/r01_micro_valu_ops.txt); quad_cycle = every instruction at 4 cycles "
+                                        "(rounds 1-4's 'ceiling')"},
                      "hbm": {"achieved_alg_gbs": round(achieved, 1), "peak_gbs": HBM_PEAK_GBS,
                              "frac_alg": round(achieved / HBM_PEAK_GBS, 4),
                              "traffic_bytes_per_launch": traffic,
@@ -1376,19 +1621,23 @@ def main():
                              "alg_bytes_per_launch": round((B_prim + B_bnc) / 2.0) if P == 1 else round(B_step / (2 * P)),
                              "alg_bytes_per_step": round(B_step),
                              "note": ("achieved_alg_gbs = algorithmic bytes per trace launch (B_ray, SURVEY §8d) / mean "
-                                      "HIP-event launch time" if P == 1 else
+                                      "HIP-event launch time" if P == 1 and F == 1 else
                                       f"achieved_alg_gbs = algorithmic bytes (B_ray, SURVEY §8d) of all 2 x {P} trace "
                                       "launches of a step / the step's wall time") + "; the bytes are served mostly "
                                      "from L2 / MALL: traffic = fabric bytes per launch from " + (traffic_src or "no PMC pass")
                                      + " (2 x FETCH_SIZE + WRITE_SIZE, includes Infinity-Cache hits), so HBM does not "
                                      "bind this loop"},
-                     "units_busy": units, "single_stream": single, "step": step_valu,
-                     "note": "bound = VALU issue (DESIGN.md §3.1): achieved = rays/s of the dominant launch (one launch "
-                             "at a time, HIP events on its stream), peak = the same launch's VALU-issue ceiling = 1024 "
-                             "SIMDs x 2.4 GHz / VALU issue cycles per ray from the PMC pass " + (units_src or "(none)")
-                             + " (tools/pmc_units.sh -> tools/pmc_units_summary.py -> profiles/units_latest.json); "
-                             "frac <= 1 by construction up to run-to-run variation of the cycles per ray"},
+                     "single_stream": single, "step": step_valu,
+                     "note": "bound = VALU issue: achieved = rays/s of the dominant launch (one launch at a time, HIP "
+                             "events on its stream); peak = the hard issue bound of the same instruction stream = 1024 "
+                             "SIMDs x 2.4 GHz / (2 cycles x wave64 VALU instructions per ray), the instructions per ray "
+                             "from the PMC pass " + (units_src or "(none)") + " (tools/pmc_units.sh -> "
+                             "tools/pmc_units_summary.py -> profiles/units_latest.json); frac <= 1 by construction. "
+                             "binding_unit = the busiest of VALU (against the same 2-cycle bound), TD and TA in that PMC "
+                             "run"},
         "cpu_baseline": cpu,
+        "oracle_identical": None if oracle_check is None else oracle_check["identical"],
+        "oracle_check": oracle_check,
     }
     print(json.dumps(result), flush=True)
     if world > 1 or rccl1:

@@ -86,8 +86,9 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern TTStatus tt_ctx_destroy(IntPtr ctx);
         [DllImport(Lib)] public static extern IntPtr tt_last_error(IntPtr ctx);
         [DllImport(Lib)] public static extern int tt_device_count();
-        [DllImport(Lib)] public static extern TTStatus tt_stream_create(int device, out IntPtr stream);
+        [DllImport(Lib)] public static extern TTStatus tt_stream_create(int device, out TTStreamHandle stream);
         [DllImport(Lib)] public static extern TTStatus tt_stream_destroy(IntPtr stream);
+        [DllImport(Lib)] public static extern uint tt_stream_live_count();
         // Element types are the reference's own host structs: BVHNode8DataCompressed (80 B),
         // CudaTriangle (88 B), int, MyMeshDataCompacted (88 B), MaterialData (252 B).
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload(IntPtr ctx,
@@ -149,6 +150,14 @@ namespace TrueTrace.Hip
             int* presorted, void* nodes, uint maxNodes, out uint nNodes, int* cwbvhIndices, out uint bvh2Depth);
         [DllImport(Lib)] public static extern unsafe TTStatus tt_bvh2_build_device(IntPtr ctx, float* aabbs, uint n,
             int* presorted, int* finalIndices, float* nodeAabbs, int* nodeLeft, uint* nodeCount, out uint maxDepth);
+    }
+
+    /// A stream made by tt_stream_create, destroyed (tt_stream_destroy: synchronise + destroy) when released.
+    public sealed class TTStreamHandle : SafeHandle
+    {
+        public TTStreamHandle() : base(IntPtr.Zero, true) { }
+        public override bool IsInvalid => handle == IntPtr.Zero;
+        protected override bool ReleaseHandle() => Native.tt_stream_destroy(handle) == TTStatus.Ok;
     }
 
     /// Replaces `cmd.DispatchCompute(IntersectionShader, TraceKernel, CurBounceInfoBuffer, 0)`
@@ -219,14 +228,20 @@ namespace TrueTrace.Hip
         public void ShareScene(TrueTraceHip lender) { Check(Native.tt_ctx_share_scene(m_ctx, lender.m_ctx)); }
 
         /// A hipStream_t on a hardware queue of its own (tt_stream_create) for a concurrently traced half of
-        /// the frame: pass it as TTConfig.stream of that half's context; StreamDestroy after disposing it.
-        public static IntPtr StreamCreate(int device)
+        /// the frame: pass handle.DangerousGetHandle() as the hipStream of that half's tracer and dispose the
+        /// handle after the tracer. The handle is a SafeHandle: a finalizer or a domain reload that skips
+        /// Dispose still destroys the stream (and the library destroys any stream left at process exit).
+        public static TTStreamHandle StreamCreate(int device)
         {
-            var st = Native.tt_stream_create(device, out IntPtr s);
-            if (st != TTStatus.Ok) throw new InvalidOperationException($"tt_stream_create: {st}");
+            var st = Native.tt_stream_create(device, out TTStreamHandle s);
+            if (st != TTStatus.Ok)
+            {
+                s?.SetHandleAsInvalid();
+                throw new InvalidOperationException($"tt_stream_create: {st}");
+            }
             return s;
         }
-        public static void StreamDestroy(IntPtr stream) { Native.tt_stream_destroy(stream); }
+        public static void StreamDestroy(TTStreamHandle stream) { stream?.Dispose(); }
 
         /// TraceDevice that also writes ray i's 16-byte hit record to hitsOut[i] (HIP device memory, 16-byte
         /// aligned, nRays records): the buffer a multi-GPU host gathers (tt_trace_closest_hits).

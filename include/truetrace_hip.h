@@ -222,7 +222,14 @@ int32_t tt_device_count(void);
  * The calling thread's current device is left unchanged. Destroy with tt_stream_destroy (it
  * synchronises the stream first). */
 tt_status tt_stream_create(int32_t device, void** stream);
+/* Synchronises and destroys a stream tt_stream_create made; TT_ERR_INVALID_ARG for any other handle
+ * (or one destroyed already). Streams still alive when the process exits are synchronised and
+ * destroyed by the library from an exit handler that runs before the HIP runtime's own teardown (a
+ * CU-mask queue alive at that point crashes the exit, SIGSEGV in __cxa_finalize), so a host that
+ * exits without tt_stream_destroy -- or a Unity domain reload that skips it -- ends cleanly. */
 tt_status tt_stream_destroy(void* stream);
+/* Streams made by tt_stream_create and not destroyed yet. */
+uint32_t tt_stream_live_count(void);
 
 /* ---------------------------------------------------------- scene */
 /* Replaces AssetManager.SetMeshTraceBuffers (AssetManager.cs:75-88): copies the
@@ -352,6 +359,7 @@ tt_status tt_scene_read_tris(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cud
 
 /* Copies nodes [first, first+count) of the scene in HBM back to the host (e.g. the TLAS after
  * tt_tlas_refit; the reference reads its refit TLAS back for nothing, but editors and tests do).
+ * On a frame-slot context (tt_ctx_share_blas) nodes [0, n_tlas_nodes) are its own TLAS.
  * Synchronizes the context stream. */
 tt_status tt_scene_read_nodes(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cwbvh_node* out);
 
@@ -368,6 +376,25 @@ tt_status tt_scene_read_nodes(tt_ctx* ctx, uint32_t first, uint32_t count, tt_cw
  * tt_ctx_destroy (destroy the borrowers first); dst refuses every scene-mutating call. Same device;
  * src must not itself borrow. Synchronizes both streams. */
 tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src);
+
+/* Makes `dst` a frame slot over `src`'s scene: dst traces src's BLAS nodes, triangles, materials and
+ * atlases (no copy, as tt_ctx_share_scene) but has a TLAS of its own -- a copy of the TLAS nodes
+ * [0, n_tlas_nodes) (the refit's count, AssetManager.cs:995: the TLAS region at the front of the node
+ * array), of TLASBVH8Indices and of _MeshData, taken from src's device buffers as they are now. The
+ * reference refits the TLAS and rewrites every _MeshData record each frame before it traces
+ * (AssetManager.cs:1767-1826); with one scene shared by frames in flight those writes would have to
+ * wait for every in-flight frame's traces. On dst, tt_tlas_refit, tt_scene_update_meshdata and
+ * tt_scene_update_nodes (its TLAS nodes only) change dst's TLAS alone and are ordered only on dst's
+ * stream: no wait on src or on other slots, and neither src nor other slots see them. src's own
+ * TLAS-side updates (tt_tlas_refit, tt_scene_update_meshdata, TLAS-only node rewrites) are not seen by
+ * dst and do not wait for it; src's BLAS-side updates (tt_blas_refit) are seen by dst and ordered
+ * against its launches as with tt_ctx_share_scene, and a BLAS-side node rewrite through
+ * tt_scene_update_nodes is refused while frame slots exist (TT_ERR_UNSUPPORTED). The TLAS copy lives
+ * in one of 8 regions src's upload reserved behind its nodes (8 x the TLAS region; TT_ERR_UNSUPPORTED
+ * when all are in use). Precondition: every node the TLAS walk reaches lies in [0, n_tlas_nodes)
+ * (TT_ERR_INVALID_ARG otherwise). dst refuses tt_blas_refit and uploads. Same device; src must not
+ * itself borrow. Synchronizes both streams. */
+tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes);
 
 /* Bytes of HBM the scene occupies (device copies + derived traversal layouts). */
 tt_status tt_scene_bytes(const tt_ctx* ctx, uint64_t* bytes);
@@ -584,10 +611,12 @@ typedef struct tt_camera {
     int32_t jitter;             /* 1: random(0,pixel)-0.5 sub-pixel jitter (the !UseReCur path) */
     int32_t frames_accumulated; /* random() seed inputs (non-ASVGF branch)                      */
     int32_t max_bounce;
-    uint32_t flags;             /* TT_TRACE_DEVICE_PTRS                                          */
+    uint32_t flags;             /* TT_TRACE_DEVICE_PTRS [| TT_TRACE_ASYNC]                      */
 } tt_camera;
 
-/* Writes W*H RayData (hits = (0,0,asuint(FarPlane),0)) into GlobalRays[pixel]. */
+/* Writes W*H RayData (hits = (0,0,asuint(FarPlane),0)) into GlobalRays[pixel]. With device rays and
+ * TT_TRACE_ASYNC the call returns without waiting (the camera is staged through pinned memory), so a
+ * whole frame -- Generate, trace, enqueue, indirect trace -- is issued with no host synchronization. */
 tt_status tt_generate_primary(tt_ctx* ctx, const tt_camera* cam, tt_ray_data* global_rays);
 
 /* Diffuse-lobe next-bounce enqueue for the rays traced at p->bounce (the subset of kernel_shade

@@ -62,6 +62,8 @@ def test_stream_create_without_device_is_loud():
     assert h.value is None
     assert L.tt_stream_create(0, None) == tthip.TT_ERR_INVALID_ARG
     assert L.tt_stream_destroy(None) == tthip.TT_ERR_INVALID_ARG
+    assert L.tt_stream_destroy(C.c_void_p(0x1000)) == tthip.TT_ERR_INVALID_ARG  # not made by tt_stream_create
+    assert L.tt_stream_live_count() == 0
 
 
 def test_null_context_is_rejected():

@@ -418,6 +418,39 @@ def test_sponza_1080p_primary_and_bounce_full_parity(engine, sponza):
     assert s2.node_visits == int(cnt2["node_visits"].sum())
 
 
+@pytest.mark.parametrize("frames", [0, 1, 2])
+def test_sponza_1080p_jittered_frames_through_the_timed_kernels(engine, sponza, frames):
+    """bench.py's exact workload and kernels: the reference's default jittered Generate (frames_accumulated =
+    frames, one per frame slot), the primary launch through tt_trace_kernel<false,false,1> and the bounce-1
+    launch through <false,false,2> -- the non-stats instantiations the bench times (trace_both runs the STATS
+    ones) -- with every hit record and _PrimaryTriangleInfo texel poisoned first, so a record the kernels
+    fail to write cannot pass as the oracle's."""
+    W, H = 1920, 1080
+    WH = W * H
+    c2w, ip = tthip.unity_camera((-10, 2, 0), (1, 0, 0), (0, 1, 0), 60, W, H, 0.3, FAR)
+    engine.upload(sponza)
+    rays = np.zeros(2 * WH, tthip.RAY_DTYPE)
+    engine.generate(rays, c2w, ip, W, H, 0.3, FAR, jitter=1, frames=frames, max_bounce=1)
+    engine.trace(rays, WH, 0, FAR, W, H)
+    nb = engine.enqueue_bounce(rays, WH, 0, FAR, W, H, frames=frames, max_bounce=1)
+    assert nb > 0.9 * WH
+    rays["hits"][:WH] = 0xA5A5A5A5
+    rays["hits"][WH:WH + nb] = 0xA5A5A5A5
+    colors = np.zeros(WH, tthip.COL_DTYPE)
+    colors["Data"][:, 3] = 1.0
+    rg, rc = rays.copy(), rays.copy()
+    ig0, ic0, ig1, ic1 = (np.full((WH, 4), 0xA5A5A5A5, np.uint32) for _ in range(4))
+    s0 = engine.trace(rg, WH, 0, FAR, W, H, info=ig0)  # stats=False: the non-stats kernel
+    s1 = engine.trace(rg, nb, 1, FAR, W, H, info=ig1, colors=colors)
+    assert s0.node_visits == 0 and s1.node_visits == 0  # no counters: not the STATS instantiation
+    assert O.trace(sponza, rc, WH, 0, FAR, W, H, info=ic0, nthreads=CPU_THREADS)[0] == 0
+    assert O.trace(sponza, rc, nb, 1, FAR, W, H, info=ic1, colors=colors, nthreads=CPU_THREADS)[0] == 0
+    assert_same(rg, rc, ig0, ic0, 0, WH)
+    assert_same(rg, rc, ig1, ic1, WH, nb)
+    # a record neither side writes (the Reps bound) keeps the poison on both; nearly every ray gets one
+    assert int(np.all(rg["hits"][:WH] == 0xA5A5A5A5, axis=1).sum()) < 16
+
+
 def test_sponza_4k_properties(engine, sponza):
     """At C5's ray count (3840x2160): determinism (two launches give identical bytes) and a
     strided 1/64 sample against the oracle."""

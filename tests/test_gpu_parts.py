@@ -195,9 +195,11 @@ def test_shared_scene_mutations_are_ordered_without_host_sync():
     finally:
         ref.close()
 
-    st_a, st_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    lender = tthip.Engine(0, stream=st_a.cuda_stream)
-    borrower = tthip.Engine(0, stream=st_b.cuda_stream)
+    # streams on HW queues of their own: two pool streams may share one queue, which would run the calls in
+    # submission order whatever the library's events say, and let the test pass without them
+    owned = [tthip.DedicatedStream(torch, dev) for _ in range(2)]
+    lender = tthip.Engine(0, stream=owned[0].stream.cuda_stream)
+    borrower = tthip.Engine(0, stream=owned[1].stream.cuda_stream)
 
     def busy(e, k=12):
         for _ in range(k):
@@ -234,6 +236,8 @@ def test_shared_scene_mutations_are_ordered_without_host_sync():
             assert torch.equal(r3.view(-1, 48)[: W * H, 32:48], exp["a"]), ("after both", rep)
     finally:
         lender.close()
+        for d in owned:
+            d.close()
     assert borrower.h is None
 
 

@@ -16,7 +16,9 @@
 #              (tools/profile_round.sh -> traffic JSON; profiles/traffic_latest.json is fed from it)
 #   pmcu       the PMC unit passes behind roofline (tools/pmc_units.sh -> profiles/units_latest.json)
 #   diag       per-block execution counts (TT_DIAG_BLOCKS build, tools/diag_blocks.py)
-#   replay     strong-scaling replay of every rank's N-GPU shard on this GPU (tools/strong_replay.py)
+#   replay     strong-scaling replay of every rank's N-GPU shard on this GPU (tools/strong_replay.py; REPLAY_ARGS)
+#   replaykt   the same replay under rocprofv3 --kernel-trace (REPLAY_ARGS; per-rank launch overlap)
+#   lifecycle  the GPU tests of stream teardown, root-leaf bookkeeping and the timed kernels' jittered parity
 #   gloo2      the 2-rank bench rehearsal on this GPU (gloo collectives, C5 tiles included)
 #   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
@@ -69,6 +71,12 @@ for stage in "$@"; do
     diag) run diag 200 env TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_diag.so \
               python -u tools/diag_blocks.py c2 || exit $? ;;
     replay) run replay 900 python -u tools/strong_replay.py --configs c2,c5 ${REPLAY_ARGS:-} || exit $? ;;
+    replaykt) export TMPDIR=/tmp
+              run replaykt 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/kt" -o kt -- \
+                  python -u tools/strong_replay.py --configs c2 ${REPLAY_ARGS:---ns 8 --layouts 1x6} || exit $? ;;
+    lifecycle) run lifecycle 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+                   tests/test_gpu_lifecycle.py "tests/test_gpu_parity.py::test_sponza_1080p_jittered_frames_through_the_timed_kernels" \
+                   -m gpu || exit $? ;;
     longray) run longray 300 python -u tools/long_ray_chain.py || exit $? ;;
     c4loc) export TMPDIR=/tmp
            for v in ${AB_LIBS:-cur n128}; do  # C4 one-launch time + L2 hit / miss and fabric reads per variant

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -15,6 +16,10 @@
 #include "tt_refit.h"
 
 #define TT_RING 256u
+// Overlay regions behind a scene's nodes (tt_ctx_share_blas): this many frame-slot TLASes per lender
+#ifndef TT_TLAS_SLOTS
+#define TT_TLAS_SLOTS 8u
+#endif
 
 hipError_t tt_launch_trace(const TraceArgs& a, bool stats, bool matcheck, int info, uint32_t grid, hipStream_t st);
 uint32_t tt_trace_chunk_rays();
@@ -196,12 +201,28 @@ struct tt_ctx {
     // tt_ctx_share_scene: a borrower traces its lender's scene buffers (read-only) on its own stream
     tt_ctx* lender = nullptr;  // set on a borrower
     int borrowers = 0;         // on a lender: contexts currently tracing its scene
+    // node array sizes: the scene's nodes, and the device array (+ TT_TLAS_SLOTS overlay regions of
+    // tlas_res nodes each behind them, tt_ctx_share_blas)
+    uint32_t n_nodes_scene = 0, n_nodes_dev = 0, tlas_res = 0;
+    // tt_ctx_share_blas: a borrower with a TLAS of its own (a frame slot's TLAS refit and _MeshData rewrite
+    // never wait for, or are seen by, the other slots): its TLAS nodes [0, n_tlas_own) live in overlay region
+    // ovl_slot of the lender's node array, at kernel node index tlas_base; TLASBVH8Indices, _MeshData and the
+    // derived MeshGpu / LeafMesh records are its own buffers. host.nodes then holds only those TLAS nodes.
+    bool ovl = false;
+    uint32_t ovl_slot = 0, tlas_base = 0, n_tlas_own = 0;
+    uint32_t ovl_used = 0;     // lender: overlay regions in use (bit per slot)
     // Cross-stream order of a shared scene (the reference rewrites the TLAS and _MeshData every frame,
     // then dispatches, AssetManager.cs:1821-1825): a lender mutation waits for the borrowers' launches
-    // already enqueued, and a borrower launch waits for the lender's mutations already enqueued.
+    // already enqueued, and a borrower launch waits for the lender's mutations already enqueued. An
+    // overlay borrower reads only the lender's BLAS part, so it orders only against BLAS-side mutations.
+    // The lender's share state below (and its host node 0, which plain borrowers read for TT_ROOT_LEAF) is
+    // guarded by `mu`, so a lender and its borrowers may be driven from different host threads.
+    std::mutex mu;
     std::vector<tt_ctx*> borrower_list;  // lender: the contexts tracing its scene
     hipEvent_t ev_scene = nullptr;       // lender: after its last scene mutation (recorded while borrowed)
     uint64_t scene_mut = 0;              // lender: mutations recorded in ev_scene so far
+    hipEvent_t ev_blas = nullptr;        // lender: after its last BLAS-side mutation (overlay borrowers wait)
+    uint64_t blas_mut = 0;               // lender: BLAS-side mutations recorded in ev_blas so far
     hipEvent_t ev_read = nullptr;        // borrower: after its last launch that reads the shared scene
     uint64_t read_seq = 0;               // borrower: reads recorded in ev_read so far
     uint64_t read_waited = 0;            // borrower: reads the lender's stream already waits for
@@ -209,10 +230,15 @@ struct tt_ctx {
 };
 
 // Scene-mutating calls are refused on a borrower (update the lender), and reallocating ones on a
-// lender that has borrowers (their pointers would dangle).
+// lender that has borrowers (their pointers would dangle). TT_REFUSE_BORROWER_TLAS lets an overlay
+// borrower (tt_ctx_share_blas) mutate its own TLAS-side state.
 #define TT_REFUSE_BORROWER(c)                                                                              \
     do {                                                                                                   \
         if ((c)->lender) return fail((c), TT_ERR_INVALID_ARG, "this context traces a shared scene: update the context it shares from"); \
+    } while (0)
+#define TT_REFUSE_BORROWER_TLAS(c)                                                                         \
+    do {                                                                                                   \
+        if ((c)->lender && !(c)->ovl) return fail((c), TT_ERR_INVALID_ARG, "this context traces a shared scene: update the context it shares from"); \
     } while (0)
 #define TT_REFUSE_LENDER(c)                                                                                \
     do {                                                                                                   \
@@ -240,33 +266,47 @@ static hipError_t lazy_event(hipEvent_t& ev) {
     return ev ? hipSuccess : hipEventCreateWithFlags(&ev, hipEventDisableTiming);
 }
 static hipError_t scene_read_begin(tt_ctx* c) {
-    const tt_ctx* L = c->lender;
-    if (!L || L->scene_mut == c->mut_waited) return hipSuccess;
-    const hipError_t e = hipStreamWaitEvent(c->stream, L->ev_scene, 0);
-    if (e == hipSuccess) c->mut_waited = L->scene_mut;
+    tt_ctx* L = c->lender;
+    if (!L) return hipSuccess;
+    std::lock_guard<std::mutex> lk(L->mu);
+    const uint64_t seq = c->ovl ? L->blas_mut : L->scene_mut;
+    if (seq == c->mut_waited) return hipSuccess;
+    const hipError_t e = hipStreamWaitEvent(c->stream, c->ovl ? L->ev_blas : L->ev_scene, 0);
+    if (e == hipSuccess) c->mut_waited = seq;
     return e;
 }
 static hipError_t scene_read_end(tt_ctx* c) {
-    if (!c->lender) return hipSuccess;
+    tt_ctx* L = c->lender;
+    if (!L) return hipSuccess;
+    std::lock_guard<std::mutex> lk(L->mu);
     hipError_t e = lazy_event(c->ev_read);
     if (e == hipSuccess) e = hipEventRecord(c->ev_read, c->stream);
     if (e == hipSuccess) c->read_seq++;
     return e;
 }
-static hipError_t scene_write_begin(tt_ctx* c) {
+// blas: the mutation touches what overlay borrowers read too (BLAS nodes, triangles); otherwise only the
+// lender's TLAS-side state (TLAS nodes, _MeshData), which only plain borrowers read.
+static hipError_t scene_write_begin(tt_ctx* c, bool blas) {
+    std::lock_guard<std::mutex> lk(c->mu);
     for (tt_ctx* b : c->borrower_list) {
-        if (b->read_seq == b->read_waited) continue;
+        if (b->read_seq == b->read_waited || (b->ovl && !blas)) continue;
         const hipError_t e = hipStreamWaitEvent(c->stream, b->ev_read, 0);
         if (e != hipSuccess) return e;
         b->read_waited = b->read_seq;
     }
     return hipSuccess;
 }
-static hipError_t scene_write_end(tt_ctx* c) {
+static hipError_t scene_write_end(tt_ctx* c, bool blas) {
+    std::lock_guard<std::mutex> lk(c->mu);
     if (c->borrower_list.empty()) return hipSuccess;  // a later borrower syncs the stream when it shares
     hipError_t e = lazy_event(c->ev_scene);
     if (e == hipSuccess) e = hipEventRecord(c->ev_scene, c->stream);
     if (e == hipSuccess) c->scene_mut++;
+    if (e == hipSuccess && blas) {
+        e = lazy_event(c->ev_blas);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_blas, c->stream);
+        if (e == hipSuccess) c->blas_mut++;
+    }
     return e;
 }
 // The node array the kernels read: the reference's (80-B stride) or its strided copy, refreshed on the
@@ -282,9 +322,13 @@ static hipError_t refresh_node_copy(tt_ctx* c, uint32_t first, uint32_t count) {
 static void unlink_borrower(tt_ctx* b) {
     tt_ctx* L = b->lender;
     if (!L) return;
+    std::lock_guard<std::mutex> lk(L->mu);
     L->borrowers--;
     L->borrower_list.erase(std::remove(L->borrower_list.begin(), L->borrower_list.end(), b), L->borrower_list.end());
+    if (b->ovl) L->ovl_used &= ~(1u << b->ovl_slot);
     b->lender = nullptr;
+    b->ovl = false;
+    b->tlas_base = 0;
 }
 
 namespace {
@@ -316,10 +360,24 @@ tt_status hip_fail(tt_ctx* c, hipError_t e, const char* what) {
 // and mesh record must be in range, so the GPU kernel needs no per-access bounds checks.
 struct Validator {
     const SceneHost& s;
+    // the nodes a walk reads: TLAS-level walks tl[0, n_tl), BLAS-level walks bl[0, n_bl). A context's own
+    // scene: both are its host.nodes. An overlay borrower (tt_ctx_share_blas): its TLAS copy, and the lender's
+    // nodes and material words, exactly as its kernels address them (TLAS at tlas_base, BLASes shared).
+    const tt_cwbvh_node* tl;
+    uint32_t n_tl;
+    const tt_cwbvh_node* bl;
+    uint32_t n_bl;
+    const std::vector<uint32_t>* matdat;
     std::vector<uint32_t> epoch_of;
     uint32_t epoch = 0;
     std::string why;
-    explicit Validator(const SceneHost& h) : s(h), epoch_of(h.nodes.size(), 0u) {}
+    explicit Validator(const SceneHost& h)
+        : s(h), tl(h.nodes.data()), n_tl((uint32_t)h.nodes.size()), bl(h.nodes.data()), n_bl((uint32_t)h.nodes.size()),
+          matdat(&h.matdat), epoch_of(h.nodes.size(), 0u) {}
+    Validator(const SceneHost& own, const SceneHost& blas)
+        : s(own), tl(own.nodes.data()), n_tl((uint32_t)own.nodes.size()), bl(blas.nodes.data()),
+          n_bl((uint32_t)blas.nodes.size()), matdat(&blas.matdat),
+          epoch_of(std::max(own.nodes.size(), blas.nodes.size()), 0u) {}
 
     uint32_t max_matdat = 0;
     std::vector<uint32_t> tlas_visit;  // nodes reached by the last TLAS-level walk
@@ -333,15 +391,16 @@ struct Validator {
         while (!work.empty()) {
             const uint32_t ni = work.back();
             work.pop_back();
-            if (ni >= s.nodes.size()) {
-                why = "node index " + std::to_string(ni) + " out of range";
+            if (ni >= (tlas_level ? n_tl : n_bl)) {
+                why = "node index " + std::to_string(ni) + " out of range" +
+                      (tlas_level && tl != bl ? " of the context's own TLAS nodes" : "");
                 return false;
             }
             if (epoch_of[ni] == epoch) continue;
             epoch_of[ni] = epoch;
             if (tlas_level) tlas_visit.push_back(ni);
             else blas_visit.push_back(ni);
-            const tt_cwbvh_node& n = s.nodes[ni];
+            const tt_cwbvh_node& n = tlas_level ? tl[ni] : bl[ni];
             const uint32_t imask = n.e_imask >> 24;
             for (int k = 0; k < 8; k++) {
                 const uint32_t meta = (n.meta[k >> 2] >> ((k & 3) * 8)) & 0xffu;
@@ -377,8 +436,8 @@ struct Validator {
                         } else if (t >= s.n_tris) {
                             why = "triangle index out of range";
                             return false;
-                        } else if (!s.matdat.empty()) {
-                            max_matdat = std::max(max_matdat, s.matdat[(size_t)t]);
+                        } else if (!matdat->empty()) {
+                            max_matdat = std::max(max_matdat, (*matdat)[(size_t)t]);
                         }
                     }
                 }
@@ -398,7 +457,7 @@ struct Validator {
     }
 
     bool run() {
-        if (s.nodes.empty() || s.mesh.empty()) {
+        if (n_tl == 0 || n_bl == 0 || s.mesh.empty()) {
             why = "empty scene";
             return false;
         }
@@ -597,6 +656,42 @@ int32_t tt_device_count(void) {
 
 const char* tt_last_error(const tt_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+}  // extern "C"
+
+// Streams made by tt_stream_create that the caller has not destroyed yet. A queue created with a CU mask
+// that is still alive when the HIP runtime's own static destructors run takes the process down in
+// __cxa_finalize (SIGSEGV, gpurun_out/qmap.out under rocprofv3), so the library destroys what is left
+// from an exit handler. It is registered after the first stream is made -- after the HIP runtime has
+// initialised and registered its own destructors -- and exit handlers run in reverse order of
+// registration, so it runs before the runtime tears down. A host that destroys its streams (or a
+// Unity domain reload that misses StreamDestroy) is covered either way.
+namespace {
+std::mutex g_streams_mu;
+std::vector<std::pair<int, hipStream_t>> g_streams;
+bool g_streams_handler = false;
+
+void release_live_streams() {
+    std::vector<std::pair<int, hipStream_t>> live;
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        live.swap(g_streams);
+    }
+    for (auto& ds : live) {
+        if (hipSetDevice(ds.first) != hipSuccess) continue;
+        (void)hipStreamSynchronize(ds.second);
+        (void)hipStreamDestroy(ds.second);
+    }
+    (void)hipGetLastError();
+}
+}  // namespace
+
+extern "C" {
+
+uint32_t tt_stream_live_count(void) {
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    return (uint32_t)g_streams.size();
+}
+
 tt_status tt_stream_create(int32_t device, void** stream) {
     if (!stream) return TT_ERR_INVALID_ARG;
     *stream = nullptr;
@@ -622,13 +717,25 @@ tt_status tt_stream_create(int32_t device, void** stream) {
         }
     }
     (void)hipSetDevice(prev);  // the caller's current device is left as it was
-    if (st == TT_OK) *stream = s;
+    if (st == TT_OK) {
+        *stream = s;
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        g_streams.emplace_back(device, s);
+        if (!g_streams_handler) g_streams_handler = std::atexit(release_live_streams) == 0;
+    }
     return st;
 }
 
 tt_status tt_stream_destroy(void* stream) {
     if (!stream) return TT_ERR_INVALID_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        auto it = std::find_if(g_streams.begin(), g_streams.end(),
+                               [s](const std::pair<int, hipStream_t>& ds) { return ds.second == s; });
+        if (it == g_streams.end()) return TT_ERR_INVALID_ARG;  // not ours, or destroyed already
+        g_streams.erase(it);
+    }
     const hipError_t a = hipStreamSynchronize(s);
     const hipError_t b = hipStreamDestroy(s);
     return (a == hipSuccess && b == hipSuccess) ? TT_OK : TT_ERR_HIP;
@@ -737,6 +844,7 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     unlink_borrower(c);
     if (c->ev_scene) (void)hipEventDestroy(c->ev_scene);
+    if (c->ev_blas) (void)hipEventDestroy(c->ev_blas);
     if (c->ev_read) (void)hipEventDestroy(c->ev_read);
     c->nodes.release();
     c->nodes_k.release();
@@ -888,8 +996,16 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->mat_tag.release();
     c->mat_cut.release();
     c->mat_glass.release();
+    // the TLAS region (every node the TLAS-level walk reaches lies in [0, tlas_res)) and TT_TLAS_SLOTS overlay
+    // regions of that size behind the scene's nodes, for frame slots with TLASes of their own
+    uint32_t tlas_res = 0;
+    for (uint32_t n : h.tlas_nodes) tlas_res = std::max(tlas_res, n + 1u);
+    if (TT_NODE_STRIDE != 80 ||
+        ((uint64_t)n_nodes + (uint64_t)TT_TLAS_SLOTS * tlas_res) * sizeof(tt_cwbvh_node) >= (1ull << 32))
+        tlas_res = 0;  // no overlay regions (the strided-copy knob, or a node array near the 32-bit limit)
+    const uint32_t n_nodes_dev = n_nodes + TT_TLAS_SLOTS * tlas_res;
     hipError_t e;
-    if ((e = c->nodes.alloc(n_nodes)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
+    if ((e = c->nodes.alloc(n_nodes_dev)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
         (e = c->tris.alloc(n_tris)) != hipSuccess || (e = c->tlas.alloc(n_tlas)) != hipSuccess ||
         (e = c->mesh_raw.alloc(n_mesh)) != hipSuccess || (e = c->mesh.alloc(n_mesh)) != hipSuccess ||
         (e = c->mat_tag.alloc(tags.size())) != hipSuccess)
@@ -917,6 +1033,10 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
         TT_HIP(c, hipMemcpy(c->mat_glass.p, h.glass.data(), sizeof(GlassMat) * h.glass.size(), hipMemcpyHostToDevice));
     }
     c->host = std::move(h);
+    c->n_nodes_scene = n_nodes;
+    c->n_nodes_dev = n_nodes_dev;
+    c->tlas_res = tlas_res;
+    c->ovl_used = 0;
     c->root_known = true;
     c->any_invisible = any_invisible;
     c->scene_gen++;
@@ -964,11 +1084,25 @@ tt_status tt_scene_upload_texture_atlas(tt_ctx* c, const uint16_t* rgba_half, ui
     return TT_OK;
 }
 
-// Traces on `dst` read `src`'s scene buffers (nodes, triangles, TLAS, mesh and leaf records, materials,
-// atlases) instead of a copy: two contexts tracing concurrently (the two-part layout) then share one
-// cache footprint. The borrowed buffers are read-only for `dst`.
-tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
-    if (!dst || !src) return TT_ERR_INVALID_ARG;
+}  // extern "C"
+
+namespace {
+// The host mirror a borrower keeps of its lender's scene: scalars and material records, never the node array
+// or the validation bookkeeping (an overlay borrower adds its own TLAS-side arrays, tt_ctx_share_blas)
+void copy_host_light(SceneHost& d, const SceneHost& s) {
+    d = SceneHost{};
+    d.n_tris = s.n_tris;
+    d.n_mat = s.n_mat;
+    d.any_shadow_skip = s.any_shadow_skip;
+    d.any_atlas_shadow = s.any_atlas_shadow;
+    d.any_cutout = s.any_cutout;
+    d.cut = s.cut;
+    d.glass = s.glass;
+}
+
+// Checks shared by tt_ctx_share_scene / tt_ctx_share_blas; then dst's previous scene ties are cut and the
+// lender's read-only buffers borrowed (everything but the TLAS-side buffers an overlay owns).
+tt_status share_begin(tt_ctx* dst, tt_ctx* src) {
     if (dst == src) return fail(dst, TT_ERR_INVALID_ARG, "a context cannot share its own scene");
     if (!src->has_scene) return fail(dst, TT_ERR_NO_SCENE, "the source context has no scene");
     if (src->lender) return fail(dst, TT_ERR_INVALID_ARG, "the source context shares another context's scene");
@@ -976,16 +1110,12 @@ tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
     if (dst->device != src->device) return fail(dst, TT_ERR_INVALID_ARG, "the contexts are on different devices");
     TT_HIP(dst, hipSetDevice(dst->device));
     TT_HIP(dst, hipStreamSynchronize(dst->stream));  // nothing of dst's still reads its old scene
-    TT_HIP(dst, hipStreamSynchronize(src->stream));  // src's upload has landed
+    TT_HIP(dst, hipStreamSynchronize(src->stream));  // src's upload / updates have landed
     unlink_borrower(dst);
     dst->nodes.borrow(src->nodes);
     dst->nodes_k.borrow(src->nodes_k);
     dst->tris_raw.borrow(src->tris_raw);
     dst->tris.borrow(src->tris);
-    dst->tlas.borrow(src->tlas);
-    dst->mesh_raw.borrow(src->mesh_raw);
-    dst->mesh.borrow(src->mesh);
-    dst->leaf.borrow(src->leaf);
     dst->mat_tag.borrow(src->mat_tag);
     dst->mat_cut.borrow(src->mat_cut);
     dst->mat_glass.borrow(src->mat_glass);
@@ -995,25 +1125,126 @@ tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
     dst->tex_h = src->tex_h;
     dst->atlas_w = src->atlas_w;
     dst->atlas_h = src->atlas_h;
-    dst->host = src->host;
     dst->any_invisible = src->any_invisible;
     dst->any_shadow_skip = src->any_shadow_skip;
     dst->any_atlas_shadow = src->any_atlas_shadow;
     dst->any_cutout = src->any_cutout;
+    dst->n_nodes_scene = src->n_nodes_scene;
+    dst->n_nodes_dev = src->n_nodes_dev;
+    dst->tlas_res = 0;  // a borrower never lends
+    dst->ovl = false;
+    dst->tlas_base = 0;
+    dst->n_tlas_own = 0;
+    dst->root_known = false;
+    return TT_OK;
+}
+
+void share_link(tt_ctx* dst, tt_ctx* src) {
+    std::lock_guard<std::mutex> lk(src->mu);
     dst->has_scene = true;
     dst->scene_gen++;
     dst->lender = src;
     src->borrowers++;
     src->borrower_list.push_back(dst);
-    dst->mut_waited = src->scene_mut;  // everything src enqueued so far has landed (synchronized above)
+    if (dst->ovl) src->ovl_used |= 1u << dst->ovl_slot;
+    dst->mut_waited = dst->ovl ? src->blas_mut : src->scene_mut;  // src's stream was synchronized above
     dst->read_waited = dst->read_seq;
+}
+}  // namespace
+
+extern "C" {
+
+// Traces on `dst` read `src`'s scene buffers (nodes, triangles, TLAS, mesh and leaf records, materials,
+// atlases) instead of a copy: two contexts tracing concurrently (the two-part layout) then share one
+// cache footprint. The borrowed buffers are read-only for `dst`.
+tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
+    if (!dst || !src) return TT_ERR_INVALID_ARG;
+    const tt_status st = share_begin(dst, src);
+    if (st != TT_OK) return st;
+    dst->tlas.borrow(src->tlas);
+    dst->mesh_raw.borrow(src->mesh_raw);
+    dst->mesh.borrow(src->mesh);
+    dst->leaf.borrow(src->leaf);
+    copy_host_light(dst->host, src->host);
+    share_link(dst, src);
+    return TT_OK;
+}
+
+// A frame slot's own TLAS over `src`'s BLASes (include/truetrace_hip.h). The TLAS nodes [0, n_tlas_nodes) are
+// copied from src's device array into a free overlay region behind the scene's nodes, TLASBVH8Indices and
+// _MeshData (+ MeshGpu, LeafMesh) into buffers of dst's own; the kernels address the copy through
+// TraceArgs::tlas_base (the TLAS-level NodeOffset), so the BLAS nodes and triangles stay one shared copy.
+tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
+    if (!dst || !src) return TT_ERR_INVALID_ARG;
+    if (src->has_scene && !src->lender && src->tlas_res == 0)
+        return fail(dst, TT_ERR_UNSUPPORTED, "the source scene has no overlay regions (TT_NODE_STRIDE != 80, or a node "
+                                             "array near the 32-bit offset limit)");
+    if (src->has_scene && !src->lender && (n_tlas_nodes == 0 || n_tlas_nodes > src->tlas_res))
+        return fail(dst, TT_ERR_INVALID_ARG, "tt_ctx_share_blas: n_tlas_nodes %u outside (0, %u] (the TLAS region)",
+                    n_tlas_nodes, src->tlas_res);
+    uint32_t slot = TT_TLAS_SLOTS;
+    if (src->has_scene && !src->lender) {
+        std::lock_guard<std::mutex> lk(src->mu);
+        for (uint32_t k = 0; k < TT_TLAS_SLOTS; k++)
+            if (!((src->ovl_used >> k) & 1u)) {
+                slot = k;
+                break;
+            }
+    }
+    const bool same_slot = dst->ovl && dst->lender == src;  // a re-share keeps its region
+    if (same_slot) slot = dst->ovl_slot;
+    if (slot == TT_TLAS_SLOTS && src->has_scene && !src->lender)
+        return fail(dst, TT_ERR_UNSUPPORTED, "all %u overlay regions of the source scene are in use", TT_TLAS_SLOTS);
+    const tt_status st = share_begin(dst, src);
+    if (st != TT_OK) return st;
+    // the TLAS-side state, as the device holds it now (a device TLAS refit leaves src's host copy stale)
+    SceneHost& h = dst->host;
+    {
+        std::lock_guard<std::mutex> lk(src->mu);
+        copy_host_light(h, src->host);
+        h.tlas = src->host.tlas;
+        h.mesh = src->host.mesh;
+        h.blas_ok = src->host.blas_ok;
+    }
+    h.nodes.resize(n_tlas_nodes);
+    TT_HIP(dst, hipMemcpy(h.nodes.data(), src->nodes.p, sizeof(tt_cwbvh_node) * n_tlas_nodes, hipMemcpyDeviceToHost));
+    {
+        std::lock_guard<std::mutex> lk(src->mu);
+        Validator v(h, src->host);
+        if (!v.walk(0, 0, 0, true))
+            return fail(dst, TT_ERR_INVALID_ARG, "tt_ctx_share_blas: the TLAS leaves [0, %u): %s", n_tlas_nodes, v.why.c_str());
+        h.is_tlas_node.assign(n_tlas_nodes, 0u);
+        h.tlas_nodes = v.tlas_visit;
+        for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
+    }
+    const uint32_t n_tlas = (uint32_t)h.tlas.size(), n_mesh = (uint32_t)h.mesh.size();
+    hipError_t e;
+    if ((e = dst->tlas.alloc(n_tlas)) != hipSuccess || (e = dst->mesh_raw.alloc(n_mesh)) != hipSuccess ||
+        (e = dst->mesh.alloc(n_mesh)) != hipSuccess || (e = dst->leaf.alloc(src->leaf.n)) != hipSuccess)
+        return hip_fail(dst, e, "overlay TLAS-side buffers");
+    dst->ovl = true;
+    dst->ovl_slot = slot;
+    dst->n_tlas_own = n_tlas_nodes;
+    dst->tlas_base = src->n_nodes_scene + slot * src->tlas_res;
+    TT_HIP(dst, hipMemcpyAsync(dst->nodes.p + dst->tlas_base, src->nodes.p, sizeof(tt_cwbvh_node) * n_tlas_nodes,
+                               hipMemcpyDeviceToDevice, dst->stream));
+    TT_HIP(dst, hipMemcpyAsync(dst->tlas.p, src->tlas.p, sizeof(int32_t) * n_tlas, hipMemcpyDeviceToDevice, dst->stream));
+    TT_HIP(dst, hipMemcpyAsync(dst->mesh_raw.p, src->mesh_raw.p, sizeof(tt_mesh_data) * n_mesh, hipMemcpyDeviceToDevice,
+                               dst->stream));
+    TT_HIP(dst, hipMemcpyAsync(dst->mesh.p, src->mesh.p, sizeof(MeshGpu) * n_mesh, hipMemcpyDeviceToDevice, dst->stream));
+    TT_HIP(dst, hipMemcpyAsync(dst->leaf.p, src->leaf.p, sizeof(LeafMesh) * src->leaf.n, hipMemcpyDeviceToDevice,
+                               dst->stream));
+    TT_HIP(dst, hipStreamSynchronize(dst->stream));
+    dst->root_known = true;  // its host TLAS copy is what the device holds
+    share_link(dst, src);
     return TT_OK;
 }
 
 tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh, uint32_t flags) {
     if (!c) return TT_ERR_INVALID_ARG;
-    TT_REFUSE_BORROWER(c);
+    TT_REFUSE_BORROWER_TLAS(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
+    // (an overlay borrower's host.nodes are its own TLAS nodes: it refits those, in its overlay region)
     if (!mesh_aabbs || n_tlas_nodes == 0 || n_tlas_nodes > c->host.nodes.size())
         return fail(c, TT_ERR_INVALID_ARG, "tt_tlas_refit: null boxes or n_tlas_nodes out of range");
     if (n_mesh < c->host.mesh.size())
@@ -1037,13 +1268,16 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
         d_boxes = c->st_boxes.p;
     }
     uint32_t slot;
-    TT_HIP(c, scene_write_begin(c));
+    if (!c->ovl) TT_HIP(c, scene_write_begin(c, false));  // (an overlay's TLAS is read by nobody else)
     TT_HIP(c, ring_open(c, slot));
-    TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p, c->stream));
+    TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p + c->tlas_base, c->stream));
     TT_HIP(c, refresh_node_copy(c, 0, n_tlas_nodes));
-    c->root_known = false;  // node 0 was rewritten on the device
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->root_known = false;  // node 0 was rewritten on the device
+    }
     TT_HIP(c, ring_close(c, slot));
-    TT_HIP(c, scene_write_end(c));
+    if (!c->ovl) TT_HIP(c, scene_write_end(c, false));
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1116,13 +1350,13 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     a.tris88 = c->tris_raw.p + tri_base;
     a.tripos = c->tris.p + tri_base;
     uint32_t slot;
-    TT_HIP(c, scene_write_begin(c));
+    TT_HIP(c, scene_write_begin(c, true));
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_blas_construct(a, c->stream));
     TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
     TT_HIP(c, refresh_node_copy(c, node_base, R.n_nodes));
     TT_HIP(c, ring_close(c, slot));
-    TT_HIP(c, scene_write_end(c));
+    TT_HIP(c, scene_write_end(c, true));
     if (!(p->flags & TT_TRACE_ASYNC) || !dev) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1142,11 +1376,18 @@ tt_status tt_scene_read_tris(tt_ctx* c, uint32_t first, uint32_t count, tt_cuda_
 tt_status tt_scene_read_nodes(tt_ctx* c, uint32_t first, uint32_t count, tt_cwbvh_node* out) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
-    if (!out || (uint64_t)first + count > c->host.nodes.size())
+    if (!out || (uint64_t)first + count > c->n_nodes_scene)
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_nodes: range out of bounds");
     TT_HIP(c, hipSetDevice(c->device));
     TT_HIP(c, scene_read_begin(c));
-    TT_HIP(c, hipMemcpyAsync(out, c->nodes.p + first, sizeof(tt_cwbvh_node) * count, hipMemcpyDeviceToHost, c->stream));
+    // the scene as this context traces it: an overlay borrower's TLAS nodes [0, n_tlas_own) from its region
+    const uint32_t own_end = c->ovl ? std::max(first, std::min(first + count, c->n_tlas_own)) : first;
+    if (own_end > first)
+        TT_HIP(c, hipMemcpyAsync(out, c->nodes.p + c->tlas_base + first, sizeof(tt_cwbvh_node) * (own_end - first),
+                                 hipMemcpyDeviceToHost, c->stream));
+    if (first + count > own_end)
+        TT_HIP(c, hipMemcpyAsync(out + (own_end - first), c->nodes.p + own_end,
+                                 sizeof(tt_cwbvh_node) * (first + count - own_end), hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1215,56 +1456,77 @@ tt_status refresh_leaves(tt_ctx* c) {
 
 tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {
     if (!c) return TT_ERR_INVALID_ARG;
-    TT_REFUSE_BORROWER(c);
+    TT_REFUSE_BORROWER_TLAS(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!nodes || (uint64_t)first + count > c->host.nodes.size())
-        return fail(c, TT_ERR_INVALID_ARG, "node update range out of bounds");
+        return fail(c, TT_ERR_INVALID_ARG, c->ovl ? "node update range out of bounds: a frame-slot TLAS (tt_ctx_share_blas) "
+                                                    "rewrites only its own TLAS nodes"
+                                                  : "node update range out of bounds");
     if (count == 0) return TT_OK;
     SceneHost& h = c->host;
-    std::vector<tt_cwbvh_node> saved(h.nodes.begin() + first, h.nodes.begin() + first + count);
-    std::copy(nodes, nodes + count, h.nodes.begin() + first);
-    // A rewrite of TLAS-level nodes only (the per-frame case: BVH8AggregatedBuffer.SetData of the
-    // TLAS region) re-walks the TLAS level; the BLASes were validated at upload and are unchanged.
-    // Any other rewrite re-validates the whole scene.
-    // (a node that a validated BLAS also reaches -- a TLAS rewrite may have re-pointed a child into one
-    // -- takes the full check: its triangle indices matter at BLAS level)
-    bool tlas_only = true;
-    for (uint32_t i = first; i < first + count && tlas_only; i++)
-        tlas_only = h.is_tlas_node[i] != 0 && h.is_blas_node[i] == 0;
-    Validator v(h);
-    const bool ok = tlas_only ? v.walk(0, 0, 0, true) : v.run();
-    if (!ok) {
-        std::copy(saved.begin(), saved.end(), h.nodes.begin() + first);
-        return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after node update: %s", v.why.c_str());
-    }
-    if (tlas_only) {
-        for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 0u;
-        h.tlas_nodes = v.tlas_visit;
-        for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
-    } else {
-        remember_validation(h, v);
+    tt_ctx* L = c->ovl ? c->lender : nullptr;
+    bool tlas_only = true, blas_side = false;
+    {
+        std::lock_guard<std::mutex> lk(L ? L->mu : c->mu);  // the nodes the walks read; node 0 (TT_ROOT_LEAF)
+        std::vector<tt_cwbvh_node> saved(h.nodes.begin() + first, h.nodes.begin() + first + count);
+        std::copy(nodes, nodes + count, h.nodes.begin() + first);
+        // A rewrite of TLAS-level nodes only (the per-frame case: BVH8AggregatedBuffer.SetData of the
+        // TLAS region) re-walks the TLAS level; the BLASes were validated at upload and are unchanged.
+        // Any other rewrite re-validates the whole scene.
+        // (a node that a validated BLAS also reaches -- a TLAS rewrite may have re-pointed a child into one
+        // -- takes the full check: its triangle indices matter at BLAS level)
+        // blas_side: the rewrite touches what frame-slot TLASes read too (a BLAS node, or a node outside the
+        // TLAS region); on a frame slot every node of its range is its own TLAS region's
+        const std::vector<uint8_t>& blas_nodes = L ? L->host.is_blas_node : h.is_blas_node;
+        for (uint32_t i = first; i < first + count; i++) {
+            tlas_only = tlas_only && (L || h.is_tlas_node[i] != 0) && blas_nodes[i] == 0;
+            blas_side = blas_side || blas_nodes[i] != 0 || (!L && i >= c->tlas_res);
+        }
+        const char* refuse = nullptr;
+        if (!tlas_only && L) refuse = "a frame-slot TLAS (tt_ctx_share_blas) rewrites TLAS nodes only";
+        if (blas_side && !L && c->ovl_used)
+            refuse = "a BLAS-side node rewrite while frame-slot TLASes (tt_ctx_share_blas) share this scene";
+        if (refuse) {
+            std::copy(saved.begin(), saved.end(), h.nodes.begin() + first);
+            return fail(c, L ? TT_ERR_INVALID_ARG : TT_ERR_UNSUPPORTED, "%s", refuse);
+        }
+        Validator v = L ? Validator(h, L->host) : Validator(h);
+        const bool ok = tlas_only ? v.walk(0, 0, 0, true) : v.run();
+        if (!ok) {
+            std::copy(saved.begin(), saved.end(), h.nodes.begin() + first);
+            return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after node update: %s", v.why.c_str());
+        }
+        if (tlas_only) {
+            for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 0u;
+            h.tlas_nodes = v.tlas_visit;
+            for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
+        } else {
+            remember_validation(h, v);
+        }
+        if (first == 0) c->root_known = true;  // node 0 is the host's again
     }
     TT_HIP(c, hipSetDevice(c->device));
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, nodes, sizeof(tt_cwbvh_node) * count, pinned));
-    TT_HIP(c, scene_write_begin(c));
-    TT_HIP(c, hipMemcpyAsync(c->nodes.p + first, pinned, sizeof(tt_cwbvh_node) * count, hipMemcpyHostToDevice, c->stream));
+    if (!c->ovl) TT_HIP(c, scene_write_begin(c, blas_side));
+    TT_HIP(c, hipMemcpyAsync(c->nodes.p + c->tlas_base + first, pinned, sizeof(tt_cwbvh_node) * count,
+                             hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
     TT_HIP(c, refresh_node_copy(c, first, count));
-    TT_HIP(c, scene_write_end(c));
+    if (!c->ovl) TT_HIP(c, scene_write_end(c, blas_side));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
-    if (first == 0) c->root_known = true;  // node 0 is the host's again
     return TT_OK;
 }
 
 tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, const tt_mesh_data* md) {
     if (!c) return TT_ERR_INVALID_ARG;
-    TT_REFUSE_BORROWER(c);
+    TT_REFUSE_BORROWER_TLAS(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!md || (uint64_t)first + count > c->host.mesh.size())
         return fail(c, TT_ERR_INVALID_ARG, "meshdata update range out of bounds");
     if (count == 0) return TT_OK;
     SceneHost& h = c->host;
+    tt_ctx* L = c->ovl ? c->lender : nullptr;  // a frame-slot TLAS: its records, the lender's BLASes
     // Only records whose BLAS reference (root, NodeOffset, TriOffset) changed need a check, and only
     // against the BLASes validated so far; a BLAS never seen is walked once and remembered. The
     // per-frame transform update (MeshDataBuffer.SetData, AssetManager.cs:1825) changes none.
@@ -1282,11 +1544,15 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
         if (std::binary_search(h.blas_ok.begin(), h.blas_ok.end(), k) ||
             std::find(added.begin(), added.end(), k) != added.end())
             continue;
-        Validator v(h);
+        std::lock_guard<std::mutex> lk(L ? L->mu : c->mu);
+        Validator v = L ? Validator(h, L->host) : Validator(h);
         if (!v.walk_mesh(r))
             return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: %s", v.why.c_str());
         added.push_back(k);
-        for (uint32_t n : v.blas_visit) h.is_blas_node[n] = 1u;  // (kept even if a later record fails: conservative)
+        // (kept even if a later record fails: conservative; an overlay's BLASes are marked in the lender's
+        // bookkeeping, so a later lender rewrite of those nodes is refused while overlays exist)
+        std::vector<uint8_t>& blas_nodes = L ? L->host.is_blas_node : h.is_blas_node;
+        for (uint32_t n : v.blas_visit) blas_nodes[n] = 1u;
     }
     if (!added.empty()) {
         h.blas_ok.insert(h.blas_ok.end(), added.begin(), added.end());
@@ -1298,7 +1564,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     // (MeshGpu) and patches the TLAS leaf records that name an updated mesh, on the stream
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, md, sizeof(tt_mesh_data) * count, pinned));
-    TT_HIP(c, scene_write_begin(c));
+    if (!c->ovl) TT_HIP(c, scene_write_begin(c, false));  // (an overlay's records are read by nobody else)
     TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, pinned, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
     const uint32_t n_tlas = (uint32_t)h.tlas.size();
@@ -1306,7 +1572,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream, c->mesh_raw.p, c->mesh.p,
                        c->leaf.p, c->tlas.p, n_tlas, first, count);
     TT_HIP(c, hipGetLastError());
-    TT_HIP(c, scene_write_end(c));
+    if (!c->ovl) TT_HIP(c, scene_write_end(c, false));
     return TT_OK;
 }
 
@@ -1412,7 +1678,8 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     TraceArgs a;
     std::memset(&a, 0, sizeof(a));
     a.nodes = kernel_nodes(c);
-    a.n_nodes = (uint32_t)c->host.nodes.size();
+    a.n_nodes = c->n_nodes_dev;  // (the overlay regions included: a frame-slot TLAS lives there)
+    a.tlas_base = c->tlas_base;
     a.tris = c->tris.p;
     a.n_tris = c->host.n_tris;
     a.tlas = c->tlas.p;
@@ -1444,10 +1711,14 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     a.div_width = fastdiv_make(std::max(1u, p->screen_width));
     a.div_tiles = fastdiv_make(std::max(1u, p->screen_width >> 3));
     a.hits_out = reinterpret_cast<uint4*>(hits_out);
-    {  // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root, when the host knows the device's node 0
-        const tt_ctx* owner = c->lender ? c->lender : c;
-        if (owner->root_known && !owner->host.nodes.empty())
+    {  // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root, when the host knows the device's node 0 (the lender's,
+       // or a frame-slot TLAS's own)
+        tt_ctx* owner = (c->lender && !c->ovl) ? c->lender : c;
+        std::lock_guard<std::mutex> lk(owner->mu);
+        if (owner->root_known && !owner->host.nodes.empty()) {
             a.root = root_leaf_of(reinterpret_cast<const uint32_t*>(owner->host.nodes.data()));
+            a.root.base_child += c->tlas_base;
+        }
     }
 #ifdef TT_DIAG_BLOCKS  // diagnostic builds only: the block counters' device buffer (tools/diag_blocks.py)
     if (const char* dp = std::getenv("TT_DIAG_PTR"))
@@ -1655,7 +1926,8 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     ShadowArgs a;
     std::memset(&a, 0, sizeof(a));
     a.nodes = kernel_nodes(c);
-    a.n_nodes = (uint32_t)c->host.nodes.size();
+    a.n_nodes = c->n_nodes_dev;  // (the overlay regions included: a frame-slot TLAS lives there)
+    a.tlas_base = c->tlas_base;
     a.tris = c->tris.p;
     a.n_tris = c->host.n_tris;
     a.tlas = c->tlas.p;
@@ -1786,8 +2058,17 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
     float m[32];
     std::memcpy(m, cam->cam_to_world, 64);
     std::memcpy(m + 16, cam->cam_inv_proj, 64);
-    TT_HIP(c, hipMemcpyAsync(c->cam.p, m, sizeof(m), hipMemcpyHostToDevice, c->stream));
     const bool dev = (cam->flags & TT_TRACE_DEVICE_PTRS) != 0;
+    // TT_TRACE_ASYNC with device rays: the camera goes through the pinned staging slots, nothing waits
+    const bool async = dev && (cam->flags & TT_TRACE_ASYNC);
+    if (async) {
+        void* pinned = nullptr;
+        TT_HIP(c, stage_begin(c, m, sizeof(m), pinned));
+        TT_HIP(c, hipMemcpyAsync(c->cam.p, pinned, sizeof(m), hipMemcpyHostToDevice, c->stream));
+        TT_HIP(c, stage_end(c));
+    } else {
+        TT_HIP(c, hipMemcpyAsync(c->cam.p, m, sizeof(m), hipMemcpyHostToDevice, c->stream));
+    }
     tt_ray_data* d = rays;
     if (!dev) {
         if (c->st_rays.n < wh) TT_HIP(c, c->st_rays.alloc(wh));
@@ -1801,7 +2082,7 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
                                  cam->jitter, cam->frames_accumulated, cam->max_bounce, d, c->stream));
     TT_HIP(c, ring_close(c, slot));
     if (!dev) TT_HIP(c, hipMemcpyAsync(rays, d, sizeof(tt_ray_data) * wh, hipMemcpyDeviceToHost, c->stream));
-    TT_HIP(c, hipStreamSynchronize(c->stream));
+    if (!async) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
 

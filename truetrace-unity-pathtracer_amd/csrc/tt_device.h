@@ -208,6 +208,8 @@ struct TraceArgs {
     uint32_t* chunk_cost;        // per ray chunk: max Reps of its rays (atomicMax, rays with Reps >= TT_ORDER_MIN_REPS)
     uint4* hits_out;             // nullable (tt_trace_closest_hits): ray i's hit record also at hits_out[i]
     RootLeaf root;               // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root (root.ok = 0: the generic path)
+    uint32_t tlas_base;          // node index of the context's TLAS node 0: 0, or its frame-slot overlay region
+                                 // (tt_ctx_share_blas); the TLAS-level NodeOffset
 };
 
 // Adaptive-order builder (tt_order.hip): one block per scheduler segment sorts the segment's
@@ -246,6 +248,7 @@ struct ShadowArgs {
     uint32_t width, height;
     int32_t bounce;
     uint32_t flags;
+    uint32_t tlas_base;          // as TraceArgs::tlas_base
 };
 
 // The launch's ray count: the host value, or the device-resident count clamped to it (a wave-uniform

@@ -284,7 +284,7 @@ __device__ void shadow_wide_phase(const ShadowArgs& A, ShadowWide& st, uint2 (*s
         if (st.active && st.tg.y == 0u && (st.cg.y & 0xff000000u) == 0u) {
             if (stack_size != 0) {
                 if (stack_size == st.tlas_ss) {
-                    st.NodeOffset = 0;
+                    st.NodeOffset = (int32_t)A.tlas_base;
                     st.TriOffset = 0;
                     st.tlas_ss = -1;
                     st.ray = st.wray;
@@ -431,11 +431,11 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
                 ray.iz = rcp_rn(ray.dz);
                 wray = ray;
                 oct = octant_inv4(ray);
-                cg = make_uint2(0u, 0x80000000u);
+                cg = make_uint2(A.tlas_base, 0x80000000u);
                 tg = make_uint2(0u, 0u);
                 stack_size = 0;
                 tlas_ss = -1;
-                NodeOffset = 0;
+                NodeOffset = (int32_t)A.tlas_base;
                 TriOffset = 0;
                 MatOffset = 0;
                 Reps = 0;
@@ -533,7 +533,7 @@ __device__ __forceinline__ void shadow_body(const ShadowArgs& A) {
         if (tg.y == 0u && (cg.y & 0xff000000u) == 0u) {
             if (stack_size != 0) {
                 if (stack_size == tlas_ss) {
-                    NodeOffset = 0;
+                    NodeOffset = (int32_t)A.tlas_base;
                     TriOffset = 0;
                     tlas_ss = -1;
                     ray = wray;

@@ -374,11 +374,11 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 best.v = 0.0f;
                 best.mesh_id = 0;
                 best.tri_id = -1;
-                cg = make_uint2(0u, 0x80000000u);
+                cg = make_uint2(A.tlas_base, 0x80000000u);  // the TLAS root: node 0 of the context's TLAS
                 tg = make_uint2(0u, 0u);
                 stack_size = 0;
                 tlas_ss = -1;
-                NodeOffset = 0;
+                NodeOffset = (int32_t)A.tlas_base;  // TLAS level (0, or a frame-slot TLAS's region)
                 TriOffset = 0;
                 MatOffset = 0;
                 mesh_id = -1;
@@ -494,7 +494,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 TT_DB(11);
                 if (stack_size == tlas_ss) {
                     TT_DB(12);
-                    NodeOffset = 0;
+                    NodeOffset = (int32_t)A.tlas_base;
                     TriOffset = 0;
                     tlas_ss = -1;
                     ray = world_ray();

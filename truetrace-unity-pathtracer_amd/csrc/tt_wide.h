@@ -334,7 +334,7 @@ __device__ void wide_phase(const TraceArgs& A, WideState& st, uint2 (*s_stack)[T
         if (st.active && st.tg.y == 0u && (st.cg.y & 0xff000000u) == 0u) {
             if (stack_size != 0) {
                 if (stack_size == st.tlas_ss) {
-                    st.NodeOffset = 0;
+                    st.NodeOffset = (int32_t)A.tlas_base;
                     st.TriOffset = 0;
                     st.tlas_ss = -1;
                     st.ray = st.wray;

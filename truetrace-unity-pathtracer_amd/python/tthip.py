@@ -285,6 +285,8 @@ def hip_lib():
             L.tt_enqueue_diffuse_bounce_indirect.argtypes = [vp, C.POINTER(TraceParams), vp, vp, i32, i32, vp]
         if hasattr(L, "tt_ctx_share_scene"):
             L.tt_ctx_share_scene.argtypes = [vp, vp]
+        if hasattr(L, "tt_ctx_share_blas"):
+            L.tt_ctx_share_blas.argtypes = [vp, vp, u32]
         if hasattr(L, "tt_trace_closest_hits"):
             L.tt_trace_closest_hits.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
@@ -302,6 +304,8 @@ def hip_lib():
             L.tt_stream_create.restype = i32
             L.tt_stream_destroy.argtypes = [vp]
             L.tt_stream_destroy.restype = i32
+        if hasattr(L, "tt_stream_live_count"):
+            L.tt_stream_live_count.restype = u32
         L.tt_async_overflows.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.tt_ctx_stream.argtypes = [vp]
         L.tt_ctx_stream.restype = vp
@@ -725,6 +729,19 @@ class Engine:
             src._borrowers = []
         src._borrowers.append(weakref.ref(self))
 
+    def share_blas(self, src: "Engine", n_tlas_nodes: int):
+        """tt_ctx_share_blas: a frame slot over `src`'s scene -- src's BLASes and triangles (no copy) under a TLAS,
+        TLASBVH8Indices and _MeshData of this context's own (copied from src now), which tlas_refit /
+        update_meshdata / update_nodes on this context change without waiting for src or other slots."""
+        import weakref
+
+        self._check(self.L.tt_ctx_share_blas(self.h, src.h, int(n_tlas_nodes)), "tt_ctx_share_blas")
+        self._unlink_lender()
+        self._lender = src
+        if not hasattr(src, "_borrowers"):
+            src._borrowers = []
+        src._borrowers.append(weakref.ref(self))
+
     __del__ = close
 
     @property
@@ -902,13 +919,13 @@ class Engine:
         return out
 
     def generate(self, rays, cam_to_world, cam_inv_proj, width, height, near, far, jitter=0, frames=0,
-                 max_bounce=3, device=False):
+                 max_bounce=3, device=False, asynchronous=False):
         cam = Camera()
         cam.cam_to_world[:] = unity_colmajor(cam_to_world)
         cam.cam_inv_proj[:] = unity_colmajor(cam_inv_proj)
         cam.near_plane, cam.far_plane, cam.width, cam.height = near, far, width, height
         cam.jitter, cam.frames_accumulated, cam.max_bounce = jitter, frames, max_bounce
-        cam.flags = TT_TRACE_DEVICE_PTRS if device else 0
+        cam.flags = (TT_TRACE_DEVICE_PTRS if device else 0) | (TT_TRACE_ASYNC if (device and asynchronous) else 0)
         self._check(self.L.tt_generate_primary(self.h, C.byref(cam), _ptr(rays)), "tt_generate_primary")
 
     def enqueue_bounce(self, rays, n_rays, bounce, far_plane, width, height, frames=0, max_bounce=3,

@@ -9,7 +9,11 @@ tiles under tile sharding) as
   * F **frame slots**: frame k runs on slot k % F. Each slot has its own ray, _PrimaryTriangleInfo
     and hit-record buffers and its own streams, so frame k + 1's primary launches (which depend on
     nothing of frame k) run while frame k's bounce-1 launches drain. Inside a frame the order is the
-    reference's: a part's bounce-1 launch follows its primary launch on the same stream.
+    reference's: a part's bounce-1 launch follows its primary launch on the same stream. With
+    ``slot_stride`` s > 0 slot f traces sample k + f s wherever the plan names sample k, so the frames in
+    flight carry their own jitter, as a renderer's consecutive frames do (Generate's random(0,
+    pixel_index) depends on frames_accumulated, RayGenKernels.compute:45-46); s = 0 replicates one
+    sample in every slot.
 
 All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). Every stream the
 layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.dedicated_stream:
@@ -53,21 +57,28 @@ class FrameLayout:
     plan: per part, [(sample k, pixel indices)] -- the rays of sample k (``make_full(k)``: a W*H
     RayData buffer of that sample's Generate) at those pixels, back to back in the part's buffer.
     bounce: trace bounce 1 too (False: primary only, the C5 config).
-    lend: the engine whose scene every context traces (slot 0 / part 0 reuses it)."""
+    lend: the engine whose scene every context traces (slot 0 / part 0 reuses it, on lend's own stream).
+    slot_stride: slot f traces sample k + f * slot_stride where the plan names sample k (module docstring)."""
 
     def __init__(self, torch, tthip, lend, dev, W: int, H: int, far: float, plan, make_full: Callable,
-                 slots: int = 1, bounce: bool = True, info: bool = True, colors=None, frames: int = 0):
+                 slots: int = 1, bounce: bool = True, info: bool = True, colors=None, frames: int = 0,
+                 slot_stride: int = 0):
         self.torch, self.tthip, self.dev = torch, tthip, dev
         self.W, self.H, self.far = W, H, far
         self.P, self.F = len(plan), max(1, int(slots))
         self.bounce, self.colors, self.frames = bounce, colors, frames
+        self.stride = max(0, int(slot_stride))
+        self.plan = plan
         WH = W * H
         self.engines = []  # (engine, stream) per context, lend's first; contexts created here are closed by close()
         self.own = []
         self.n_streams = 0  # process-wide dedicated streams taken so far (tthip.dedicated_stream)
         self.pool_streams = os.environ.get("TT_LAYOUT_POOL_STREAMS", "0") == "1"
         self.slots: List[List[Part]] = []
-        base_stream = torch.cuda.current_stream(dev)
+        # slot 0 / part 0 issues on lend's own stream: the gather orders against p.stream, so it must be
+        # the stream lend's launches actually go to (not whatever stream torch has current)
+        cur = torch.cuda.current_stream(dev)
+        base_stream = cur if cur.cuda_stream == lend.stream else torch.cuda.ExternalStream(lend.stream, device=dev)
         self.info0 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if info else None for _ in range(self.F)]
         self.info1 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if (info and bounce) else None
                       for _ in range(self.F)]
@@ -88,14 +99,14 @@ class FrameLayout:
                 p.rays = torch.zeros(((WH + p.n) if bounce else max(p.n, 1)) * 48, dtype=torch.uint8, device=dev)
                 row.append(p)
             self.slots.append(row)
-        # fill the parts' primary rays, sample by sample
-        for k in sorted({k for lst in plan for k, _ in lst}):
+        # fill the parts' primary rays, sample by sample (slot f: the plan's sample k is sample k + f * stride)
+        for k in sorted({self.sample_of(f, kk) for f in range(self.F) for lst in plan for kk, _ in lst}):
             full = make_full(k)
-            for row in self.slots:
+            for f, row in enumerate(self.slots):
                 for p, lst in zip(row, plan):
                     o = 0
                     for kk, pix in lst:
-                        if kk == k and len(pix):
+                        if self.sample_of(f, kk) == k and len(pix):
                             p.rays.view(-1, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
                         o += len(pix)
             del full
@@ -104,8 +115,9 @@ class FrameLayout:
         for f, row in enumerate(self.slots):
             for p in row:
                 p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, stats=True)
-                if bounce:
-                    p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=frames, max_bounce=1, device=True)
+                if bounce:  # (the bounce direction's hash seed: the slot's sample, as Generate's)
+                    p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=self.sample_of(f, frames),
+                                                max_bounce=1, device=True)
                     p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=self.info1[f], colors=colors,
                                           device=True, stats=True)
                 p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
@@ -124,13 +136,29 @@ class FrameLayout:
         return st
 
     # ---------------------------------------------------------------- sizes
+    def sample_of(self, f: int, k: int) -> int:
+        """The sample slot f traces where the plan names sample k."""
+        return int(k) + int(f) * self.stride
+
     @property
     def parts(self) -> List[Part]:
-        """Slot 0's parts (every slot traces the same rays)."""
+        """Slot 0's parts (with slot_stride > 0 the other slots trace other samples: rays_in_frames)."""
         return self.slots[0]
 
     def rays_per_frame(self) -> int:
+        """Slot 0's rays per frame (primary + bounce 1)."""
         return int(sum(p.n + p.nb for p in self.parts))
+
+    def rays_of_slot(self, f: int) -> int:
+        return int(sum(p.n + p.nb for p in self.slots[f]))
+
+    def rays_in_frames(self, k0: int, k1: int) -> int:
+        """Rays traced by frames k0 .. k1 - 1 (frame k on slot k % F)."""
+        return int(sum(self.rays_of_slot(k % self.F) for k in range(k0, k1)))
+
+    def last_slot(self) -> int:
+        """The slot of the most recent frame."""
+        return (self.k - 1) % self.F
 
     def n_prim(self) -> int:
         return int(sum(p.n for p in self.parts))
@@ -218,6 +246,34 @@ class FrameLayout:
 
     def streams(self):
         return [p.stream for row in self.slots for p in row]
+
+    # ---------------------------------------------------------------- record checks (bench.py's oracle leg)
+    POISON = 0xA5
+
+    def poison_records(self):
+        """Fills every slot's hit records (RayData.hits of its primary and bounce-1 rays) and its
+        _PrimaryTriangleInfo buffers with the byte POISON, so that a record the following launches do not
+        write stays visible, and returns host copies of that state (snapshot())."""
+        WH = self.W * self.H
+        for f, row in enumerate(self.slots):
+            for p in row:
+                v = p.rays.view(-1, 48)
+                v[: p.n, 32:48] = self.POISON
+                if self.bounce and p.nb:
+                    v[WH: WH + p.nb, 32:48] = self.POISON
+            for b in (self.info0[f], self.info1[f]):
+                if b is not None:
+                    b.fill_(self.POISON)
+        self.torch.cuda.synchronize(self.dev)
+        return self.snapshot()
+
+    def snapshot(self):
+        """Host copies per slot: {"rays": [per part uint8 array], "info0": array or None, "info1": ...}."""
+        self.torch.cuda.synchronize(self.dev)
+        return [{"rays": [p.rays.cpu().numpy() for p in row],
+                 "info0": None if self.info0[f] is None else self.info0[f].cpu().numpy(),
+                 "info1": None if self.info1[f] is None else self.info1[f].cpu().numpy()}
+                for f, row in enumerate(self.slots)]
 
     def timing_reset(self):
         for row in self.slots:
