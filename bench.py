@@ -475,6 +475,29 @@ def aux_configs(torch, tthip, eng, dev, args, which):
     return out
 
 
+def lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, near, far, world, args):
+    """The strong-scaling deal of 64x64 tiles to ranks: round-robin (--deal rr), or
+    longest-processing-time first (--deal lpt, default) by the tile costs of a previous frame -- here sample
+    0 traced once at setup on every rank's own GPU with TT_TRACE_ADAPTIVE_ORDER, whose per-8x8-chunk cost
+    map (tt_trace_chunk_costs: the chunk's longest ray in node steps) is summed per tile. The trace is
+    deterministic, so every rank computes the same deal without a collective. Returns (owner or None, info)."""
+    if args.deal != "lpt" or world == 1:
+        return None, {"deal": "round-robin"}
+    full = torch.zeros(W * H * 48, dtype=torch.uint8, device=dev)
+    eng.generate(full, c2w, ip, W, H, near, far, jitter=1, frames=0, max_bounce=1, device=True)
+    eng.trace(full, W * H, 0, far, W, H, device=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER)
+    cc = eng.chunk_costs(0)
+    del full
+    costs = ttdist.tile_costs_from_chunks(cc, W, H)
+    owner = ttdist.lpt_owner(costs, world)
+    loads = np.bincount(owner, weights=costs, minlength=world)
+    rr = np.bincount(np.arange(len(costs)) % world, weights=costs, minlength=world)
+    return owner, {"deal": "lpt", "cost_source": "sample 0, tt_trace_chunk_costs (per 8x8 chunk: longest ray's node steps,"
+                                                 " floor 24) summed per 64x64 tile",
+                   "max_over_mean_cost": round(float(loads.max() / loads.mean()), 4),
+                   "round_robin_max_over_mean_cost": round(float(rr.max() / rr.mean()), 4)}
+
+
 def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
     """The reference's dynamic frame (AssetManager.cs:1767-1826: every _MeshData record rewritten and the TLAS
     refit, then the traces) with N1_SLOTS frames in flight: slot f is a context with a TLAS, TLASBVH8Indices and
@@ -632,8 +655,9 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         del solo
         el1 = min(el1a, el1b)
         rec["n1_ms_per_frame_by_layout_rank"] = {"2x1": round(el1a, 4), f"1x{N1_SLOTS}": round(el1b, 4)}
-        lay, el_n = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)])
-        rec.update(rays_this_rank=lay.n_prim(), build_s=round(build_s, 1))
+        owner, deal = lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, T.NEAR, far, world, args)
+        lay, el_n = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)])
+        rec.update(rays_this_rank=lay.n_prim(), build_s=round(build_s, 1), tile_deal=deal)
     except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
         ok = 0
         rec["error"] = f"rank {rank}: {type(e).__name__}: {e}"
@@ -671,7 +695,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     lay.close()
     if rank != 0:
         return None
-    frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl, sizes)], sizes, W, H, world, P)
+    frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl, sizes)], sizes, W, H, world, P, owner=owner)
     full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
     eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=last_sample, max_bounce=1, device=True)
     eng.trace(full, WH, 0, far, W, H, device=True)
@@ -903,6 +927,10 @@ def main():
                          "(tools/strong_replay.py, profiles/r04/replay/: C2 N = 8 0.135 ms per frame vs 0.155 / "
                          "0.150 with 4 / 3 slots and 0.223-0.271 with 2x2 / 2x1 / 3x1; C5 4K N = 8 0.241 vs 0.270 / "
                          "0.312)")
+    ap.add_argument("--deal", choices=["lpt", "rr"], default="lpt",
+                    help="strong-scaling tile deal (N > 1): lpt = longest-processing-time first by a previous frame's "
+                         "tile costs (tt_trace_chunk_costs of sample 0, computed identically on every rank), rr = "
+                         "round-robin")
     ap.add_argument("--strong-parts", type=int, default=1,
                     help="tile-interleaved parts per rank of the strong-scaling tile layouts (see --strong-slots)")
     ap.add_argument("--no-spp-aux", action="store_true",
@@ -1065,10 +1093,13 @@ def main():
         lay.timed_rays = lay.rays_in_frames(k0, lay.k)  # the K frames' rays (slots differ with their jitter)
         return el_
 
+    # the strong-scaling deal of tiles to ranks (--deal: LPT by a previous frame's tile costs, or round-robin)
+    owner, deal_info = lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, 0.3, far, world, args) \
+        if (tiles or args.deal == "lpt") and world > 1 else (None, {"deal": "none (one rank)"})
     if spp:  # this rank's (sample, tile) units of the N-sample frame (ttdist.spp_part_pixels)
         plan = ttdist.spp_part_pixels(W, H, world, rank, P)
     elif split:  # this rank's pixels of the one frame, compacted in tile order, split into P parts
-        plan = [[(frames, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P)]
+        plan = [[(frames, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)]
     else:  # the whole frame, one launch per bounce in the kernel's own tile order
         plan = [[(frames, np.arange(WH, dtype=np.int64))]]
     layout = layout_of(plan, F)
@@ -1245,7 +1276,8 @@ def main():
             frame = fr[0]
         else:
             if tiles:
-                frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P)
+                frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P,
+                                              owner=owner)
             elif split:
                 own = torch.cat([p.prim_hits for p in layout.slots[(layout.k - 1) % F]]).cpu()
                 frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
@@ -1271,7 +1303,8 @@ def main():
     strong = None
     if world > 1 and not args.no_strong:
         if spp:
-            lay_s = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P_strong)], F_strong)
+            lay_s = layout_of([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P_strong, owner=owner)],
+                              F_strong)
             lay_s.attach_gather(dist, world, rank, red_dev)
         else:
             lay_s = layout  # the headline already is the strong-scaling layout
@@ -1286,7 +1319,8 @@ def main():
         par = None
         if rank == 0:
             sz_s, gl_s = lay_s.last_gathered()
-            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H, world, lay_s.P)
+            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H, world, lay_s.P,
+                                        owner=owner)
             par = bool(np.array_equal(fr1, one_gpu_frame(lay_s.sample_of(lay_s.last_slot(), 0))))
         ms_n = float(tmax.item()) * 1e3 / args.steps
         strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
@@ -1296,8 +1330,8 @@ def main():
                   "n1_ms_per_frame": round(solo_ms, 4), "n1_rays_per_frame": int(solo_rays),
                   "n1_ms_per_frame_by_layout": solo_layouts,
                   "efficiency": round(solo_ms / (world * ms_n), 4),
-                  "gather_identical_to_1gpu": par,
-                  "layout": "one 1080p frame (1 sample): 64x64 tiles round-robin over the ranks, each rank's tiles "
+                  "gather_identical_to_1gpu": par, "tile_deal": deal_info,
+                  "layout": "one 1080p frame (1 sample): 64x64 tiles dealt over the ranks (tile_deal), each rank's tiles "
                             f"as {lay_s.P} parts x {lay_s.F} frame slots, + one RCCL gather of the frame's primary "
                             "hit records per frame; efficiency = t(N = 1 frame in the faster single-GPU layout, "
                             "every rank's GPU at once, fastest) / (N x t(N))"}

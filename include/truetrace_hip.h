@@ -481,6 +481,15 @@ tt_status tt_trace_closest_hits(tt_ctx* ctx, const tt_trace_params* p, tt_ray_da
 tt_status tt_trace_closest_indirect(tt_ctx* ctx, const tt_trace_params* p, const uint32_t* n_rays_dev,
                                     tt_ray_data* global_rays, uint32_t* primary_info,
                                     const tt_col_data* global_colors);
+
+/* The per-chunk costs the last TT_TRACE_ADAPTIVE_ORDER launch of bounce index `bounce` recorded on this
+ * context (one uint32 per 64-ray chunk: the chunk's largest Reps count, 0 when every ray of the chunk
+ * stayed below 32 node steps). A full-frame launch (n_rays == W*H, W and H multiples of 8) indexes
+ * chunks by 8x8 pixel tile, (y / 8) * (W / 8) + x / 8; otherwise chunk i holds rays [64 i, 64 i + 64)
+ * of the launch. Copies min(max, chunks) values and sets *n to that count (0 before any flagged
+ * launch). Synchronizes the context stream. Hosts use it to balance screen tiles over GPUs by the
+ * previous frame's cost (bench.py's strong-scaling deal). */
+tt_status tt_trace_chunk_costs(tt_ctx* ctx, int32_t bounce, uint32_t* costs, uint32_t max, uint32_t* n);
 /* Per-call GPU durations (HIP events on the context stream, in issue order) since the last
  * tt_timing_reset (ring of 256 entries). One entry per call of tt_trace_closest and
  * tt_trace_shadow (the trace kernel alone), tt_generate_primary (the generate kernel),

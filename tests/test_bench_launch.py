@@ -79,10 +79,11 @@ def _port():
 
 @pytest.mark.gpu
 def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
-    """The full bench through the self-launch path: 2 ranks on the one GPU (gloo collectives),
-    the metric's spp layout (a 2-sample frame's tiles over the ranks, weak scaling) with one gather per
-    step; rank 0's JSON line reports 2 GPUs and gathered samples identical to one GPU tracing each
-    whole frame, and the strong-scaling tile layout beside it (one frame, same gather) identical too."""
+    """The full bench through the self-launch path: 2 ranks on the one GPU (gloo collectives), the
+    headline's strong-scaling tile layout (one 1080p frame's tiles dealt LPT by a previous frame's costs,
+    one gather per step); rank 0's JSON line reports 2 GPUs and a gathered frame identical to one GPU
+    tracing the whole frame, and the weak-scaling spp layout beside it (a 2-sample frame, same gather)
+    identical too."""
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
                         "--no-shadow", "--no-c5-tiles", "--steady-steps", "0"],
                        env=_env(TT_BENCH_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=170)
@@ -92,11 +93,14 @@ def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
     c = d["config"]
     assert c["dist_world_size"] == 2 and c["launcher"] == "bench.py self-launch"
     assert c["gather_identical_to_1gpu"] is True
-    assert d["scaling"] == "weak" and c["samples_per_frame"] == 2
-    assert c["rays_per_step_all_ranks"] > 8_000_000  # two 1080p samples, primary + bounce 1
+    assert d["scaling"] == "strong" and c["samples_per_frame"] == 1
+    assert 4_000_000 < c["rays_per_step_all_ranks"] < 4_200_000  # one 1080p frame, primary + bounce 1
     st = c["aux_strong_tiles"]
     assert st["scaling"] == "strong" and st["gather_identical_to_1gpu"] is True
+    assert st["tile_deal"]["deal"] == "lpt" and st["tile_deal"]["max_over_mean_cost"] < 1.05
     assert 4_000_000 < st["rays_per_frame_all_ranks"] < 4_200_000
     assert st["frame_slots"] >= 1 and 4_000_000 < st["n1_rays_per_frame"] < 4_200_000
     assert 0.0 < st["efficiency"]
     assert abs(st["efficiency"] - st["n1_ms_per_frame"] / (2 * st["ms_per_frame"])) < 0.01
+    w = c["aux_spp_weak"]
+    assert w["scaling"] == "weak" and w["samples_per_frame"] == 2 and w["gather_identical_to_1gpu"] is True

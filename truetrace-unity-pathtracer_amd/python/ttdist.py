@@ -27,14 +27,61 @@ from typing import List
 import numpy as np
 
 
-def tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64, block: int = 8) -> np.ndarray:
-    """Pixel indices owned by ``rank`` under round-robin tile sharding, in tile order. Inside a
-    tile the pixels run in ``block``x``block`` sub-blocks (row-major blocks, row-major pixels in a
-    block), so the 64 rays a wave dequeues together are an 8x8 screen patch, as the trace
-    kernel's own swizzle makes them for full-frame batches."""
+def lpt_owner(costs, world: int) -> np.ndarray:
+    """Longest-processing-time-first deal of tiles to ranks: tiles in descending cost (ties: lower tile
+    id first), each to the rank with the least cost so far (ties: lower rank). Deterministic, so every
+    rank computes the same deal from the same costs. Returns owner[tile]."""
+    costs = np.asarray(costs, np.float64)
+    order = np.lexsort((np.arange(len(costs)), -costs))
+    loads = np.zeros(world, np.float64)
+    owner = np.zeros(len(costs), np.int64)
+    for t in order:
+        r = int(np.argmin(loads))
+        owner[t] = r
+        loads[r] += costs[t]
+    return owner
+
+
+def tile_costs_from_chunks(chunk_costs, width: int, height: int, tile: int = 64, floor: int = 24) -> np.ndarray:
+    """Per-tile cost of a full-frame launch from its 8x8-chunk cost map (tthip.Engine.chunk_costs, bounce 0
+    with TT_TRACE_ADAPTIVE_ORDER): the sum over the tile's chunks of max(chunk cost, floor) -- the map
+    records a chunk's largest Reps count only when it reaches 32 node steps, so `floor` stands for the
+    cheap chunks (C2's mean is ~16 node steps per ray)."""
+    cw, ch = width // 8, height // 8
+    cm = np.maximum(np.asarray(chunk_costs, np.float64)[: cw * ch].reshape(ch, cw), floor)
+    tx, ty = (width + tile - 1) // tile, (height + tile - 1) // tile
+    k = tile // 8
+    out = np.zeros(tx * ty, np.float64)
+    for t in range(tx * ty):
+        x0, y0 = (t % tx) * k, (t // tx) * k
+        out[t] = cm[y0:y0 + k, x0:x0 + k].sum()
+    return out
+
+
+def _rank_tiles(n_t: int, world: int, rank: int, owner=None):
+    return range(rank, n_t, world) if owner is None else [int(t) for t in np.nonzero(np.asarray(owner) == rank)[0]]
+
+
+def virtual_owner(owner, world: int, parts: int) -> np.ndarray:
+    """A deal of tiles to ranks, with each rank's tiles split into ``parts`` interleaved parts: part s of
+    rank r is virtual rank s * world + r (its tiles in increasing id, every parts-th one), as part_pixels."""
+    owner = np.asarray(owner)
+    out = np.zeros_like(owner)
+    for r in range(world):
+        for i, t in enumerate(np.nonzero(owner == r)[0]):
+            out[t] = (i % parts) * world + r
+    return out
+
+
+def tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64, block: int = 8,
+                owner=None) -> np.ndarray:
+    """Pixel indices owned by ``rank`` in tile order: round-robin tile sharding (tile t to rank t % world), or
+    the deal ``owner[t]`` (lpt_owner). Inside a tile the pixels run in ``block``x``block`` sub-blocks
+    (row-major blocks, row-major pixels in a block), so the 64 rays a wave dequeues together are an 8x8
+    screen patch, as the trace kernel's own swizzle makes them for full-frame batches."""
     tx, ty = (width + tile - 1) // tile, (height + tile - 1) // tile
     out = []
-    for t in range(rank, tx * ty, world):
+    for t in _rank_tiles(tx * ty, world, rank, owner):
         x0, y0 = (t % tx) * tile, (t // tx) * tile
         ys, xs = np.meshgrid(np.arange(y0, min(y0 + tile, height)), np.arange(x0, min(x0 + tile, width)),
                              indexing="ij")
@@ -44,8 +91,8 @@ def tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64, 
     return np.concatenate(out).astype(np.int64) if out else np.zeros(0, np.int64)
 
 
-def shard_sizes(width: int, height: int, world: int, tile: int = 64) -> List[int]:
-    return [len(tile_pixels(width, height, world, r, tile)) for r in range(world)]
+def shard_sizes(width: int, height: int, world: int, tile: int = 64, owner=None) -> List[int]:
+    return [len(tile_pixels(width, height, world, r, tile, owner=owner)) for r in range(world)]
 
 
 def gather_hits(hits, world: int, rank: int, dst: int = 0):
@@ -68,24 +115,26 @@ def gather_hits(hits, world: int, rank: int, dst: int = 0):
     return [o[: int(s.item())] for o, s in zip(out, sizes)]
 
 
-def assemble_tiles(parts, width: int, height: int, world: int, tile: int = 64) -> np.ndarray:
+def assemble_tiles(parts, width: int, height: int, world: int, tile: int = 64, owner=None) -> np.ndarray:
     """Scatters gathered per-rank hit records back into screen order (W*H, 4)."""
     full = np.zeros((width * height, 4), np.uint32)
     for r, part in enumerate(parts):
-        pix = tile_pixels(width, height, world, r, tile)
+        pix = tile_pixels(width, height, world, r, tile, owner=owner)
         arr = part.cpu().numpy() if hasattr(part, "cpu") else np.asarray(part)
         full[pix] = arr.view(np.uint32).reshape(-1, 4)
     return full
 
 
-def part_pixels(width: int, height: int, world: int, rank: int, parts: int, tile: int = 64):
+def part_pixels(width: int, height: int, world: int, rank: int, parts: int, tile: int = 64, owner=None):
     """A rank's tiles split into ``parts`` tile-interleaved parts (traced on concurrent streams):
     part s of rank r is virtual rank s * world + r of world * parts, so the union over s is exactly
-    tile_pixels(width, height, world, rank)."""
-    return [tile_pixels(width, height, world * parts, s * world + rank, tile) for s in range(parts)]
+    tile_pixels(width, height, world, rank) (with a deal ``owner``: virtual_owner)."""
+    vo = None if owner is None else virtual_owner(owner, world, parts)
+    return [tile_pixels(width, height, world * parts, s * world + rank, tile, owner=vo) for s in range(parts)]
 
 
-def assemble_parts(gathered, part_sizes, width: int, height: int, world: int, parts: int, tile: int = 64) -> np.ndarray:
+def assemble_parts(gathered, part_sizes, width: int, height: int, world: int, parts: int, tile: int = 64,
+                   owner=None) -> np.ndarray:
     """Screen-order hit records from one gathered block per rank: rank r's block holds its parts'
     records back to back (part_sizes[r][s] records each)."""
     virt = [None] * (world * parts)
@@ -97,7 +146,8 @@ def assemble_parts(gathered, part_sizes, width: int, height: int, world: int, pa
             n = int(part_sizes[r][s])
             virt[s * world + r] = arr[o:o + n]
             o += n
-    return assemble_tiles(virt, width, height, world * parts, tile)
+    vo = None if owner is None else virtual_owner(owner, world, parts)
+    return assemble_tiles(virt, width, height, world * parts, tile, owner=vo)
 
 
 def n_tiles(width: int, height: int, tile: int = 64) -> int:

@@ -287,6 +287,9 @@ def hip_lib():
             L.tt_ctx_share_scene.argtypes = [vp, vp]
         if hasattr(L, "tt_ctx_share_blas"):
             L.tt_ctx_share_blas.argtypes = [vp, vp, u32]
+        if hasattr(L, "tt_trace_chunk_costs"):
+            L.tt_trace_chunk_costs.argtypes = [vp, i32, vp, u32, C.POINTER(u32)]
+            L.tt_trace_chunk_costs.restype = i32
         if hasattr(L, "tt_trace_closest_hits"):
             L.tt_trace_closest_hits.argtypes = [vp, C.POINTER(TraceParams), vp, vp, vp, vp]
         L.tt_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
@@ -728,6 +731,15 @@ class Engine:
         if not hasattr(src, "_borrowers"):
             src._borrowers = []
         src._borrowers.append(weakref.ref(self))
+
+    def chunk_costs(self, bounce: int = 0, max_chunks: int = 1 << 22) -> np.ndarray:
+        """tt_trace_chunk_costs: the last TT_TRACE_ADAPTIVE_ORDER launch's per-64-ray-chunk costs (max Reps;
+        full-frame launches: one per 8x8 pixel tile, row-major over the (W/8) x (H/8) tile grid)."""
+        out = np.zeros(max_chunks, np.uint32)
+        n = C.c_uint32()
+        self._check(self.L.tt_trace_chunk_costs(self.h, int(bounce), out.ctypes.data, max_chunks, C.byref(n)),
+                    "tt_trace_chunk_costs")
+        return out[: n.value].copy()
 
     def share_blas(self, src: "Engine", n_tlas_nodes: int):
         """tt_ctx_share_blas: a frame slot over `src`'s scene -- src's BLASes and triangles (no copy) under a TLAS,
