@@ -124,6 +124,9 @@ namespace TrueTrace.Hip
             IntPtr globalRays, IntPtr primaryInfo, IntPtr globalColors, IntPtr hitsOut);
         // dst traces src's scene buffers (no copy) on its own stream: the parts of a frame share one scene
         [DllImport(Lib)] public static extern TTStatus tt_ctx_share_scene(IntPtr dst, IntPtr src);
+        [DllImport(Lib)] public static extern TTStatus tt_ctx_share_blas(IntPtr dst, IntPtr src, uint nTlasNodes);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_chunk_costs(IntPtr ctx, int bounce, uint* costs,
+            uint max, out uint n);
         [DllImport(Lib)] public static extern TTStatus tt_async_overflows(IntPtr ctx, out ulong count);
         [DllImport(Lib)] public static extern IntPtr tt_ctx_stream(IntPtr ctx);
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
@@ -225,7 +228,27 @@ namespace TrueTrace.Hip
         /// Trace `lender`'s scene on this context's stream without a copy (tt_ctx_share_scene): e.g. the second
         /// half of a frame traced concurrently on its own context. Update the scene through the lender;
         /// dispose this context before the lender.
-        public void ShareScene(TrueTraceHip lender) { Check(Native.tt_ctx_share_scene(m_ctx, lender.m_ctx)); }
+        public void ShareScene(TrueTraceHipTracer lender) { Check(Native.tt_ctx_share_scene(m_ctx, lender.m_ctx)); }
+
+        /// A frame slot over `lender`'s scene (tt_ctx_share_blas): the lender's BLASes and triangles without a copy,
+        /// under a TLAS, TLASBVH8Indices and _MeshData of this context's own (copied now). This frame's
+        /// RefitTLAS / SetMeshData on THIS tracer (AssetManager.cs:1821-1825) then neither wait for nor touch the
+        /// other frames in flight. `tlasNodeCount`: the TLAS region at the front of the node array.
+        public void ShareBlas(TrueTraceHipTracer lender, uint tlasNodeCount)
+        {
+            Check(Native.tt_ctx_share_blas(m_ctx, lender.m_ctx, tlasNodeCount));
+        }
+
+        /// The per-64-ray-chunk costs the last AdaptiveOrder trace of `bounce` recorded (tt_trace_chunk_costs): one
+        /// value per 8x8 pixel tile for a full-frame launch -- the input of a multi-GPU host's tile balancing.
+        public unsafe uint[] ChunkCosts(int bounce, uint maxChunks)
+        {
+            var a = new uint[maxChunks];
+            uint n;
+            fixed (uint* p = a) Check(Native.tt_trace_chunk_costs(m_ctx, bounce, p, maxChunks, out n));
+            Array.Resize(ref a, (int)n);
+            return a;
+        }
 
         /// A hipStream_t on a hardware queue of its own (tt_stream_create) for a concurrently traced half of
         /// the frame: pass handle.DangerousGetHandle() as the hipStream of that half's tracer and dispose the
