@@ -219,6 +219,18 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             TT_DB(8);
             const uint32_t mo = firstbithigh(tg.y);
             tg.y &= ~(1u << mo);
+#if TT_ROOT_COPY
+            // the BLAS root's copy for this TLAS leaf (TraceArgs::rc_base): its address does not depend on the
+            // LeafMesh load, so its two cache lines are fetched beside it and the root's node step (next
+            // iteration) hits in cache instead of waiting on a second dependent fetch
+            uint32_t pf0 = 0u, pf1 = 0u;
+            const bool rc = A.rc_base != 0u;
+            if (rc) {
+                const uint32_t ro = node_offset(A.rc_base + 8u * (tg.x + mo));
+                pf0 = buffer_load4(nodes, ro);
+                pf1 = buffer_load4(nodes, ro + 64u);
+            }
+#endif
             const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
             const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
             const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
@@ -245,7 +257,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 nr.iz = rcp_rn(nr.dz);
                 ray = nr;
                 oct = octant_inv4(ray);
+#if TT_ROOT_COPY
+                cg = make_uint2(rc ? A.rc_base + 8u * (tg.x + mo) : (uint32_t)mo4.w, 0x80000000u);
+                asm volatile("" ::"v"(pf0), "v"(pf1));  // (the prefetch registers stay reserved until here)
+#else
                 cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
+#endif
                 if (STATS) c_blas++;
             } else {
                 tg.y = TT_IDLE;
