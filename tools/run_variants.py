@@ -67,7 +67,8 @@ names = [os.path.basename(l)[len("libtruetrace_hip_"):-3] for l in libs]
 order = sys.argv[1:] or names  # a name may repeat (re-measure for noise)
 for spec in order:  # "name" or "name@B": B = TT_BLOCKS_PER_CU cap (256-thread blocks per CU)
     name, _, bpc = spec.partition("@")
-    lib = libs[names.index(name)]
+    lib = (os.path.join(REPO, "truetrace-unity-pathtracer_amd", "lib", "libtruetrace_hip.so") if name == "product"
+           else libs[names.index(name)])
     env = dict(os.environ, TT_HIP_LIB=lib, REPO=REPO)
     if bpc:
         env["TT_BLOCKS_PER_CU"] = bpc
