@@ -10,16 +10,20 @@ resident in HBM in the reference's 2*W*H ping-pong RayData buffer. Ray generatio
 bounce enqueue run once during setup (they are the caller's kernels, not the trace).
 
 Multi-GPU (``bench.py --gpus N``, self-launched, or under ``torchrun --nproc-per-node N``): one process
-per GPU, scene replicated per GPU. Default layout ``--shard spp`` (weak scaling, per-GPU work fixed):
-the job at N GPUs is an N-sample 1080p frame (sample k = the reference's Generate with
-frames_accumulated = k); its (sample, 64x64 screen tile) units are dealt round-robin to the ranks
-(SURVEY.md §8(e)'s tile sharding), so each rank traces one frame's worth of tiles' primary rays and
-their bounce-1 rays, and the primary hit records of all N samples go to rank 0 in ONE RCCL gather
-over xGMI -- inside the timed step (on a second stream, overlapped with the bounce-1 trace).
-``value`` = all ranks' rays / the slowest rank's time. The strong-scaling layout (ONE 1-sample
-frame's tiles over the ranks, same gather) is measured beside it as ``config.aux_strong_tiles`` and
-is the headline with ``--shard tiles``; ``--shard sample`` has every rank trace its own full-frame
-sample with no collective (``config.aux_sample_sharded``).
+per GPU, scene replicated per GPU. Default layout ``--shard tiles`` (strong scaling, the north star's
+layout): ONE 1080p frame's 64x64 screen tiles are dealt to the ranks -- longest-
+processing-time first by a previous frame's tile costs (``--deal lpt``; ``rr`` = round-robin) -- each
+rank traces its tiles' primary rays and their bounce-1 rays (1 part x 6 frame slots per rank, every slot
+its own jittered sample), and the frame's primary hit records go to rank 0 in ONE RCCL gather over xGMI
+-- inside the timed step (on a second stream, overlapped with the bounce-1 trace). ``value`` = all
+ranks' rays / the slowest rank's time; the efficiency against the N = 1 frame is in
+``config.aux_strong_tiles``. Beside it: ``config.aux_spp_weak`` (weak scaling: an N-sample frame's
+(sample, tile) units round-robin, a frame's worth per rank, same gather; the headline with ``--shard
+spp``) and, with ``--shard sample``, every rank tracing its own full-frame sample with no collective.
+
+N = 1: the whole frame as one launch per bounce with 3 frames in flight, every frame slot its own jittered
+sample; after the timed steps every slot's records (both bounces, both _PrimaryTriangleInfo forms) are
+compared with the oracle traced from the same pre-state (``oracle_check``, ``oracle_identical``).
 
 Streams: torch and the engine share ONE stream (a torch.cuda.Stream made current before any
 allocation and passed to tt_ctx_create), so every torch copy / collective and every engine launch

@@ -241,11 +241,14 @@ def test_shared_scene_mutations_are_ordered_without_host_sync():
     assert borrower.h is None
 
 
-def test_frame_slots_equal_one_launch():
+@pytest.mark.parametrize("stride", [0, 1])
+def test_frame_slots_equal_one_launch(stride):
     """bench.py's N = 1 layout (ttlayout.FrameLayout: the whole frame as one launch per bounce, 3 frames in
     flight on contexts that borrow one scene, streams on dedicated HW queues), several frames issued
     back to back: every slot's primary hit records and _PrimaryTriangleInfo equal one context tracing
-    the frame, and its bounce-1 records equal the single context's bounce-1 launch."""
+    the frame its slot traces -- the same sample in every slot (stride 0), or slot f's own jittered sample
+    f (stride 1, the bench's layout since round 5) -- and its bounce-1 records equal that context's
+    bounce-1 launch."""
     import torch
 
     import ttlayout
@@ -261,29 +264,32 @@ def test_frame_slots_equal_one_launch():
         colors = np.zeros(WH, tthip.COL_DTYPE)
         colors["Data"][:, 3] = 1.0
         colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
-        one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
-        info1 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize(dev)
-        base.generate(one, c2w, ip, W, H, T.NEAR, FAR, jitter=1, frames=0, max_bounce=1, device=True)
-        base.trace(one, WH, 0, FAR, W, H, info=info1, device=True)
-        torch.cuda.synchronize(dev)
-        ref_info0 = info1.cpu().numpy()  # the bounce-0 form
-        info1.zero_()
-        nb1 = base.enqueue_bounce(one, WH, 0, FAR, W, H, frames=0, max_bounce=1, device=True)
-        base.trace(one, nb1, 1, FAR, W, H, info=info1, colors=colors_t, device=True)
-        torch.cuda.synchronize(dev)
-        ref_prim = one.view(2 * WH, 48)[:WH, 32:48].cpu().numpy()
-        ref_bnc = one.view(2 * WH, 48)[WH:WH + nb1, 32:48].cpu().numpy()
-        ref_info1 = info1.cpu().numpy()  # the GlobalColors-gated bounce-1 form
+        refs = {}
+        for k in sorted({f * stride for f in range(3)}):
+            one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            info1 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            base.generate(one, c2w, ip, W, H, T.NEAR, FAR, jitter=1, frames=k, max_bounce=1, device=True)
+            base.trace(one, WH, 0, FAR, W, H, info=info1, device=True)
+            torch.cuda.synchronize(dev)
+            info0 = info1.cpu().numpy()  # the bounce-0 form
+            info1.zero_()
+            nb1 = base.enqueue_bounce(one, WH, 0, FAR, W, H, frames=k, max_bounce=1, device=True)
+            base.trace(one, nb1, 1, FAR, W, H, info=info1, colors=colors_t, device=True)
+            torch.cuda.synchronize(dev)
+            refs[k] = (nb1, one.view(2 * WH, 48)[:WH, 32:48].cpu().numpy(),
+                       one.view(2 * WH, 48)[WH:WH + nb1, 32:48].cpu().numpy(), info0, info1.cpu().numpy())
+            del one
         make_full = ttlayout.full_frame_maker(torch, base, dev, W, H, c2w, ip, T.NEAR, FAR)
         lay = ttlayout.FrameLayout(torch, tthip, base, dev, W, H, FAR, [[(0, np.arange(WH, dtype=np.int64))]],
-                                   make_full, slots=3, bounce=True, info=True, colors=colors_t)
+                                   make_full, slots=3, bounce=True, info=True, colors=colors_t, slot_stride=stride)
         try:
             for _ in range(7):  # asynchronous, three frames in flight
                 lay.step()
             torch.cuda.synchronize(dev)
             for f, row in enumerate(lay.slots):
                 p = row[0]
+                nb1, ref_prim, ref_bnc, ref_info0, ref_info1 = refs[lay.sample_of(f, 0)]
                 assert p.n == WH and p.nb == nb1
                 prim = p.rays.view(-1, 48)[:WH, 32:48].cpu().numpy()
                 assert np.array_equal(prim, ref_prim), f"slot {f}: primary records"
@@ -291,6 +297,8 @@ def test_frame_slots_equal_one_launch():
                 assert np.array_equal(bnc, ref_bnc), f"slot {f}: bounce-1 records"
                 assert np.array_equal(lay.info0[f].cpu().numpy(), ref_info0), f"slot {f}: bounce-0 info"
                 assert np.array_equal(lay.info1[f].cpu().numpy(), ref_info1), f"slot {f}: bounce-1 info"
+            if stride:
+                assert len({lay.rays_of_slot(f) for f in range(3)}) > 1  # the jitter changes the bounce counts
         finally:
             lay.close()
     finally:

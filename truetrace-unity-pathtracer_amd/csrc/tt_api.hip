@@ -735,7 +735,11 @@ tt_status tt_stream_create(int32_t device, void** stream) {
         *stream = s;
         std::lock_guard<std::mutex> lk(g_streams_mu);
         g_streams.emplace_back(device, s);
-        if (!g_streams_handler) g_streams_handler = std::atexit(release_live_streams) == 0;
+        static const bool handler_on = [] {  // TT_STREAM_EXIT_HANDLER=0: diagnosis only (the exit-time teardown off)
+            const char* e = std::getenv("TT_STREAM_EXIT_HANDLER");
+            return !(e && e[0] == '0');
+        }();
+        if (!g_streams_handler && handler_on) g_streams_handler = std::atexit(release_live_streams) == 0;
     }
     return st;
 }
