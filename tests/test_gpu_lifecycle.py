@@ -19,7 +19,7 @@ CHILD = os.path.join(REPO, "tests", "native", "stream_exit_child.py")
 
 
 def _run(cmd, tmp):
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=tmp,
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=90, cwd=tmp,
                        env=dict(os.environ, PYTHONUNBUFFERED="1"))
     return r
 
@@ -34,8 +34,8 @@ def test_exit_with_live_dedicated_streams(tmp_path, mode):
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     assert "live 3" in r.stdout and "ok" in r.stdout
     prof = shutil.which("rocprofv3")
-    if prof is None:
-        pytest.skip("rocprofv3 not on PATH")
+    if prof is None or os.environ.get("TT_TEST_ROCPROF") != "1":
+        pytest.skip("the rocprofv3 leg runs in its own GPU call (TT_TEST_ROCPROF=1, tools/gpu/job.sh lifecycle)")
     r = _run([prof, "--kernel-trace", "-d", str(tmp_path / "prof"), "-o", "run", "--"] + args, str(tmp_path))
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     assert "ok" in r.stdout

@@ -74,7 +74,7 @@ for stage in "$@"; do
     replaykt) export TMPDIR=/tmp
               run replaykt 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/kt" -o kt -- \
                   python -u tools/strong_replay.py --configs c2 ${REPLAY_ARGS:---ns 8 --layouts 1x6} || exit $? ;;
-    lifecycle) run lifecycle 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+    lifecycle) run lifecycle 600 env TT_TEST_ROCPROF=1 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
                    tests/test_gpu_lifecycle.py "tests/test_gpu_parity.py::test_sponza_1080p_jittered_frames_through_the_timed_kernels" \
                    -m gpu || exit $? ;;
     longray) run longray 300 python -u tools/long_ray_chain.py || exit $? ;;
