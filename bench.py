@@ -545,7 +545,10 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
         e.tlas_refit(T_, boxes[k & 1], device=True, asynchronous=True)
         e.generate(b["rays"], c2w, ip, W, H, T.NEAR, far, jitter=1, frames=k, max_bounce=1, device=True,
                    asynchronous=True)
-        e.trace(b["rays"], WH, 0, far, W, H, info=b["i0"], device=True, asynchronous=True)
+        # (the adaptive order on the primaries, INTEGRATION.md §5's advice for scenes beyond the L2s: each slot's
+        # launch ordered by its own previous frame -- another pose and jitter)
+        e.trace(b["rays"], WH, 0, far, W, H, info=b["i0"], device=True, asynchronous=True,
+                flags=tthip.TT_TRACE_ADAPTIVE_ORDER if args.dyn_adaptive else 0)
         e.enqueue_bounce_indirect(b["rays"], None, WH, b["cnt"], 0, far, W, H, frames=k, max_bounce=1)
         e.trace_indirect(b["rays"], b["cnt"], WH, 1, far, W, H, info=b["i1"], colors=colors_t)
         with torch.cuda.stream(streams[f]):
@@ -576,6 +579,7 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
     # the serial reference: one context, the same calls for each slot's last frame, synchronously
     ref = tthip.Engine(dev.index)
     same = True
+    diff = []
     try:
         ref.upload(sc4)
         rr = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
@@ -592,14 +596,22 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
             torch.cuda.synchronize(dev)
             a = rr.view(-1, 48).cpu().numpy()
             gv = g["rays"].reshape(-1, 48)
-            same = same and nb_ref == g["nb"] and np.array_equal(a[:WH], gv[:WH]) \
-                and np.array_equal(a[WH:WH + nb_ref], gv[WH:WH + nb_ref]) \
-                and np.array_equal(r0.cpu().numpy(), g["i0"]) and np.array_equal(r1.cpu().numpy(), g["i1"])
+            # the bounce-1 _PrimaryTriangleInfo texels this frame writes: the pixels of its bounce-1 rays (the
+            # others keep an earlier frame's texel, on either side)
+            pix = gv[WH:WH + g["nb"], 12:16].copy().view(np.uint32).reshape(-1).astype(np.int64)
+            i1a, i1b = r1.cpu().numpy().reshape(-1, 16), g["i1"].reshape(-1, 16)
+            d = {"frame": kk, "bounce_count": nb_ref == g["nb"], "primary_records": bool(np.array_equal(a[:WH], gv[:WH])),
+                 "bounce_records": bool(np.array_equal(a[WH:WH + nb_ref], gv[WH:WH + nb_ref])),
+                 "info_bounce0": bool(np.array_equal(r0.cpu().numpy(), g["i0"])),
+                 "info_bounce1": bool(nb_ref == g["nb"] and np.array_equal(i1a[pix], i1b[pix]))}
+            diff.append(d)
+            same = same and all(v for k_, v in d.items() if k_ != "frame")
     finally:
         ref.close()
     return {"slots": S, "frames": reps, "ms_per_frame": round(ms, 4), "mrays_s": round(rays / reps / ms / 1e3, 1),
+            "adaptive_order_primary": bool(args.dyn_adaptive),
             "rays_per_frame_mean": int(round(rays / reps)), "host_ms_per_frame_median": round(float(np.median(host_ms)), 4),
-            "identical_to_serial": bool(same),
+            "identical_to_serial": bool(same), "checks": diff,
             "note": f"frame k on slot k % {S}, each slot a context with its own TLAS / _MeshData over the shared BLASes "
                     "(tt_ctx_share_blas): update_meshdata (all records) + tlas_refit + Generate (frames_accumulated = k) + "
                     "primary + enqueue (device count) + indirect bounce-1, all asynchronous; each slot's last frame "
@@ -951,6 +963,8 @@ def main():
                          "use the metric's kernel instantiation and would mix into its rocprof average)")
     ap.add_argument("--no-c5-tiles", action="store_true",
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
+    ap.add_argument("--dyn-adaptive", type=int, default=1,
+                    help="aux dyn frame slots: TT_TRACE_ADAPTIVE_ORDER on each slot's primary launch (1, default) or not")
     ap.add_argument("--aux", default="c3,c4,dyn,refit,c5",
                     help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,dyn,refit,c5;"
                          " '' = none)")
@@ -1122,6 +1136,11 @@ def main():
         f"tris/ray {s_bnc.tri_tests / max(parts[0].nb, 1):.2f}; reps_exhausted {s_prim.reps_exhausted + s_bnc.reps_exhausted}"
         f"; parts {P}, frame slots {F}" + (f"; {world}-sample frame (spp)" if spp else ""))
 
+    # N = 1: the records the timed launches write are checked against the oracle afterwards (oracle_check):
+    # every slot's hit records and _PrimaryTriangleInfo are poisoned now and the host state kept as the oracle's
+    # input -- before the legs below, whose GPU work brings the clocks back up after these host copies
+    pre_state = layout.poison_records() if (world == 1 and not args.no_oracle_check) else None
+
     # The two auxiliary legs that trace the metric's own scene -- the single-stream leg (N = 1) and the
     # sample-sharded layout (N > 1) -- run BEFORE the timed region: they are sustained GPU work, so the
     # timed steps start with the engine clocks settled instead of ramping through the first ~30 ms
@@ -1212,9 +1231,6 @@ def main():
     G = layout.attach_gather(dist, world, rank, red_dev) if tiles else None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
-    # N = 1: the records the timed launches write are checked against the oracle afterwards (oracle_check):
-    # poison every slot's hit records and _PrimaryTriangleInfo first, keep the host state as the oracle's input
-    pre_state = layout.poison_records() if (world == 1 and not args.no_oracle_check) else None
     elapsed = timed(layout)
     lm = layout.launch_ms()  # part 0's launches, the last <= 128 frames of its slot
     launch_ms = lm.reshape(-1)
