@@ -8,6 +8,7 @@
 #   smoke      __graft_entry__.smoke() (the driver runs it before the bench)
 #   blocks     the headline per persistent-grid size: BLOCKS="20 16 12" blocks per CU (TT_BLOCKS_PER_CU), REPS
 #   quick      bench without aux configs / CPU baseline (layout and headline only)
+#   dyn        bench headline + the C4 dynamic frame legs (aux dyn), per TT_BLOCKS_PER_CU in BLOCKS (0 = default)
 #   slots2     quick with 2 frame slots (frame k + 1's primaries overlap frame k's bounce-1 launches)
 #   layouts    the N = 1 headline per parts x slots layout: LAYOUTS="2x1 2x2 1x3", REPS=2 (profiles/r04/ab/r04k_*)
 #   testlib    the GPU suite with a variant library: LIB=name (lib/variants/libtruetrace_hip_NAME.so)
@@ -56,6 +57,10 @@ for stage in "$@"; do
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     quick) run quick 300 python -u bench.py --steps 20 --warmup 5 --aux "" --cpu-seconds 2 || exit $? ;;
+    dyn) for b in ${BLOCKS:-0}; do  # the headline + the C4 dynamic frame (one launch and frame slots) per grid cap
+             run "dyn_b$b" 400 env TT_BLOCKS_PER_CU=$b python -u bench.py --steps 20 --warmup 5 --aux dyn \
+                 --no-cpu-baseline --no-recur --no-shadow ${DYN_ARGS:-} || exit $?
+         done ;;
     slots2) run slots2 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --slots 2 || exit $? ;;
     layouts) for i in $(seq ${REPS:-2}); do for l in ${LAYOUTS:-2x1 2x2 1x3}; do  # N = 1 headline per parts x slots
                  run "n1_${l}_$i" 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --no-recur \
