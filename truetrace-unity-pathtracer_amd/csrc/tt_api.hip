@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -701,6 +702,37 @@ void release_live_streams() {
 
 extern "C" {
 
+}  // extern "C"
+
+namespace {
+// A profiler that wraps the HIP API (rocprofv3's tool keeps a per-stream table, built lazily by the first
+// kernel launch it sees on a stream) registers that table's destructor when the table is built -- after the
+// exit handler registered at tt_stream_create -- so at exit the table would be gone before the handler's
+// hipStreamDestroy calls reach the wrapper ("'get_stream_stack()' Must be non nullptr"). The handler is
+// registered once more after the first launch on one of the library's streams (note_stream_launch), which
+// puts it ahead of anything built up to then; running it twice is harmless (the first run empties the list).
+std::atomic<bool> g_late_handler{false};
+bool stream_exit_handler_on() {
+    static const bool on = [] {  // TT_STREAM_EXIT_HANDLER=0: diagnosis only (the exit-time teardown off)
+        const char* e = std::getenv("TT_STREAM_EXIT_HANDLER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+void note_stream_launch(hipStream_t s) {
+    if (g_late_handler.load(std::memory_order_relaxed) || !stream_exit_handler_on()) return;
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    if (g_late_handler.load(std::memory_order_relaxed)) return;
+    for (auto& ds : g_streams)
+        if (ds.second == s) {
+            g_late_handler = std::atexit(release_live_streams) == 0;
+            break;
+        }
+}
+}  // namespace
+
+extern "C" {
+
 uint32_t tt_stream_live_count(void) {
     std::lock_guard<std::mutex> lk(g_streams_mu);
     return (uint32_t)g_streams.size();
@@ -735,11 +767,7 @@ tt_status tt_stream_create(int32_t device, void** stream) {
         *stream = s;
         std::lock_guard<std::mutex> lk(g_streams_mu);
         g_streams.emplace_back(device, s);
-        static const bool handler_on = [] {  // TT_STREAM_EXIT_HANDLER=0: diagnosis only (the exit-time teardown off)
-            const char* e = std::getenv("TT_STREAM_EXIT_HANDLER");
-            return !(e && e[0] == '0');
-        }();
-        if (!g_streams_handler && handler_on) g_streams_handler = std::atexit(release_live_streams) == 0;
+        if (!g_streams_handler && stream_exit_handler_on()) g_streams_handler = std::atexit(release_live_streams) == 0;
     }
     return st;
 }
@@ -1828,6 +1856,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
         a.order = os->order.p;
     }
     TT_HIP(c, tt_launch_trace(a, want_stats, matcheck, info_mode, grid, c->stream));
+    note_stream_launch(c->stream);
     if (os) {
         os->cur ^= 1u;
         os->valid = true;
@@ -2015,6 +2044,7 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     c->ctl_zero[0] = c->ctl_zero[1] = false;  // the any-hit kernel zeroes nothing
     TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
+    note_stream_launch(c->stream);
     TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     if (accumulate) TT_HIP(c, tt_launch_shadow_accumulate(&a, d_vis, c->stream));
     TT_HIP(c, scene_read_end(c));
@@ -2134,6 +2164,7 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_launch_generate(c->cam.p, c->cam.p + 16, cam->width, cam->height, cam->near_plane, cam->far_plane,
                                  cam->jitter, cam->frames_accumulated, cam->max_bounce, d, c->stream));
+    note_stream_launch(c->stream);
     TT_HIP(c, ring_close(c, slot));
     if (!dev) TT_HIP(c, hipMemcpyAsync(rays, d, sizeof(tt_ray_data) * wh, hipMemcpyDeviceToHost, c->stream));
     if (!async) TT_HIP(c, hipStreamSynchronize(c->stream));
