@@ -19,9 +19,10 @@ CHILD = os.path.join(REPO, "tests", "native", "stream_exit_child.py")
 
 
 def _run(cmd, tmp):
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=90, cwd=tmp,
-                       env=dict(os.environ, PYTHONUNBUFFERED="1"))
-    return r
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    if env.get("TT_HIP_LIB"):  # (the child runs in tmp: a variant library named relative to the repo)
+        env["TT_HIP_LIB"] = os.path.abspath(env["TT_HIP_LIB"])
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=90, cwd=tmp, env=env)
 
 
 @pytest.mark.parametrize("mode", ["contexts-destroyed", "keep-contexts"])

@@ -66,7 +66,7 @@ for stage in "$@"; do
                  run "n1_${l}_$i" 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --no-recur \
                      --no-shadow --parts ${l%x*} --slots ${l#*x} || exit $?
              done; done ;;
-    testlib) lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_${LIB:?set LIB=variant name}.so
+    testlib) lib=$PWD/truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_${LIB:?set LIB=variant name}.so
              run "tests_$LIB" 600 env TT_HIP_LIB=$lib python -u -m pytest tests -m gpu -x -q --timeout 300 \
                  --timeout-method thread || exit $? ;;
     newtests) run newtests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parts.py \
