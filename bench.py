@@ -432,7 +432,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                    "tlas_refit_gpu_ms_median": round(float(np.median(refit_ms)), 4),
                    "note": "frame = update_meshdata (all records, host array, async) + tlas_refit (device boxes) + "
                            "Generate + primary trace + enqueue (returns the count: one sync) + bounce-1 trace",
-                   f"frame_slots_{N1_SLOTS}": slots_rec}
+                   "frame_slots": slots_rec}
         except Exception as e:  # auxiliary: record, never lose the metric line
             rec["error"] = f"{type(e).__name__}: {e}"
         out["c4_dynamic_frame"] = rec
@@ -520,7 +520,7 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
     colors = np.zeros(WH, tthip.COL_DTYPE)
     colors["Data"][:, 3] = 1.0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
-    S = N1_SLOTS
+    S = max(1, args.dyn_slots)
     engs, streams = [eng], [torch.cuda.ExternalStream(eng.stream, device=dev)]
     for f in range(1, S):
         st = tthip.dedicated_stream(torch, dev, f - 1)
@@ -963,6 +963,8 @@ def main():
                          "use the metric's kernel instantiation and would mix into its rocprof average)")
     ap.add_argument("--no-c5-tiles", action="store_true",
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
+    ap.add_argument("--dyn-slots", type=int, default=N1_SLOTS,
+                    help="aux dyn: frame slots (contexts with TLASes of their own) of the dynamic-frame leg")
     ap.add_argument("--dyn-adaptive", type=int, default=1,
                     help="aux dyn frame slots: TT_TRACE_ADAPTIVE_ORDER on each slot's primary launch (1, default) or not")
     ap.add_argument("--aux", default="c3,c4,dyn,refit,c5",
