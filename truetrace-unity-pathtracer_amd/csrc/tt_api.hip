@@ -213,7 +213,6 @@ struct tt_ctx {
     bool ovl = false;
     uint32_t ovl_slot = 0, tlas_base = 0, n_tlas_own = 0;
     uint32_t ovl_used = 0;     // lender: overlay regions in use (bit per slot)
-    uint32_t rc_base = 0;      // TT_ROOT_COPY builds: the BLAS-root copies' region (tt_root_copy_kernel); 0 = none
     // Cross-stream order of a shared scene (the reference rewrites the TLAS and _MeshData every frame,
     // then dispatches, AssetManager.cs:1821-1825): a lender mutation waits for the borrowers' launches
     // already enqueued, and a borrower launch waits for the lender's mutations already enqueued. An
@@ -633,18 +632,6 @@ __global__ void tt_update_mesh_kernel(const tt_mesh_data* __restrict__ raw, Mesh
     }
 }
 
-// TT_ROOT_COPY: the BLAS root node of TLAS leaf i copied to node index rc_base + 8 i (128-B aligned), so the
-// kernels can fetch it at an address that does not depend on the LeafMesh load (TraceArgs::rc_base). Run
-// after every change of the leaf records or of BLAS nodes.
-__global__ void tt_root_copy_kernel(uint4* __restrict__ nodes, const LeafMesh* __restrict__ leaf, uint32_t n_tlas,
-                                    uint32_t rc_base) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_tlas) return;
-    const uint32_t root = (uint32_t)leaf[i].m.root;
-#pragma unroll
-    for (int k = 0; k < 5; k++) nodes[(size_t)(rc_base + 8u * i) * 5u + k] = nodes[(size_t)root * 5u + k];
-}
-
 bool is_device_ptr(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -1010,14 +997,6 @@ tt_status tt_sync(tt_ctx* c) {
 
 namespace {
 tt_status refresh_leaves(tt_ctx* c);
-// TT_ROOT_COPY: refresh every TLAS leaf's BLAS-root copy on the context stream
-hipError_t refresh_root_copies(tt_ctx* c) {
-    if (!c->rc_base) return hipSuccess;
-    const uint32_t n = (uint32_t)c->host.tlas.size();
-    hipLaunchKernelGGL(tt_root_copy_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream,
-                       reinterpret_cast<uint4*>(c->nodes.p), c->leaf.p, n, c->rc_base);
-    return hipGetLastError();
-}
 }
 
 tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris,
@@ -1057,13 +1036,7 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     if (TT_NODE_STRIDE != 80 ||
         ((uint64_t)n_nodes + (uint64_t)TT_TLAS_SLOTS * tlas_res) * sizeof(tt_cwbvh_node) >= (1ull << 32))
         tlas_res = 0;  // no overlay regions (the strided-copy knob, or a node array near the 32-bit limit)
-    uint32_t n_nodes_dev = n_nodes + TT_TLAS_SLOTS * tlas_res;
-    uint32_t rc_base = 0;
-    if (TT_ROOT_COPY && TT_NODE_STRIDE == 80 &&
-        ((uint64_t)((n_nodes_dev + 7u) & ~7u) + 8ull * n_tlas) * sizeof(tt_cwbvh_node) < (1ull << 32)) {
-        rc_base = (n_nodes_dev + 7u) & ~7u;
-        n_nodes_dev = rc_base + 8u * n_tlas;
-    }
+    const uint32_t n_nodes_dev = n_nodes + TT_TLAS_SLOTS * tlas_res;
     hipError_t e;
     if ((e = c->nodes.alloc(n_nodes_dev)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
         (e = c->tris.alloc(n_tris)) != hipSuccess || (e = c->tlas.alloc(n_tlas)) != hipSuccess ||
@@ -1096,7 +1069,6 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     c->n_nodes_scene = n_nodes;
     c->n_nodes_dev = n_nodes_dev;
     c->tlas_res = tlas_res;
-    c->rc_base = rc_base;
     c->ovl_used = 0;
     c->root_known = true;
     c->any_invisible = any_invisible;
@@ -1109,8 +1081,6 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
         const tt_status st = refresh_leaves(c);
         if (st != TT_OK) return st;
     }
-    TT_HIP(c, refresh_root_copies(c));
-    TT_HIP(c, hipStreamSynchronize(c->stream));
     c->has_scene = true;
     return TT_OK;
 }
@@ -1195,7 +1165,6 @@ tt_status share_begin(tt_ctx* dst, tt_ctx* src) {
     dst->n_nodes_scene = src->n_nodes_scene;
     dst->n_nodes_dev = src->n_nodes_dev;
     dst->tlas_res = 0;  // a borrower never lends
-    dst->rc_base = 0;
     dst->ovl = false;
     dst->tlas_base = 0;
     dst->n_tlas_own = 0;
@@ -1418,7 +1387,6 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_blas_construct(a, c->stream));
     TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
-    TT_HIP(c, refresh_root_copies(c));
     TT_HIP(c, refresh_node_copy(c, node_base, R.n_nodes));
     TT_HIP(c, ring_close(c, slot));
     TT_HIP(c, scene_write_end(c, true));
@@ -1578,7 +1546,6 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
                              hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
     TT_HIP(c, refresh_node_copy(c, first, count));
-    if (blas_side && !c->ovl) TT_HIP(c, refresh_root_copies(c));
     if (!c->ovl) TT_HIP(c, scene_write_end(c, blas_side));
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
     return TT_OK;
@@ -1638,7 +1605,6 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream, c->mesh_raw.p, c->mesh.p,
                        c->leaf.p, c->tlas.p, n_tlas, first, count);
     TT_HIP(c, hipGetLastError());
-    if (!c->ovl) TT_HIP(c, refresh_root_copies(c));
     if (!c->ovl) TT_HIP(c, scene_write_end(c, false));
     return TT_OK;
 }
@@ -1747,7 +1713,6 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     a.nodes = kernel_nodes(c);
     a.n_nodes = c->n_nodes_dev;  // (the overlay regions included: a frame-slot TLAS lives there)
     a.tlas_base = c->tlas_base;
-    a.rc_base = c->ovl ? 0u : (c->lender ? c->lender->rc_base : c->rc_base);  // (a frame slot's leaves are its own)
     a.tris = c->tris.p;
     a.n_tris = c->host.n_tris;
     a.tlas = c->tlas.p;

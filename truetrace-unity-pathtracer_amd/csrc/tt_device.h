@@ -47,10 +47,6 @@ static_assert(sizeof(TriPos) == 48, "TriPos size");
 
 // Traversal-layout mesh record, 64 B: W2L rows 0-2 (row-major, 12 floats) + the four offsets
 // IntersectBVH reads on a TLAS->BLAS switch (IntersectionKernels.compute:197-213).
-#ifndef TT_ROOT_COPY
-#define TT_ROOT_COPY 0  // 1: TLAS leaf -> BLAS switches step a per-leaf copy of the BLAS root (TraceArgs::rc_base)
-#endif
-
 struct MeshGpu {
     float m[12];      // m[r*4+c] = W2L(r, c)
     int32_t TriOffset;
@@ -214,8 +210,6 @@ struct TraceArgs {
     RootLeaf root;               // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root (root.ok = 0: the generic path)
     uint32_t tlas_base;          // node index of the context's TLAS node 0: 0, or its frame-slot overlay region
                                  // (tt_ctx_share_blas); the TLAS-level NodeOffset
-    uint32_t rc_base;            // TT_ROOT_COPY builds: node index of TLAS leaf 0's BLAS-root copy (leaf i at
-                                 // rc_base + 8 i, 128-B aligned); 0 = off
 };
 
 // Adaptive-order builder (tt_order.hip): one block per scheduler segment sorts the segment's

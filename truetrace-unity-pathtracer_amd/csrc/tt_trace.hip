@@ -187,29 +187,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
     uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
     uint32_t d_lead_same = 0, d_uniform = 0;  // node-step uniformity (lanes sharing the first lane's node)
-#if TT_WRAY_RELOAD
-    // the world-space ray (ray2, IntersectionKernels.compute:151) re-read from GlobalRays[ray_index] (origin and
-    // direction are never written by the trace) with the same reciprocals as the ray's start: 9 VGPRs fewer in
-    // the loop, which is what holds the plain kernels at 80 VGPRs (6 waves per SIMD, TT_FAST_WAVES)
-    auto world_ray = [&]() -> LaneRay {
-        const uint4* rp = reinterpret_cast<const uint4*>(A.rays + ray_index);
-        const uint4 r0 = rp[0], r1 = rp[1];
-        LaneRay r;
-        r.ox = __uint_as_float(r0.x);
-        r.oy = __uint_as_float(r0.y);
-        r.oz = __uint_as_float(r0.z);
-        r.dx = __uint_as_float(r1.x);
-        r.dy = __uint_as_float(r1.y);
-        r.dz = __uint_as_float(r1.z);
-        r.ix = rcp_rn(r.dx);
-        r.iy = rcp_rn(r.dy);
-        r.iz = rcp_rn(r.dz);
-        return r;
-    };
-#else
     // the world-space ray (ray2, IntersectionKernels.compute:151), kept in registers
     auto world_ray = [&]() -> LaneRay { return wray; };
-#endif
 
 #if TT_ROOT_LEAF
     const bool rl_ok = A.root.ok != 0u;  // a kernel argument: wave-uniform
@@ -219,18 +198,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             TT_DB(8);
             const uint32_t mo = firstbithigh(tg.y);
             tg.y &= ~(1u << mo);
-#if TT_ROOT_COPY
-            // the BLAS root's copy for this TLAS leaf (TraceArgs::rc_base): its address does not depend on the
-            // LeafMesh load, so its two cache lines are fetched beside it and the root's node step (next
-            // iteration) hits in cache instead of waiting on a second dependent fetch
-            uint32_t pf0 = 0u, pf1 = 0u;
-            const bool rc = A.rc_base != 0u;
-            if (rc) {
-                const uint32_t ro = node_offset(A.rc_base + 8u * (tg.x + mo));
-                pf0 = buffer_load4(nodes, ro);
-                pf1 = buffer_load4(nodes, ro + 64u);
-            }
-#endif
             const float4* mp = reinterpret_cast<const float4*>(A.leaf + (tg.x + mo));  // LeafMesh
             const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
             const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
@@ -257,12 +224,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 nr.iz = rcp_rn(nr.dz);
                 ray = nr;
                 oct = octant_inv4(ray);
-#if TT_ROOT_COPY
-                cg = make_uint2(rc ? A.rc_base + 8u * (tg.x + mo) : (uint32_t)mo4.w, 0x80000000u);
-                asm volatile("" ::"v"(pf0), "v"(pf1));  // (the prefetch registers stay reserved until here)
-#else
                 cg = make_uint2((uint32_t)mo4.w, 0x80000000u);
-#endif
                 if (STATS) c_blas++;
             } else {
                 tg.y = TT_IDLE;
@@ -384,7 +346,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 ray.ix = rcp_rn(ray.dx);
                 ray.iy = rcp_rn(ray.dy);
                 ray.iz = rcp_rn(ray.dz);
-                if (!TT_WRAY_RELOAD) wray = ray;
+                wray = ray;
                 oct = octant_inv4(ray);
                 best.t = A.far_plane;
                 best.u = 0.0f;
@@ -548,20 +510,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     }
 }
 
-// TT_FAST_WAVES (with TT_WRAY_RELOAD; off in the product until its parity run): the closest-hit kernels
-// without STATS / material checks held to that many waves per SIMD (80 VGPRs at 6, 12-20 B of scratch);
-// the STATS and material-check forms keep the compiler's bound. Measured +1.4% (profiles/r04/ab/r04w_*)
-#if TT_FAST_WAVES > 0
-#define TT_FAST_BOUNDS(FAST) __launch_bounds__(TT_BLOCK) __attribute__((amdgpu_waves_per_eu((FAST) ? TT_FAST_WAVES : 1)))
-#else
-#define TT_FAST_BOUNDS(FAST) TT_BOUNDS
-#endif
 template <bool STATS, bool MATCHECK, int INFO>
-__global__ TT_FAST_BOUNDS(!STATS && !MATCHECK && TT_WAVES_PER_EU == 0) void tt_trace_kernel(TraceArgs A) {
+__global__ TT_BOUNDS void tt_trace_kernel(TraceArgs A) {
     trace_body<STATS, MATCHECK, INFO, false, false>(A);
 }
 template <bool MATCHECK, int INFO>
-__global__ TT_FAST_BOUNDS(!MATCHECK && TT_WAVES_PER_EU == 0) void tt_trace_kernel_indirect(TraceArgs A) {
+__global__ TT_BOUNDS void tt_trace_kernel_indirect(TraceArgs A) {
     trace_body<false, MATCHECK, INFO, true, false>(A);
 }
 // (held at 5 waves per SIMD like the direct kernels: the cost record would otherwise cost INFO = 2 a

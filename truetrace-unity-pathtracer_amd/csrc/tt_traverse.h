@@ -41,12 +41,6 @@
 #ifndef TT_LDS_STACK
 #define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
 #endif
-#ifndef TT_WRAY_RELOAD
-#define TT_WRAY_RELOAD 0  // 1: the world ray re-read from GlobalRays when needed instead of kept in registers
-#endif
-#ifndef TT_FAST_WAVES
-#define TT_FAST_WAVES 0   // > 0: waves per SIMD of the plain closest-hit kernels (tt_trace.hip TT_FAST_BOUNDS)
-#endif
 #ifndef TT_WAVES_PER_EU
 #define TT_WAVES_PER_EU 0 // __launch_bounds__ min waves per SIMD (0: compiler default)
 #endif
