@@ -8,7 +8,7 @@ ROOT=${GRAFT_REPO_ROOT:-$PWD}
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-recur --aux refit > $OUT/trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc/fetch -o fetch --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-recur --no-shadow --no-single --aux '' > $OUT/pmc_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc/write -o write --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-recur --no-shadow --no-single --aux '' > $OUT/pmc_write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-oracle-check --no-recur --aux refit > $OUT/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc/fetch -o fetch --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-oracle-check --no-recur --no-shadow --no-single --aux '' > $OUT/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc/write -o write --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-oracle-check --no-recur --no-shadow --no-single --aux '' > $OUT/pmc_write.log 2>&1
 python tools/pmc_traffic.py $OUT/pmc gpurun_out/traffic_$TAG.json
