@@ -11,8 +11,8 @@ bounce enqueue run once during setup (they are the caller's kernels, not the tra
 
 Multi-GPU (``bench.py --gpus N``, self-launched, or under ``torchrun --nproc-per-node N``): one process
 per GPU, scene replicated per GPU. Default layout ``--shard tiles`` (strong scaling, the north star's
-layout): ONE 1080p frame's 64x64 screen tiles are dealt to the ranks -- longest-
-processing-time first by a previous frame's tile costs (``--deal lpt``; ``rr`` = round-robin) -- each
+layout): ONE 1080p frame's 64x64 screen tiles are dealt to the ranks -- round-robin
+(``--deal rr``), or longest-processing-time first by a previous frame's tile costs (``--deal lpt``) -- each
 rank traces its tiles' primary rays and their bounce-1 rays (1 part x 6 frame slots per rank, every slot
 its own jittered sample), and the frame's primary hit records go to rank 0 in ONE RCCL gather over xGMI
 -- inside the timed step (on a second stream, overlapped with the bounce-1 trace). ``value`` = all
@@ -943,10 +943,12 @@ def main():
                          "(tools/strong_replay.py, profiles/r04/replay/: C2 N = 8 0.135 ms per frame vs 0.155 / "
                          "0.150 with 4 / 3 slots and 0.223-0.271 with 2x2 / 2x1 / 3x1; C5 4K N = 8 0.241 vs 0.270 / "
                          "0.312)")
-    ap.add_argument("--deal", choices=["lpt", "rr"], default="lpt",
-                    help="strong-scaling tile deal (N > 1): lpt = longest-processing-time first by a previous frame's "
-                         "tile costs (tt_trace_chunk_costs of sample 0, computed identically on every rank), rr = "
-                         "round-robin")
+    ap.add_argument("--deal", choices=["lpt", "rr"], default="rr",
+                    help="strong-scaling tile deal (N > 1): rr (default) = round-robin; lpt = longest-processing-time "
+                         "first by a previous frame's tile costs (tt_trace_chunk_costs of sample 0, computed identically "
+                         "on every rank). The one-GPU replay of every rank's N = 8 shard measured lpt no better "
+                         "(profiles/r05/replay/: C2 0.616 vs 0.626, C5 4K 0.552 vs 0.576): C2's ranks are within noise "
+                         "either way and C5's slowest rank is set by one degenerate ray's chain, not by its tile load")
     ap.add_argument("--strong-parts", type=int, default=1,
                     help="tile-interleaved parts per rank of the strong-scaling tile layouts (see --strong-slots)")
     ap.add_argument("--no-spp-aux", action="store_true",

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Strong-scaling prediction on ONE GPU (VERDICT r3 "Next 1"): replays, one rank at a
 time, exactly the launches every rank of an N-GPU strong-scaling run issues -- its 64x64 round-robin
-tiles (dealt longest-processing-time first by sample 0's tile costs, --deal lpt, or round-robin) as P
+tiles (dealt round-robin, or longest-processing-time first by sample 0's tile costs with --deal lpt) as P
 tile-interleaved parts x F frame slots, every slot its own jittered sample (ttlayout.FrameLayout, the layout
 bench.py runs for the N > 1 headline / aux_c5_tiles) -- and predicts
 
@@ -40,9 +40,9 @@ def main():
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to replay per N")
     ap.add_argument("--tile", type=int, default=64, help="screen tile edge of the round-robin sharding")
     ap.add_argument("--n1-slots", type=int, default=3, help="frame slots of the N = 1 one-launch reference")
-    ap.add_argument("--deal", choices=["rr", "lpt"], default="lpt",
-                    help="tile deal at N > 1: lpt (bench.py's default: longest-processing-time first by sample 0's tile "
-                         "costs, tt_trace_chunk_costs) or rr (round-robin)")
+    ap.add_argument("--deal", choices=["rr", "lpt"], default="rr",
+                    help="tile deal at N > 1: rr (round-robin, bench.py's default) or lpt (longest-processing-time first "
+                         "by sample 0's tile costs, tt_trace_chunk_costs)")
     ap.add_argument("--slot-stride", type=int, default=1,
                     help="slot f traces sample f * stride (bench.py: 1, every frame in flight its own jitter; 0: one "
                          "sample replicated in every slot, rounds 1-4)")
