@@ -5,7 +5,7 @@ the kernel executes it.
 
 Inputs (no GPU needed):
   * the ISA of csrc/tt_trace.hip for gfx950 (hipcc -S with line tables, compiled here with the product flags);
-  * per-ray wave executions of the node step and the triangle pass (profiles/r04/diag/diag_blocks_c2.json,
+  * per-ray wave executions of the node step and the triangle pass (profiles/r05/diag/diag_blocks_c2.json,
     tools/diag_blocks.py on the bench's C2 launches);
   * VALU instructions per ray and the busy fractions of the same kernels (profiles/units_latest.json, PMC);
   * per-instruction issue costs measured on gfx950 (profiles/r01_micro_valu_ops.txt, tools/micro/valu_ops.hip:
@@ -91,7 +91,7 @@ def region_of(block):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--isa", default="/tmp/tt_trace_mix.s")
-    ap.add_argument("--diag", default=os.path.join(REPO, "profiles", "r04", "diag", "diag_blocks_c2.json"))
+    ap.add_argument("--diag", default=os.path.join(REPO, "profiles", "r05", "diag", "diag_blocks_c2.json"))
     ap.add_argument("--units", default=os.path.join(REPO, "profiles", "units_latest.json"))
     ap.add_argument("--no-write", action="store_true")
     a = ap.parse_args()
