@@ -541,10 +541,12 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
         f = k % S
         e, b = engs[f], bufs[f]
         t0 = time.perf_counter()
-        e.update_meshdata(0, mds[k & 1])
-        e.tlas_refit(T_, boxes[k & 1], device=True, asynchronous=True)
-        e.generate(b["rays"], c2w, ip, W, H, T.NEAR, far, jitter=1, frames=k, max_bounce=1, device=True,
-                   asynchronous=True)
+        if "noupdate" not in args.dyn_diag:  # (diagnosis: which per-frame call costs what, --dyn-diag)
+            e.update_meshdata(0, mds[k & 1])
+            e.tlas_refit(T_, boxes[k & 1], device=True, asynchronous=True)
+        if "nogen" not in args.dyn_diag or k < S:
+            e.generate(b["rays"], c2w, ip, W, H, T.NEAR, far, jitter=1, frames=k, max_bounce=1, device=True,
+                       asynchronous=True)
         # (the adaptive order on the primaries, INTEGRATION.md §5's advice for scenes beyond the L2s: each slot's
         # launch ordered by its own previous frame -- another pose and jitter)
         e.trace(b["rays"], WH, 0, far, W, H, info=b["i0"], device=True, asynchronous=True,
@@ -609,7 +611,7 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
     finally:
         ref.close()
     return {"slots": S, "frames": reps, "ms_per_frame": round(ms, 4), "mrays_s": round(rays / reps / ms / 1e3, 1),
-            "adaptive_order_primary": bool(args.dyn_adaptive),
+            "adaptive_order_primary": bool(args.dyn_adaptive), "diagnosis": args.dyn_diag or None,
             "rays_per_frame_mean": int(round(rays / reps)), "host_ms_per_frame_median": round(float(np.median(host_ms)), 4),
             "identical_to_serial": bool(same), "checks": diff,
             "note": f"frame k on slot k % {S}, each slot a context with its own TLAS / _MeshData over the shared BLASes "
@@ -967,6 +969,9 @@ def main():
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
     ap.add_argument("--dyn-slots", type=int, default=N1_SLOTS,
                     help="aux dyn: frame slots (contexts with TLASes of their own) of the dynamic-frame leg")
+    ap.add_argument("--dyn-diag", default="",
+                    help="aux dyn frame slots, diagnosis only (the record check then fails by design): comma list of "
+                         "noupdate (no _MeshData rewrite / TLAS refit), nogen (Generate only in each slot's first frame)")
     ap.add_argument("--dyn-adaptive", type=int, default=1,
                     help="aux dyn frame slots: TT_TRACE_ADAPTIVE_ORDER on each slot's primary launch (1, default) or not")
     ap.add_argument("--aux", default="c3,c4,dyn,refit,c5",
