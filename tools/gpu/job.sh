@@ -9,6 +9,7 @@
 #   blocks     the headline per persistent-grid size: BLOCKS="20 16 12" blocks per CU (TT_BLOCKS_PER_CU), REPS
 #   quick      bench without aux configs / CPU baseline (layout and headline only)
 #   dyn        bench headline + the C4 dynamic frame legs (aux dyn), per TT_BLOCKS_PER_CU in BLOCKS (0 = default)
+#   dyndiag    the C4 dynamic frame with per-frame calls left out (DIAGS="none noupdate nogen noupdate,nogen")
 #   slots2     quick with 2 frame slots (frame k + 1's primaries overlap frame k's bounce-1 launches)
 #   layouts    the N = 1 headline per parts x slots layout: LAYOUTS="2x1 2x2 1x3", REPS=2 (profiles/r04/ab/r04k_*)
 #   testlib    the GPU suite with a variant library: LIB=name (lib/variants/libtruetrace_hip_NAME.so)
@@ -25,7 +26,8 @@
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
 #   order      tools/exp_order.py per TT_ORDER_HOT threshold (ORDER_HOT, ORDER_CFGS, ORDER_ARGS)
 #   sweep      randomized parity sweep (tools/parity_sweep.py): SWEEP_N plain + SWEEP_N variants/adaptive + SWEEP_N
-#              degenerate-direction cases from seed SWEEP_SEED
+#              degenerate-direction cases + SWEEP_N frame-slot cases from seed SWEEP_SEED
+#   sweepslots the frame-slot sweep alone (SWEEP_MODES, default "slots": instanced cases also traced by a moved slot)
 #   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
 #   ab         the bench headline per variant: AB_LIBS="product n128 ..." (lib/variants/libtruetrace_hip_NAME.so),
 #              AB_ARGS extra bench.py flags, REPS rounds of the list in turn
@@ -61,6 +63,10 @@ for stage in "$@"; do
              run "dyn_b$b" 400 env TT_BLOCKS_PER_CU=$b python -u bench.py --steps 20 --warmup 5 --aux dyn \
                  --no-cpu-baseline --no-recur --no-shadow ${DYN_ARGS:-} || exit $?
          done ;;
+    dyndiag) for d in ${DIAGS:-none noupdate nogen noupdate,nogen}; do  # the C4 dynamic frame without one per-frame call
+                 run "dyndiag_$d" 400 python -u bench.py --steps 20 --warmup 5 --aux dyn --no-cpu-baseline --no-recur \
+                     --no-shadow --no-oracle-check --dyn-diag "$d" ${DYN_ARGS:-} || exit $?
+             done ;;
     slots2) run slots2 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --slots 2 || exit $? ;;
     layouts) for i in $(seq ${REPS:-2}); do for l in ${LAYOUTS:-2x1 2x2 1x3}; do  # N = 1 headline per parts x slots
                  run "n1_${l}_$i" 300 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --no-recur \
@@ -104,7 +110,10 @@ for stage in "$@"; do
     sweep) n=${SWEEP_N:-300}; s0=${SWEEP_SEED:-40000}  # plain; trace variants + adaptive order; + degenerate directions
            run sweep_plain 900 python -u tools/parity_sweep.py $n $s0 || exit $?
            run sweep_var 900 python -u tools/parity_sweep.py $n $((s0 + 1000)) variants,adaptive || exit $?
-           run sweep_axis 900 python -u tools/parity_sweep.py $n $((s0 + 2000)) axis,variants,adaptive || exit $? ;;
+           run sweep_axis 900 python -u tools/parity_sweep.py $n $((s0 + 2000)) axis,variants,adaptive || exit $?
+           run sweep_slots 900 python -u tools/parity_sweep.py $n $((s0 + 3000)) slots,adaptive || exit $? ;;
+    sweepslots) run sweep_slots 900 python -u tools/parity_sweep.py ${SWEEP_N:-300} ${SWEEP_SEED:-43000} \
+               ${SWEEP_MODES:-slots} || exit $? ;;
     variants) run variants 900 python -u tools/run_variants.py || exit $? ;;
     ab) for i in $(seq ${REPS:-1}); do for v in ${AB_LIBS:-product}; do  # the bench headline per library variant, in turn
             lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so

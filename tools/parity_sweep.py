@@ -34,22 +34,27 @@ ADAPTIVE = "adaptive" in MODES
 # rays with a zero component), and 3% of every case's primary rays get one or two components replaced by
 # +0.0 or -0.0 (inf / NaN slabs in the node test: the C5 bench frame's longest ray is one of these)
 AXIS = "axis" in MODES
+# "slots": every instanced case is also traced by a frame slot (tt_ctx_share_blas) whose instances were all
+# moved (its own _MeshData rewrite + TLAS refit): primary + info, bounce 1 and NEE rays against the oracle on
+# the scene as the slot holds it (its TLAS nodes read back, its _MeshData)
+SLOTS = "slots" in MODES
 FLAG_SETS = (0, tthip.TT_TRACE_IGNORE_GLASS, tthip.TT_TRACE_IGNORE_BACKFACING,
              tthip.TT_TRACE_IGNORE_GLASS | tthip.TT_TRACE_IGNORE_BACKFACING)
 eng = tthip.Engine(0)
 bad_total, rays_total = 0, 0
 
 
-def compare(sc, rays, n, bounce, W, H, info=True, flags=0):
+def compare(sc, rays, n, bounce, W, H, info=True, flags=0, e=None):
+    e = eng if e is None else e
     rg, rc = rays.copy(), rays.copy()
     ig = np.zeros((W * H, 4), np.uint32) if info else None
     ic = np.zeros((W * H, 4), np.uint32) if info else None
     if ADAPTIVE:
         r0 = rays.copy()
-        eng.trace(r0, n, bounce, FAR, W, H, info=None, flags=flags | tthip.TT_TRACE_ADAPTIVE_ORDER)
-        eng.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags | tthip.TT_TRACE_ADAPTIVE_ORDER)
+        e.trace(r0, n, bounce, FAR, W, H, info=None, flags=flags | tthip.TT_TRACE_ADAPTIVE_ORDER)
+        e.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags | tthip.TT_TRACE_ADAPTIVE_ORDER)
     else:
-        eng.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags)
+        e.trace(rg, n, bounce, FAR, W, H, info=ig, flags=flags)
     st, _ = O.trace(sc, rc, n, bounce, FAR, W, H, info=ic, nthreads=CPU_THREADS, flags=flags)
     assert st == 0
     off = W * H if bounce % 2 else 0
@@ -59,14 +64,30 @@ def compare(sc, rays, n, bounce, W, H, info=True, flags=0):
     return bad, rg
 
 
-def shadow_compare(sc, sr, W, H):
+def moved(sc, rng):
+    """sc's _MeshData and instance boxes with every record but the first moved by a random offset."""
+    md = sc.meshdata.copy()
+    box = np.ascontiguousarray(sc.meta["mesh_aabbs"], np.float32).copy()
+    for i in range(1, len(md)):
+        d = rng.normal(0, 1.0, 3)
+        w2l = md["W2L"][i].astype(np.float64).reshape(4, 4).T
+        sh = np.eye(4)
+        sh[:3, 3] = -d
+        md["W2L"][i] = tthip.unity_colmajor(w2l @ sh)
+        box[i, 0:3] += d.astype(np.float32)
+        box[i, 3:6] += d.astype(np.float32)
+    return md, box
+
+
+def shadow_compare(sc, sr, W, H, e=None):
+    e = eng if e is None else e
     n = len(sr)
     out = []
     for side in (0, 1):
         r = sr.copy()
         vis = np.zeros((n, 4), np.float32)
         if side == 0:
-            eng.trace_shadow(r, n, 0, W, H, visibility=vis)
+            e.trace_shadow(r, n, 0, W, H, visibility=vis)
         else:
             assert O.shadow(sc, r, n, 0, W, H, visibility=vis, nthreads=CPU_THREADS)[0] == 0
         out.append((r, vis))
@@ -117,10 +138,31 @@ for k in range(N):
     sr = hb.nee_rays_from_hits(rg, W * H, tuple(rng.uniform(-2, 2, 3) + [0, 3, 0]), seed)
     bs = shadow_compare(sc, sr, W, H) if len(sr) else 0
     n_rays = W * H + nb + len(sr)
+    bsl = 0
+    if SLOTS and kind == "instanced":
+        slot = tthip.Engine(0)
+        try:
+            slot.share_blas(eng, sc.tlas_nodes)
+            md, box = moved(sc, rng)
+            slot.update_meshdata(0, md)
+            slot.tlas_refit(sc.tlas_nodes, box)
+            ss = tthip.Scene(slot.scene_nodes(0, len(sc.nodes)), sc.tris, sc.tlas, md, sc.materials,
+                             tlas_nodes=sc.tlas_nodes)
+            s0, sg = compare(ss, rays, W * H, 0, W, H, flags=flags, e=slot)
+            s1r = sg.copy()
+            snb = slot.enqueue_bounce(s1r, W * H, 0, FAR, W, H, frames=k, max_bounce=2)
+            s1, _ = compare(ss, s1r, snb, 1, W, H, info=False, flags=flags, e=slot) if snb else (0, None)
+            ssr = hb.nee_rays_from_hits(sg, W * H, tuple(rng.uniform(-2, 2, 3) + [0, 3, 0]), seed)
+            ssh = shadow_compare(ss, ssr, W, H, e=slot) if len(ssr) else 0
+            bsl = s0 + s1 + ssh
+            n_rays += W * H + snb + len(ssr)
+        finally:
+            slot.close()
     rays_total += n_rays
-    bad_total += b0 + b1 + bs
+    bad_total += b0 + b1 + bs + bsl
     print(f"case {k:3d} {kind:9s} seed {seed} flags {flags:#04x} tris {len(sc.tris):6d} {W}x{H}: primary+info mismatches {b0}, "
-          f"bounce-1 ({nb} rays) {b1}, shadow ({len(sr)} rays) {bs}", flush=True)
+          f"bounce-1 ({nb} rays) {b1}, shadow ({len(sr)} rays) {bs}" + (f", frame slot {bsl}" if SLOTS and kind == "instanced"
+                                                                          else ""), flush=True)
 print(f"SUMMARY: {N} cases, {rays_total} rays traced on the GPU and the oracle, {bad_total} mismatching records, "
       f"{time.time() - t0:.0f} s", flush=True)
 sys.exit(1 if bad_total else 0)
