@@ -1,6 +1,8 @@
 // tt_api.hip — the C ABI of include/truetrace_hip.h: context lifecycle, scene upload with
 // structural validation, trace dispatch (the kernel_trace replacement) and the normal resolve.
 #include <hip/hip_runtime.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -692,13 +694,15 @@ extern "C" {
 }  // extern "C"
 
 namespace {
-// A profiler that wraps the HIP API (rocprofv3's tool keeps a per-stream table, built lazily by the first
-// kernel launch it sees on a stream) registers that table's destructor when the table is built -- after the
-// exit handler registered at tt_stream_create -- so at exit the table would be gone before the handler's
-// hipStreamDestroy calls reach the wrapper ("'get_stream_stack()' Must be non nullptr"). The handler is
-// registered once more after the first launch on one of the library's streams (note_stream_launch), which
-// puts it ahead of anything built up to then; running it twice is harmless (the first run empties the list).
-std::atomic<bool> g_late_handler{false};
+// A profiler that wraps the HIP API (rocprofv3's tool) keeps per-thread state that its stream calls need
+// ("'get_stream_stack()' Must be non nullptr"), and exit() destroys a thread's thread_local objects BEFORE it
+// runs any atexit handler: from the atexit handler alone, the hipStreamDestroy calls abort under the tool.
+// So the teardown is armed a second way: a thread_local guard, constructed on the first launch on one of the
+// library's streams (after the tool's own per-thread state exists, so destroyed before it: glibc runs a
+// thread's TLS destructors in reverse order of construction), whose destructor tears the streams down when
+// the MAIN thread's thread_locals are destroyed -- i.e. from exit() -- and does nothing when another thread
+// ends (the process goes on). The atexit handler stays for a process whose launches all came from other
+// threads; a second run finds the list empty.
 bool stream_exit_handler_on() {
     static const bool on = [] {  // TT_STREAM_EXIT_HANDLER=0: diagnosis only (the exit-time teardown off)
         const char* e = std::getenv("TT_STREAM_EXIT_HANDLER");
@@ -706,15 +710,22 @@ bool stream_exit_handler_on() {
     }();
     return on;
 }
+struct MainThreadExitGuard {
+    ~MainThreadExitGuard() {
+        if ((pid_t)syscall(SYS_gettid) == getpid()) release_live_streams();
+    }
+};
 void note_stream_launch(hipStream_t s) {
-    if (g_late_handler.load(std::memory_order_relaxed) || !stream_exit_handler_on()) return;
-    std::lock_guard<std::mutex> lk(g_streams_mu);
-    if (g_late_handler.load(std::memory_order_relaxed)) return;
-    for (auto& ds : g_streams)
-        if (ds.second == s) {
-            g_late_handler = std::atexit(release_live_streams) == 0;
-            break;
-        }
+    thread_local bool armed = false;
+    if (armed || !stream_exit_handler_on()) return;
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        if (std::none_of(g_streams.begin(), g_streams.end(), [s](const std::pair<int, hipStream_t>& ds) { return ds.second == s; }))
+            return;
+    }
+    armed = true;
+    thread_local MainThreadExitGuard guard;
+    (void)&guard;
 }
 }  // namespace
 
