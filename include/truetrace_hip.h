@@ -224,9 +224,11 @@ int32_t tt_device_count(void);
 tt_status tt_stream_create(int32_t device, void** stream);
 /* Synchronises and destroys a stream tt_stream_create made; TT_ERR_INVALID_ARG for any other handle
  * (or one destroyed already). Streams still alive when the process exits are synchronised and
- * destroyed by the library from an exit handler that runs before the HIP runtime's own teardown (a
- * CU-mask queue alive at that point crashes the exit, SIGSEGV in __cxa_finalize), so a host that
- * exits without tt_stream_destroy -- or a Unity domain reload that skips it -- ends cleanly. */
+ * destroyed by the library before the HIP runtime's own teardown (a CU-mask queue alive at that point
+ * crashes the exit, SIGSEGV in __cxa_finalize): from the main thread's thread_local destructors (armed by
+ * the first launch on such a stream, so they also run ahead of a profiler's per-thread state, e.g. under
+ * rocprofv3) and, for launches made only from other threads, from an atexit handler. A host that exits
+ * without tt_stream_destroy -- or a Unity domain reload that skips it -- ends cleanly. */
 tt_status tt_stream_destroy(void* stream);
 /* Streams made by tt_stream_create and not destroyed yet. */
 uint32_t tt_stream_live_count(void);

@@ -20,7 +20,7 @@
 #   diag       per-block execution counts (TT_DIAG_BLOCKS build, tools/diag_blocks.py)
 #   replay     strong-scaling replay of every rank's N-GPU shard on this GPU (tools/strong_replay.py; REPLAY_ARGS)
 #   replaykt   the same replay under rocprofv3 --kernel-trace (REPLAY_ARGS; per-rank launch overlap)
-#   lifecycle  the GPU tests of stream teardown, root-leaf bookkeeping and the timed kernels' jittered parity
+#   lifecycle  the GPU tests of stream teardown (rocprofv3 leg included), root-leaf bookkeeping and the timed kernels' jittered parity
 #   gloo2      the 2-rank bench rehearsal on this GPU (gloo collectives, C5 tiles included)
 #   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
