@@ -28,7 +28,9 @@ compared with the oracle traced from the same pre-state (``oracle_check``, ``ora
 Streams: torch and the engine share ONE stream (a torch.cuda.Stream made current before any
 allocation and passed to tt_ctx_create), so every torch copy / collective and every engine launch
 is ordered, and every per-launch time comes from HIP events on that stream (the engine's own
-timing ring, tt_timing_read).
+timing ring, tt_timing_read). Only one context of a frame layout records them (tt_ctx_set_timing: the
+markers cost ~5% of a strong-scaled rank's frame), and at N > 1 none inside the timed region: the launch
+times then come from K more steps right after it.
 """
 from __future__ import annotations
 
@@ -173,6 +175,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 e1 = tthip.Engine(dev.index, stream=streams[-1].cuda_stream)
                 extra_engs.append(e1)
                 e1.share_scene(eng)  # one scene copy for all parts (tt_ctx_share_scene)
+                e1.set_timing(False)  # (wall clock; no per-launch markers, tt_ctx_set_timing)
             chains = [[] for _ in range(n_frames)]  # chains[f]: per part (engine, bufs, counts)
             base = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
             for f in range(n_frames):
@@ -233,6 +236,7 @@ def aux_configs(torch, tthip, eng, dev, args, which):
             for f in range(1, N1_SLOTS):
                 e1 = tthip.Engine(dev.index, stream=tthip.dedicated_stream(torch, dev, f - 1).cuda_stream)
                 e1.share_scene(eng)
+                e1.set_timing(False)  # (wall clock; no per-launch markers, tt_ctx_set_timing)
                 engs.append(e1)
             for f, e in enumerate(engs):
                 chains.append((e, [([b.clone() for b in bufs] if f else bufs, counts) for bufs, counts in fr],
@@ -526,6 +530,7 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
         st = tthip.dedicated_stream(torch, dev, f - 1)
         e = tthip.Engine(dev.index, stream=st.cuda_stream)
         e.share_blas(eng, T_)
+        e.set_timing(False)  # (wall clock; no per-launch markers, tt_ctx_set_timing)
         engs.append(e)
         streams.append(st)
     bufs = [dict(rays=torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev),
@@ -860,9 +865,10 @@ def free_port() -> int:
 def launch_ranks(n: int, argv, timeout=None) -> int:
     """`bench.py --gpus N` without a launcher: starts N rank processes of this script (one per GPU,
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, as torchrun would),
-    before this process touches the GPU. Rank 0 prints the JSON line. Returns the worst exit code
-    (a rank killed by a signal counts as 128 + signal); once one rank fails the others are
-    terminated so none is left blocked in a collective."""
+    before this process touches the GPU. Rank 0 prints the JSON line. Returns the first failing rank's
+    exit code (a rank killed by a signal counts as 128 + signal), 0 when all succeed; once one rank
+    fails the others get a few seconds to finish, then are terminated so none is left blocked in a
+    collective (the ranks terminated that way do not mask the first failure's code)."""
     import signal
     import subprocess
 
@@ -876,11 +882,15 @@ def launch_ranks(n: int, argv, timeout=None) -> int:
     log(f"launched {n} ranks (pids {[p.pid for p in procs]}), master 127.0.0.1:{port}")
     t0 = time.time()
     rcs = [None] * n
+    first_fail = None
+    t_fail = None
     while any(rc is None for rc in rcs):
         for i, p in enumerate(procs):
             if rcs[i] is None:
                 rcs[i] = p.poll()
-        failed = [rc for rc in rcs if rc not in (None, 0)]
+                if rcs[i] not in (None, 0) and first_fail is None:
+                    first_fail, t_fail = rcs[i], time.time()
+        failed = first_fail is not None and time.time() - t_fail > 5.0  # (a grace period to finish)
         late = timeout is not None and time.time() - t0 > timeout
         if (failed or late) and any(rc is None for rc in rcs):
             log(f"rank exit codes {rcs}{' (timeout)' if late else ''}: terminating the remaining ranks")
@@ -898,9 +908,10 @@ def launch_ranks(n: int, argv, timeout=None) -> int:
                 rcs = [rc if rc else 124 for rc in rcs]
             break
         time.sleep(0.2)
-    codes = [(128 - rc) if rc < 0 else rc for rc in rcs]  # Popen: -signal for a killed child
+    code = lambda rc: (128 - rc) if rc < 0 else rc  # Popen: -signal for a killed child
+    codes = [code(rc) for rc in rcs]
     log(f"rank exit codes {codes}")
-    return max(codes)
+    return code(first_fail) if first_fail is not None else max(codes)
 
 
 def main():
@@ -1240,7 +1251,16 @@ def main():
     G = layout.attach_gather(dist, world, rank, red_dev) if tiles else None
     # (the gloo rehearsal's host-side collective blocks the host in the copy, so there it serialises)
     gather_overlapped = tiles and red_dev.type == "cuda"
+    # N > 1: no per-launch timing markers inside the timed region (at a rank's 1/N shard they cost ~5% of
+    # the frame, profiles/r05/events/); the launch times below come from K more steps right after it
+    layout.time_none = world > 1
     elapsed = timed(layout)
+    if world > 1:
+        layout.time_none = False
+        layout.timing_reset()
+        for _ in range(args.steps):
+            layout.step()
+        torch.cuda.synchronize(dev)
     lm = layout.launch_ms()  # part 0's launches, the last <= 128 frames of its slot
     launch_ms = lm.reshape(-1)
     total_rays = float(layout.timed_rays)

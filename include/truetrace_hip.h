@@ -500,6 +500,12 @@ tt_status tt_trace_chunk_costs(tt_ctx* ctx, int32_t bounce, uint32_t* costs, uin
  * Synchronizes. */
 tt_status tt_timing_reset(tt_ctx* ctx);
 tt_status tt_timing_read(tt_ctx* ctx, float* ms, uint32_t max, uint32_t* n);
+/* Per-call timing on (default) or off. Off: asynchronous calls (TT_TRACE_ASYNC, device-resident counts)
+ * record no HIP events and add no entry; synchronous trace calls still time their kernel (stats->kernel_ms).
+ * Each timed call puts two stream-ordered event markers around its kernel, which costs little beside a
+ * whole-frame launch but ~15-20% of a strong-scaled rank's small launches (profiles/r05/events/): a host
+ * with several frames in flight keeps timing on for the one context it measures, if any. */
+tt_status tt_ctx_set_timing(tt_ctx* ctx, int32_t enabled);
 
 /* SIMD-efficiency diagnostics of the last synchronous TT_TRACE_STATS launch: wave loop
  * iterations, iterations with node-phase work, node-phase lanes, iterations with triangle-phase

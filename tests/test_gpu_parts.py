@@ -241,6 +241,125 @@ def test_shared_scene_mutations_are_ordered_without_host_sync():
     assert borrower.h is None
 
 
+def test_shared_scene_sections_from_two_threads():
+    """The lender and a borrower driven from two host threads at once: the lender flips
+    the pose (update_meshdata + a device tlas_refit, asynchronous) while the borrower issues asynchronous
+    traces, none waiting on the host. The library holds the lender's mutex across each read / write
+    section, so every borrower trace sees the scene between two whole calls: its records equal those of
+    one of the four states the lender passes through ((_MeshData, TLAS boxes) of pose a / b: a+a, b+a after
+    the records' rewrite, b+b after the refit, a+b, ...) exactly.
+    The borrower records no event per launch (tt_api.hip SceneRead); the lender records one on the
+    borrower's stream per mutation."""
+    import threading
+
+    import torch
+
+    from test_gpu_parity import refit_scene
+
+    rng = np.random.default_rng(11)
+    a = refit_scene(34)
+    b = refit_scene(34, offsets=rng.normal(0, 1.5, (120, 3)))
+    dev = torch.device("cuda:0")
+    W, H = 160, 90
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, 0.3, FAR)
+    boxes = {k: torch.from_numpy(np.ascontiguousarray(s.meta["mesh_aabbs"], np.float32)).to(dev)
+             for k, s in (("a", a), ("b", b))}
+    md = {"a": a.meshdata, "b": b.meshdata}
+    ref = tthip.Engine(0)
+    try:
+        ref.upload(a)
+        rays0 = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        ref.generate(rays0, c2w, ip, W, H, 0.3, FAR, jitter=1, frames=0, max_bounce=1, device=True)
+        exp = {}
+        for km in ("a", "b"):
+            for kb in ("a", "b"):
+                ref.update_meshdata(0, md[km])
+                ref.tlas_refit(a.tlas_nodes, boxes[kb], device=True)
+                r = rays0.clone()
+                torch.cuda.synchronize(dev)
+                ref.trace(r, W * H, 0, FAR, W, H, device=True)
+                exp[km + kb] = r.view(-1, 48)[: W * H, 32:48].clone()
+        assert not torch.equal(exp["aa"], exp["bb"])
+    finally:
+        ref.close()
+    owned = [tthip.DedicatedStream(torch, dev) for _ in range(2)]
+    lender = tthip.Engine(0, stream=owned[0].stream.cuda_stream)
+    borrower = tthip.Engine(0, stream=owned[1].stream.cuda_stream)
+    n_traces = 40
+    outs = [rays0.clone() for _ in range(n_traces)]
+    errors = []
+    try:
+        lender.upload(a)
+        lender.update_meshdata(0, md["a"])
+        lender.tlas_refit(a.tlas_nodes, boxes["a"], device=True)
+        borrower.share_scene(lender)
+        torch.cuda.synchronize(dev)
+
+        def mutate():
+            try:
+                for i in range(n_traces):
+                    k = "b" if i % 2 == 0 else "a"
+                    lender.update_meshdata(0, md[k])
+                    lender.tlas_refit(a.tlas_nodes, boxes[k], device=True, asynchronous=True)
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errors.append(e)
+
+        def trace():
+            try:
+                for r in outs:
+                    borrower.trace(r, W * H, 0, FAR, W, H, device=True, asynchronous=True)
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        th = [threading.Thread(target=mutate), threading.Thread(target=trace)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize(dev)
+        assert not errors, errors
+        for i, r in enumerate(outs):
+            got = r.view(-1, 48)[: W * H, 32:48]
+            assert any(torch.equal(got, v) for v in exp.values()), f"trace {i} saw a torn scene"
+    finally:
+        lender.close()
+        for d in owned:
+            d.close()
+
+
+def test_timing_switch():
+    """tt_ctx_set_timing: off, asynchronous traces add no timing entry (no HIP-event markers); synchronous
+    traces still report their kernel time; on again, asynchronous traces are timed."""
+    import torch
+
+    dev = torch.device("cuda:0")
+    sc = tthip.single_object_scene(tthip.Mesh.soup(5, 4000, 1.0, 0.1))
+    W, H = 128, 64
+    c2w, ip = tthip.unity_camera((0.2, 0.3, 3.0), (-0.05, -0.1, -1.0), (0, 1, 0), 50.0, W, H, 0.05, FAR)
+    e = tthip.Engine(0)
+    try:
+        e.upload(sc)
+        rays = torch.zeros(2 * W * H * 48, dtype=torch.uint8, device=dev)
+        e.generate(rays, c2w, ip, W, H, 0.05, FAR, jitter=1, frames=0, max_bounce=1, device=True)
+        torch.cuda.synchronize(dev)
+        e.timing_reset()
+        e.set_timing(False)
+        for _ in range(3):
+            e.trace(rays, W * H, 0, FAR, W, H, device=True, asynchronous=True)
+        assert len(e.timing_read()) == 0
+        s = e.trace(rays, W * H, 0, FAR, W, H, device=True, stats=True)
+        assert s.kernel_ms > 0 and len(e.timing_read()) == 1
+        e.set_timing(True)
+        e.timing_reset()
+        for _ in range(3):
+            e.trace(rays, W * H, 0, FAR, W, H, device=True, asynchronous=True)
+        ms = e.timing_read()
+        assert len(ms) == 3 and (ms > 0).all()
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("stride", [0, 1])
 def test_frame_slots_equal_one_launch(stride):
     """bench.py's N = 1 layout (ttlayout.FrameLayout: the whole frame as one launch per bounce, 3 frames in

@@ -62,6 +62,8 @@ def main():
            "tile": args.tile, "steps": args.steps, "deal": args.deal, "slot_stride": args.slot_stride, "configs": {}}
 
     def frame_ms(lay):
+        # as bench.py at N > 1: no per-launch timing markers in the timed frames (tt_ctx_set_timing)
+        lay.time_none = not os.environ.get("TT_REPLAY_TIMED_SLOT")
         for _ in range(args.warmup):
             lay.step()
         torch.cuda.synchronize(dev)

@@ -124,6 +124,7 @@ struct tt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // last launch (aliases into the ring)
     hipEvent_t ring0[256] = {}, ring1[256] = {};
     uint32_t ring_n = 0, ring_base = 0;
+    bool timing = true;  // tt_ctx_set_timing: asynchronous launches record their HIP-event pair
     std::string err;
     // scene
     bool has_scene = false;
@@ -220,15 +221,17 @@ struct tt_ctx {
     // already enqueued, and a borrower launch waits for the lender's mutations already enqueued. An
     // overlay borrower reads only the lender's BLAS part, so it orders only against BLAS-side mutations.
     // The lender's share state below (and its host node 0, which plain borrowers read for TT_ROOT_LEAF) is
-    // guarded by `mu`, so a lender and its borrowers may be driven from different host threads.
-    std::mutex mu;
+    // guarded by `mu`, so a lender and its borrowers may be driven from different host threads; `mu` is held
+    // across each read / write section (SceneRead / SceneWrite), so their enqueues are atomic against each
+    // other. Recursive: a section's own calls (the root-leaf copy, the refit's bookkeeping) lock it again.
+    std::recursive_mutex mu;
     std::vector<tt_ctx*> borrower_list;  // lender: the contexts tracing its scene
     hipEvent_t ev_scene = nullptr;       // lender: after its last scene mutation (recorded while borrowed)
     uint64_t scene_mut = 0;              // lender: mutations recorded in ev_scene so far
     hipEvent_t ev_blas = nullptr;        // lender: after its last BLAS-side mutation (overlay borrowers wait)
     uint64_t blas_mut = 0;               // lender: BLAS-side mutations recorded in ev_blas so far
-    hipEvent_t ev_read = nullptr;        // borrower: after its last launch that reads the shared scene
-    uint64_t read_seq = 0;               // borrower: reads recorded in ev_read so far
+    hipEvent_t ev_read = nullptr;        // borrower: recorded on its stream by a lender mutation (SceneWrite)
+    uint64_t read_seq = 0;               // borrower: read sections enqueued so far
     uint64_t read_waited = 0;            // borrower: reads the lender's stream already waits for
     uint64_t mut_waited = 0;             // borrower: lender mutations this stream already waits for
 };
@@ -250,11 +253,15 @@ struct tt_ctx {
     } while (0)
 
 // Per-call timing ring entries (tt_timing_read) around device work issued on the context stream.
+// (with timing off -- tt_ctx_set_timing -- the calls that use these record nothing: they are all asynchronous
+// or report no kernel time)
 static hipError_t ring_open(tt_ctx* c, uint32_t& slot) {
     slot = c->ring_n % TT_RING;
+    if (!c->timing) return hipSuccess;
     return hipEventRecord(c->ring0[slot], c->stream);
 }
 static hipError_t ring_close(tt_ctx* c, uint32_t slot) {
+    if (!c->timing) return hipSuccess;
     const hipError_t e = hipEventRecord(c->ring1[slot], c->stream);
     c->ring_n++;
     c->ev0 = c->ring0[slot];
@@ -262,57 +269,90 @@ static hipError_t ring_close(tt_ctx* c, uint32_t slot) {
     return e;
 }
 
-// Shared-scene ordering (tt_ctx_share_scene). A borrower's launch that reads the lender's scene
-// buffers is bracketed by scene_read_begin / _end, a lender's scene mutation by scene_write_begin /
-// _end. Events are only waited on when something new was recorded since the last wait, so a borrower
-// of a static scene adds one event record per launch and no waits.
+// Shared-scene ordering (tt_ctx_share_scene / tt_ctx_share_blas). A borrower's enqueues that read the
+// lender's scene buffers form a read section, a lender's scene mutation a write section; both hold the
+// lender's mutex from first to last enqueue, so sections of the contexts sharing one scene are atomic
+// against each other whichever host threads drive them. A read section makes the borrower's stream wait
+// for the lender mutations enqueued before it (one wait per new mutation) and counts one read. A write
+// section makes the lender's stream wait for every borrower stream with reads counted since the last such
+// wait, by recording an event on that stream right then -- one record per borrower per mutation and
+// nothing per launch (round 5 recorded one after every borrower launch: with the launch-timing pair, the
+// per-launch markers cost 15-20% of a strong-scaled rank's frame, profiles/r05/events/) -- and, at its end,
+// records the mutation for later readers. An overlay borrower (tt_ctx_share_blas) reads only the lender's
+// BLAS part, so it orders only against BLAS-side mutations.
 static hipError_t lazy_event(hipEvent_t& ev) {
     return ev ? hipSuccess : hipEventCreateWithFlags(&ev, hipEventDisableTiming);
 }
-static hipError_t scene_read_begin(tt_ctx* c) {
-    tt_ctx* L = c->lender;
-    if (!L) return hipSuccess;
-    std::lock_guard<std::mutex> lk(L->mu);
-    const uint64_t seq = c->ovl ? L->blas_mut : L->scene_mut;
-    if (seq == c->mut_waited) return hipSuccess;
-    const hipError_t e = hipStreamWaitEvent(c->stream, c->ovl ? L->ev_blas : L->ev_scene, 0);
-    if (e == hipSuccess) c->mut_waited = seq;
-    return e;
-}
-static hipError_t scene_read_end(tt_ctx* c) {
-    tt_ctx* L = c->lender;
-    if (!L) return hipSuccess;
-    std::lock_guard<std::mutex> lk(L->mu);
-    hipError_t e = lazy_event(c->ev_read);
-    if (e == hipSuccess) e = hipEventRecord(c->ev_read, c->stream);
-    if (e == hipSuccess) c->read_seq++;
-    return e;
-}
+class SceneRead {
+  public:
+    explicit SceneRead(tt_ctx* c) : L_(c->lender) {
+        if (!L_) return;
+        L_->mu.lock();
+        const uint64_t seq = c->ovl ? L_->blas_mut : L_->scene_mut;
+        if (seq != c->mut_waited) {
+            err = hipStreamWaitEvent(c->stream, c->ovl ? L_->ev_blas : L_->ev_scene, 0);
+            if (err == hipSuccess) c->mut_waited = seq;
+        }
+        c->read_seq++;
+    }
+    SceneRead(const SceneRead&) = delete;
+    SceneRead& operator=(const SceneRead&) = delete;
+    ~SceneRead() { end(); }
+    void end() {
+        if (L_) L_->mu.unlock();
+        L_ = nullptr;
+    }
+    hipError_t err = hipSuccess;
+
+  private:
+    tt_ctx* L_;
+};
 // blas: the mutation touches what overlay borrowers read too (BLAS nodes, triangles); otherwise only the
-// lender's TLAS-side state (TLAS nodes, _MeshData), which only plain borrowers read.
-static hipError_t scene_write_begin(tt_ctx* c, bool blas) {
-    std::lock_guard<std::mutex> lk(c->mu);
-    for (tt_ctx* b : c->borrower_list) {
-        if (b->read_seq == b->read_waited || (b->ovl && !blas)) continue;
-        const hipError_t e = hipStreamWaitEvent(c->stream, b->ev_read, 0);
-        if (e != hipSuccess) return e;
-        b->read_waited = b->read_seq;
+// lender's TLAS-side state (TLAS nodes, _MeshData), which only plain borrowers read. active = false: no
+// section (an overlay borrower's own TLAS-side state is read by nobody else).
+class SceneWrite {
+  public:
+    SceneWrite(tt_ctx* c, bool blas, bool active = true) : c_(active ? c : nullptr), blas_(blas) {
+        if (!c_) return;
+        c_->mu.lock();
+        for (tt_ctx* b : c_->borrower_list) {
+            if (b->read_seq == b->read_waited || (b->ovl && !blas_)) continue;
+            if ((err = lazy_event(b->ev_read)) != hipSuccess || (err = hipEventRecord(b->ev_read, b->stream)) != hipSuccess ||
+                (err = hipStreamWaitEvent(c_->stream, b->ev_read, 0)) != hipSuccess)
+                return;
+            b->read_waited = b->read_seq;
+        }
     }
-    return hipSuccess;
-}
-static hipError_t scene_write_end(tt_ctx* c, bool blas) {
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (c->borrower_list.empty()) return hipSuccess;  // a later borrower syncs the stream when it shares
-    hipError_t e = lazy_event(c->ev_scene);
-    if (e == hipSuccess) e = hipEventRecord(c->ev_scene, c->stream);
-    if (e == hipSuccess) c->scene_mut++;
-    if (e == hipSuccess && blas) {
-        e = lazy_event(c->ev_blas);
-        if (e == hipSuccess) e = hipEventRecord(c->ev_blas, c->stream);
-        if (e == hipSuccess) c->blas_mut++;
+    SceneWrite(const SceneWrite&) = delete;
+    SceneWrite& operator=(const SceneWrite&) = delete;
+    ~SceneWrite() {
+        if (c_) c_->mu.unlock();
     }
-    return e;
-}
+    // after the mutation is enqueued: records it for the borrowers (a later borrower syncs the stream when
+    // it shares, so nothing is recorded without one) and leaves the section
+    hipError_t end() {
+        if (!c_) return hipSuccess;
+        hipError_t e = hipSuccess;
+        if (!c_->borrower_list.empty()) {
+            e = lazy_event(c_->ev_scene);
+            if (e == hipSuccess) e = hipEventRecord(c_->ev_scene, c_->stream);
+            if (e == hipSuccess) c_->scene_mut++;
+            if (e == hipSuccess && blas_) {
+                e = lazy_event(c_->ev_blas);
+                if (e == hipSuccess) e = hipEventRecord(c_->ev_blas, c_->stream);
+                if (e == hipSuccess) c_->blas_mut++;
+            }
+        }
+        c_->mu.unlock();
+        c_ = nullptr;
+        return e;
+    }
+    hipError_t err = hipSuccess;
+
+  private:
+    tt_ctx* c_;
+    bool blas_;
+};
 // The node array the kernels read: the reference's (80-B stride) or its strided copy, refreshed on the
 // context stream after every write to `nodes` (nodes [first, first + count)).
 static const uint4* kernel_nodes(const tt_ctx* c) {
@@ -326,7 +366,7 @@ static hipError_t refresh_node_copy(tt_ctx* c, uint32_t first, uint32_t count) {
 static void unlink_borrower(tt_ctx* b) {
     tt_ctx* L = b->lender;
     if (!L) return;
-    std::lock_guard<std::mutex> lk(L->mu);
+    std::lock_guard<std::recursive_mutex> lk(L->mu);
     L->borrowers--;
     L->borrower_list.erase(std::remove(L->borrower_list.begin(), L->borrower_list.end(), b), L->borrower_list.end());
     if (b->ovl) L->ovl_used &= ~(1u << b->ovl_slot);
@@ -942,6 +982,12 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     return TT_OK;
 }
 
+tt_status tt_ctx_set_timing(tt_ctx* c, int32_t enabled) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    c->timing = enabled != 0;
+    return TT_OK;
+}
+
 tt_status tt_timing_reset(tt_ctx* c) {
     if (!c) return TT_ERR_INVALID_ARG;
     TT_HIP(c, hipStreamSynchronize(c->stream));
@@ -1184,7 +1230,7 @@ tt_status share_begin(tt_ctx* dst, tt_ctx* src) {
 }
 
 void share_link(tt_ctx* dst, tt_ctx* src) {
-    std::lock_guard<std::mutex> lk(src->mu);
+    std::lock_guard<std::recursive_mutex> lk(src->mu);
     dst->has_scene = true;
     dst->scene_gen++;
     dst->lender = src;
@@ -1228,7 +1274,7 @@ tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
                     n_tlas_nodes, src->tlas_res);
     uint32_t slot = TT_TLAS_SLOTS;
     if (src->has_scene && !src->lender) {
-        std::lock_guard<std::mutex> lk(src->mu);
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
         for (uint32_t k = 0; k < TT_TLAS_SLOTS; k++)
             if (!((src->ovl_used >> k) & 1u)) {
                 slot = k;
@@ -1244,7 +1290,7 @@ tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
     // the TLAS-side state, as the device holds it now (a device TLAS refit leaves src's host copy stale)
     SceneHost& h = dst->host;
     {
-        std::lock_guard<std::mutex> lk(src->mu);
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
         copy_host_light(h, src->host);
         h.tlas = src->host.tlas;
         h.mesh = src->host.mesh;
@@ -1253,7 +1299,7 @@ tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
     h.nodes.resize(n_tlas_nodes);
     TT_HIP(dst, hipMemcpy(h.nodes.data(), src->nodes.p, sizeof(tt_cwbvh_node) * n_tlas_nodes, hipMemcpyDeviceToHost));
     {
-        std::lock_guard<std::mutex> lk(src->mu);
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
         Validator v(h, src->host);
         if (!v.walk(0, 0, 0, true))
             return fail(dst, TT_ERR_INVALID_ARG, "tt_ctx_share_blas: the TLAS leaves [0, %u): %s", n_tlas_nodes, v.why.c_str());
@@ -1312,16 +1358,17 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
         d_boxes = c->st_boxes.p;
     }
     uint32_t slot;
-    if (!c->ovl) TT_HIP(c, scene_write_begin(c, false));  // (an overlay's TLAS is read by nobody else)
+    SceneWrite sw(c, false, !c->ovl);  // (an overlay's TLAS is read by nobody else)
+    TT_HIP(c, sw.err);
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p + c->tlas_base, c->stream));
     TT_HIP(c, refresh_node_copy(c, 0, n_tlas_nodes));
     {
-        std::lock_guard<std::mutex> lk(c->mu);
+        std::lock_guard<std::recursive_mutex> lk(c->mu);
         c->root_known = false;  // node 0 was rewritten on the device
     }
     TT_HIP(c, ring_close(c, slot));
-    if (!c->ovl) TT_HIP(c, scene_write_end(c, false));
+    TT_HIP(c, sw.end());
     if (!(flags & TT_TRACE_ASYNC) || !(flags & TT_TRACE_DEVICE_PTRS)) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1394,13 +1441,14 @@ tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* v
     a.tris88 = c->tris_raw.p + tri_base;
     a.tripos = c->tris.p + tri_base;
     uint32_t slot;
-    TT_HIP(c, scene_write_begin(c, true));
+    SceneWrite sw(c, true);
+    TT_HIP(c, sw.err);
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_blas_construct(a, c->stream));
     TT_HIP(c, tt_refit_run(R.dev, R.boxes.p, nullptr, c->nodes.p + node_base, c->stream));
     TT_HIP(c, refresh_node_copy(c, node_base, R.n_nodes));
     TT_HIP(c, ring_close(c, slot));
-    TT_HIP(c, scene_write_end(c, true));
+    TT_HIP(c, sw.end());
     if (!(p->flags & TT_TRACE_ASYNC) || !dev) TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1411,8 +1459,10 @@ tt_status tt_scene_read_tris(tt_ctx* c, uint32_t first, uint32_t count, tt_cuda_
     if (!out || (uint64_t)first + count > c->host.n_tris)
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_tris: range out of bounds");
     TT_HIP(c, hipSetDevice(c->device));
-    TT_HIP(c, scene_read_begin(c));
+    SceneRead sr(c);
+    TT_HIP(c, sr.err);
     TT_HIP(c, hipMemcpyAsync(out, c->tris_raw.p + first, sizeof(tt_cuda_triangle) * count, hipMemcpyDeviceToHost, c->stream));
+    sr.end();
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1423,7 +1473,8 @@ tt_status tt_scene_read_nodes(tt_ctx* c, uint32_t first, uint32_t count, tt_cwbv
     if (!out || (uint64_t)first + count > c->n_nodes_scene)
         return fail(c, TT_ERR_INVALID_ARG, "tt_scene_read_nodes: range out of bounds");
     TT_HIP(c, hipSetDevice(c->device));
-    TT_HIP(c, scene_read_begin(c));
+    SceneRead sr(c);
+    TT_HIP(c, sr.err);
     // the scene as this context traces it: an overlay borrower's TLAS nodes [0, n_tlas_own) from its region
     const uint32_t own_end = c->ovl ? std::max(first, std::min(first + count, c->n_tlas_own)) : first;
     if (own_end > first)
@@ -1432,6 +1483,7 @@ tt_status tt_scene_read_nodes(tt_ctx* c, uint32_t first, uint32_t count, tt_cwbv
     if (first + count > own_end)
         TT_HIP(c, hipMemcpyAsync(out + (own_end - first), c->nodes.p + own_end,
                                  sizeof(tt_cwbvh_node) * (first + count - own_end), hipMemcpyDeviceToHost, c->stream));
+    sr.end();
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1511,7 +1563,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     tt_ctx* L = c->ovl ? c->lender : nullptr;
     bool tlas_only = true, blas_side = false;
     {
-        std::lock_guard<std::mutex> lk(L ? L->mu : c->mu);  // the nodes the walks read; node 0 (TT_ROOT_LEAF)
+        std::lock_guard<std::recursive_mutex> lk(L ? L->mu : c->mu);  // the nodes the walks read; node 0 (TT_ROOT_LEAF)
         std::vector<tt_cwbvh_node> saved(h.nodes.begin() + first, h.nodes.begin() + first + count);
         std::copy(nodes, nodes + count, h.nodes.begin() + first);
         // A rewrite of TLAS-level nodes only (the per-frame case: BVH8AggregatedBuffer.SetData of the
@@ -1552,12 +1604,13 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, hipSetDevice(c->device));
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, nodes, sizeof(tt_cwbvh_node) * count, pinned));
-    if (!c->ovl) TT_HIP(c, scene_write_begin(c, blas_side));
+    SceneWrite sw(c, blas_side, !c->ovl);
+    TT_HIP(c, sw.err);
     TT_HIP(c, hipMemcpyAsync(c->nodes.p + c->tlas_base + first, pinned, sizeof(tt_cwbvh_node) * count,
                              hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
     TT_HIP(c, refresh_node_copy(c, first, count));
-    if (!c->ovl) TT_HIP(c, scene_write_end(c, blas_side));
+    TT_HIP(c, sw.end());
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
     return TT_OK;
 }
@@ -1588,7 +1641,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
         if (std::binary_search(h.blas_ok.begin(), h.blas_ok.end(), k) ||
             std::find(added.begin(), added.end(), k) != added.end())
             continue;
-        std::lock_guard<std::mutex> lk(L ? L->mu : c->mu);
+        std::lock_guard<std::recursive_mutex> lk(L ? L->mu : c->mu);
         Validator v = L ? Validator(h, L->host) : Validator(h);
         if (!v.walk_mesh(r))
             return fail(c, TT_ERR_INVALID_ARG, "scene validation failed after meshdata update: %s", v.why.c_str());
@@ -1608,7 +1661,8 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     // (MeshGpu) and patches the TLAS leaf records that name an updated mesh, on the stream
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, md, sizeof(tt_mesh_data) * count, pinned));
-    if (!c->ovl) TT_HIP(c, scene_write_begin(c, false));  // (an overlay's records are read by nobody else)
+    SceneWrite sw(c, false, !c->ovl);  // (an overlay's records are read by nobody else)
+    TT_HIP(c, sw.err);
     TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, pinned, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
     const uint32_t n_tlas = (uint32_t)h.tlas.size();
@@ -1616,7 +1670,7 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream, c->mesh_raw.p, c->mesh.p,
                        c->leaf.p, c->tlas.p, n_tlas, first, count);
     TT_HIP(c, hipGetLastError());
-    if (!c->ovl) TT_HIP(c, scene_write_end(c, false));
+    TT_HIP(c, sw.end());
     return TT_OK;
 }
 
@@ -1758,7 +1812,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     {  // TT_ROOT_LEAF: node 0 as a one-leaf TLAS root, when the host knows the device's node 0 (the lender's,
        // or a frame-slot TLAS's own)
         tt_ctx* owner = (c->lender && !c->ovl) ? c->lender : c;
-        std::lock_guard<std::mutex> lk(owner->mu);
+        std::lock_guard<std::recursive_mutex> lk(owner->mu);
         if (owner->root_known && !owner->host.nodes.empty()) {
             a.root = root_leaf_of(reinterpret_cast<const uint32_t*>(owner->host.nodes.data()));
             a.root.base_child += c->tlas_base;
@@ -1809,9 +1863,11 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     static const bool always_reset = std::getenv("TT_CTL_ALWAYS_RESET") != nullptr;  // A/B knob
     if (!async || want_stats || !c->ctl_zero[ci] || always_reset)
         TT_HIP(c, hipMemsetAsync(c->ctl + ci, 0, sizeof(TraceControl), c->stream));
-    TT_HIP(c, scene_read_begin(c));
+    SceneRead sr(c);
+    TT_HIP(c, sr.err);
     const uint32_t slot = c->ring_n % TT_RING;
-    TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
+    const bool ring = c->timing || !async;  // (a synchronous call reports its kernel time)
+    if (ring) TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     c->ctl_zero[0] = c->ctl_zero[1] = false;
     static const bool record_only = std::getenv("TT_ORDER_RECORD_ONLY") != nullptr;  // A/B knob: costs, no order
     if (os && os->valid && record_only)  // the order kernel (which clears the map this launch fills) is skipped
@@ -1840,11 +1896,13 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     }
     c->ctl_zero[ci ^ 1u] = true;
     c->ctl_cur = ci ^ 1u;
-    TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
-    TT_HIP(c, scene_read_end(c));
-    c->ring_n++;
-    c->ev0 = c->ring0[slot];
-    c->ev1 = c->ring1[slot];
+    if (ring) TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
+    sr.end();
+    if (ring) {
+        c->ring_n++;
+        c->ev0 = c->ring0[slot];
+        c->ev1 = c->ring1[slot];
+    }
     if (async) return TT_OK;
     TraceControl ctl;
     TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl + ci, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
@@ -2015,18 +2073,22 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
     const uint32_t grid =
         std::max(1u, std::min(c->shadow_grid_of[(want_stats ? 2 : 0) + (matcheck ? 1 : 0)], blocks_needed));
     TT_HIP(c, hipMemsetAsync(c->ctl + c->ctl_cur, 0, sizeof(TraceControl), c->stream));
-    TT_HIP(c, scene_read_begin(c));
+    SceneRead sr(c);
+    TT_HIP(c, sr.err);
     const uint32_t slot = c->ring_n % TT_RING;
-    TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
+    const bool ring = c->timing || !async;  // (a synchronous call reports its kernel time)
+    if (ring) TT_HIP(c, hipEventRecord(c->ring0[slot], c->stream));
     c->ctl_zero[0] = c->ctl_zero[1] = false;  // the any-hit kernel zeroes nothing
     TT_HIP(c, tt_launch_shadow(&a, grid, c->stream, want_stats ? 1 : 0, matcheck ? 1 : 0));
     note_stream_launch(c->stream);
-    TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
+    if (ring) TT_HIP(c, hipEventRecord(c->ring1[slot], c->stream));
     if (accumulate) TT_HIP(c, tt_launch_shadow_accumulate(&a, d_vis, c->stream));
-    TT_HIP(c, scene_read_end(c));
-    c->ring_n++;
-    c->ev0 = c->ring0[slot];
-    c->ev1 = c->ring1[slot];
+    sr.end();
+    if (ring) {
+        c->ring_n++;
+        c->ev0 = c->ring0[slot];
+        c->ev1 = c->ring1[slot];
+    }
     if (async) return TT_OK;
     TraceControl ctl;
     TT_HIP(c, hipMemcpyAsync(&ctl, c->ctl + c->ctl_cur, sizeof(ctl), hipMemcpyDeviceToHost, c->stream));
@@ -2099,10 +2161,11 @@ tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_d
         if (c->st_normals.n < (size_t)6 * p->n_rays) TT_HIP(c, c->st_normals.alloc((size_t)6 * p->n_rays));
         d_out = c->st_normals.p;
     }
-    TT_HIP(c, scene_read_begin(c));
+    SceneRead sr(c);
+    TT_HIP(c, sr.err);
     TT_HIP(c, tt_launch_resolve(d_rays, off, p->n_rays, p->far_plane, c->tris_raw.p, (uint32_t)c->tris_raw.n,
                                 c->mesh_raw.p, (uint32_t)c->mesh_raw.n, d_out, c->stream));
-    TT_HIP(c, scene_read_end(c));
+    sr.end();
     if (!dev) TT_HIP(c, hipMemcpyAsync(normals6, d_out, sizeof(float) * 6 * p->n_rays, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
@@ -2180,13 +2243,14 @@ static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_
         TT_HIP(c, hipMemcpyAsync(d + src, rays + src, sizeof(tt_ray_data) * p->n_rays, hipMemcpyHostToDevice, c->stream));
     }
     uint32_t slot;
-    TT_HIP(c, scene_read_begin(c));
+    SceneRead sr(c);
+    TT_HIP(c, sr.err);
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 4 * ctl_words, c->stream));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
                                c->mesh_raw.p, c->counter.p, c->stream, n_dev, n_next_dev));
     TT_HIP(c, ring_close(c, slot));
-    TT_HIP(c, scene_read_end(c));
+    sr.end();
     if (n_next_dev) {  // BufferSizes[CurBounce + 1].tracerays stays on the GPU: no host round trip
         if (n_next) *n_next = 0;
         return TT_OK;

@@ -323,6 +323,8 @@ def hip_lib():
         L.tt_selftest_rcp.restype = i32
         L.tt_timing_reset.argtypes = [vp]
         L.tt_timing_read.argtypes = [vp, vp, u32, C.POINTER(u32)]
+        L.tt_ctx_set_timing.argtypes = [vp, i32]
+        L.tt_ctx_set_timing.restype = i32
         for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
                   "tt_scene_update_meshdata", "tt_scene_bytes", "tt_trace_closest", "tt_sync", "tt_resolve_normals",
                   "tt_generate_primary", "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read"]:
@@ -803,6 +805,10 @@ class Engine:
 
     def timing_reset(self):
         self._check(self.L.tt_timing_reset(self.h), "tt_timing_reset")
+
+    def set_timing(self, enabled: bool):
+        """tt_ctx_set_timing: off, asynchronous calls record no HIP events (and add no timing entry)."""
+        self._check(self.L.tt_ctx_set_timing(self.h, 1 if enabled else 0), "tt_ctx_set_timing")
 
     def timing_read(self) -> np.ndarray:
         ms = np.zeros(256, np.float32)

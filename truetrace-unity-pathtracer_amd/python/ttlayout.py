@@ -74,6 +74,16 @@ class FrameLayout:
         self.own = []
         self.n_streams = 0  # process-wide dedicated streams taken so far (tthip.dedicated_stream)
         self.pool_streams = os.environ.get("TT_LAYOUT_POOL_STREAMS", "0") == "1"
+        # per-launch timing (two HIP-event markers around every kernel) only where it is read: part 0 of the
+        # slot that traces the first frame after timing_reset (launch_ms), and lend's context (slot 0 / part
+        # 0, whose timing the caller owns). On every other context it is off (tt_ctx_set_timing): at a
+        # strong-scaled rank's launch sizes the markers cost 15-20% of the frame (profiles/r05/events/).
+        # A/B knob: TT_LAYOUT_TIME_ALL=1 keeps it on everywhere.
+        self.time_all = os.environ.get("TT_LAYOUT_TIME_ALL", "0") == "1"
+        # time_none: no context times anything from the next timing_reset on, lend's included (a caller that
+        # keeps the markers out of a timed region and samples launch times afterwards, bench.py at N > 1)
+        self.time_none = False
+        self.lend_off = False
         self.slots: List[List[Part]] = []
         # slot 0 / part 0 issues on lend's own stream: the gather orders against p.stream, so it must be
         # the stream lend's launches actually go to (not whatever stream torch has current)
@@ -92,6 +102,8 @@ class FrameLayout:
                     st = self.new_stream()
                     e = tthip.Engine(dev.index, stream=st.cuda_stream)
                     e.share_scene(lend)  # ONE scene copy: one cache footprint for all contexts
+                    if not self.time_all:
+                        e.set_timing(False)
                     self.own.append(e)
                     p.eng, p.stream = e, st
                 p.n = int(sum(len(pix) for _, pix in lst))
@@ -275,21 +287,35 @@ class FrameLayout:
                  "info1": None if self.info1[f] is None else self.info1[f].cpu().numpy()}
                 for f, row in enumerate(self.slots)]
 
+    def timed(self, f: int, s: int) -> bool:
+        """Whether slot f / part s records per-launch times (see __init__)."""
+        if self.time_none:
+            return False
+        return self.time_all or (f, s) in ((0, 0), (self.k_reset % self.F, 0))
+
     def timing_reset(self):
-        for row in self.slots:
-            for p in row:
-                p.eng.timing_reset()
         self.k_reset = self.k
+        for f, row in enumerate(self.slots):
+            for s, p in enumerate(row):
+                if not (f == 0 and s == 0) or self.time_none or self.lend_off:
+                    # (lend's own setting is the caller's, except while time_none turned it off)
+                    p.eng.set_timing(self.timed(f, s))
+                p.eng.timing_reset()
+        self.lend_off = self.time_none
 
     def launch_ms(self, ring: int = 256) -> Optional[np.ndarray]:
         """Part 0's per-launch HIP-event times of the last frames its slot traced since timing_reset
-        (rows: frames, columns: primary[, bounce-1]) -- slot 0's, or the first slot that traced one;
-        every context's ring is drained."""
+        (rows: frames, columns: primary[, bounce-1]) -- the slot of the first frame after timing_reset
+        (under TT_LAYOUT_TIME_ALL=1: the first slot that traced one); every timed context's ring is drained."""
         per = 2 if self.bounce else 1
         out = None
-        for f, row in enumerate(self.slots):
+        first = self.k_reset % self.F
+        for f in [first] + [g for g in range(self.F) if g != first]:
+            row = self.slots[f]
             mine = sum(1 for k in range(self.k_reset, self.k) if k % self.F == f)
             for s, p in enumerate(row):
+                if not self.timed(f, s):
+                    continue
                 ms = np.asarray(p.eng.timing_read(), np.float64)
                 rows = min(mine, ring // per)
                 assert len(ms) == rows * per, (len(ms), rows, per)
