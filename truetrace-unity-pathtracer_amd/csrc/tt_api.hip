@@ -38,7 +38,7 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
                             const tt_mesh_data* md, uint32_t* counter, hipStream_t st, const uint32_t* n_dev,
-                            uint32_t* n_next_dev);
+                            uint32_t* n_next_dev, uint32_t* ctl_next, uint32_t ctl_next_words);
 uint32_t tt_bounce_tiles(uint32_t n);
 hipError_t tt_launch_resolve(const tt_ray_data* rays, uint32_t ray_offset, uint32_t n, float far_plane,
                              const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* md, uint32_t n_mesh,
@@ -174,8 +174,8 @@ struct tt_ctx {
     DevBuf<uint32_t> st_info;
     DevBuf<tt_col_data> st_colors;
     DevBuf<float> st_normals;
-    DevBuf<float> cam;          // 32 floats: cam_to_world | cam_inv_proj
-    DevBuf<uint32_t> counter;   // bounce enqueue counter
+    DevBuf<uint32_t> counter;   // bounce enqueue counters: two blocks of counter_words, used in turn
+    uint32_t counter_words = 0, counter_cur = 0;
     DevBuf<uint2> spill;        // deep traversal-stack entries (tt_trace_spill_entries() per thread)
     uint32_t spill_threads = 0; // grid threads the spill area is sized for (max over all grids)
     DevBuf<tt_shadow_ray> st_shadow;
@@ -653,20 +653,24 @@ void derive_tri(const tt_cuda_triangle& t, TriPos& o) {
 
 // The traversal records of updated _MeshData entries [first, first + count) (derive_mesh), and
 // every TLAS leaf record whose TLASBVH8Indices entry names one of them (derive_leaves).
-__global__ void tt_update_mesh_kernel(const tt_mesh_data* __restrict__ raw, MeshGpu* __restrict__ mesh,
-                                      LeafMesh* __restrict__ leaf, const int32_t* __restrict__ tlas, uint32_t n_tlas,
-                                      uint32_t first, uint32_t count) {
+// src: records [first, first + count), read in place from the pinned staging buffer (host memory the
+// GPU reads over the bus: no copy operation on the stream), also stored to _MeshData (raw).
+__global__ void tt_update_mesh_kernel(const tt_mesh_data* __restrict__ src, tt_mesh_data* __restrict__ raw,
+                                      MeshGpu* __restrict__ mesh, LeafMesh* __restrict__ leaf,
+                                      const int32_t* __restrict__ tlas, uint32_t n_tlas, uint32_t first, uint32_t count) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
+        const tt_mesh_data r = src[i];
+        raw[first + i] = r;
         MeshGpu g;
-        derive_mesh(raw[first + i], g);
+        derive_mesh(r, g);
         mesh[first + i] = g;
     }
     if (i < n_tlas) {
         const int32_t m = tlas[i];
         if (m >= 0 && (uint32_t)m - first < count) {
             LeafMesh l;
-            derive_mesh(raw[m], l.m);
+            derive_mesh(src[(uint32_t)m - first], l.m);
             l.mesh_id = m;
             l.pad[0] = l.pad[1] = l.pad[2] = 0;
             leaf[i] = l;
@@ -960,7 +964,6 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     c->st_info.release();
     c->st_colors.release();
     c->st_normals.release();
-    c->cam.release();
     c->counter.release();
     c->spill.release();
     for (auto& os : c->ord) {  // TT_TRACE_ADAPTIVE_ORDER state
@@ -1657,19 +1660,22 @@ tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, co
     }
     std::memcpy(h.mesh.data() + first, md, sizeof(tt_mesh_data) * count);
     TT_HIP(c, hipSetDevice(c->device));
-    // the raw records go to _MeshData in HBM; one small kernel derives the traversal records
-    // (MeshGpu) and patches the TLAS leaf records that name an updated mesh, on the stream
+    // one small kernel on the stream reads the records in place from the pinned staging slot, stores them
+    // to _MeshData in HBM, derives the traversal records (MeshGpu) and patches the TLAS leaf records that
+    // name an updated mesh (no copy operation: each one waits for a free CU slot beside the trace grids)
     void* pinned = nullptr;
     TT_HIP(c, stage_begin(c, md, sizeof(tt_mesh_data) * count, pinned));
     SceneWrite sw(c, false, !c->ovl);  // (an overlay's records are read by nobody else)
     TT_HIP(c, sw.err);
-    TT_HIP(c, hipMemcpyAsync(c->mesh_raw.p + first, pinned, sizeof(tt_mesh_data) * count, hipMemcpyHostToDevice, c->stream));
-    TT_HIP(c, stage_end(c));
+    void* src = nullptr;
+    TT_HIP(c, hipHostGetDevicePointer(&src, pinned, 0));
     const uint32_t n_tlas = (uint32_t)h.tlas.size();
     const uint32_t n = std::max(count, n_tlas);
-    hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream, c->mesh_raw.p, c->mesh.p,
-                       c->leaf.p, c->tlas.p, n_tlas, first, count);
+    hipLaunchKernelGGL(tt_update_mesh_kernel, dim3((n + 255u) / 256u), dim3(256), 0, c->stream,
+                       static_cast<const tt_mesh_data*>(src), c->mesh_raw.p, c->mesh.p, c->leaf.p, c->tlas.p, n_tlas, first,
+                       count);
     TT_HIP(c, hipGetLastError());
+    TT_HIP(c, stage_end(c));  // (after the kernel: it reads the staging slot)
     TT_HIP(c, sw.end());
     return TT_OK;
 }
@@ -2177,21 +2183,9 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
     const uint64_t wh = (uint64_t)cam->width * cam->height;
     if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
     TT_HIP(c, hipSetDevice(c->device));
-    if (c->cam.n < 32) TT_HIP(c, c->cam.alloc(32));
-    float m[32];
-    std::memcpy(m, cam->cam_to_world, 64);
-    std::memcpy(m + 16, cam->cam_inv_proj, 64);
     const bool dev = (cam->flags & TT_TRACE_DEVICE_PTRS) != 0;
-    // TT_TRACE_ASYNC with device rays: the camera goes through the pinned staging slots, nothing waits
+    // TT_TRACE_ASYNC with device rays: nothing waits (the camera goes in the kernel arguments)
     const bool async = dev && (cam->flags & TT_TRACE_ASYNC);
-    if (async) {
-        void* pinned = nullptr;
-        TT_HIP(c, stage_begin(c, m, sizeof(m), pinned));
-        TT_HIP(c, hipMemcpyAsync(c->cam.p, pinned, sizeof(m), hipMemcpyHostToDevice, c->stream));
-        TT_HIP(c, stage_end(c));
-    } else {
-        TT_HIP(c, hipMemcpyAsync(c->cam.p, m, sizeof(m), hipMemcpyHostToDevice, c->stream));
-    }
     tt_ray_data* d = rays;
     if (!dev) {
         if (c->st_rays.n < wh) TT_HIP(c, c->st_rays.alloc(wh));
@@ -2201,7 +2195,7 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
     }
     uint32_t slot;
     TT_HIP(c, ring_open(c, slot));
-    TT_HIP(c, tt_launch_generate(c->cam.p, c->cam.p + 16, cam->width, cam->height, cam->near_plane, cam->far_plane,
+    TT_HIP(c, tt_launch_generate(cam->cam_to_world, cam->cam_inv_proj, cam->width, cam->height, cam->near_plane, cam->far_plane,
                                  cam->jitter, cam->frames_accumulated, cam->max_bounce, d, c->stream));
     note_stream_launch(c->stream);
     TT_HIP(c, ring_close(c, slot));
@@ -2231,8 +2225,19 @@ static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_
     }
     TT_HIP(c, hipSetDevice(c->device));
     // [0] survivor count, [1] tile ticket, [2..3] pad, then one 64-bit look-back word per tile
+    // two counter blocks, used in turn: each enqueue zeroes the other block for the next one (no fill
+    // between enqueues); a larger capacity reallocates and fills both
     const size_t ctl_words = 4 + 2 * (size_t)tt_bounce_tiles(p->n_rays);
-    if (c->counter.n < ctl_words) TT_HIP(c, c->counter.alloc(ctl_words));
+    if (c->counter_words < ctl_words) {
+        TT_HIP(c, hipStreamSynchronize(c->stream));  // (the old blocks may be in use)
+        c->counter.release();
+        TT_HIP(c, c->counter.alloc(2 * ctl_words));
+        TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 2 * 4 * ctl_words, c->stream));
+        c->counter_words = (uint32_t)ctl_words;
+        c->counter_cur = 0;
+    }
+    uint32_t* const ctl_cur = c->counter.p + (size_t)c->counter_cur * c->counter_words;
+    uint32_t* const ctl_next = c->counter.p + (size_t)(c->counter_cur ^ 1u) * c->counter_words;
     tt_ray_data* d = rays;
     if (!dev) {
         if (c->st_rays.n < 2 * wh) {
@@ -2246,9 +2251,9 @@ static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_
     SceneRead sr(c);
     TT_HIP(c, sr.err);
     TT_HIP(c, ring_open(c, slot));
-    TT_HIP(c, hipMemsetAsync(c->counter.p, 0, 4 * ctl_words, c->stream));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
-                               c->mesh_raw.p, c->counter.p, c->stream, n_dev, n_next_dev));
+                               c->mesh_raw.p, ctl_cur, c->stream, n_dev, n_next_dev, ctl_next, c->counter_words));
+    c->counter_cur ^= 1u;
     TT_HIP(c, ring_close(c, slot));
     sr.end();
     if (n_next_dev) {  // BufferSizes[CurBounce + 1].tracerays stays on the GPU: no host round trip
@@ -2256,7 +2261,7 @@ static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_
         return TT_OK;
     }
     uint32_t cnt = 0;
-    TT_HIP(c, hipMemcpyAsync(&cnt, c->counter.p, 4, hipMemcpyDeviceToHost, c->stream));
+    TT_HIP(c, hipMemcpyAsync(&cnt, ctl_cur, 4, hipMemcpyDeviceToHost, c->stream));
     TT_HIP(c, hipStreamSynchronize(c->stream));
     if (!dev && cnt) {
         TT_HIP(c, hipMemcpy(rays + dst, d + dst, sizeof(tt_ray_data) * cnt, hipMemcpyDeviceToHost));

@@ -79,7 +79,12 @@ __device__ __forceinline__ float3 mul_inv(const float* W, float3 x) {
                        fma_(M(2, 2), x.z, fma_(M(1, 2), x.y, M(0, 2) * x.x)));
 }
 
-__global__ __launch_bounds__(256) void tt_generate_kernel(const float* __restrict__ c2w, const float* __restrict__ ip,
+// the camera travels in the kernel arguments (no staging copy per frame: a copy is one more small
+// operation on the stream that waits for a free CU slot beside the persistent trace grids)
+struct CamArgs {
+    float c2w[16], ip[16];
+};
+__global__ __launch_bounds__(256) void tt_generate_kernel(const CamArgs cam,
                                                           uint32_t width, uint32_t height, float near_plane,
                                                           float far_plane, int32_t jitter, int32_t frames,
                                                           int32_t max_bounce, tt_ray_data* __restrict__ rays) {
@@ -92,8 +97,8 @@ __global__ __launch_bounds__(256) void tt_generate_kernel(const float* __restric
         jx = r.x - 0.5f;
         jy = r.y - 0.5f;
     }
-    auto C = [&](int r, int c) { return c2w[c * 4 + r]; };
-    auto P = [&](int r, int c) { return ip[c * 4 + r]; };
+    auto C = [&](int r, int c) { return cam.c2w[c * 4 + r]; };
+    auto P = [&](int r, int c) { return cam.ip[c * 4 + r]; };
     const float uvx = ((float)x + jx) / (float)width * 2.0f - 1.0f;
     const float uvy = ((float)y + jy) / (float)height * 2.0f - 1.0f;
     const float3 origin = make_float3(C(0, 3), C(1, 3), C(2, 3));
@@ -240,10 +245,16 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
                                                         int32_t max_bounce, const tt_cuda_triangle* __restrict__ tris,
                                                         const tt_mesh_data* __restrict__ md, uint32_t* __restrict__ ctl,
                                                         unsigned long long* __restrict__ lb, uint32_t n_tiles,
-                                                        const uint32_t* __restrict__ n_dev, uint32_t* __restrict__ n_next_dev) {
+                                                        const uint32_t* __restrict__ n_dev, uint32_t* __restrict__ n_next_dev,
+                                                        uint32_t* __restrict__ ctl_next, uint32_t ctl_next_words) {
     __shared__ uint32_t s_tile, s_prefix;
     __shared__ uint32_t s_cnt[TT_BOUNCE_K][TT_BOUNCE_WAVES];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    // the next enqueue on this stream uses the other counter block: zero it now (plain vector stores; it
+    // starts after this launch completes), so no fill kernel runs between enqueues
+    if (ctl_next)
+        for (uint32_t w = blockIdx.x * TT_BOUNCE_BLOCK + tid; w < ctl_next_words; w += gridDim.x * TT_BOUNCE_BLOCK)
+            ctl_next[w] = 0u;
     if (tid == 0) s_tile = atomicAdd(&ctl[1], 1u);  // tiles in ticket order: look-back never waits on an unstarted block
     __syncthreads();
     const uint32_t tile = s_tile;
@@ -317,9 +328,15 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
 
 }  // namespace
 
+// c2w, ip: HOST arrays (column-major 4x4 each), copied into the kernel arguments
 hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uint32_t h, float near_plane, float far_plane,
                               int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays, hipStream_t st) {
-    hipLaunchKernelGGL(tt_generate_kernel, dim3((w + 255u) / 256u, h), dim3(256), 0, st, c2w, ip, w, h, near_plane, far_plane,
+    CamArgs cam;
+    for (int i = 0; i < 16; i++) {
+        cam.c2w[i] = c2w[i];
+        cam.ip[i] = ip[i];
+    }
+    hipLaunchKernelGGL(tt_generate_kernel, dim3((w + 255u) / 256u, h), dim3(256), 0, st, cam, w, h, near_plane, far_plane,
                        jitter, frames, max_bounce, rays);
     return hipGetLastError();
 }
@@ -327,20 +344,26 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
 uint32_t tt_bounce_tiles(uint32_t n) { return (n + TT_BOUNCE_TILE - 1u) / TT_BOUNCE_TILE; }
 
 // counter: [0] survivor count, [1] tile ticket, then tt_bounce_tiles(n) 64-bit status words; all
-// zeroed by the caller before the launch.
+// zero at the launch (the caller's fill, or the previous launch's ctl_next). ctl_next (nullable): the
+// ctl_next_words words this launch zeroes for the next one.
 // n_dev (nullable): device-resident ray count, clamped to n (then n is the capacity the grid covers);
 // n_next_dev (nullable): receives the survivor count on the device.
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
                             const tt_mesh_data* md, uint32_t* counter, hipStream_t st, const uint32_t* n_dev,
-                            uint32_t* n_next_dev) {
+                            uint32_t* n_next_dev, uint32_t* ctl_next, uint32_t ctl_next_words) {
     if (n == 0) {
+        if (ctl_next) {  // (this block stays zero: the next launch's block is the caller's to fill)
+            const hipError_t e = hipMemsetAsync(ctl_next, 0, 4 * (size_t)ctl_next_words, st);
+            if (e != hipSuccess) return e;
+        }
         if (n_next_dev) return hipMemsetAsync(n_next_dev, 0, 4, st);
         return hipSuccess;
     }
     const uint32_t tiles = tt_bounce_tiles(n);
     hipLaunchKernelGGL(tt_bounce_kernel, dim3(tiles), dim3(TT_BOUNCE_BLOCK), 0, st, rays, src_off, dst_off, n, far_plane,
                        cur_bounce, frames, max_bounce, tris, md, counter,
-                       reinterpret_cast<unsigned long long*>(counter + 4), tiles, n_dev, n_next_dev);
+                       reinterpret_cast<unsigned long long*>(counter + 4), tiles, n_dev, n_next_dev, ctl_next,
+                       ctl_next_words);
     return hipGetLastError();
 }
