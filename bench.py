@@ -655,8 +655,9 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, far)
 
         def timed_layout(plan, slots=F):
+            # every frame slot its own jittered samples, cycling through args.cycle of them (ttlayout docstring)
             lay_ = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots, bounce=False,
-                                        info=False, slot_stride=1)  # every frame slot its own jittered sample
+                                        info=False, slot_stride=1, cycle=args.cycle)
             for _ in range(max(2, args.warmup)):
                 lay_.step()
             torch.cuda.synchronize(dev)
@@ -715,7 +716,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     tgm = torch.tensor([el_g], dtype=torch.float64, device=red_dev)
     dist.all_reduce(tgm, op=dist.ReduceOp.MAX)
     sizes, gl = lay.last_gathered() if rank == 0 else (None, None)
-    last_sample = lay.sample_of(lay.last_slot(), 0)
+    last_sample = lay.last_sample(0)
     lay.close()
     if rank != 0:
         return None
@@ -981,6 +982,8 @@ def main():
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
     ap.add_argument("--dyn-slots", type=int, default=N1_SLOTS,
                     help="aux dyn: frame slots (contexts with TLASes of their own) of the dynamic-frame leg")
+    ap.add_argument("--cycle", type=int, default=6,
+                    help="samples each frame slot cycles through in the N > 1 layouts (and aux_c5_tiles); 1 at N = 1")
     ap.add_argument("--dyn-diag", default="",
                     help="aux dyn frame slots, diagnosis only (the record check then fails by design): comma list of "
                          "noupdate (no _MeshData rewrite / TLAS refit), nogen (Generate only in each slot's first frame)")
@@ -1107,9 +1110,13 @@ def main():
     def layout_of(plan, slots):
         # every frame slot traces its own jittered sample (slot f: sample k + f * S where the plan names
         # sample k, S = the plan's samples), as a renderer's frames in flight do (RayGenKernels.compute:45-46)
+        # At N > 1 each slot also cycles through args.cycle samples over its frames (a rare costly ray then recurs
+        # in one frame of `cycle` on its slot, not in every frame of it); N = 1 keeps one sample per slot, whose
+        # records the oracle check compares.
         n_samples = 1 + max(k for lst in plan for k, _ in lst)
         return ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots,
-                                    bounce=True, info=True, colors=colors_t, frames=frames, slot_stride=n_samples)
+                                    bounce=True, info=True, colors=colors_t, frames=frames, slot_stride=n_samples,
+                                    cycle=args.cycle if world > 1 else 1)
 
     def timed(lay):
         """W untimed steps, then exactly K steps between barrier + synchronize pairs: this rank's seconds."""
@@ -1149,8 +1156,8 @@ def main():
     B_prim = alg_bytes(s_prim, 0, parts[0].n)  # part 0's launches (the engine ring below)
     B_bnc = alg_bytes(s_bnc, 1, parts[0].nb)
     # all parts' launches of a step, averaged over the frame slots (each traces its own jittered sample)
-    B_step = sum(alg_bytes(p.s_prim, 0, p.n) + alg_bytes(p.s_bnc, 1, p.nb) for row in layout.slots
-                 for p in row) / layout.F
+    B_step = sum(alg_bytes(p.s_prim_r[r], 0, p.n) + alg_bytes(p.s_bnc_r[r], 1, p.nb_r[r]) for row in layout.slots
+                 for p in row for r in range(layout.R)) / (layout.F * layout.R)
     log(f"rank {rank}: primary {n_prim} rays nodes/ray {s_prim.node_visits / max(parts[0].n, 1):.2f} "
         f"tris/ray {s_prim.tri_tests / max(parts[0].n, 1):.2f} "
         f"hits {s_prim.hits}; bounce {nb} rays nodes/ray {s_bnc.node_visits / max(parts[0].nb, 1):.2f} "
@@ -1318,10 +1325,11 @@ def main():
     if G is not None:
         sizes, gather_list = layout.last_gathered()  # the last step's gather (steady-state steps included)
     if (split or F > 1) and rank == 0:
-        last = layout.last_slot()  # the last frame's slot: its samples are sample_of(last, k)
+        last = layout.last_slot()  # the last frame's slot; its samples are layout.last_sample(k)
+        r_last = layout.cycle_of(layout.k - 1)
         if spp:
             fr = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gather_list, sizes)], W, H, world, P)
-            gather_parity = all(bool(np.array_equal(fr[k], one_gpu_frame(layout.sample_of(last, k))))
+            gather_parity = all(bool(np.array_equal(fr[k], one_gpu_frame(layout.last_sample(k))))
                                 for k in range(world))
             frame = fr[0]
         else:
@@ -1329,11 +1337,11 @@ def main():
                 frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P,
                                               owner=owner)
             elif split:
-                own = torch.cat([p.prim_hits for p in layout.slots[(layout.k - 1) % F]]).cpu()
+                own = torch.cat([p.prim_hits_r[r_last] for p in layout.slots[last]]).cpu()
                 frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
             else:  # one part per slot in the kernel's own order: the last frame's records are in screen order
-                frame = layout.slots[(layout.k - 1) % F][0].prim_hits.contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
-            gather_parity = bool(np.array_equal(frame, one_gpu_frame(layout.sample_of(last, frames))))
+                frame = layout.slots[last][0].prim_hits_r[r_last].contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
+            gather_parity = bool(np.array_equal(frame, one_gpu_frame(layout.last_sample(frames))))
         log(f"gathered frame(s): {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels in sample 0, "
             f"{world if spp else 1} sample(s) identical to single-GPU traces: {gather_parity}")
 
@@ -1606,7 +1614,7 @@ def main():
     i2 = units_k.get("2", {}).get("valu_instr_per_ray")
     if i1 and i2:
         rays1 = sum(p.n for row in layout.slots for p in row) / layout.F
-        rays2 = sum(p.nb for row in layout.slots for p in row) / layout.F
+        rays2 = sum(p.nb_r[r] for row in layout.slots for p in row for r in range(layout.R)) / (layout.F * layout.R)
         instr = rays1 * i1 + rays2 * i2
         hard_ms = instr * 2.0 / (SIMDS * CLK) * 1e3
         step_valu = {"issue_bound_2cyc_ms": round(hard_ms, 4), "ms_per_step": round(ms_per_step, 4),

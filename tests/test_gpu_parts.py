@@ -360,14 +360,15 @@ def test_timing_switch():
         e.close()
 
 
-@pytest.mark.parametrize("stride", [0, 1])
-def test_frame_slots_equal_one_launch(stride):
+@pytest.mark.parametrize("stride,cycle", [(0, 1), (1, 1), (1, 2)])
+def test_frame_slots_equal_one_launch(stride, cycle):
     """bench.py's N = 1 layout (ttlayout.FrameLayout: the whole frame as one launch per bounce, 3 frames in
     flight on contexts that borrow one scene, streams on dedicated HW queues), several frames issued
     back to back: every slot's primary hit records and _PrimaryTriangleInfo equal one context tracing
     the frame its slot traces -- the same sample in every slot (stride 0), or slot f's own jittered sample
-    f (stride 1, the bench's layout since round 5) -- and its bounce-1 records equal that context's
-    bounce-1 launch."""
+    f (stride 1, the bench's layout since round 5), or with cycle 2 the two samples each slot alternates
+    between (bench.py --cycle at N > 1: every buffer of the cycle checked) -- and its bounce-1 records equal
+    that context's bounce-1 launch."""
     import torch
 
     import ttlayout
@@ -384,7 +385,7 @@ def test_frame_slots_equal_one_launch(stride):
         colors["Data"][:, 3] = 1.0
         colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
         refs = {}
-        for k in sorted({f * stride for f in range(3)}):
+        for k in sorted({stride * (f + 3 * r) for f in range(3) for r in range(cycle)}):
             one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
             info1 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
             torch.cuda.synchronize(dev)
@@ -401,21 +402,31 @@ def test_frame_slots_equal_one_launch(stride):
             del one
         make_full = ttlayout.full_frame_maker(torch, base, dev, W, H, c2w, ip, T.NEAR, FAR)
         lay = ttlayout.FrameLayout(torch, tthip, base, dev, W, H, FAR, [[(0, np.arange(WH, dtype=np.int64))]],
-                                   make_full, slots=3, bounce=True, info=True, colors=colors_t, slot_stride=stride)
+                                   make_full, slots=3, bounce=True, info=True, colors=colors_t, slot_stride=stride,
+                                   cycle=cycle)
         try:
-            for _ in range(7):  # asynchronous, three frames in flight
+            for _ in range(6 * cycle + 1):  # asynchronous, three frames in flight; every cycle buffer traced
                 lay.step()
             torch.cuda.synchronize(dev)
             for f, row in enumerate(lay.slots):
                 p = row[0]
-                nb1, ref_prim, ref_bnc, ref_info0, ref_info1 = refs[lay.sample_of(f, 0)]
-                assert p.n == WH and p.nb == nb1
-                prim = p.rays.view(-1, 48)[:WH, 32:48].cpu().numpy()
-                assert np.array_equal(prim, ref_prim), f"slot {f}: primary records"
-                bnc = p.rays.view(-1, 48)[WH:WH + p.nb, 32:48].cpu().numpy()
-                assert np.array_equal(bnc, ref_bnc), f"slot {f}: bounce-1 records"
-                assert np.array_equal(lay.info0[f].cpu().numpy(), ref_info0), f"slot {f}: bounce-0 info"
-                assert np.array_equal(lay.info1[f].cpu().numpy(), ref_info1), f"slot {f}: bounce-1 info"
+                r_last = lay.cycle_of(max(k for k in range(lay.k) if k % 3 == f))
+                for r in range(cycle):
+                    nb1, ref_prim, ref_bnc, ref_info0, ref_info1 = refs[lay.sample_of(f, 0, r)]
+                    assert p.n == WH and p.nb_r[r] == nb1
+                    prim = p.rays_r[r].view(-1, 48)[:WH, 32:48].cpu().numpy()
+                    assert np.array_equal(prim, ref_prim), f"slot {f} cycle {r}: primary records"
+                    bnc = p.rays_r[r].view(-1, 48)[WH:WH + nb1, 32:48].cpu().numpy()
+                    assert np.array_equal(bnc, ref_bnc), f"slot {f} cycle {r}: bounce-1 records"
+                    if r == r_last:
+                        assert np.array_equal(lay.info0[f].cpu().numpy(), ref_info0), f"slot {f}: bounce-0 info"
+                        # the bounce-1 form is written at the frame's bounce-1 pixels only (the slot's other
+                        # cycle sample wrote others before): compare there
+                        pix = p.rays_r[r].view(-1, 48)[WH:WH + nb1, 12:16].cpu().numpy().copy().view(np.uint32)[:, 0]
+                        got1 = lay.info1[f].cpu().numpy().reshape(-1, 16)[pix]
+                        assert np.array_equal(got1, ref_info1.reshape(-1, 16)[pix]), f"slot {f}: bounce-1 info"
+                        if cycle == 1:
+                            assert np.array_equal(lay.info1[f].cpu().numpy(), ref_info1), f"slot {f}: bounce-1 info"
             if stride:
                 assert len({lay.rays_of_slot(f) for f in range(3)}) > 1  # the jitter changes the bounce counts
         finally:

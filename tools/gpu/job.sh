@@ -28,6 +28,7 @@
 #   sweep      randomized parity sweep (tools/parity_sweep.py): SWEEP_N plain + SWEEP_N variants/adaptive + SWEEP_N
 #              degenerate-direction cases + SWEEP_N frame-slot cases from seed SWEEP_SEED
 #   sweepslots the frame-slot sweep alone (SWEEP_MODES, default "slots": instanced cases also traced by a moved slot)
+#   ordercheck the shared-scene ordering tests on the no-ordering variant (expected to fail)
 #   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
 #   ab         the bench headline per variant: AB_LIBS="product n128 ..." (lib/variants/libtruetrace_hip_NAME.so),
 #              AB_ARGS extra bench.py flags, REPS rounds of the list in turn
@@ -114,6 +115,12 @@ for stage in "$@"; do
            run sweep_slots 900 python -u tools/parity_sweep.py $n $((s0 + 3000)) slots,adaptive || exit $? ;;
     sweepslots) run sweep_slots 900 python -u tools/parity_sweep.py ${SWEEP_N:-300} ${SWEEP_SEED:-43000} \
                ${SWEEP_MODES:-slots} || exit $? ;;
+    ordercheck) # the shared-scene ordering tests against the variant whose sections order nothing (make variant
+                # NAME=noorder VFLAGS=-DTT_NO_SCENE_ORDER): they must FAIL there (the job goes on either way)
+                run ordercheck 300 env TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_noorder.so \
+                    python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_parts.py \
+                    -k "ordered or sections" -m gpu
+                echo "[job] ordercheck rc=$? (expected non-zero)" >&2 ;;
     variants) run variants 900 python -u tools/run_variants.py || exit $? ;;
     ab) for i in $(seq ${REPS:-1}); do for v in ${AB_LIBS:-product}; do  # the bench headline per library variant, in turn
             lib=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so

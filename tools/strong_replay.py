@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--deal", choices=["rr", "lpt"], default="rr",
                     help="tile deal at N > 1: rr (round-robin, bench.py's default) or lpt (longest-processing-time first "
                          "by sample 0's tile costs, tt_trace_chunk_costs)")
+    ap.add_argument("--cycle", type=int, default=6,
+                    help="samples each slot cycles through (bench.py --cycle, its N > 1 layouts); 1: one per slot")
     ap.add_argument("--slot-stride", type=int, default=1,
                     help="slot f traces sample f * stride (bench.py: 1, every frame in flight its own jitter; 0: one "
                          "sample replicated in every slot, rounds 1-4)")
@@ -59,6 +61,7 @@ def main():
     eng = tthip.Engine(0, stream=stream.cuda_stream)
     tthip.set_build_engine(eng, min_tris=100_000)
     out = {"tool": "tools/strong_replay.py", "device": torch.cuda.get_device_name(0), "slots": args.slots,
+           "cycle": args.cycle,
            "tile": args.tile, "steps": args.steps, "deal": args.deal, "slot_stride": args.slot_stride, "configs": {}}
 
     def frame_ms(lay):
@@ -111,7 +114,7 @@ def main():
                             [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile, owner=owner)])
                     lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR, plan, make_full,
                                                slots=F, bounce=bounce, info=True, colors=colors,
-                                               slot_stride=args.slot_stride)
+                                               slot_stride=args.slot_stride, cycle=args.cycle)
                     ms = frame_ms(lay)
                     per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
                     lay.close()

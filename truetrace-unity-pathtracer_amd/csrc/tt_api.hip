@@ -283,10 +283,19 @@ static hipError_t ring_close(tt_ctx* c, uint32_t slot) {
 static hipError_t lazy_event(hipEvent_t& ev) {
     return ev ? hipSuccess : hipEventCreateWithFlags(&ev, hipEventDisableTiming);
 }
+// TT_NO_SCENE_ORDER: a diagnostic variant build only (make variant NAME=noorder VFLAGS=-DTT_NO_SCENE_ORDER): the
+// sections take the lock but order nothing, to show the ordering tests fail without them.
+#ifndef TT_NO_SCENE_ORDER
+#define TT_NO_SCENE_ORDER 0
+#endif
 class SceneRead {
   public:
     explicit SceneRead(tt_ctx* c) : L_(c->lender) {
         if (!L_) return;
+        if (TT_NO_SCENE_ORDER) {
+            L_->mu.lock();
+            return;
+        }
         L_->mu.lock();
         const uint64_t seq = c->ovl ? L_->blas_mut : L_->scene_mut;
         if (seq != c->mut_waited) {
@@ -315,6 +324,7 @@ class SceneWrite {
     SceneWrite(tt_ctx* c, bool blas, bool active = true) : c_(active ? c : nullptr), blas_(blas) {
         if (!c_) return;
         c_->mu.lock();
+        if (TT_NO_SCENE_ORDER) return;
         for (tt_ctx* b : c_->borrower_list) {
             if (b->read_seq == b->read_waited || (b->ovl && !blas_)) continue;
             if ((err = lazy_event(b->ev_read)) != hipSuccess || (err = hipEventRecord(b->ev_read, b->stream)) != hipSuccess ||
@@ -333,7 +343,7 @@ class SceneWrite {
     hipError_t end() {
         if (!c_) return hipSuccess;
         hipError_t e = hipSuccess;
-        if (!c_->borrower_list.empty()) {
+        if (!c_->borrower_list.empty() && !TT_NO_SCENE_ORDER) {
             e = lazy_event(c_->ev_scene);
             if (e == hipSuccess) e = hipEventRecord(c_->ev_scene, c_->stream);
             if (e == hipSuccess) c_->scene_mut++;

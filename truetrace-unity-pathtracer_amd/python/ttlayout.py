@@ -13,7 +13,9 @@ tiles under tile sharding) as
     ``slot_stride`` s > 0 slot f traces sample k + f s wherever the plan names sample k, so the frames in
     flight carry their own jitter, as a renderer's consecutive frames do (Generate's random(0,
     pixel_index) depends on frames_accumulated, RayGenKernels.compute:45-46); s = 0 replicates one
-    sample in every slot.
+    sample in every slot. With ``cycle`` R > 1 each slot also cycles through R samples over its
+    successive frames (slot f's r-th frame traces sample k + s (f + F (r mod R))), so a rare costly
+    ray -- C5's degenerate one -- recurs in one frame of R on its slot instead of in every frame of it.
 
 All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). Every stream the
 layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.dedicated_stream:
@@ -62,12 +64,13 @@ class FrameLayout:
 
     def __init__(self, torch, tthip, lend, dev, W: int, H: int, far: float, plan, make_full: Callable,
                  slots: int = 1, bounce: bool = True, info: bool = True, colors=None, frames: int = 0,
-                 slot_stride: int = 0):
+                 slot_stride: int = 0, cycle: int = 1):
         self.torch, self.tthip, self.dev = torch, tthip, dev
         self.W, self.H, self.far = W, H, far
         self.P, self.F = len(plan), max(1, int(slots))
         self.bounce, self.colors, self.frames = bounce, colors, frames
         self.stride = max(0, int(slot_stride))
+        self.R = max(1, int(cycle))
         self.plan = plan
         WH = W * H
         self.engines = []  # (engine, stream) per context, lend's first; contexts created here are closed by close()
@@ -107,32 +110,45 @@ class FrameLayout:
                     self.own.append(e)
                     p.eng, p.stream = e, st
                 p.n = int(sum(len(pix) for _, pix in lst))
-                # GlobalRays ping-pong: bounce-1 rays live at [W*H, W*H + nb) (odd bounces, the API's offset)
-                p.rays = torch.zeros(((WH + p.n) if bounce else max(p.n, 1)) * 48, dtype=torch.uint8, device=dev)
+                # GlobalRays ping-pong: bounce-1 rays live at [W*H, W*H + nb) (odd bounces, the API's offset);
+                # one buffer per sample the slot cycles through
+                p.rays_r = [torch.zeros(((WH + p.n) if bounce else max(p.n, 1)) * 48, dtype=torch.uint8, device=dev)
+                            for _ in range(self.R)]
+                p.rays = p.rays_r[0]
                 row.append(p)
             self.slots.append(row)
-        # fill the parts' primary rays, sample by sample (slot f: the plan's sample k is sample k + f * stride)
-        for k in sorted({self.sample_of(f, kk) for f in range(self.F) for lst in plan for kk, _ in lst}):
+        # fill the parts' primary rays, sample by sample (slot f, cycle r: the plan's sample k is
+        # sample_of(f, k, r))
+        fr = [(f, r) for f in range(self.F) for r in range(self.R)]
+        for k in sorted({self.sample_of(f, kk, r) for f, r in fr for lst in plan for kk, _ in lst}):
             full = make_full(k)
-            for f, row in enumerate(self.slots):
-                for p, lst in zip(row, plan):
+            for f, r in fr:
+                for p, lst in zip(self.slots[f], plan):
                     o = 0
                     for kk, pix in lst:
-                        if self.sample_of(f, kk) == k and len(pix):
-                            p.rays.view(-1, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
+                        if self.sample_of(f, kk, r) == k and len(pix):
+                            p.rays_r[r].view(-1, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
                         o += len(pix)
             del full
         torch.cuda.synchronize(dev)
-        # setup: one stats trace per bounce (part counters) and the bounce-1 enqueue, on every slot
+        # setup: one stats trace per bounce (part counters) and the bounce-1 enqueue, per slot and cycle sample
         for f, row in enumerate(self.slots):
             for p in row:
-                p.s_prim = p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, stats=True)
-                if bounce:  # (the bounce direction's hash seed: the slot's sample, as Generate's)
-                    p.nb = p.eng.enqueue_bounce(p.rays, p.n, 0, far, W, H, frames=self.sample_of(f, frames),
-                                                max_bounce=1, device=True)
-                    p.s_bnc = p.eng.trace(p.rays, p.nb, 1, far, W, H, info=self.info1[f], colors=colors,
-                                          device=True, stats=True)
-                p.prim_hits = p.rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32)
+                p.s_prim_r, p.nb_r, p.s_bnc_r, p.prim_hits_r = [], [], [], []
+                for r in range(self.R):
+                    rays = p.rays_r[r]
+                    p.s_prim_r.append(p.eng.trace(rays, p.n, 0, far, W, H, info=self.info0[f], device=True,
+                                                  stats=True))
+                    if bounce:  # (the bounce direction's hash seed: the slot's sample, as Generate's)
+                        p.nb_r.append(p.eng.enqueue_bounce(rays, p.n, 0, far, W, H, frames=self.sample_of(f, frames, r),
+                                                           max_bounce=1, device=True))
+                        p.s_bnc_r.append(p.eng.trace(rays, p.nb_r[-1], 1, far, W, H, info=self.info1[f], colors=colors,
+                                                     device=True, stats=True))
+                    else:
+                        p.nb_r.append(0)
+                        p.s_bnc_r.append(None)
+                    p.prim_hits_r.append(rays[: p.n * 48].view(p.n, 48)[:, 32:48].view(torch.int32))
+                p.s_prim, p.nb, p.s_bnc, p.prim_hits = p.s_prim_r[0], p.nb_r[0], p.s_bnc_r[0], p.prim_hits_r[0]
                 p.hit_slices = []
         torch.cuda.synchronize(dev)
         self.gather = None
@@ -148,9 +164,21 @@ class FrameLayout:
         return st
 
     # ---------------------------------------------------------------- sizes
-    def sample_of(self, f: int, k: int) -> int:
-        """The sample slot f traces where the plan names sample k."""
-        return int(k) + int(f) * self.stride
+    def sample_of(self, f: int, k: int, r: int = 0) -> int:
+        """The sample slot f traces in its cycle position r where the plan names sample k."""
+        return int(k) + self.stride * (int(f) + self.F * (int(r) % self.R))
+
+    def cycle_of(self, k: int) -> int:
+        """The cycle position of frame k (its slot's (k // F)-th frame)."""
+        return (int(k) // self.F) % self.R
+
+    def frame_sample(self, k: int, kk: int) -> int:
+        """The sample frame k traces where the plan names sample kk."""
+        return self.sample_of(int(k) % self.F, kk, self.cycle_of(k))
+
+    def last_sample(self, kk: int) -> int:
+        """The sample the most recent frame traced where the plan names sample kk."""
+        return self.frame_sample(self.k - 1, kk)
 
     @property
     def parts(self) -> List[Part]:
@@ -161,12 +189,12 @@ class FrameLayout:
         """Slot 0's rays per frame (primary + bounce 1)."""
         return int(sum(p.n + p.nb for p in self.parts))
 
-    def rays_of_slot(self, f: int) -> int:
-        return int(sum(p.n + p.nb for p in self.slots[f]))
+    def rays_of_slot(self, f: int, r: int = 0) -> int:
+        return int(sum(p.n + p.nb_r[r] for p in self.slots[f]))
 
     def rays_in_frames(self, k0: int, k1: int) -> int:
-        """Rays traced by frames k0 .. k1 - 1 (frame k on slot k % F)."""
-        return int(sum(self.rays_of_slot(k % self.F) for k in range(k0, k1)))
+        """Rays traced by frames k0 .. k1 - 1 (frame k on slot k % F, cycle position cycle_of(k))."""
+        return int(sum(self.rays_of_slot(k % self.F, self.cycle_of(k)) for k in range(k0, k1)))
 
     def last_slot(self) -> int:
         """The slot of the most recent frame."""
@@ -221,6 +249,7 @@ class FrameLayout:
         k = self.k
         self.k += 1
         f = k % self.F
+        r = self.cycle_of(k)
         row = self.slots[f]
         g = self.gather
         W, H, far = self.W, self.H, self.far
@@ -229,10 +258,10 @@ class FrameLayout:
             if g is not None and g.stream_hits:
                 if g.used[b]:
                     p.stream.wait_event(g.done[b])  # the gather that last read send buffer b is done
-                p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, asynchronous=True,
+                p.eng.trace(p.rays_r[r], p.n, 0, far, W, H, info=self.info0[f], device=True, asynchronous=True,
                             hits_out=p.hit_slices[b])
             else:
-                p.eng.trace(p.rays, p.n, 0, far, W, H, info=self.info0[f], device=True, asynchronous=True)
+                p.eng.trace(p.rays_r[r], p.n, 0, far, W, H, info=self.info0[f], device=True, asynchronous=True)
         if g is not None:
             torch = self.torch
             for p in row:
@@ -240,7 +269,7 @@ class FrameLayout:
             with torch.cuda.stream(g.comm):
                 if not g.stream_hits:
                     for p in row:
-                        p.hit_slices[0].copy_(p.prim_hits)
+                        p.hit_slices[0].copy_(p.prim_hits_r[r])
                     g.copied.record(g.comm)
                 g.dist.gather(g.bufs[b], g.lists[b], dst=0)
                 if g.stream_hits:
@@ -249,7 +278,7 @@ class FrameLayout:
             g.last = b
         if self.bounce:
             for p in row:
-                p.eng.trace(p.rays, p.nb, 1, far, W, H, info=self.info1[f], colors=self.colors, device=True,
+                p.eng.trace(p.rays_r[r], p.nb_r[r], 1, far, W, H, info=self.info1[f], colors=self.colors, device=True,
                             asynchronous=True)
         if g is not None and not g.stream_hits:
             for p in row:
@@ -265,7 +294,8 @@ class FrameLayout:
     def poison_records(self):
         """Fills every slot's hit records (RayData.hits of its primary and bounce-1 rays) and its
         _PrimaryTriangleInfo buffers with the byte POISON, so that a record the following launches do not
-        write stays visible, and returns host copies of that state (snapshot())."""
+        write stays visible, and returns host copies of that state (snapshot()). (cycle 1 layouts only)"""
+        assert self.R == 1, "record checks need cycle 1"
         WH = self.W * self.H
         for f, row in enumerate(self.slots):
             for p in row:
