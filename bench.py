@@ -1379,7 +1379,7 @@ def main():
             sz_s, gl_s = lay_s.last_gathered()
             fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H, world, lay_s.P,
                                         owner=owner)
-            par = bool(np.array_equal(fr1, one_gpu_frame(lay_s.sample_of(lay_s.last_slot(), 0))))
+            par = bool(np.array_equal(fr1, one_gpu_frame(lay_s.last_sample(0))))
         ms_n = float(tmax.item()) * 1e3 / args.steps
         strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
                   "scaling": "strong", "ranks": world, "parts_per_rank": lay_s.P, "frame_slots": lay_s.F,
@@ -1417,8 +1417,7 @@ def main():
         if rank == 0:
             sz_w, gl_w = lay_w.last_gathered()
             fr_w = ttdist.assemble_spp([g[:sum(n)] for g, n in zip(gl_w, sz_w)], W, H, world, 1)
-            lw = lay_w.last_slot()
-            par_w = all(bool(np.array_equal(fr_w[k], one_gpu_frame(lay_w.sample_of(lw, k)))) for k in range(world))
+            par_w = all(bool(np.array_equal(fr_w[k], one_gpu_frame(lay_w.last_sample(k)))) for k in range(world))
         spp_aux = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
                    "scaling": "weak", "ranks": world, "parts_per_rank": lay_w.P, "frame_slots": lay_w.F,
                    "ms_per_step": round(float(tmax.item()) * 1e3 / args.steps, 4),

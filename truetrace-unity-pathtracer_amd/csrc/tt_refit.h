@@ -28,14 +28,7 @@ struct RefitDev {
     uint32_t* arrive = nullptr;
     float* bb = nullptr;
     uint32_t n_pairs = 0, n_nodes = 0, n_starts = 0;
-    // small trees (n_pairs <= TT_REFIT_ONE_WG_PAIRS): one workgroup, level by level (refit_levels)
-    int32_t* order = nullptr;     // NodePair ids, deepest level first
-    uint32_t* level_off = nullptr;  // n_levels + 1 offsets into order, deepest level first
-    uint32_t n_levels = 0;
 };
-// NodePairs up to which the refit runs as ONE workgroup stepping through the levels (one barrier per level,
-// no cross-workgroup hand-off); larger trees (deforming BLASes) climb with arrival counters (refit_tree).
-constexpr uint32_t TT_REFIT_ONE_WG_PAIRS = 16384;
 
 bool tt_refit_build_plan(const tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, RefitPlan& R);
 hipError_t tt_refit_prepare(const RefitPlan& R, const tt_cwbvh_node* host_nodes, uint32_t n_tlas_nodes, RefitDev& d);

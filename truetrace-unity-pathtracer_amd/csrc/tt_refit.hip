@@ -17,14 +17,11 @@
 // and climbs on. Boxes are handed between threads (and XCDs) with write-through sc1 stores, a
 // vmcnt(0) drain and an agent-scope atomic; the completing thread reads them with sc1 loads
 // (MI355X_MICROARCH.md, inter-workgroup visibility). The counters are reset by the thread that
-// completed them, so consecutive refits need no memset. A small tree (the TLAS: up to
-// TT_REFIT_ONE_WG_PAIRS NodePairs) runs instead as one workgroup stepping through the levels
-// (refit_levels: one barrier per level, no cross-workgroup hand-off). On the context stream, so a
-// trace enqueued after it sees the new nodes.
+// completed them, so consecutive refits need no memset. On the context stream, so a trace
+// enqueued after it sees the new nodes.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -203,34 +200,6 @@ __global__ void refit_tree(RefitTreeArgs t) {
     }
 }
 
-// A small tree (the TLAS) as ONE workgroup, level by level, deepest first: every NodePair of a level
-// is computed by some thread of the block -- a leaf NodePair's union, or an internal one's union +
-// NodeUpdate + NodeCompress from its children's boxes (one level deeper, so complete) -- then one
-// barrier. The same per-pair arithmetic as refit_tree, in the same slot order, so the nodes are the
-// same bytes; what goes is the per-level cross-workgroup hand-off (store, drain, agent-scope atomic,
-// acquire) of the climbing form, which sets a small tree's latency.
-constexpr int kLevelBlock = 1024;
-__global__ __launch_bounds__(kLevelBlock) void refit_levels(RefitTreeArgs t, const int32_t* __restrict__ order,
-                                                           const uint32_t* __restrict__ level_off, uint32_t n_levels) {
-    const __amdgpu_buffer_rsrc_t bb = __builtin_amdgcn_make_buffer_rsrc(t.bb, 0, (int)(t.n_pairs * 32u), 0x00020000);
-    for (uint32_t L = 0; L < n_levels; L++) {
-        const uint32_t lo = level_off[L], hi = level_off[L + 1];
-        for (uint32_t i = lo + threadIdx.x; i < hi; i += kLevelBlock) {
-            const int32_t p = order[i];
-            float box[6];
-            const int32_t nd = t.node_of[p];
-            if (nd < 0)
-                leaf_union(p, t.fwd, t.box_idx, t.boxes, box);
-            else
-                internal_pair(p, t.fwd, bb, t.nodes + nd, box);
-            if (p != 0) st_box(bb, p, box);
-        }
-        // the level's boxes (write-through stores, read back L1-bypassing by other waves) before the next
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-}
-
 // ------------------------------------------------------------------ Construct (BLAS refit)
 // The reference leaves normalize / round / the mul association to DXC; pinned here and in the
 // oracle: mul rows as fmaf(m2, z, fmaf(m1, y, m0 * x)) (+ m3), normalize(v) = v * (1 / sqrt(dot))
@@ -391,8 +360,7 @@ bool tt_refit_build_plan(const tt_cwbvh_node* nodes, uint32_t n_tlas_nodes, Refi
 }
 
 void tt_refit_free(RefitDev& d) {
-    for (void* p : {(void*)d.starts, (void*)d.fwd, (void*)d.parent, (void*)d.node_of, (void*)d.arrive, (void*)d.bb,
-                    (void*)d.order, (void*)d.level_off})
+    for (void* p : {(void*)d.starts, (void*)d.fwd, (void*)d.parent, (void*)d.node_of, (void*)d.arrive, (void*)d.bb})
         if (p) (void)hipFree(p);
     d = RefitDev();
 }
@@ -420,16 +388,6 @@ hipError_t tt_refit_prepare(const RefitPlan& R, const tt_cwbvh_node* host_nodes,
     if ((e = up(&d.starts, starts)) != hipSuccess || (e = up(&d.fwd, R.fwd)) != hipSuccess ||
         (e = up(&d.parent, R.parent)) != hipSuccess || (e = up(&d.node_of, node_of)) != hipSuccess)
         return e;
-    if (N <= TT_REFIT_ONE_WG_PAIRS) {  // refit_levels: the pairs deepest level first
-        std::vector<int32_t> order;
-        std::vector<uint32_t> off{0u};
-        for (size_t L = R.layers.size(); L-- > 0;) {
-            order.insert(order.end(), R.layers[L].begin(), R.layers[L].end());
-            off.push_back((uint32_t)order.size());
-        }
-        d.n_levels = (uint32_t)R.layers.size();
-        if ((e = up(&d.order, order)) != hipSuccess || (e = up(&d.level_off, off)) != hipSuccess) return e;
-    }
     if ((e = hipMalloc(reinterpret_cast<void**>(&d.arrive), sizeof(uint32_t) * N)) != hipSuccess) return e;
     if ((e = hipMemset(d.arrive, 0, sizeof(uint32_t) * N)) != hipSuccess) return e;
     return hipMalloc(reinterpret_cast<void**>(&d.bb), 8 * sizeof(float) * N);
@@ -439,11 +397,7 @@ hipError_t tt_refit_prepare(const RefitPlan& R, const tt_cwbvh_node* host_nodes,
 hipError_t tt_refit_run(RefitDev& d, const float* boxes, const int32_t* box_index, tt_cwbvh_node* nodes, hipStream_t st) {
     if (!d.n_starts) return hipSuccess;
     RefitTreeArgs t{d.starts, d.n_starts, d.fwd, d.parent, d.node_of, d.arrive, d.bb, d.n_pairs, boxes, box_index, nodes};
-    static const bool climb = std::getenv("TT_REFIT_CLIMB") != nullptr;  // A/B knob: the climbing form always
-    if (d.order && !climb)
-        hipLaunchKernelGGL(refit_levels, dim3(1), dim3(kLevelBlock), 0, st, t, d.order, d.level_off, d.n_levels);
-    else
-        hipLaunchKernelGGL(refit_tree, dim3(grid_of(d.n_starts)), dim3(kBlock), 0, st, t);
+    hipLaunchKernelGGL(refit_tree, dim3(grid_of(d.n_starts)), dim3(kBlock), 0, st, t);
     return hipGetLastError();
 }
 
