@@ -364,7 +364,8 @@ class SceneWrite {
     bool blas_;
 };
 // The node array the kernels read: the reference's (80-B stride) or its strided copy, refreshed on the
-// context stream after every write to `nodes` (nodes [first, first + count)).
+// context stream after every write to `nodes` (device node indices [first, first + count): a frame slot's
+// TLAS sits at tlas_base).
 static const uint4* kernel_nodes(const tt_ctx* c) {
     return TT_NODE_STRIDE == 80 ? reinterpret_cast<const uint4*>(c->nodes.p) : reinterpret_cast<const uint4*>(c->nodes_k.p);
 }
@@ -1103,9 +1104,8 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     // regions of that size behind the scene's nodes, for frame slots with TLASes of their own
     uint32_t tlas_res = 0;
     for (uint32_t n : h.tlas_nodes) tlas_res = std::max(tlas_res, n + 1u);
-    if (TT_NODE_STRIDE != 80 ||
-        ((uint64_t)n_nodes + (uint64_t)TT_TLAS_SLOTS * tlas_res) * sizeof(tt_cwbvh_node) >= (1ull << 32))
-        tlas_res = 0;  // no overlay regions (the strided-copy knob, or a node array near the 32-bit limit)
+    if (((uint64_t)n_nodes + (uint64_t)TT_TLAS_SLOTS * tlas_res) * TT_NODE_STRIDE >= (1ull << 32))
+        tlas_res = 0;  // no overlay regions (a node array near the 32-bit limit of the kernels' buffer loads)
     const uint32_t n_nodes_dev = n_nodes + TT_TLAS_SLOTS * tlas_res;
     hipError_t e;
     if ((e = c->nodes.alloc(n_nodes_dev)) != hipSuccess || (e = c->tris_raw.alloc(n_tris)) != hipSuccess ||
@@ -1116,8 +1116,8 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
     TT_HIP(c, hipMemcpy(c->nodes.p, nodes, sizeof(tt_cwbvh_node) * n_nodes, hipMemcpyHostToDevice));
     if (TT_NODE_STRIDE != 80) {
         c->nodes_k.release();
-        if ((e = c->nodes_k.alloc((size_t)n_nodes * TT_NODE_STRIDE)) != hipSuccess) return hip_fail(c, e, "node copy");
-        TT_HIP(c, hipMemsetAsync(c->nodes_k.p, 0, (size_t)n_nodes * TT_NODE_STRIDE, c->stream));
+        if ((e = c->nodes_k.alloc((size_t)n_nodes_dev * TT_NODE_STRIDE)) != hipSuccess) return hip_fail(c, e, "node copy");
+        TT_HIP(c, hipMemsetAsync(c->nodes_k.p, 0, (size_t)n_nodes_dev * TT_NODE_STRIDE, c->stream));
         TT_HIP(c, refresh_node_copy(c, 0, n_nodes));
         TT_HIP(c, hipStreamSynchronize(c->stream));
     }
@@ -1331,6 +1331,7 @@ tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
     dst->tlas_base = src->n_nodes_scene + slot * src->tlas_res;
     TT_HIP(dst, hipMemcpyAsync(dst->nodes.p + dst->tlas_base, src->nodes.p, sizeof(tt_cwbvh_node) * n_tlas_nodes,
                                hipMemcpyDeviceToDevice, dst->stream));
+    TT_HIP(dst, refresh_node_copy(dst, dst->tlas_base, n_tlas_nodes));
     TT_HIP(dst, hipMemcpyAsync(dst->tlas.p, src->tlas.p, sizeof(int32_t) * n_tlas, hipMemcpyDeviceToDevice, dst->stream));
     TT_HIP(dst, hipMemcpyAsync(dst->mesh_raw.p, src->mesh_raw.p, sizeof(tt_mesh_data) * n_mesh, hipMemcpyDeviceToDevice,
                                dst->stream));
@@ -1375,7 +1376,7 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
     TT_HIP(c, sw.err);
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_refit_run(c->refit, d_boxes, c->tlas.p, c->nodes.p + c->tlas_base, c->stream));
-    TT_HIP(c, refresh_node_copy(c, 0, n_tlas_nodes));
+    TT_HIP(c, refresh_node_copy(c, c->tlas_base, n_tlas_nodes));
     {
         std::lock_guard<std::recursive_mutex> lk(c->mu);
         c->root_known = false;  // node 0 was rewritten on the device
@@ -1622,7 +1623,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
     TT_HIP(c, hipMemcpyAsync(c->nodes.p + c->tlas_base + first, pinned, sizeof(tt_cwbvh_node) * count,
                              hipMemcpyHostToDevice, c->stream));
     TT_HIP(c, stage_end(c));
-    TT_HIP(c, refresh_node_copy(c, first, count));
+    TT_HIP(c, refresh_node_copy(c, c->tlas_base + first, count));
     TT_HIP(c, sw.end());
     c->scene_gen++;  // a rewritten TLAS may have a new topology: the refit plan is rebuilt
     return TT_OK;
