@@ -422,10 +422,15 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                 eng.tlas_refit(sc4.tlas_nodes, boxes[k & 1], device=True, asynchronous=True)
             refit_ms = ring_tail(eng, 1, reps)[:, 0]
             eng.upload(sc4)  # leave the scene as built
-            try:
-                slots_rec = dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H)
-            except Exception as e:  # noqa: BLE001
-                slots_rec = {"error": f"{type(e).__name__}: {e}"}
+            # the frame-slot counts (--dyn-slots, a comma list): the first is `frame_slots`, the others go
+            # under `frame_slots_more` (more frames in flight hide more of each frame's serial small work)
+            slots_recs = []
+            for S_ in [int(v) for v in str(args.dyn_slots).split(",") if v.strip()]:
+                try:
+                    slots_recs.append(dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H, S_))
+                except Exception as e:  # noqa: BLE001
+                    slots_recs.append({"slots": S_, "error": f"{type(e).__name__}: {e}"})
+            slots_rec = slots_recs[0] if slots_recs else None
             eng.upload(sc4)
             rays_f = W * H + float(np.mean(nbs))
             rec = {"instances_updated": n_md, "tlas_nodes": int(sc4.tlas_nodes), "frames": reps,
@@ -436,7 +441,8 @@ def aux_configs(torch, tthip, eng, dev, args, which):
                    "tlas_refit_gpu_ms_median": round(float(np.median(refit_ms)), 4),
                    "note": "frame = update_meshdata (all records, host array, async) + tlas_refit (device boxes) + "
                            "Generate + primary trace + enqueue (returns the count: one sync) + bounce-1 trace",
-                   "frame_slots": slots_rec}
+                   "frame_slots": slots_rec,
+                   "frame_slots_more": {str(r_.get("slots")): r_ for r_ in slots_recs[1:]}}
         except Exception as e:  # auxiliary: record, never lose the metric line
             rec["error"] = f"{type(e).__name__}: {e}"
         out["c4_dynamic_frame"] = rec
@@ -506,7 +512,7 @@ def lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, near, far, world, ar
                    "round_robin_max_over_mean_cost": round(float(rr.max() / rr.mean()), 4)}
 
 
-def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
+def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H, S):
     """The reference's dynamic frame (AssetManager.cs:1767-1826: every _MeshData record rewritten and the TLAS
     refit, then the traces) with N1_SLOTS frames in flight: slot f is a context with a TLAS, TLASBVH8Indices and
     _MeshData of its own over `eng`'s BLASes and triangles (tt_ctx_share_blas; slot 0 is `eng` itself), on a
@@ -524,7 +530,7 @@ def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H):
     colors = np.zeros(WH, tthip.COL_DTYPE)
     colors["Data"][:, 3] = 1.0
     colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
-    S = max(1, args.dyn_slots)
+    S = max(1, int(S))
     engs, streams = [eng], [torch.cuda.ExternalStream(eng.stream, device=dev)]
     for f in range(1, S):
         st = tthip.dedicated_stream(torch, dev, f - 1)
@@ -980,8 +986,9 @@ def main():
                          "use the metric's kernel instantiation and would mix into its rocprof average)")
     ap.add_argument("--no-c5-tiles", action="store_true",
                     help="N > 1: skip the tile-sharded San-Miguel 4K frame + hit gather run after the metric")
-    ap.add_argument("--dyn-slots", type=int, default=N1_SLOTS,
-                    help="aux dyn: frame slots (contexts with TLASes of their own) of the dynamic-frame leg")
+    ap.add_argument("--dyn-slots", default=f"{N1_SLOTS},6",
+                    help="aux dyn: frame-slot counts (contexts with TLASes of their own) of the dynamic-frame leg, a "
+                         "comma list: the first is the record's frame_slots, the others frame_slots_more")
     ap.add_argument("--cycle", type=int, default=6,
                     help="samples each frame slot cycles through in the N > 1 layouts (and aux_c5_tiles); 1 at N = 1")
     ap.add_argument("--dyn-diag", default="",
