@@ -1677,7 +1677,8 @@ def main():
                              "per-launch times are HIP events on it"
                              + (f" (part 0 / slot 0 of {P} x {F}: its launches overlap the others')"
                                 if P * F > 1 else ""),
-                   "parts_per_rank": P, "frame_slots": F, "parts_share_one_scene_copy": P * F > 1,
+                   "parts_per_rank": P, "frame_slots": F, "samples_cycled_per_slot": layout.R,
+                   "parts_share_one_scene_copy": P * F > 1,
                    "samples_per_frame": world if spp else 1,
                    "dist_world_size": dist_world, "dist_backend": backend if dist_world else None,
                    "launcher": ("bench.py self-launch" if os.environ.get("TT_BENCH_SELF_LAUNCHED") == "1"
