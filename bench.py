@@ -512,6 +512,33 @@ def lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, near, far, world, ar
                    "round_robin_max_over_mean_cost": round(float(rr.max() / rr.mean()), 4)}
 
 
+def node_fetch_model(dom, s_prim, s_bnc, parts):
+    """The dominant launch's node visits per second against the rate one MI355X sustains for scattered 80-B node
+    fetches (tools/micro/coop_fetch.hip -> profiles/node_fetch_latest.json): from L2-resident tables and from a
+    table the size of the scene's node set. A model of the memory path the node loads use (their texture-data
+    busy, roofline.binding_unit), not a bound: the kernel's visits mix L1 / L2 hits of the hot top levels with
+    misses."""
+    try:
+        nf = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                         "node_fetch_latest.json")))["scatter_gnodes_s"]
+    except (OSError, ValueError, KeyError):
+        return None
+    if not dom:
+        return None
+    bounce = dom["kernel"].endswith("2>")
+    st, n = (s_bnc, parts[0].nb) if bounce else (s_prim, parts[0].n)
+    if not n:
+        return None
+    npr = st.node_visits / n
+    g = dom["grays_s"] * npr
+    l2 = max(nf.get("table_1MiB", 0.0), nf.get("table_2MiB", 0.0))
+    return {"kernel": dom["kernel"], "nodes_per_ray": round(npr, 3), "launch_gnodes_s": round(g, 2),
+            "scatter_l2_resident_gnodes_s": l2, "frac_l2_resident": round(g / l2, 4) if l2 else None,
+            "scatter_40MiB_gnodes_s": nf.get("table_40MiB"),
+            "note": "a model, not a bound: node visits per second of the dominant launch vs the scattered 80-B node "
+                    "fetch rate of tools/micro/coop_fetch.hip (profiles/node_fetch_latest.json)"}
+
+
 def dyn_frame_slots(torch, tthip, eng, dev, sc4, mds, boxes, args, W, H, S):
     """The reference's dynamic frame (AssetManager.cs:1767-1826: every _MeshData record rewritten and the TLAS
     refit, then the traces) with N1_SLOTS frames in flight: slot f is a context with a TLAS, TLASBVH8Indices and
@@ -1704,7 +1731,8 @@ def main():
                      "units_busy_pmc": dom["units_busy_pmc"] if dom else None,
                      "traffic": traffic,
                      "per_launch": valu,
-                     "models": {"mix_grays_s": dom["mix_model_grays_s"] if dom else None,
+                     "models": {"node_fetch": node_fetch_model(dom, s_prim, s_bnc, parts),
+                                "mix_grays_s": dom["mix_model_grays_s"] if dom else None,
                                 "frac_mix": dom["frac_mix_model"] if dom else None,
                                 "quad_cycle_grays_s": dom["quad_cycle_model_grays_s"] if dom else None,
                                 "frac_quad_cycle": dom["frac_quad_cycle_model"] if dom else None,
