@@ -433,3 +433,55 @@ def test_frame_slots_equal_one_launch(stride, cycle):
             lay.close()
     finally:
         base.close()
+
+
+def test_enqueue_counter_blocks_survive_empty_and_indirect_calls():
+    """The bounce enqueue uses two counter blocks in turn, each launch zeroing the other for the next one
+    (tt_api.hip enqueue_call). Real, empty (0 rays), indirect (device count) and real calls in a mixed sequence
+    on one context must each return the count and the records of a fresh context's single enqueue."""
+    import torch
+
+    dev = torch.device("cuda:0")
+    sc = tthip.single_object_scene(tthip.Mesh.soup(9, 8000, 1.0, 0.1))
+    W, H = 160, 96
+    WH = W * H
+    c2w, ip = tthip.unity_camera((0.2, 0.3, 3.0), (-0.05, -0.1, -1.0), (0, 1, 0), 55.0, W, H, 0.05, FAR)
+
+    def primary(e, frame):
+        r = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+        e.generate(r, c2w, ip, W, H, 0.05, FAR, jitter=1, frames=frame, max_bounce=2, device=True)
+        e.trace(r, WH, 0, FAR, W, H, device=True)
+        return r
+
+    ref = tthip.Engine(0)
+    want = {}
+    try:
+        ref.upload(sc)
+        for frame in (0, 1, 2):
+            r = primary(ref, frame)
+            nb = ref.enqueue_bounce(r, WH, 0, FAR, W, H, frames=frame, max_bounce=2, device=True)
+            want[frame] = (nb, r.view(-1, 48)[WH:WH + nb].cpu().numpy())
+    finally:
+        ref.close()
+    e = tthip.Engine(0)
+    try:
+        e.upload(sc)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        seq = [("real", 0), ("empty", None), ("real", 1), ("empty", None), ("empty", None), ("indirect", 2),
+               ("real", 0), ("indirect", 1), ("real", 2)]
+        for kind, frame in seq:
+            if kind == "empty":
+                r = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+                assert e.enqueue_bounce(r, 0, 0, FAR, W, H, frames=0, max_bounce=2, device=True) == 0
+                continue
+            r = primary(e, frame)
+            if kind == "real":
+                nb = e.enqueue_bounce(r, WH, 0, FAR, W, H, frames=frame, max_bounce=2, device=True)
+            else:
+                e.enqueue_bounce_indirect(r, None, WH, cnt, 0, FAR, W, H, frames=frame, max_bounce=2)
+                torch.cuda.synchronize(dev)
+                nb = int(cnt.item())
+            assert nb == want[frame][0], (kind, frame)
+            assert np.array_equal(r.view(-1, 48)[WH:WH + nb].cpu().numpy(), want[frame][1]), (kind, frame)
+    finally:
+        e.close()
