@@ -512,6 +512,25 @@ def lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, near, far, world, ar
                    "round_robin_max_over_mean_cost": round(float(rr.max() / rr.mean()), 4)}
 
 
+def split_batched_gather(blocks, sizes, B):
+    """A gather of B-frame launches (FrameLayout batch B): every rank's block holds its parts back to back, each
+    part's records the B frames' back to back. Returns per frame b: (blocks, sizes) as assemble_parts takes them."""
+    out = []
+    for b in range(B):
+        fb, sb = [], []
+        for g, n in zip(blocks, sizes):
+            rows, ns, o = [], [], 0
+            for n_p in n:
+                m = n_p // B
+                rows.append(g[o + b * m:o + (b + 1) * m])
+                ns.append(m)
+                o += n_p
+            fb.append(np.concatenate(rows) if rows else g[:0])
+            sb.append(ns)
+        out.append((fb, sb))
+    return out
+
+
 def node_fetch_model(dom, s_prim, s_bnc, parts):
     """The dominant launch's node visits per second against the rate one MI355X sustains for scattered 80-B node
     fetches (tools/micro/coop_fetch.hip -> profiles/node_fetch_latest.json): from L2-resident tables and from a
@@ -1016,6 +1035,9 @@ def main():
     ap.add_argument("--dyn-slots", default=f"{N1_SLOTS},6",
                     help="aux dyn: frame-slot counts (contexts with TLASes of their own) of the dynamic-frame leg, a "
                          "comma list: the first is the record's frame_slots, the others frame_slots_more")
+    ap.add_argument("--batch", type=int, default=2,
+                    help="N > 1 strong-scaling headline: frames each launch traces at once (FrameLayout batch; 1 = one "
+                         "frame per launch); N = 1 always 1")
     ap.add_argument("--cycle", type=int, default=6,
                     help="samples each frame slot cycles through in the N > 1 layouts (and aux_c5_tiles); 1 at N = 1")
     ap.add_argument("--dyn-diag", default="",
@@ -1090,6 +1112,7 @@ def main():
     dist_world = dist.get_world_size() if (world > 1 or rccl1) else None
     tiles = (world > 1 or rccl1) and args.shard in ("tiles", "spp")
     spp = tiles and args.shard == "spp"  # the N-sample frame (weak scaling); "tiles": one frame (strong)
+    B_batch = max(1, args.batch) if (world > 1 and tiles and not spp) else 1  # frames per launch (--batch)
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -1141,7 +1164,7 @@ def main():
     split = tiles or P > 1
     make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, 0.3, far, jitter=jitter)
 
-    def layout_of(plan, slots):
+    def layout_of(plan, slots, batch=1):
         # every frame slot traces its own jittered sample (slot f: sample k + f * S where the plan names
         # sample k, S = the plan's samples), as a renderer's frames in flight do (RayGenKernels.compute:45-46)
         # At N > 1 each slot also cycles through args.cycle samples over its frames (a rare costly ray then recurs
@@ -1150,7 +1173,7 @@ def main():
         n_samples = 1 + max(k for lst in plan for k, _ in lst)
         return ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots,
                                     bounce=True, info=True, colors=colors_t, frames=frames, slot_stride=n_samples,
-                                    cycle=args.cycle if world > 1 else 1)
+                                    cycle=args.cycle if world > 1 else 1, batch=batch)
 
     def timed(lay):
         """W untimed steps, then exactly K steps between barrier + synchronize pairs: this rank's seconds."""
@@ -1179,10 +1202,12 @@ def main():
     if spp:  # this rank's (sample, tile) units of the N-sample frame (ttdist.spp_part_pixels)
         plan = ttdist.spp_part_pixels(W, H, world, rank, P)
     elif split:  # this rank's pixels of the one frame, compacted in tile order, split into P parts
-        plan = [[(frames, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)]
+        # (at N > 1 each launch traces `batch` frames of the rank's tiles at once: FrameLayout batch)
+        plan = [[(frames + b, pix) for b in range(B_batch)]
+                for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)]
     else:  # the whole frame, one launch per bounce in the kernel's own tile order
         plan = [[(frames, np.arange(WH, dtype=np.int64))]]
-    layout = layout_of(plan, F)
+    layout = layout_of(plan, F, batch=B_batch if (split and not spp) else 1)
     parts = layout.parts
     n_prim, nb = layout.n_prim(), layout.n_bounce()
     rays_per_step = n_prim + nb
@@ -1367,7 +1392,13 @@ def main():
                                 for k in range(world))
             frame = fr[0]
         else:
-            if tiles:
+            if tiles and layout.B > 1:  # every frame of the last batched launch, each against one GPU
+                per_frame = split_batched_gather([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, layout.B)
+                frames_b = [ttdist.assemble_parts(fb, sb, W, H, world, P, owner=owner) for fb, sb in per_frame]
+                batch_parity = all(bool(np.array_equal(frames_b[b], one_gpu_frame(layout.last_sample(frames + b))))
+                                   for b in range(layout.B))
+                frame = frames_b[0]
+            elif tiles:
                 frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gather_list, sizes)], sizes, W, H, world, P,
                                               owner=owner)
             elif split:
@@ -1376,6 +1407,8 @@ def main():
             else:  # one part per slot in the kernel's own order: the last frame's records are in screen order
                 frame = layout.slots[last][0].prim_hits_r[r_last].contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
             gather_parity = bool(np.array_equal(frame, one_gpu_frame(layout.last_sample(frames))))
+            if tiles and layout.B > 1:
+                gather_parity = gather_parity and batch_parity
         log(f"gathered frame(s): {int((frame[:, 1] != 0xFFFFFFFF).sum())} primary hits of {WH} pixels in sample 0, "
             f"{world if spp else 1} sample(s) identical to single-GPU traces: {gather_parity}")
 
@@ -1411,21 +1444,23 @@ def main():
         par = None
         if rank == 0:
             sz_s, gl_s = lay_s.last_gathered()
-            fr1 = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, W, H, world, lay_s.P,
-                                        owner=owner)
-            par = bool(np.array_equal(fr1, one_gpu_frame(lay_s.last_sample(0))))
-        ms_n = float(tmax.item()) * 1e3 / args.steps
+            per_frame = split_batched_gather([g[:sum(n)] for g, n in zip(gl_s, sz_s)], sz_s, lay_s.B)
+            par = all(bool(np.array_equal(ttdist.assemble_parts(fb, sb, W, H, world, lay_s.P, owner=owner),
+                                          one_gpu_frame(lay_s.last_sample(b))))
+                      for b, (fb, sb) in enumerate(per_frame))
+        ms_n = float(tmax.item()) * 1e3 / args.steps / lay_s.B  # per frame (a step traces B frames)
         strong = {"value": round(float(rsum.item()) / float(tmax.item()) / 1e6, 2), "unit": "Mrays/s",
                   "scaling": "strong", "ranks": world, "parts_per_rank": lay_s.P, "frame_slots": lay_s.F,
                   "ms_per_frame": round(ms_n, 4),
-                  "rays_per_frame_all_ranks": int(round(float(rsum.item()) / args.steps)),
+                  "rays_per_frame_all_ranks": int(round(float(rsum.item()) / args.steps / lay_s.B)),
+                  "frames_per_launch": lay_s.B,
                   "n1_ms_per_frame": round(solo_ms, 4), "n1_rays_per_frame": int(solo_rays),
                   "n1_ms_per_frame_by_layout": solo_layouts,
                   "efficiency": round(solo_ms / (world * ms_n), 4),
                   "gather_identical_to_1gpu": par, "tile_deal": deal_info,
                   "layout": "one 1080p frame (1 sample): 64x64 tiles dealt over the ranks (tile_deal), each rank's tiles "
-                            f"as {lay_s.P} parts x {lay_s.F} frame slots, + one RCCL gather of the frame's primary "
-                            "hit records per frame; efficiency = t(N = 1 frame in the faster single-GPU layout, "
+                            f"as {lay_s.P} parts x {lay_s.F} frame slots (each launch tracing {lay_s.B} frame(s)), + "
+                            "one RCCL gather of the frames' primary hit records per step; efficiency = t(N = 1 frame in the faster single-GPU layout, "
                             "every rank's GPU at once, fastest) / (N x t(N))"}
         if lay_s is not layout:
             lay_s.close()
@@ -1682,7 +1717,8 @@ def main():
         "config": {"workload": "sponza_primary_plus_1_bounce_1080p", "scene": "Sponza-shaped CWBVH8 (C2)",
                    "tris": int(len(scene.tris)), "cwbvh_nodes": int(len(scene.nodes)), "width": W, "height": H,
                    "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_rank0": int(rays_per_step),
-                   "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "jitter": jitter,
+                   "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "frames_per_step": layout.B,
+                   "jitter": jitter,
                    "seed": hex(args.seed),
                    "parallelism": ((f"single GPU, full frame as {P} tile-interleaved parts on {P} streams"
                                     if P > 1 else "single GPU, full frame as one launch per bounce in the kernel's "

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--deal", choices=["rr", "lpt"], default="rr",
                     help="tile deal at N > 1: rr (round-robin, bench.py's default) or lpt (longest-processing-time first "
                          "by sample 0's tile costs, tt_trace_chunk_costs)")
+    ap.add_argument("--batch", type=int, default=2,
+                    help="B frames of a rank's shard in each launch, as bench.py --batch (N > 1 rows; "
+                         "ms per frame = ms per step / B; FrameLayout batch: each frame its own texels)")
     ap.add_argument("--cycle", type=int, default=6,
                     help="samples each slot cycles through (bench.py --cycle, its N > 1 layouts); 1: one per slot")
     ap.add_argument("--slot-stride", type=int, default=1,
@@ -110,12 +113,14 @@ def main():
             for P, F in layouts:
                 per = []
                 for r in ranks:
+                    B = max(1, args.batch) if (n > 1 and P > 0) else 1  # frames per launch (N > 1 rows only)
                     plan = ([[(0, np.arange(W * H, dtype=np.int64))]] if P == 0 else  # P = 0: native whole frame
-                            [[(0, pix)] for pix in ttdist.part_pixels(W, H, n, r, P, args.tile, owner=owner)])
+                            [[(b, pix) for b in range(B)]
+                             for pix in ttdist.part_pixels(W, H, n, r, P, args.tile, owner=owner)])
                     lay = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, T.FAR, plan, make_full,
                                                slots=F, bounce=bounce, info=True, colors=colors,
-                                               slot_stride=args.slot_stride, cycle=args.cycle)
-                    ms = frame_ms(lay)
+                                               slot_stride=args.slot_stride * B, cycle=args.cycle, batch=B)
+                    ms = frame_ms(lay) / B
                     per.append({"rank": r, "rays": lay.rays_per_frame(), "ms_per_frame": round(ms, 4)})
                     lay.close()
                     del lay

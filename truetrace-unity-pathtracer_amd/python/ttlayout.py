@@ -16,6 +16,10 @@ tiles under tile sharding) as
     sample in every slot. With ``cycle`` R > 1 each slot also cycles through R samples over its
     successive frames (slot f's r-th frame traces sample k + s (f + F (r mod R))), so a rare costly
     ray -- C5's degenerate one -- recurs in one frame of R on its slot instead of in every frame of it.
+    With ``batch`` B > 1 each part's plan holds B samples of the same pixels back to back and every launch
+    traces all B frames at once: frame b's rays carry PixelIndex + b W H and the launches are issued for a
+    screen B times as tall (W x B H), so each frame writes its own _PrimaryTriangleInfo texels (info buffers
+    and the GlobalColors copy are B W H) -- fewer, larger launches for the small shards of strong scaling.
 
 All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). Every stream the
 layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.dedicated_stream:
@@ -64,15 +68,23 @@ class FrameLayout:
 
     def __init__(self, torch, tthip, lend, dev, W: int, H: int, far: float, plan, make_full: Callable,
                  slots: int = 1, bounce: bool = True, info: bool = True, colors=None, frames: int = 0,
-                 slot_stride: int = 0, cycle: int = 1):
+                 slot_stride: int = 0, cycle: int = 1, batch: int = 1):
         self.torch, self.tthip, self.dev = torch, tthip, dev
         self.W, self.H, self.far = W, H, far
         self.P, self.F = len(plan), max(1, int(slots))
         self.bounce, self.colors, self.frames = bounce, colors, frames
         self.stride = max(0, int(slot_stride))
         self.R = max(1, int(cycle))
+        self.B = max(1, int(batch))
+        if self.B > 1:
+            assert all(len(lst) == self.B for lst in plan), "batch B: every part's plan holds B (sample, pixels) entries"
+        self.Hs = H * self.B  # the screen height the launches are issued for (W x B H)
         self.plan = plan
         WH = W * H
+        WHs = WH * self.B
+        if colors is not None and self.B > 1:
+            colors = torch.cat([colors] * self.B)  # GlobalColors of the B-frames-tall screen
+            self.colors = colors
         self.engines = []  # (engine, stream) per context, lend's first; contexts created here are closed by close()
         self.own = []
         self.n_streams = 0  # process-wide dedicated streams taken so far (tthip.dedicated_stream)
@@ -92,8 +104,8 @@ class FrameLayout:
         # the stream lend's launches actually go to (not whatever stream torch has current)
         cur = torch.cuda.current_stream(dev)
         base_stream = cur if cur.cuda_stream == lend.stream else torch.cuda.ExternalStream(lend.stream, device=dev)
-        self.info0 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if info else None for _ in range(self.F)]
-        self.info1 = [torch.zeros(WH * 16, dtype=torch.uint8, device=dev) if (info and bounce) else None
+        self.info0 = [torch.zeros(WHs * 16, dtype=torch.uint8, device=dev) if info else None for _ in range(self.F)]
+        self.info1 = [torch.zeros(WHs * 16, dtype=torch.uint8, device=dev) if (info and bounce) else None
                       for _ in range(self.F)]
         for f in range(self.F):
             row = []
@@ -112,7 +124,7 @@ class FrameLayout:
                 p.n = int(sum(len(pix) for _, pix in lst))
                 # GlobalRays ping-pong: bounce-1 rays live at [W*H, W*H + nb) (odd bounces, the API's offset);
                 # one buffer per sample the slot cycles through
-                p.rays_r = [torch.zeros(((WH + p.n) if bounce else max(p.n, 1)) * 48, dtype=torch.uint8, device=dev)
+                p.rays_r = [torch.zeros(((WHs + p.n) if bounce else max(p.n, 1)) * 48, dtype=torch.uint8, device=dev)
                             for _ in range(self.R)]
                 p.rays = p.rays_r[0]
                 row.append(p)
@@ -125,9 +137,13 @@ class FrameLayout:
             for f, r in fr:
                 for p, lst in zip(self.slots[f], plan):
                     o = 0
-                    for kk, pix in lst:
+                    for j, (kk, pix) in enumerate(lst):
                         if self.sample_of(f, kk, r) == k and len(pix):
-                            p.rays_r[r].view(-1, 48)[o:o + len(pix)] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
+                            seg = p.rays_r[r].view(-1, 48)[o:o + len(pix)]
+                            seg[:] = full.view(WH, 48)[torch.from_numpy(pix).to(dev)]
+                            if self.B > 1 and j:  # frame j of the batch: PixelIndex + j W H
+                                pi = seg[:, 12:16].contiguous().view(torch.int32).view(-1) + j * WH
+                                seg[:, 12:16] = pi.view(torch.uint8).view(-1, 4)
                         o += len(pix)
             del full
         torch.cuda.synchronize(dev)
@@ -137,12 +153,13 @@ class FrameLayout:
                 p.s_prim_r, p.nb_r, p.s_bnc_r, p.prim_hits_r = [], [], [], []
                 for r in range(self.R):
                     rays = p.rays_r[r]
-                    p.s_prim_r.append(p.eng.trace(rays, p.n, 0, far, W, H, info=self.info0[f], device=True,
+                    Hs = self.Hs
+                    p.s_prim_r.append(p.eng.trace(rays, p.n, 0, far, W, Hs, info=self.info0[f], device=True,
                                                   stats=True))
                     if bounce:  # (the bounce direction's hash seed: the slot's sample, as Generate's)
-                        p.nb_r.append(p.eng.enqueue_bounce(rays, p.n, 0, far, W, H, frames=self.sample_of(f, frames, r),
+                        p.nb_r.append(p.eng.enqueue_bounce(rays, p.n, 0, far, W, Hs, frames=self.sample_of(f, frames, r),
                                                            max_bounce=1, device=True))
-                        p.s_bnc_r.append(p.eng.trace(rays, p.nb_r[-1], 1, far, W, H, info=self.info1[f], colors=colors,
+                        p.s_bnc_r.append(p.eng.trace(rays, p.nb_r[-1], 1, far, W, Hs, info=self.info1[f], colors=colors,
                                                      device=True, stats=True))
                     else:
                         p.nb_r.append(0)
@@ -252,7 +269,7 @@ class FrameLayout:
         r = self.cycle_of(k)
         row = self.slots[f]
         g = self.gather
-        W, H, far = self.W, self.H, self.far
+        W, H, far = self.W, self.Hs, self.far
         b = (f + self.F * ((k // self.F) % 2)) % g.nbuf if g is not None else 0
         for p in row:
             if g is not None and g.stream_hits:
@@ -294,8 +311,8 @@ class FrameLayout:
     def poison_records(self):
         """Fills every slot's hit records (RayData.hits of its primary and bounce-1 rays) and its
         _PrimaryTriangleInfo buffers with the byte POISON, so that a record the following launches do not
-        write stays visible, and returns host copies of that state (snapshot()). (cycle 1 layouts only)"""
-        assert self.R == 1, "record checks need cycle 1"
+        write stays visible, and returns host copies of that state (snapshot()). (cycle 1, batch 1 layouts only)"""
+        assert self.R == 1 and self.B == 1, "record checks need cycle 1 and batch 1"
         WH = self.W * self.H
         for f, row in enumerate(self.slots):
             for p in row:
