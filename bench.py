@@ -706,10 +706,11 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         c2w, ip = T.C5_VIEW.camera(W, H)
         make_full = ttlayout.full_frame_maker(torch, eng, dev, W, H, c2w, ip, T.NEAR, far)
 
-        def timed_layout(plan, slots=F):
-            # every frame slot its own jittered samples, cycling through args.cycle of them (ttlayout docstring)
+        def timed_layout(plan, slots=F, batch=1):
+            # every frame slot its own jittered samples, cycling through args.cycle of them (ttlayout docstring);
+            # batch: frames per launch (the rank's shards at N > 1, bench.py --batch)
             lay_ = ttlayout.FrameLayout(torch, tthip, eng, dev, W, H, far, plan, make_full, slots=slots, bounce=False,
-                                        info=False, slot_stride=1, cycle=args.cycle)
+                                        info=False, slot_stride=batch, cycle=args.cycle, batch=batch)
             for _ in range(max(2, args.warmup)):
                 lay_.step()
             torch.cuda.synchronize(dev)
@@ -719,7 +720,7 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
             for _ in range(reps):
                 lay_.step()
             torch.cuda.synchronize(dev)
-            el = (time.perf_counter() - tp) * 1e3 / reps
+            el = (time.perf_counter() - tp) * 1e3 / reps / batch  # per frame
             lay_.launch_ms()
             return lay_, el
 
@@ -733,7 +734,9 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
         el1 = min(el1a, el1b)
         rec["n1_ms_per_frame_by_layout_rank"] = {"2x1": round(el1a, 4), f"1x{N1_SLOTS}": round(el1b, 4)}
         owner, deal = lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, T.NEAR, far, world, args)
-        lay, el_n = timed_layout([[(0, pix)] for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)])
+        B5 = max(1, args.batch)
+        lay, el_n = timed_layout([[(b, pix) for b in range(B5)]
+                                  for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)], batch=B5)
         rec.update(rays_this_rank=lay.n_prim(), build_s=round(build_s, 1), tile_deal=deal)
     except Exception as e:  # noqa: BLE001 — auxiliary; agreed on below
         ok = 0
@@ -763,27 +766,31 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     torch.cuda.synchronize(dev)
     dist.barrier()
     torch.cuda.synchronize(dev)
-    el_g = (time.perf_counter() - tg) * 1e3 / reps
+    el_g = (time.perf_counter() - tg) * 1e3 / reps / lay.B  # per frame
     lay.launch_ms()
     tgm = torch.tensor([el_g], dtype=torch.float64, device=red_dev)
     dist.all_reduce(tgm, op=dist.ReduceOp.MAX)
     sizes, gl = lay.last_gathered() if rank == 0 else (None, None)
-    last_sample = lay.last_sample(0)
+    B5 = lay.B
+    last_samples = [lay.last_sample(b) for b in range(B5)]
     lay.close()
     if rank != 0:
         return None
-    frame = ttdist.assemble_parts([g[:sum(n)] for g, n in zip(gl, sizes)], sizes, W, H, world, P, owner=owner)
-    full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
-    eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=last_sample, max_bounce=1, device=True)
-    eng.trace(full, WH, 0, far, W, H, device=True)
-    ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+    identical = True
+    for b, (fb, sb) in enumerate(split_batched_gather([g[:sum(n)] for g, n in zip(gl, sizes)], sizes, B5)):
+        frame = ttdist.assemble_parts(fb, sb, W, H, world, P, owner=owner)
+        full = torch.zeros(WH * 48, dtype=torch.uint8, device=dev)
+        eng.generate(full, c2w, ip, W, H, T.NEAR, far, jitter=1, frames=last_samples[b], max_bounce=1, device=True)
+        eng.trace(full, WH, 0, far, W, H, device=True)
+        ref = full.view(WH, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+        identical = identical and bool(np.array_equal(frame, ref))
     ms1, msn, msg = float(t1.item()), float(tn.item()), float(tgm.item())
     rec.update(config="c5_san_miguel_4k_tiles", ranks=world, tile=64, parts_per_rank=P, frame_slots=F,
                frame_rays=WH, n1_ms_per_frame=round(ms1, 4), ms_per_frame_slowest_rank=round(msn, 4),
                efficiency=round(ms1 / (world * msn), 4), mrays_s_frame=round(WH / msn / 1e3, 1),
                with_gather=dict(ms_per_frame_slowest_rank=round(msg, 4), efficiency=round(ms1 / (world * msg), 4),
                                 mrays_s_frame=round(WH / msg / 1e3, 1)),
-               identical_to_1gpu=bool(np.array_equal(frame, ref)),
+               identical_to_1gpu=identical, frames_per_launch=B5,
                note="efficiency = t(N = 1: the whole 4K frame in the faster single-GPU layout, on every rank's GPU "
                     "at once, fastest) / (N x t(N), slowest rank); with_gather: the per-frame RCCL gather of the hit "
                     "records to rank 0 inside the timed frames")
