@@ -130,6 +130,7 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern TTStatus tt_async_overflows(IntPtr ctx, out ulong count);
         // per-call timing markers on (default) / off for asynchronous calls
         [DllImport(Lib)] public static extern TTStatus tt_ctx_set_timing(IntPtr ctx, int enabled);
+        [DllImport(Lib)] public static extern TTStatus tt_ctx_set_frame_pixels(IntPtr ctx, uint framePixels);
         [DllImport(Lib)] public static extern IntPtr tt_ctx_stream(IntPtr ctx);
         // _AlphaAtlas texels (R8, row-major width x height), read back once per scene change.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload_alpha_atlas(IntPtr ctx, byte* texels,
@@ -244,6 +245,9 @@ namespace TrueTrace.Hip
         /// Per-call GPU timing (tt_ctx_set_timing): off, asynchronous calls put no event markers around their
         /// kernels -- the setting for every frame-slot context but the one a host measures, if any.
         public void SetTiming(bool enabled) { Check(Native.tt_ctx_set_timing(m_ctx, enabled ? 1 : 0)); }
+        /// Batched frames on a B-tall screen (tt_ctx_set_frame_pixels): frame j's bounce random numbers are
+        /// those of its own pixel at frames + j; 0 = PixelIndex as-is.
+        public void SetFramePixels(uint framePixels) { Check(Native.tt_ctx_set_frame_pixels(m_ctx, framePixels)); }
 
         /// The per-64-ray-chunk costs the last AdaptiveOrder trace of `bounce` recorded (tt_trace_chunk_costs): one
         /// value per 8x8 pixel tile for a full-frame launch -- the input of a multi-GPU host's tile balancing.

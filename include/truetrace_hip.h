@@ -506,6 +506,13 @@ tt_status tt_timing_read(tt_ctx* ctx, float* ms, uint32_t max, uint32_t* n);
  * whole-frame launch but ~15-20% of a strong-scaled rank's small launches (profiles/r05/events/): a host
  * with several frames in flight keeps timing on for the one context it measures, if any. */
 tt_status tt_ctx_set_timing(tt_ctx* ctx, int32_t enabled);
+/* Several frames traced as one batch on a screen B times as tall (frame j's rays carry PixelIndex + j *
+ * frame_pixels, so each frame keeps its own _PrimaryTriangleInfo / GlobalColors texels): with frame_pixels
+ * = W * H of one frame, tt_enqueue_diffuse_bounce(_indirect) draws the bounce direction of a ray with
+ * PixelIndex p from pixel p mod frame_pixels at frames + p / frame_pixels -- frame j's bounce rays are those
+ * of the same pixels traced alone with frames_accumulated = frames + j (RayTracingShader.compute:52-84's
+ * random(1, pixel) per frame). 0 (the default): PixelIndex as-is, the reference's form. */
+tt_status tt_ctx_set_frame_pixels(tt_ctx* ctx, uint32_t frame_pixels);
 
 /* SIMD-efficiency diagnostics of the last synchronous TT_TRACE_STATS launch: wave loop
  * iterations, iterations with node-phase work, node-phase lanes, iterations with triangle-phase

@@ -435,6 +435,85 @@ def test_frame_slots_equal_one_launch(stride, cycle):
         base.close()
 
 
+@pytest.mark.parametrize("cycle", [1, 2])
+def test_batched_frames_equal_frames_traced_alone(cycle):
+    """bench.py at N > 1 (--batch 2): a rank's tiles as 2 parts x 3 frame slots, every launch tracing two
+    frames of those tiles on a 2H-tall screen (frame j's PixelIndex + j W H, tt_ctx_set_frame_pixels(W H)).
+    For every slot, cycle position and frame: the primary hit records, the bounce-1 rays (origin, direction,
+    pdf -- drawn from the frame-local pixel at the frame's own sample) and their hit records, and the bounce-0
+    _PrimaryTriangleInfo texels equal one context tracing the whole frame at that sample alone."""
+    import torch
+
+    import ttdist
+    import ttlayout
+
+    W, H, B, F, P = 640, 384, 2, 3, 2
+    WH = W * H
+    dev = torch.device("cuda:0")
+    scene = T.c2_sponza()
+    c2w, ip = T.C2_VIEW.camera(W, H)
+    base = tthip.Engine(0, stream=tthip.dedicated_stream(torch, dev, -1).cuda_stream)
+    try:
+        base.upload(scene)
+        colors = np.zeros(WH, tthip.COL_DTYPE)
+        colors["Data"][:, 3] = 1.0
+        colors_t = torch.from_numpy(colors.view(np.uint8)).to(dev)
+        refs = {}
+        for k in range(F * cycle * B):  # every sample the layout traces: j + B (f + F r)
+            one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
+            info0 = torch.zeros(WH * 16, dtype=torch.uint8, device=dev)
+            base.generate(one, c2w, ip, W, H, T.NEAR, FAR, jitter=1, frames=k, max_bounce=1, device=True)
+            base.trace(one, WH, 0, FAR, W, H, info=info0, device=True)
+            nb1 = base.enqueue_bounce(one, WH, 0, FAR, W, H, frames=k, max_bounce=1, device=True)
+            base.trace(one, nb1, 1, FAR, W, H, colors=colors_t, device=True)
+            torch.cuda.synchronize(dev)
+            a = one.view(2 * WH, 48).cpu().numpy()
+            bnc = a[WH:WH + nb1]
+            refs[k] = (a[:WH, 32:48], {int(px): row for px, row in zip(bnc[:, 12:16].copy().view(np.uint32)[:, 0], bnc)},
+                       info0.cpu().numpy().reshape(WH, 16))
+            del one
+        pix_parts = ttdist.part_pixels(W, H, 2, 0, P)
+        plan = [[(b, pix) for b in range(B)] for pix in pix_parts]
+        make_full = ttlayout.full_frame_maker(torch, base, dev, W, H, c2w, ip, T.NEAR, FAR)
+        lay = ttlayout.FrameLayout(torch, tthip, base, dev, W, H, FAR, plan, make_full, slots=F, bounce=True,
+                                   info=True, colors=colors_t, slot_stride=B, cycle=cycle, batch=B)
+        try:
+            for _ in range(2 * F * cycle + 1):
+                lay.step()
+            torch.cuda.synchronize(dev)
+            for f, row in enumerate(lay.slots):
+                r_last = lay.cycle_of(max(k for k in range(lay.k) if k % F == f))
+                for r in range(cycle):
+                    for p, pix in zip(row, pix_parts):
+                        m = len(pix)
+                        a = p.rays_r[r].view(-1, 48).cpu().numpy()
+                        bnc = a[WH * B:WH * B + p.nb_r[r]]
+                        bpi = bnc[:, 12:16].copy().view(np.uint32)[:, 0]
+                        assert p.n == B * m and int(bpi.max()) < B * WH
+                        for j in range(B):
+                            s = lay.sample_of(f, j, r)
+                            ref_prim, ref_bnc, ref_info0 = refs[s]
+                            where = f"slot {f} cycle {r} frame {j} (sample {s})"
+                            assert np.array_equal(a[j * m:(j + 1) * m, 32:48], ref_prim[pix]), where + ": primary records"
+                            mine = bnc[(bpi >= j * WH) & (bpi < (j + 1) * WH)]
+                            want = [ref_bnc[int(px)] for px in pix if int(px) in ref_bnc]
+                            assert len(mine) == len(want), where + ": bounce-1 ray count"
+                            mine = mine[np.argsort(mine[:, 12:16].copy().view(np.uint32)[:, 0], kind="stable")]
+                            want = np.stack(want) if want else np.zeros((0, 48), np.uint8)
+                            want = want[np.argsort(want[:, 12:16].copy().view(np.uint32)[:, 0], kind="stable")]
+                            assert np.array_equal(mine[:, 12:16].copy().view(np.uint32)[:, 0],
+                                                  want[:, 12:16].copy().view(np.uint32)[:, 0] + j * WH), where
+                            assert np.array_equal(mine[:, :12], want[:, :12]), where + ": bounce-1 origins"
+                            assert np.array_equal(mine[:, 16:48], want[:, 16:48]), where + ": bounce-1 rays / records"
+                            if r == r_last:
+                                got = lay.info0[f].cpu().numpy().reshape(B * WH, 16)[j * WH + pix]
+                                assert np.array_equal(got, ref_info0[pix]), where + ": bounce-0 info"
+        finally:
+            lay.close()
+    finally:
+        base.close()
+
+
 def test_enqueue_counter_blocks_survive_empty_and_indirect_calls():
     """The bounce enqueue uses two counter blocks in turn, each launch zeroing the other for the next one
     (tt_api.hip enqueue_call). Real, empty (0 rays), indirect (device count) and real calls in a mixed sequence

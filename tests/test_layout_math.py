@@ -46,3 +46,33 @@ def test_rays_in_frames_follow_the_cycle():
     assert lay.rays_in_frames(4, 17) == want
     lay.k = 9
     assert lay.last_slot() == 0 and lay.last_sample(0) == lay.frame_sample(8, 0) == 0 + F * 1
+
+
+def test_batched_frames_each_trace_their_own_sample():
+    # bench.py --batch B at N > 1: a plan names samples 0..B-1 per part and slot_stride = B, so frame j of a
+    # launch on slot f in cycle position r traces j + B (f + F r): B F R distinct samples, none shared
+    F, R, B = 3, 2, 2
+    lay = _layout(F=F, R=R, stride=B)
+    seen = [lay.sample_of(f, j, r) for r in range(R) for f in range(F) for j in range(B)]
+    assert sorted(seen) == list(range(F * R * B))
+    assert lay.sample_of(2, 1, 1) == 1 + B * (2 + F * 1)
+
+
+def test_split_batched_gather_recovers_every_frame():
+    import numpy as np
+
+    import bench
+
+    B, sizes_frame = 2, [[5, 3], [4]]  # two ranks: rank 0 two parts, rank 1 one part (per-frame record counts)
+    frames = [[[np.full((n, 4), 100 * b + 10 * r + p, np.uint32) for p, n in enumerate(ns)]
+               for r, ns in enumerate(sizes_frame)] for b in range(B)]
+    blocks, sizes = [], []
+    for r, ns in enumerate(sizes_frame):  # each part's records: the B frames back to back
+        blocks.append(np.concatenate([np.concatenate([frames[b][r][p] for b in range(B)]) for p in range(len(ns))]))
+        sizes.append([B * n for n in ns])
+    out = bench.split_batched_gather(blocks, sizes, B)
+    assert len(out) == B
+    for b, (fb, sb) in enumerate(out):
+        assert sb == sizes_frame
+        for r in range(len(sizes_frame)):
+            assert np.array_equal(fb[r], np.concatenate(frames[b][r]))

@@ -38,7 +38,8 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
                             const tt_mesh_data* md, uint32_t* counter, hipStream_t st, const uint32_t* n_dev,
-                            uint32_t* n_next_dev, uint32_t* ctl_next, uint32_t ctl_next_words);
+                            uint32_t* n_next_dev, uint32_t* ctl_next, uint32_t ctl_next_words,
+                            uint32_t frame_pixels);
 uint32_t tt_bounce_tiles(uint32_t n);
 hipError_t tt_launch_resolve(const tt_ray_data* rays, uint32_t ray_offset, uint32_t n, float far_plane,
                              const tt_cuda_triangle* tris, uint32_t n_tris, const tt_mesh_data* md, uint32_t n_mesh,
@@ -125,6 +126,7 @@ struct tt_ctx {
     hipEvent_t ring0[256] = {}, ring1[256] = {};
     uint32_t ring_n = 0, ring_base = 0;
     bool timing = true;  // tt_ctx_set_timing: asynchronous launches record their HIP-event pair
+    uint32_t frame_pixels = 0;  // tt_ctx_set_frame_pixels: batched frames' bounce random numbers (0: off)
     std::string err;
     // scene
     bool has_scene = false;
@@ -999,6 +1001,13 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
 tt_status tt_ctx_set_timing(tt_ctx* c, int32_t enabled) {
     if (!c) return TT_ERR_INVALID_ARG;
     c->timing = enabled != 0;
+    return TT_OK;
+}
+
+tt_status tt_ctx_set_frame_pixels(tt_ctx* c, uint32_t frame_pixels) {
+    if (!c) return TT_ERR_INVALID_ARG;
+    if (frame_pixels > 0x7fffffffu) return fail(c, TT_ERR_INVALID_ARG, "frame_pixels above 2^31 - 1");
+    c->frame_pixels = frame_pixels;
     return TT_OK;
 }
 
@@ -2263,7 +2272,8 @@ static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_
     TT_HIP(c, sr.err);
     TT_HIP(c, ring_open(c, slot));
     TT_HIP(c, tt_launch_bounce(d, src, dst, p->n_rays, p->far_plane, p->bounce, frames, max_bounce, c->tris_raw.p,
-                               c->mesh_raw.p, ctl_cur, c->stream, n_dev, n_next_dev, ctl_next, c->counter_words));
+                               c->mesh_raw.p, ctl_cur, c->stream, n_dev, n_next_dev, ctl_next, c->counter_words,
+                               c->frame_pixels));
     c->counter_cur ^= 1u;
     TT_HIP(c, ring_close(c, slot));
     sr.end();

@@ -246,7 +246,8 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
                                                         const tt_mesh_data* __restrict__ md, uint32_t* __restrict__ ctl,
                                                         unsigned long long* __restrict__ lb, uint32_t n_tiles,
                                                         const uint32_t* __restrict__ n_dev, uint32_t* __restrict__ n_next_dev,
-                                                        uint32_t* __restrict__ ctl_next, uint32_t ctl_next_words) {
+                                                        uint32_t* __restrict__ ctl_next, uint32_t ctl_next_words,
+                                                        uint32_t frame_pixels) {
     __shared__ uint32_t s_tile, s_prefix;
     __shared__ uint32_t s_cnt[TT_BOUNCE_K][TT_BOUNCE_WAVES];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -278,7 +279,16 @@ __global__ __launch_bounds__(TT_BOUNCE_BLOCK) void tt_bounce_kernel(tt_ray_data*
             R[k].h = rp[2];
             const float t = __uint_as_float(R[k].h.z);
             if (t < far_plane && (int32_t)R[k].h.y >= 0) {
-                om[k] = cosine_sample(R[k].a.w, frames, max_bounce, cur_bounce, &pdf[k]);
+                // batched frames (tt_ctx_set_frame_pixels): PixelIndex p is pixel p mod n of frame p / n, whose
+                // random numbers are that pixel's at frames + p / n; 0: PixelIndex as-is (the reference's form)
+                uint32_t px = R[k].a.w;
+                int32_t fr = frames;
+                if (frame_pixels) {
+                    const uint32_t j = px / frame_pixels;
+                    px -= j * frame_pixels;
+                    fr += (int32_t)j;
+                }
+                om[k] = cosine_sample(px, fr, max_bounce, cur_bounce, &pdf[k]);
                 ok = pdf[k] > 0.0f;
             }
         }
@@ -351,7 +361,8 @@ uint32_t tt_bounce_tiles(uint32_t n) { return (n + TT_BOUNCE_TILE - 1u) / TT_BOU
 hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_off, uint32_t n, float far_plane,
                             int32_t cur_bounce, int32_t frames, int32_t max_bounce, const tt_cuda_triangle* tris,
                             const tt_mesh_data* md, uint32_t* counter, hipStream_t st, const uint32_t* n_dev,
-                            uint32_t* n_next_dev, uint32_t* ctl_next, uint32_t ctl_next_words) {
+                            uint32_t* n_next_dev, uint32_t* ctl_next, uint32_t ctl_next_words,
+                            uint32_t frame_pixels) {
     if (n == 0) {
         if (ctl_next) {  // (this block stays zero: the next launch's block is the caller's to fill)
             const hipError_t e = hipMemsetAsync(ctl_next, 0, 4 * (size_t)ctl_next_words, st);
@@ -364,6 +375,6 @@ hipError_t tt_launch_bounce(tt_ray_data* rays, uint32_t src_off, uint32_t dst_of
     hipLaunchKernelGGL(tt_bounce_kernel, dim3(tiles), dim3(TT_BOUNCE_BLOCK), 0, st, rays, src_off, dst_off, n, far_plane,
                        cur_bounce, frames, max_bounce, tris, md, counter,
                        reinterpret_cast<unsigned long long*>(counter + 4), tiles, n_dev, n_next_dev, ctl_next,
-                       ctl_next_words);
+                       ctl_next_words, frame_pixels);
     return hipGetLastError();
 }

@@ -325,6 +325,8 @@ def hip_lib():
         L.tt_timing_read.argtypes = [vp, vp, u32, C.POINTER(u32)]
         L.tt_ctx_set_timing.argtypes = [vp, i32]
         L.tt_ctx_set_timing.restype = i32
+        L.tt_ctx_set_frame_pixels.argtypes = [vp, C.c_uint32]
+        L.tt_ctx_set_frame_pixels.restype = i32
         for s in ["tt_ctx_create", "tt_ctx_destroy", "tt_scene_upload", "tt_scene_update_nodes",
                   "tt_scene_update_meshdata", "tt_scene_bytes", "tt_trace_closest", "tt_sync", "tt_resolve_normals",
                   "tt_generate_primary", "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read"]:
@@ -809,6 +811,11 @@ class Engine:
     def set_timing(self, enabled: bool):
         """tt_ctx_set_timing: off, asynchronous calls record no HIP events (and add no timing entry)."""
         self._check(self.L.tt_ctx_set_timing(self.h, 1 if enabled else 0), "tt_ctx_set_timing")
+
+    def set_frame_pixels(self, frame_pixels: int):
+        """tt_ctx_set_frame_pixels: batched frames (PixelIndex + j W H) draw frame j's bounce random numbers
+        at frames + j from their frame-local pixel; 0 restores the reference's form."""
+        self._check(self.L.tt_ctx_set_frame_pixels(self.h, int(frame_pixels)), "tt_ctx_set_frame_pixels")
 
     def timing_read(self) -> np.ndarray:
         ms = np.zeros(256, np.float32)

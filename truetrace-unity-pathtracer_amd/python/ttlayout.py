@@ -20,6 +20,9 @@ tiles under tile sharding) as
     traces all B frames at once: frame b's rays carry PixelIndex + b W H and the launches are issued for a
     screen B times as tall (W x B H), so each frame writes its own _PrimaryTriangleInfo texels (info buffers
     and the GlobalColors copy are B W H) -- fewer, larger launches for the small shards of strong scaling.
+    Plan entry b names sample frames + b (with bounce) and every context keys the bounce enqueue's random
+    numbers on the frame-local pixel at frames + b (tt_ctx_set_frame_pixels(W H)), so frame b's bounce rays
+    are those of its pixels traced alone at its own sample.
 
 All P x F contexts trace ONE scene copy (tt_ctx_share_scene, the base engine lends). Every stream the
 layout creates (parts, slots, the gather) sits on a hardware queue of its own (tthip.dedicated_stream:
@@ -78,7 +81,11 @@ class FrameLayout:
         self.B = max(1, int(batch))
         if self.B > 1:
             assert all(len(lst) == self.B for lst in plan), "batch B: every part's plan holds B (sample, pixels) entries"
+            # the bounce enqueue draws frame b's random numbers at frames + b (tt_ctx_set_frame_pixels)
+            assert not bounce or all(int(k) == frames + b for lst in plan for b, (k, _) in enumerate(lst)), \
+                "batch B with bounce: part entry b names sample frames + b"
         self.Hs = H * self.B  # the screen height the launches are issued for (W x B H)
+        self.lend = lend
         self.plan = plan
         WH = W * H
         WHs = WH * self.B
@@ -121,6 +128,8 @@ class FrameLayout:
                         e.set_timing(False)
                     self.own.append(e)
                     p.eng, p.stream = e, st
+                if self.B > 1:  # frame b's bounce random numbers: its own pixel at frames + b
+                    p.eng.set_frame_pixels(WH)
                 p.n = int(sum(len(pix) for _, pix in lst))
                 # GlobalRays ping-pong: bounce-1 rays live at [W*H, W*H + nb) (odd bounces, the API's offset);
                 # one buffer per sample the slot cycles through
@@ -374,6 +383,9 @@ class FrameLayout:
         for e in self.own:
             e.close()
         self.own = []
+        if self.B > 1 and self.lend is not None:
+            self.lend.set_frame_pixels(0)  # lend's context back to the reference's form
+            self.lend = None
         if self.gather is not None:
             self.gather.comm = None
 
