@@ -22,6 +22,7 @@
 #   replaykt   the same replay under rocprofv3 --kernel-trace (REPLAY_ARGS; per-rank launch overlap)
 #   lifecycle  the GPU tests of stream teardown (rocprofv3 leg included), root-leaf bookkeeping and the timed kernels' jittered parity
 #   gloo2      the 2-rank bench rehearsal on this GPU (gloo collectives, C5 tiles included)
+#   gloo4      the same with 4 ranks
 #   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
 #   order      tools/exp_order.py per TT_ORDER_HOT threshold (ORDER_HOT, ORDER_CFGS, ORDER_ARGS)
@@ -107,6 +108,8 @@ for stage in "$@"; do
                done
            done ;;
     gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
+               --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
+    gloo4) run gloo4 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 4 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
     sweep) n=${SWEEP_N:-300}; s0=${SWEEP_SEED:-40000}  # plain; trace variants + adaptive order; + degenerate directions
            run sweep_plain 900 python -u tools/parity_sweep.py $n $s0 || exit $?
