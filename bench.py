@@ -1042,7 +1042,7 @@ def main():
     ap.add_argument("--dyn-slots", default=f"{N1_SLOTS},6",
                     help="aux dyn: frame-slot counts (contexts with TLASes of their own) of the dynamic-frame leg, a "
                          "comma list: the first is the record's frame_slots, the others frame_slots_more")
-    ap.add_argument("--batch", type=int, default=2,
+    ap.add_argument("--batch", type=int, default=4,
                     help="N > 1 strong-scaling headline: frames each launch traces at once (FrameLayout batch; 1 = one "
                          "frame per launch); N = 1 always 1")
     ap.add_argument("--cycle", type=int, default=6,

@@ -93,7 +93,7 @@ def test_bench_self_launch_two_ranks_gloo_on_one_gpu():
     assert c["dist_world_size"] == 2 and c["launcher"] == "bench.py self-launch"
     assert c["gather_identical_to_1gpu"] is True
     assert d["scaling"] == "strong" and c["samples_per_frame"] == 1
-    fps = c["frames_per_step"]  # frames each launch traces (bench.py --batch; 2 at N > 1)
+    fps = c["frames_per_step"]  # frames each launch traces (bench.py --batch; 4 at N > 1)
     assert fps >= 1 and 4_000_000 < c["rays_per_step_all_ranks"] / fps < 4_200_000  # 1080p frames, primary + bounce 1
     st = c["aux_strong_tiles"]
     assert st["scaling"] == "strong" and st["gather_identical_to_1gpu"] is True

@@ -437,7 +437,7 @@ def test_frame_slots_equal_one_launch(stride, cycle):
 
 @pytest.mark.parametrize("cycle", [1, 2])
 def test_batched_frames_equal_frames_traced_alone(cycle):
-    """bench.py at N > 1 (--batch 2): a rank's tiles as 2 parts x 3 frame slots, every launch tracing two
+    """bench.py at N > 1 (--batch, here 2): a rank's tiles as 2 parts x 3 frame slots, every launch tracing two
     frames of those tiles on a 2H-tall screen (frame j's PixelIndex + j W H, tt_ctx_set_frame_pixels(W H)).
     For every slot, cycle position and frame: the primary hit records, the bounce-1 rays (origin, direction,
     pdf -- drawn from the frame-local pixel at the frame's own sample) and their hit records, and the bounce-0

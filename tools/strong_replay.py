@@ -43,9 +43,13 @@ def main():
     ap.add_argument("--deal", choices=["rr", "lpt"], default="rr",
                     help="tile deal at N > 1: rr (round-robin, bench.py's default) or lpt (longest-processing-time first "
                          "by sample 0's tile costs, tt_trace_chunk_costs)")
-    ap.add_argument("--batch", type=int, default=2,
+    ap.add_argument("--batch", type=int, default=4,
                     help="B frames of a rank's shard in each launch, as bench.py --batch (N > 1 rows; "
                          "ms per frame = ms per step / B; FrameLayout batch: each frame its own texels)")
+    ap.add_argument("--n1-batched", action="store_true",
+                    help="also replay the N > 1 rows' layout (--parts x --slots, --batch frames per launch) at N = 1, the "
+                         "whole frame as one rank's shard, as a candidate for t(1): efficiency then credits batching "
+                         "only with what it gains over batching one GPU")
     ap.add_argument("--cycle", type=int, default=6,
                     help="samples each slot cycles through (bench.py --cycle, its N > 1 layouts); 1: one per slot")
     ap.add_argument("--slot-stride", type=int, default=1,
@@ -102,18 +106,20 @@ def main():
         for n in [int(x) for x in args.ns.split(",")]:
             if n == 1:  # the reference: both single-GPU layouts (2 parts x 1 slot; the whole frame as one launch in
                 # the kernel's own order with --n1-slots frames in flight, bench.py's N = 1 headline); t(1) = the faster
-                layouts = [(2, 1), (0, args.n1_slots)]
+                layouts = [(2, 1, 1), (0, args.n1_slots, 1)]
+                if args.n1_batched:
+                    layouts.append((args.parts, args.slots, max(1, args.batch)))
             elif args.layouts:
-                layouts = [tuple(int(v) for v in l.split("x")) for l in args.layouts.split(",")]
+                layouts = [tuple(int(v) for v in l.split("x")) + (max(1, args.batch),) for l in args.layouts.split(",")]
             else:
-                layouts = [(args.parts, args.slots)]
+                layouts = [(args.parts, args.slots, max(1, args.batch))]
             ranks = range(n) if args.ranks == "all" else [int(r) for r in args.ranks.split(",") if int(r) < n]
             owner = ttdist.lpt_owner(ttdist.tile_costs_from_chunks(chunk, W, H, args.tile), n) \
                 if (chunk is not None and n > 1) else None
-            for P, F in layouts:
+            for P, F, B in layouts:
                 per = []
+                B = B if P > 0 else 1  # frames per launch (N > 1 rows, and the --n1-batched N = 1 row)
                 for r in ranks:
-                    B = max(1, args.batch) if (n > 1 and P > 0) else 1  # frames per launch (N > 1 rows only)
                     plan = ([[(0, np.arange(W * H, dtype=np.int64))]] if P == 0 else  # P = 0: native whole frame
                             [[(b, pix) for b in range(B)]
                              for pix in ttdist.part_pixels(W, H, n, r, P, args.tile, owner=owner)])
@@ -128,7 +134,7 @@ def main():
                 t_n = max(p["ms_per_frame"] for p in per)
                 if n == 1:
                     t1 = t_n if t1 is None else min(t1, t_n)
-                rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": F, "ranks": per,
+                rows.append({"n_gpus": n, "parts_per_rank": P, "frame_slots": F, "frames_per_launch": B, "ranks": per,
                              "deal": "lpt" if owner is not None else "round-robin",
                              "t_frame_ms_slowest_rank": t_n,
                              "predicted_efficiency": round(t1 / (n * t_n), 3) if t1 else None,
