@@ -812,7 +812,9 @@ def oracle_records_check(scene, layout, pre, post, colors, far, W, H):
     t0 = time.perf_counter()
     hw, aff, quota = cpu_share()
     nthreads = max(1, min(aff, 64))
-    WH = W * H
+    H = layout.Hs  # a batch of B frames is one B-tall screen (FrameLayout batch): offsets, texels, colors
+    if layout.B > 1:
+        colors = np.tile(colors, layout.B)
     bad_rec = bad_info0 = bad_info1 = 0
     rays = 0
     samples = []
@@ -1042,6 +1044,10 @@ def main():
     ap.add_argument("--dyn-slots", default=f"{N1_SLOTS},6",
                     help="aux dyn: frame-slot counts (contexts with TLASes of their own) of the dynamic-frame leg, a "
                          "comma list: the first is the record's frame_slots, the others frame_slots_more")
+    ap.add_argument("--n1-batch", type=int, default=4,
+                    help="N = 1: frames each launch traces at once (the whole frame B times on a B-tall screen, each "
+                         "frame its own sample; the in-run oracle check covers every record; 1 = one frame per launch, "
+                         "rounds 1-5's headline layout)")
     ap.add_argument("--batch", type=int, default=4,
                     help="N > 1 strong-scaling headline: frames each launch traces at once (FrameLayout batch; 1 = one "
                          "frame per launch); N = 1 always 1")
@@ -1119,7 +1125,8 @@ def main():
     dist_world = dist.get_world_size() if (world > 1 or rccl1) else None
     tiles = (world > 1 or rccl1) and args.shard in ("tiles", "spp")
     spp = tiles and args.shard == "spp"  # the N-sample frame (weak scaling); "tiles": one frame (strong)
-    B_batch = max(1, args.batch) if (world > 1 and tiles and not spp) else 1  # frames per launch (--batch)
+    # frames per launch: --batch for the N > 1 strong-scaling shards, --n1-batch (opt-in) for the N = 1 frame
+    B_batch = max(1, args.batch) if (world > 1 and tiles and not spp) else (max(1, args.n1_batch) if world == 1 else 1)
     W, H = args.width, args.height
     WH = W * H
     far = 1000.0
@@ -1213,8 +1220,8 @@ def main():
         plan = [[(frames + b, pix) for b in range(B_batch)]
                 for pix in ttdist.part_pixels(W, H, world, rank, P, owner=owner)]
     else:  # the whole frame, one launch per bounce in the kernel's own tile order
-        plan = [[(frames, np.arange(WH, dtype=np.int64))]]
-    layout = layout_of(plan, F, batch=B_batch if (split and not spp) else 1)
+        plan = [[(frames + b, np.arange(WH, dtype=np.int64)) for b in range(B_batch)]]
+    layout = layout_of(plan, F, batch=B_batch if ((split and not spp) or world == 1) else 1)
     parts = layout.parts
     n_prim, nb = layout.n_prim(), layout.n_bounce()
     rays_per_step = n_prim + nb
@@ -1244,7 +1251,7 @@ def main():
     # order on the shared stream, per-launch HIP events -- the per-launch roofline and the launch
     # times rocprofv3 reports for this command's trace kernels
     single = None
-    frame_rays, frame_nb = (parts[0].rays, nb) if (P == 1 and world == 1) else (None, None)
+    frame_rays, frame_nb = (parts[0].rays, nb) if (P == 1 and world == 1 and layout.B == 1) else (None, None)
     if world == 1 and (P > 1 or F > 1):
         one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
@@ -1412,7 +1419,8 @@ def main():
                 own = torch.cat([p.prim_hits_r[r_last] for p in layout.slots[last]]).cpu()
                 frame = ttdist.assemble_parts([own], [[p.n for p in parts]], W, H, 1, P)
             else:  # one part per slot in the kernel's own order: the last frame's records are in screen order
-                frame = layout.slots[last][0].prim_hits_r[r_last].contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
+                # (a batched N = 1 launch: its first frame, the plan's sample `frames`)
+                frame = layout.slots[last][0].prim_hits_r[r_last][:WH].contiguous().cpu().numpy().view(np.uint32).reshape(WH, 4)
             gather_parity = bool(np.array_equal(frame, one_gpu_frame(layout.last_sample(frames))))
             if tiles and layout.B > 1:
                 gather_parity = gather_parity and batch_parity
@@ -1732,7 +1740,10 @@ def main():
                                     "own 8x8 tile order")
                                    + (f", {F} frame slots (frames k .. k + {F - 1} in flight on streams with HW queues "
                                       "of their own: each launch's drain overlaps the next frames' launches)"
-                                      if F > 1 else "") if world == 1 else
+                                      if F > 1 else "")
+                                   + (f"; each launch traces {layout.B} consecutive frames (each its own jittered "
+                                      f"sample) as one {W}x{H * layout.B} screen, frame j's PixelIndex + j*W*H "
+                                      "(bench.py --n1-batch)" if layout.B > 1 else "") if world == 1 else
                                    ((f"{world}-sample 1080p frame (sample k = Generate with frames_accumulated = k), "
                                      f"its (sample, 64x64 tile) units round-robin over {world} ranks (one frame's "
                                      f"worth each: weak scaling), " if spp else

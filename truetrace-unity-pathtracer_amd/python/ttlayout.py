@@ -320,9 +320,10 @@ class FrameLayout:
     def poison_records(self):
         """Fills every slot's hit records (RayData.hits of its primary and bounce-1 rays) and its
         _PrimaryTriangleInfo buffers with the byte POISON, so that a record the following launches do not
-        write stays visible, and returns host copies of that state (snapshot()). (cycle 1, batch 1 layouts only)"""
-        assert self.R == 1 and self.B == 1, "record checks need cycle 1 and batch 1"
-        WH = self.W * self.H
+        write stays visible, and returns host copies of that state (snapshot()). (cycle 1 layouts only; a
+        batch's bounce-1 rays sit at W x B H, the ping-pong offset of its B-tall screen)"""
+        assert self.R == 1, "record checks need cycle 1"
+        WH = self.W * self.Hs
         for f, row in enumerate(self.slots):
             for p in row:
                 v = p.rays.view(-1, 48)
