@@ -798,6 +798,78 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     return rec
 
 
+def group_tiles(torch, dist, tthip, scene, dev, gpu, args, rank, world, backend, red_dev, c2w, ip, far, W, H,
+                one_gpu_frame):
+    """aux_group_tiles: the LIBRARY's multi-GPU path (tt_group_*, csrc/tt_group.hip) -- what a C# host calls --
+    on this job's ranks: tt_group_unique_id on rank 0 (broadcast), tt_group_create_rank per process, the scene
+    replicated by tt_group_scene_upload, then K frames of tt_group_trace_frame: every rank generates and traces
+    its 64x64 tiles (round-robin) and their bounce-1 rays, and the primary hit records reach rank 0 in one RCCL
+    gather per frame (inside the library), scattered back to screen order. Frames are asynchronous over
+    --group-slots slots. value = all ranks' rays (primary + bounce 1) / the slowest rank's time; strong scaling
+    (one 1080p frame per step whatever N). At N = 1 the group has one member (whole frame, RCCL self-gather)."""
+    if backend != "nccl":
+        return {"skipped": "needs RCCL: one process per GPU"}
+    uid = tthip.group_unique_id() if rank == 0 else None
+    if world > 1:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    S = max(1, args.group_slots)
+    R = max(1, args.cycle) if world > 1 else S  # samples cycled (each frame its own jitter)
+    g = tthip.Group(W, H, rank=rank, world=world, uid=uid, device=gpu, slots=S, bounce=True)
+    try:
+        g.upload(scene)
+        outs = [torch.zeros((W * H, 4), dtype=torch.int32, device=dev) for _ in range(S)] if rank == 0 else [None] * S
+        torch.cuda.synchronize(dev)
+        # one synchronous frame per sample: this rank's rays of each (the bounce count is device-resident)
+        mine = []
+        for k in range(R):
+            g.trace_frame(outs[0], c2w, ip, 0.3, far, jitter=1, frames=k, max_bounce=1)
+            n_p, n_b, _ = g.frame_rays(0)
+            mine.append(float(n_p + n_b))
+        per_sample = torch.tensor(mine, dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(per_sample, op=dist.ReduceOp.SUM)
+        per_sample = per_sample.cpu().numpy()
+        for k in range(args.warmup):
+            g.trace_frame(outs[k % S], c2w, ip, 0.3, far, jitter=1, frames=k % R, max_bounce=1, asynchronous=True)
+        g.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            g.trace_frame(outs[k % S], c2w, ip, 0.3, far, jitter=1, frames=k % R, max_bounce=1, asynchronous=True)
+        g.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        el = float(el.item())
+        rays = float(sum(per_sample[k % R] for k in range(args.steps)))
+        par = None
+        if rank == 0:  # the last frame's gathered records against one GPU tracing the whole frame
+            k = args.steps - 1
+            got = outs[k % S].cpu().numpy().view(np.uint32)
+            par = bool(np.array_equal(got, one_gpu_frame(k % R)))
+        out = {"value": round(rays / el / 1e6, 2), "unit": "Mrays/s", "scaling": "strong", "ranks": world,
+               "ms_per_frame": round(el * 1e3 / args.steps, 4), "frame_slots": S, "samples_cycled": R,
+               "rays_per_frame_all_ranks": int(round(rays / args.steps)),
+               "gather_identical_to_1gpu": par,
+               "api": "tt_group_unique_id + tt_group_create_rank + tt_group_scene_upload + tt_group_trace_frame "
+                      "(TT_TRACE_ASYNC) + tt_group_sync",
+               "layout": "one 1080p frame per step: 64x64 tiles round-robin over the ranks (world 1: the whole frame), "
+                         "each rank's Generate + primary trace + bounce-1 enqueue/trace on its own device, one RCCL "
+                         "gather of the primary hit records to rank 0 per frame inside the library"}
+        if world > 1 and getattr(args, "_solo_ms", None):
+            out["efficiency_vs_n1_frame"] = round(args._solo_ms / (world * el * 1e3 / args.steps), 4)
+        return out
+    finally:
+        g.close()
+
+
 def oracle_records_check(scene, layout, pre, post, colors, far, W, H):
     """The records the bench's timed launches wrote, against the oracle (oracle/tt_oracle.c through
     tests/oracle_ctypes.py -- the checker, never the measured path). `pre`: every slot's host state after
@@ -1058,6 +1130,9 @@ def main():
                          "noupdate (no _MeshData rewrite / TLAS refit), nogen (Generate only in each slot's first frame)")
     ap.add_argument("--dyn-adaptive", type=int, default=1,
                     help="aux dyn frame slots: TT_TRACE_ADAPTIVE_ORDER on each slot's primary launch (1, default) or not")
+    ap.add_argument("--group-slots", type=int, default=4,
+                    help="frames in flight of the library's multi-GPU group leg (aux_group_tiles)")
+    ap.add_argument("--no-group", action="store_true", help="skip aux_group_tiles (the tt_group_* library path)")
     ap.add_argument("--aux", default="c3,c4,dyn,refit,c5",
                     help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,dyn,refit,c5;"
                          " '' = none)")
@@ -1125,7 +1200,7 @@ def main():
     dist_world = dist.get_world_size() if (world > 1 or rccl1) else None
     tiles = (world > 1 or rccl1) and args.shard in ("tiles", "spp")
     spp = tiles and args.shard == "spp"  # the N-sample frame (weak scaling); "tiles": one frame (strong)
-    # frames per launch: --batch for the N > 1 strong-scaling shards, --n1-batch (opt-in) for the N = 1 frame
+    # frames per launch: --batch for the N > 1 strong-scaling shards, --n1-batch (default 4: a still view accumulating samples; `interactive` reports 1) for the N = 1 frame
     B_batch = max(1, args.batch) if (world > 1 and tiles and not spp) else (max(1, args.n1_batch) if world == 1 else 1)
     W, H = args.width, args.height
     WH = W * H
@@ -1481,6 +1556,23 @@ def main():
             lay_s.close()
             del lay_s
         log(f"strong-scaling tile layout: {strong}")
+    # N = 1 with batched launches: the interactive layout beside the headline -- one frame per launch (any
+    # camera: each frame's Generate may take a new pose, RayGenKernels.compute:40-57) x N1_SLOTS frames in flight.
+    # The headline's B frames per launch need the next B cameras up front, i.e. a still view accumulating samples.
+    interactive = None
+    if world == 1 and layout.B > 1:
+        lay_i = layout_of([[(frames, np.arange(WH, dtype=np.int64))]], N1_SLOTS)
+        el_i = timed(lay_i)
+        lay_i.launch_ms()
+        ms_i = el_i * 1e3 / args.steps
+        interactive = {"value": round(lay_i.timed_rays / el_i / 1e6, 2), "unit": "Mrays/s", "ms_per_frame": round(ms_i, 4),
+                       "frames_per_launch": 1, "frame_slots": lay_i.F, "frames_in_flight": lay_i.F,
+                       "frame_latency_ms": round(lay_i.F * ms_i, 4), "camera": "per frame (any pose)",
+                       "layout": f"the whole 1080p frame, one launch per bounce, {lay_i.F} frames in flight (bench.py "
+                                 "--n1-batch 1)"}
+        lay_i.close()
+        del lay_i
+        log(f"interactive layout (1 frame per launch): {interactive}")
     layout.close()  # the borrowing contexts go before any aux leg re-uploads `eng`'s scene
 
     # N > 1 with the strong-scaling headline: the weak-scaling spp layout beside it (an N-sample frame's
@@ -1586,6 +1678,17 @@ def main():
         del scratch
         log(f"ray producers: {producers}")
 
+    group = None
+    if not args.no_group:
+        # every rank takes part (RCCL's init is collective); a failure is reported, never the metric lost
+        args._solo_ms = solo_ms
+        try:
+            group = group_tiles(torch, dist, tthip, scene, dev, gpu, args, rank, world, backend, red_dev, c2w, ip,
+                                far, W, H, one_gpu_frame)
+        except Exception as e:  # noqa: BLE001 — auxiliary
+            group = {"error": f"{type(e).__name__}: {e}"}
+        log(f"library group path (tt_group_*): {group}")
+
     aux = None
     if world == 1 and args.aux:
         aux = aux_configs(torch, tthip, eng, dev, args, set(args.aux.split(",")))
@@ -1597,6 +1700,7 @@ def main():
         except Exception as e:  # noqa: BLE001 — auxiliary, never lose the metric line
             c5t = {"error": f"{type(e).__name__}: {e}"}
             log(f"c5 tiles failed: {e}")
+
 
     if rank != 0:
         if world > 1:
@@ -1733,6 +1837,12 @@ def main():
                    "tris": int(len(scene.tris)), "cwbvh_nodes": int(len(scene.nodes)), "width": W, "height": H,
                    "primary_rays": int(n_prim), "bounce_rays": int(nb), "rays_per_step_rank0": int(rays_per_step),
                    "rays_per_step_all_ranks": int(round(total_rays / args.steps)), "frames_per_step": layout.B,
+                   # a frame is issued frames_in_flight frames before it completes: its latency is that many frame times
+                   "frames_in_flight": layout.B * F,
+                   "frame_latency_ms": round(F * ms_per_step, 4),
+                   "camera": ("static (progressive accumulation): each launch traces frames_per_step frames of one "
+                              "pose, so the next poses must be known ahead; the per-frame layout is `interactive`"
+                              if layout.B > 1 else "per frame (any pose)"),
                    "jitter": jitter,
                    "seed": hex(args.seed),
                    "parallelism": ((f"single GPU, full frame as {P} tile-interleaved parts on {P} streams"
@@ -1775,7 +1885,7 @@ def main():
                    "aux_strong_tiles": strong, "aux_spp_weak": spp_aux,
                    "aux_sample_sharded": sample_sharded, "aux_recur_unjittered": recur,
                    "aux_shadow_nee": shadow, "aux_ray_producers": producers, "aux_configs": aux,
-                   "aux_c5_tiles": c5t},
+                   "aux_c5_tiles": c5t, "aux_group_tiles": group},
         "roofline": {"bound": "valu_issue", "unit": "Grays/s",
                      "achieved": dom["grays_s"] if dom else None,
                      "peak": dom["issue_bound_2cyc_grays_s"] if dom else None,
@@ -1816,6 +1926,7 @@ def main():
                              "tools/pmc_units_summary.py -> profiles/units_latest.json); frac <= 1 by construction. "
                              "binding_unit = the busiest of VALU (against the same 2-cycle bound), TD and TA in that PMC "
                              "run"},
+        "interactive": interactive,
         "cpu_baseline": cpu,
         "oracle_identical": None if oracle_check is None else oracle_check["identical"],
         "oracle_check": oracle_check,

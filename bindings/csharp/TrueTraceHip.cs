@@ -76,12 +76,42 @@ namespace TrueTrace.Hip
         public uint flags;
     }
 
+    /// Generate's camera (RayGenKernels.compute:40-57): Unity's cameraToWorldMatrix and projectionMatrix.inverse,
+    /// column-major (the memory order of UnityEngine.Matrix4x4).
+    [StructLayout(LayoutKind.Sequential)]
+    public unsafe struct TTCamera
+    {
+        public fixed float camToWorld[16];
+        public fixed float camInvProj[16];
+        public float nearPlane, farPlane;
+        public uint width, height;
+        public int jitter;             // 1: the !UseReCur sub-pixel jitter
+        public int framesAccumulated;  // random() seed input
+        public int maxBounce;
+        public TTTraceFlags flags;     // DevicePtrs [| Async]
+    }
+
+    [Flags]
+    public enum TTGroupFlags : uint { None = 0, CopyGather = 1u << 0, Bounce = 1u << 1 }
+
+    /// tt_group_config: the screen a multi-GPU group traces, its tile edge, frames in flight and flags.
+    [StructLayout(LayoutKind.Sequential)]
+    public struct TTGroupConfig
+    {
+        public uint width, height;
+        public uint tile;      // 0: 64
+        public uint slots;     // 0: 2
+        public TTGroupFlags flags;
+        public uint pad;
+    }
+
     /// Column-major 4x4 (the memory order of UnityEngine.Matrix4x4: m00, m10, m20, m30, m01, ...).
     public struct Matrix4x4Floats { public float[] m; }
 
     public static class Native
     {
         const string Lib = "truetrace_hip";
+        [DllImport(Lib)] public static extern int tt_abi_version();
         [DllImport(Lib)] public static extern TTStatus tt_ctx_create(ref TTConfig cfg, out IntPtr ctx);
         [DllImport(Lib)] public static extern TTStatus tt_ctx_destroy(IntPtr ctx);
         [DllImport(Lib)] public static extern IntPtr tt_last_error(IntPtr ctx);
@@ -89,6 +119,8 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern TTStatus tt_stream_create(int device, out TTStreamHandle stream);
         [DllImport(Lib)] public static extern TTStatus tt_stream_destroy(IntPtr stream);
         [DllImport(Lib)] public static extern uint tt_stream_live_count();
+        // every library stream still alive, synchronised and destroyed: OnApplicationQuit / AppDomain.DomainUnload
+        [DllImport(Lib)] public static extern TTStatus tt_shutdown();
         // Element types are the reference's own host structs: BVHNode8DataCompressed (80 B),
         // CudaTriangle (88 B), int, MyMeshDataCompacted (88 B), MaterialData (252 B).
         [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_upload(IntPtr ctx,
@@ -146,6 +178,46 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern unsafe TTStatus tt_blas_refit(IntPtr ctx, ref TTBlasRefitParams p, float* vertices,
             int* indices, int* leafOfTriangle);
         [DllImport(Lib)] public static extern TTStatus tt_sync(IntPtr ctx);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_read_tris(IntPtr ctx, uint first, uint count, void* tris);
+        [DllImport(Lib)] public static extern TTStatus tt_scene_bytes(IntPtr ctx, out ulong bytes);
+        // the structural check tt_scene_upload runs, without a GPU; `why` receives the first violation
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_scene_validate(void* nodes, uint nNodes, void* tris,
+            uint nTris, int* tlasIndices, uint nTlas, void* meshData, uint nMesh, void* materials, uint nMat,
+            byte* why, uint whyLen);
+        // the producers either side of the trace (SURVEY.md §8 f2): Generate, and the diffuse next-bounce enqueue
+        // with stable compaction into the other half of GlobalRays (host count, or device-resident counts)
+        [DllImport(Lib)] public static extern TTStatus tt_generate_primary(IntPtr ctx, ref TTCamera cam, IntPtr globalRays);
+        [DllImport(Lib)] public static extern TTStatus tt_enqueue_diffuse_bounce(IntPtr ctx, ref TTTraceParams p,
+            IntPtr globalRays, int framesAccumulated, int maxBounce, out uint nNext);
+        [DllImport(Lib)] public static extern TTStatus tt_enqueue_diffuse_bounce_indirect(IntPtr ctx, ref TTTraceParams p,
+            IntPtr nRaysDev, IntPtr globalRays, int framesAccumulated, int maxBounce, IntPtr nNextDev);
+        // GetTriangleNormal per hit: float[6] (shading xyz, geometric xyz) per ray
+        [DllImport(Lib)] public static extern TTStatus tt_resolve_normals(IntPtr ctx, ref TTTraceParams p, IntPtr globalRays,
+            IntPtr normals6);
+        [DllImport(Lib)] public static extern TTStatus tt_timing_reset(IntPtr ctx);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_timing_read(IntPtr ctx, float* ms, uint max, out uint n);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_trace_diagnostics(IntPtr ctx, ulong* out8);
+        [DllImport(Lib)] public static extern TTStatus tt_selftest_rcp(IntPtr ctx, out ulong mismatches);
+        // multi-GPU tile-sharded frames (one process driving n devices, or one rank per process)
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_create(int* devices, uint n, ref TTGroupConfig cfg,
+            out IntPtr group);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_unique_id(byte* id128);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_create_rank(byte* id128, uint world, uint rank,
+            int device, ref TTGroupConfig cfg, out IntPtr group);
+        [DllImport(Lib)] public static extern TTStatus tt_group_destroy(IntPtr group);
+        [DllImport(Lib)] public static extern IntPtr tt_group_last_error(IntPtr group);
+        [DllImport(Lib)] public static extern uint tt_group_local_members(IntPtr group);
+        [DllImport(Lib)] public static extern IntPtr tt_group_member_ctx(IntPtr group, uint member);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_upload(IntPtr group,
+            void* nodes, uint nNodes, void* tris, uint nTris, int* tlasIndices, uint nTlas,
+            void* meshData, uint nMesh, void* materials, uint nMat);
+        [DllImport(Lib)] public static extern TTStatus tt_group_trace_frame(IntPtr group, ref TTCamera cam, IntPtr hitsOut,
+            uint flags);
+        [DllImport(Lib)] public static extern TTStatus tt_group_sync(IntPtr group);
+        [DllImport(Lib)] public static extern TTStatus tt_group_frame_rays(IntPtr group, uint member, out uint nPrimary,
+            out uint nBounce, out IntPtr raysDev);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_tile_pixels(uint width, uint height, uint tile,
+            uint world, uint rank, uint* pixels, uint max, out uint n);
         // BVH2Builder's three Array.Sort centroid presorts (introsort replayed, same tie order); returns
         // TTStatus.Unsupported for n <= 16 or non-finite centroids: then Array.Sort on the C# side.
         [DllImport(Lib)] public static extern unsafe TTStatus tt_bvh2_presort_device(IntPtr ctx, float* aabbs, uint n,
@@ -172,6 +244,8 @@ namespace TrueTrace.Hip
     public sealed class TrueTraceHipTracer : IDisposable
     {
         IntPtr m_ctx;
+        TTStreamHandle m_stream;  // a tt_stream_create stream this tracer issues on, kept alive while it does
+        bool m_streamRef;
 
         /// `hipStream`: the hipStream_t to issue on (IntPtr.Zero: a library-owned stream).
         public TrueTraceHipTracer(int device, ulong maxRays, IntPtr hipStream = default)
@@ -179,6 +253,99 @@ namespace TrueTrace.Hip
             var cfg = new TTConfig { device = device, flags = 0, maxRays = maxRays, stream = hipStream };
             Check(Native.tt_ctx_create(ref cfg, out m_ctx));
         }
+
+        /// Issue on a stream made by StreamCreate. The tracer holds a reference on the handle until it is
+        /// disposed, so a dropped or finalized handle never destroys the stream under a live tracer.
+        public TrueTraceHipTracer(int device, ulong maxRays, TTStreamHandle stream)
+        {
+            bool added = false;
+            stream.DangerousAddRef(ref added);
+            var cfg = new TTConfig { device = device, flags = 0, maxRays = maxRays, stream = stream.DangerousGetHandle() };
+            var st = Native.tt_ctx_create(ref cfg, out m_ctx);
+            if (st != TTStatus.Ok)
+            {
+                if (added) stream.DangerousRelease();
+                throw new InvalidOperationException($"tt_ctx_create: {st}");
+            }
+            m_stream = stream;
+            m_streamRef = added;
+        }
+
+        /// Raw context handle (e.g. for Native calls this wrapper does not cover).
+        public IntPtr Handle => m_ctx;
+
+        /// Generate (RayGenKernels.compute:40-57) into GlobalRays[pixel] on the device: the producer before the
+        /// primary trace. `async` returns without waiting.
+        public void GeneratePrimary(ref TTCamera cam, IntPtr globalRays, bool async = false)
+        {
+            cam.flags = TTTraceFlags.DevicePtrs | (async ? TTTraceFlags.Async : 0);
+            Check(Native.tt_generate_primary(m_ctx, ref cam, globalRays));
+        }
+
+        /// The diffuse next-bounce enqueue after a trace of bounce `curBounce` (kernel_shade's next-ray
+        /// production, RayTracingShader.compute:498-506): survivors compacted into the other ping-pong half;
+        /// returns their count (synchronises).
+        public uint EnqueueDiffuseBounce(IntPtr globalRays, uint nRays, int curBounce, float farPlane, int width, int height,
+                                         int framesAccumulated, int maxBounce)
+        {
+            var p = new TTTraceParams { nRays = nRays, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width,
+                                        screenHeight = (uint)height, flags = TTTraceFlags.DevicePtrs };
+            Check(Native.tt_enqueue_diffuse_bounce(m_ctx, ref p, globalRays, framesAccumulated, maxBounce, out uint n));
+            return n;
+        }
+
+        /// The same enqueue with device-resident counts (BufferSizes on the GPU): reads the traced count at
+        /// `nRaysDevice` (IntPtr.Zero: `capacity`), writes the survivor count to `nNextDevice`; no host wait, so
+        /// Generate -> TraceDevice -> EnqueueDiffuseBounceIndirect -> TraceDeviceIndirect is one device chain.
+        public void EnqueueDiffuseBounceIndirect(IntPtr globalRays, IntPtr nRaysDevice, uint capacity, int curBounce,
+                                                 float farPlane, int width, int height, int framesAccumulated,
+                                                 int maxBounce, IntPtr nNextDevice)
+        {
+            var p = new TTTraceParams { nRays = capacity, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width,
+                                        screenHeight = (uint)height, flags = TTTraceFlags.DevicePtrs };
+            Check(Native.tt_enqueue_diffuse_bounce_indirect(m_ctx, ref p, nRaysDevice, globalRays, framesAccumulated,
+                                                            maxBounce, nNextDevice));
+        }
+
+        /// GetTriangleNormal for every hit of a traced batch (float[6] per ray in HIP memory at `normals6`).
+        public void ResolveNormals(IntPtr globalRays, uint nRays, int curBounce, float farPlane, int width, int height,
+                                   IntPtr normals6)
+        {
+            var p = new TTTraceParams { nRays = nRays, bounce = curBounce, farPlane = farPlane, screenWidth = (uint)width,
+                                        screenHeight = (uint)height, flags = TTTraceFlags.DevicePtrs };
+            Check(Native.tt_resolve_normals(m_ctx, ref p, globalRays, normals6));
+        }
+
+        /// Per-call GPU times (HIP events) since the last TimingReset, in issue order.
+        public void TimingReset() { Check(Native.tt_timing_reset(m_ctx)); }
+        public unsafe float[] TimingRead()
+        {
+            var a = new float[256];
+            uint n;
+            fixed (float* p = a) Check(Native.tt_timing_read(m_ctx, p, 256, out n));
+            Array.Resize(ref a, (int)n);
+            return a;
+        }
+
+        /// tt_scene_validate: null when the buffers pass the upload's structural check, else the first violation.
+        public static unsafe string Validate<TNode, TTri, TMesh, TMat>(TNode[] nodes, TTri[] tris, int[] tlasIndices,
+                                                                       TMesh[] meshData, TMat[] materials)
+            where TNode : unmanaged where TTri : unmanaged where TMesh : unmanaged where TMat : unmanaged
+        {
+            var why = new byte[512];
+            TTStatus st;
+            fixed (TNode* n = nodes) fixed (TTri* t = tris) fixed (int* i = tlasIndices)
+            fixed (TMesh* m = meshData) fixed (TMat* mt = materials) fixed (byte* w = why)
+                st = Native.tt_scene_validate(n, (uint)nodes.Length, t, (uint)tris.Length, i, (uint)tlasIndices.Length,
+                                              m, (uint)meshData.Length, mt, (uint)materials.Length, w, (uint)why.Length);
+            if (st == TTStatus.Ok) return null;
+            int len = Array.IndexOf(why, (byte)0);
+            return $"{st}: {System.Text.Encoding.ASCII.GetString(why, 0, len < 0 ? why.Length : len)}";
+        }
+
+        /// tt_shutdown: destroys every library stream still alive. Call from OnApplicationQuit (or
+        /// AppDomain.DomainUnload) when dispatches come from a thread other than the main one, after the last one.
+        public static void Shutdown() { Native.tt_shutdown(); }
 
         /// The hipStream_t the engine issues on (for ordering the caller's own HIP work around it).
         public IntPtr Stream => Native.tt_ctx_stream(m_ctx);
@@ -261,8 +428,8 @@ namespace TrueTrace.Hip
         }
 
         /// A hipStream_t on a hardware queue of its own (tt_stream_create) for a concurrently traced half of
-        /// the frame: pass handle.DangerousGetHandle() as the hipStream of that half's tracer and dispose the
-        /// handle after the tracer. The handle is a SafeHandle: a finalizer or a domain reload that skips
+        /// the frame: pass the handle to that half's tracer (the TTStreamHandle constructor, which keeps it alive
+        /// until the tracer is disposed). The handle is a SafeHandle: a finalizer or a domain reload that skips
         /// Dispose still destroys the stream (and the library destroys any stream left at process exit).
         public static TTStreamHandle StreamCreate(int device)
         {
@@ -412,6 +579,80 @@ namespace TrueTrace.Hip
         public void Dispose()
         {
             if (m_ctx != IntPtr.Zero) { Native.tt_ctx_destroy(m_ctx); m_ctx = IntPtr.Zero; }
+            if (m_streamRef) { m_stream.DangerousRelease(); m_streamRef = false; }
+            m_stream = null;
+        }
+    }
+
+    /// C5's multi-GPU mode behind the C ABI (tt_group_*): the scene replicated per device, a frame's 64x64 tiles
+    /// dealt round-robin, each device generating and tracing its tiles (and their bounce 1), and the primary hit
+    /// records gathered to device 0 in screen order with one RCCL gather. Replaces, for a whole frame, the
+    /// Generate + per-bounce kernel_trace dispatches of RayTracingMaster.RenderImage (RayTracingMaster.cs:954-1007).
+    public sealed class TrueTraceHipGroup : IDisposable
+    {
+        IntPtr m_g;
+
+        /// One process driving `devices` (member 0 receives the gather).
+        public unsafe TrueTraceHipGroup(int[] devices, TTGroupConfig cfg)
+        {
+            fixed (int* d = devices) Check(Native.tt_group_create(d, (uint)devices.Length, ref cfg, out m_g));
+        }
+
+        /// One rank per process: every process calls this with rank 0's UniqueId() (the host distributes it).
+        public unsafe TrueTraceHipGroup(byte[] uniqueId, uint world, uint rank, int device, TTGroupConfig cfg)
+        {
+            fixed (byte* id = uniqueId) Check(Native.tt_group_create_rank(id, world, rank, device, ref cfg, out m_g));
+        }
+
+        public static unsafe byte[] UniqueId()
+        {
+            var id = new byte[128];
+            fixed (byte* p = id)
+                if (Native.tt_group_unique_id(p) != TTStatus.Ok) throw new InvalidOperationException("tt_group_unique_id");
+            return id;
+        }
+
+        /// AssetManager.SetMeshTraceBuffers on every device of the group (the scene replicated).
+        public unsafe void SetMeshTraceBuffers<TNode, TTri, TMesh, TMat>(TNode[] nodes, TTri[] tris, int[] tlasIndices,
+                                                                        TMesh[] meshData, TMat[] materials)
+            where TNode : unmanaged where TTri : unmanaged where TMesh : unmanaged where TMat : unmanaged
+        {
+            fixed (TNode* n = nodes) fixed (TTri* t = tris) fixed (int* i = tlasIndices)
+            fixed (TMesh* m = meshData) fixed (TMat* mt = materials)
+                Check(Native.tt_group_scene_upload(m_g, n, (uint)nodes.Length, t, (uint)tris.Length, i, (uint)tlasIndices.Length,
+                                                   m, (uint)meshData.Length, mt, (uint)materials.Length));
+        }
+
+        /// One frame: Generate + primary trace per device for its tiles, the gather of the primary hit records to
+        /// `hitsOut` (device 0, width*height uint4 in screen order), bounce 1 per device with TTGroupFlags.Bounce.
+        public void TraceFrame(ref TTCamera cam, IntPtr hitsOut, bool async = false)
+        {
+            Check(Native.tt_group_trace_frame(m_g, ref cam, hitsOut, async ? (uint)TTTraceFlags.Async : 0u));
+        }
+
+        public void Sync() { Check(Native.tt_group_sync(m_g)); }
+
+        /// Member m's scene context: per-frame scene updates (RefitTLAS, SetMeshData) go through it.
+        public IntPtr MemberContext(uint m) => Native.tt_group_member_ctx(m_g, m);
+        public uint LocalMembers => Native.tt_group_local_members(m_g);
+
+        /// The latest frame of member m: primary and bounce-1 counts and its RayData buffer in HIP memory.
+        public (uint primary, uint bounce, IntPtr rays) FrameRays(uint m)
+        {
+            Check(Native.tt_group_frame_rays(m_g, m, out uint a, out uint b, out IntPtr r));
+            return (a, b, r);
+        }
+
+        void Check(TTStatus st)
+        {
+            if (st != TTStatus.Ok)
+                throw new InvalidOperationException(
+                    $"truetrace_hip group: {st}: {(m_g == IntPtr.Zero ? "" : Marshal.PtrToStringAnsi(Native.tt_group_last_error(m_g)))}");
+        }
+
+        public void Dispose()
+        {
+            if (m_g != IntPtr.Zero) { Native.tt_group_destroy(m_g); m_g = IntPtr.Zero; }
         }
     }
 }

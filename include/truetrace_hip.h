@@ -661,6 +661,97 @@ tt_status tt_enqueue_diffuse_bounce_indirect(tt_ctx* ctx, const tt_trace_params*
                                              tt_ray_data* global_rays, int32_t frames_accumulated,
                                              int32_t max_bounce, uint32_t* n_next_dev);
 
+/* ------------------------------- multi-GPU tile-sharded frames */
+/* The reference traces a frame with one dispatch per bounce on one GPU
+ * (RayTracingMaster.cs:954-1007: Generate, then kernel_trace / kernel_shade per bounce). A group
+ * traces a frame over several MI355X: the scene is replicated per device, the screen is cut into
+ * tile x tile pixel tiles dealt round-robin (tile t to rank t % world), every member generates and
+ * traces the primary rays of its tiles on its own device and streams, and the 16-B primary hit
+ * records go to rank 0 with ONE RCCL gather (ncclSend / ncclRecv in a single group), where they are
+ * scattered back to screen order: hits_out[pixel] holds exactly the RayData.hits tt_generate_primary
+ * + tt_trace_closest write at GlobalRays[pixel]. Optionally each member then continues its own rays
+ * (bounce 1: tt_enqueue_diffuse_bounce_indirect + tt_trace_closest_indirect on its stream) -- the
+ * bounce chain never leaves the device.
+ *
+ * Two ways to form a group, one code path after that:
+ *   tt_group_create       one process drives n devices (ncclCommInitAll): the C# / Unity host shape;
+ *   tt_group_create_rank  one process per device (ncclCommInitRank over a tt_group_unique_id that
+ *                         the host distributes), the shape of bench.py under torch.distributed.run.
+ * RCCL is loaded at run time (dlopen "librccl.so.1": the copy a process already has, e.g. PyTorch's,
+ * or the system ROCm one); TT_GROUP_COPY_GATHER gathers with device-to-device copies instead (one
+ * process only; lets several members share one device, for tests on a one-GPU machine).
+ * Frames are asynchronous when TT_TRACE_ASYNC is set: frame k uses slot k % slots (its own rays,
+ * contexts and dedicated streams per member), so a member's next frame overlaps the previous one's
+ * drain and gather; tt_group_sync waits for everything. */
+typedef struct tt_group tt_group;
+
+enum {
+    TT_GROUP_COPY_GATHER = 1u << 0, /* gather with hipMemcpyAsync instead of RCCL (tt_group_create only)   */
+    TT_GROUP_BOUNCE = 1u << 1       /* each member traces bounce 1 of its primary hits (diffuse enqueue)  */
+};
+
+typedef struct tt_group_config {
+    uint32_t width, height; /* the screen (hits_out holds width * height records)                      */
+    uint32_t tile;          /* tile edge in pixels, a multiple of 8 (0: 64)                               */
+    uint32_t slots;         /* frames in flight per member (0: 2; at most 8)                              */
+    uint32_t flags;         /* TT_GROUP_*                                                                 */
+    uint32_t pad;
+} tt_group_config;
+
+/* One process, n devices (devices[i] is member i's HIP ordinal; member 0 is rank 0 and receives the
+ * gather). Without TT_GROUP_COPY_GATHER the devices must be distinct. */
+tt_status tt_group_create(const int32_t* devices, uint32_t n, const tt_group_config* cfg, tt_group** out);
+/* The 128-byte RCCL unique id for tt_group_create_rank (rank 0 makes it; the host broadcasts it). */
+tt_status tt_group_unique_id(uint8_t id[128]);
+/* One member per process: this process is rank `rank` of `world` and drives HIP device `device`.
+ * Every rank calls it concurrently (RCCL's init is collective). */
+tt_status tt_group_create_rank(const uint8_t id[128], uint32_t world, uint32_t rank, int32_t device,
+                               const tt_group_config* cfg, tt_group** out);
+/* Synchronizes, tears the communicators, contexts and streams down. */
+tt_status tt_group_destroy(tt_group* g);
+const char* tt_group_last_error(const tt_group* g);
+/* Members this process drives (n for tt_group_create, 1 for tt_group_create_rank). */
+uint32_t tt_group_local_members(const tt_group* g);
+/* Member m's scene context (slot 0's; the other slots share its scene, tt_ctx_share_scene): scene
+ * updates (tt_scene_update_*, tt_tlas_refit, tt_blas_refit) go through it, and every slot sees them
+ * in call order. NULL for m out of range. */
+tt_ctx* tt_group_member_ctx(tt_group* g, uint32_t m);
+/* tt_scene_upload on every local member (the scene replicated per device). */
+tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_t n_nodes,
+                                const tt_cuda_triangle* tris, uint32_t n_tris,
+                                const int32_t* tlas_indices, uint32_t n_tlas_indices,
+                                const tt_mesh_data* meshdata, uint32_t n_mesh,
+                                const tt_material* materials, uint32_t n_mat);
+/* One frame: Generate (cam: width / height must be the group's; TT_TRACE_DEVICE_PTRS implied) on every
+ * member for its tiles, the primary trace, the gather to rank 0 and, with TT_GROUP_BOUNCE, bounce 1 on
+ * every member. hits_out: on the process holding rank 0, a 16-byte-aligned DEVICE buffer on rank 0's
+ * device of width * height uint4 records (screen order); ignored (may be NULL) elsewhere.
+ * flags: TT_TRACE_ASYNC (return without waiting). */
+tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t flags);
+/* Waits for every frame issued so far (all members, all slots, the gathers). */
+tt_status tt_group_sync(tt_group* g);
+/* Of the latest frame, member m: its primary ray count, its bounce-1 ray count (0 without
+ * TT_GROUP_BOUNCE) and the device pointer of its ray buffer (RayData[width * height + primary]:
+ * primary rays at [0, primary), bounce-1 rays at [width * height, + bounce)). Synchronizes. Any
+ * output may be NULL. */
+tt_status tt_group_frame_rays(tt_group* g, uint32_t m, uint32_t* n_primary, uint32_t* n_bounce,
+                              tt_ray_data** rays_dev);
+/* The shard arithmetic (host only, no GPU): the pixels rank `rank` of `world` traces, in trace order --
+ * its tiles t = rank, rank + world, ... (row-major tile ids over ceil(W / tile) x ceil(H / tile)), inside a
+ * tile 8 x 8 pixel blocks in row-major block order, pixels row-major inside a block (so the 64 rays a
+ * wave dequeues together are one 8 x 8 screen patch). world == 1 is the identity (pixel i = ray i, the
+ * full-frame order the trace kernel swizzles itself). Writes min(count, max) indices, sets *n to count. */
+tt_status tt_group_tile_pixels(uint32_t width, uint32_t height, uint32_t tile, uint32_t world, uint32_t rank,
+                               uint32_t* pixels, uint32_t max, uint32_t* n);
+
+/* ------------------------------------------------------------- shutdown */
+/* Synchronizes and destroys every stream tt_stream_create made that is still alive. For hosts that
+ * trace from a thread other than the main one (Unity's render thread): call it before the process or
+ * the domain goes down (OnApplicationQuit / AppDomain.DomainUnload), after the last launch. Contexts
+ * still alive keep their own streams; a context on a destroyed library stream refuses further launches
+ * (TT_ERR_INVALID_ARG). Idempotent. */
+tt_status tt_shutdown(void);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -1,0 +1,240 @@
+"""The multi-GPU group behind the C ABI (tt_group_*, csrc/tt_group.hip) against the oracle and
+the single-device path.
+
+A group traces a frame tile-sharded over its members and gathers the primary hit records to rank 0 in screen
+order; each member continues its own rays with bounce 1. On this one-GPU pool a group has either one RCCL member
+(ncclCommInitAll over device 0, or ncclCommInitRank at world 1: the RCCL gather then is rank 0's send to itself)
+or several members sharing device 0 with the copy gather (TT_GROUP_COPY_GATHER): the shard, trace, gather and
+scatter code is the one a node of 8 MI355X runs.
+
+Bar: the gathered frame is bit-identical to the oracle's Generate + trace of the whole frame (and to the
+engine's own tt_generate_primary + tt_trace_closest); every member's bounce-1 rays and records are bit-identical
+to the oracle's enqueue + trace over that member's own ray list (tt_group_tile_pixels order).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import tthip
+
+from parity_util import CPU_THREADS, FAR
+
+pytestmark = pytest.mark.gpu
+
+NEAR = 0.05
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return torch
+
+
+def _hip():
+    # torch's own HIP runtime (same soname): copies of raw device pointers the group hands out
+    L = C.CDLL("libamdhip64.so.7")
+    L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    return L
+
+
+def device_rays(ptr: int, n: int) -> np.ndarray:
+    out = np.zeros(n, tthip.RAY_DTYPE)
+    if n:
+        assert _hip().hipMemcpy(out.ctypes.data, ptr, 48 * n, 2) == 0  # hipMemcpyDeviceToHost
+    return out
+
+
+@pytest.fixture(scope="module")
+def soup():
+    return tthip.single_object_scene(tthip.Mesh.soup(11, 40000, 1.0, 0.07))
+
+
+def soup_camera(W, H):
+    return tthip.unity_camera((0.3, 0.2, 2.6), (-0.1, -0.05, -1.0), (0, 1, 0), 60.0, W, H, NEAR, FAR)
+
+
+def oracle_frame(sc, c2w, ip, W, H, frames, max_bounce=1):
+    """The oracle's whole frame: Generate (jittered at `frames`) and the primary trace; returns the rays."""
+    rays = O.generate(c2w, ip, W, H, NEAR, FAR, jitter=1, frames=frames, max_bounce=max_bounce)
+    assert O.trace(sc, rays, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+    return rays
+
+
+def oracle_member(sc, full, pix, W, H, frames, max_bounce=1):
+    """The oracle's view of one member: its primary rays (the frame's rays at its pixels, in its order, hits
+    included), the enqueue of their bounce-1 rays at [W*H, + nb) and the bounce-1 trace. Returns (rays, nb)."""
+    n = len(pix)
+    r = np.zeros(W * H + n, tthip.RAY_DTYPE)
+    r[:n] = full[pix.astype(np.int64)]
+    nb = O.enqueue_bounce(sc, r, n, 0, FAR, W, H, frames=frames, max_bounce=max_bounce)
+    assert O.trace(sc, r, nb, 1, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+    return r, nb
+
+
+def check_members(g, sc, full, W, H, frames, world):
+    for m in range(g.local_members()):
+        n, nb, ptr = g.frame_rays(m)
+        pix = tthip.group_tile_pixels(W, H, world, m)
+        assert n == len(pix)
+        got = device_rays(ptr, W * H + n)
+        ref, nb_ref = oracle_member(sc, full, pix, W, H, frames)
+        assert nb == nb_ref, (m, nb, nb_ref)
+        assert np.array_equal(got[:n].view(np.uint8), ref[:n].view(np.uint8)), f"member {m}: primary rays"
+        assert np.array_equal(got[W * H:W * H + nb].view(np.uint8), ref[W * H:W * H + nb].view(np.uint8)), \
+            f"member {m}: bounce-1 rays / records"
+
+
+def test_copy_gather_three_members_equal_the_oracle_frame(soup):
+    """3 members on device 0 (copy gather), a screen that is no multiple of the tile: the gathered frame and
+    every member's bounce chain against the oracle."""
+    torch = _torch()
+    W, H, frames = 328, 200, 5
+    c2w, ip = soup_camera(W, H)
+    g = tthip.Group(W, H, devices=[0, 0, 0], bounce=True, copy=True)
+    try:
+        g.upload(soup)
+        hits = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+        g.trace_frame(hits, c2w, ip, NEAR, FAR, jitter=1, frames=frames, max_bounce=1)
+        full = oracle_frame(soup, c2w, ip, W, H, frames)
+        got = hits.cpu().numpy().view(np.uint32)
+        assert int((full["hits"][:W * H, 1] != 0xFFFFFFFF).sum()) > W * H // 4
+        assert np.array_equal(got, full["hits"][:W * H]), "gathered screen-order records"
+        check_members(g, soup, full, W, H, frames, 3)
+    finally:
+        g.close()
+
+
+def test_one_member_rccl_group_equals_the_single_launch(engine, soup):
+    """A one-device RCCL group (ncclCommInitAll over device 0; the gather is rank 0's send to itself): the frame
+    equals tt_generate_primary + tt_trace_closest on one context, and the member's bounce chain the engine's."""
+    torch = _torch()
+    W, H, frames = 320, 192, 2
+    c2w, ip = soup_camera(W, H)
+    g = tthip.Group(W, H, devices=[0], bounce=True)
+    try:
+        g.upload(soup)
+        hits = torch.zeros((W * H, 4), dtype=torch.int32, device="cuda:0")
+        g.trace_frame(hits, c2w, ip, NEAR, FAR, jitter=1, frames=frames, max_bounce=1)
+        engine.upload(soup)
+        rays = np.zeros(2 * W * H, tthip.RAY_DTYPE)
+        engine.generate(rays, c2w, ip, W, H, NEAR, FAR, jitter=1, frames=frames, max_bounce=1)
+        engine.trace(rays, W * H, 0, FAR, W, H)
+        assert np.array_equal(hits.cpu().numpy().view(np.uint32), rays["hits"][:W * H])
+        nb = engine.enqueue_bounce(rays, W * H, 0, FAR, W, H, frames=frames, max_bounce=1)
+        engine.trace(rays, nb, 1, FAR, W, H)
+        n, nb_g, ptr = g.frame_rays(0)
+        assert (n, nb_g) == (W * H, nb)
+        got = device_rays(ptr, W * H + n)
+        assert np.array_equal(got[:W * H + nb].view(np.uint8), rays[:W * H + nb].view(np.uint8))
+        full = oracle_frame(soup, c2w, ip, W, H, frames)
+        check_members(g, soup, full, W, H, frames, 1)
+    finally:
+        g.close()
+
+
+def test_rank_mode_world_one(soup):
+    """tt_group_unique_id + tt_group_create_rank (the one-process-per-GPU shape bench.py uses) at world 1."""
+    torch = _torch()
+    W, H, frames = 256, 128, 0
+    c2w, ip = soup_camera(W, H)
+    g = tthip.Group(W, H, rank=0, world=1, uid=tthip.group_unique_id(), device=0)
+    try:
+        g.upload(soup)
+        hits = torch.zeros((W * H, 4), dtype=torch.int32, device="cuda:0")
+        g.trace_frame(hits, c2w, ip, NEAR, FAR, jitter=1, frames=frames)
+        full = oracle_frame(soup, c2w, ip, W, H, frames)
+        assert np.array_equal(hits.cpu().numpy().view(np.uint32), full["hits"][:W * H])
+        assert g.frame_rays(0)[1] == 0  # no TT_GROUP_BOUNCE
+    finally:
+        g.close()
+
+
+def test_asynchronous_frames_over_slots(soup):
+    """Seven asynchronous frames over 3 slots and 2 members (each frame its own jitter and output buffer): after
+    one tt_group_sync every frame's records equal the oracle's frame."""
+    torch = _torch()
+    W, H = 192, 128
+    c2w, ip = soup_camera(W, H)
+    g = tthip.Group(W, H, devices=[0, 0], slots=3, bounce=True, copy=True)
+    try:
+        g.upload(soup)
+        outs = [torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0") for _ in range(7)]
+        for k, o in enumerate(outs):
+            g.trace_frame(o, c2w, ip, NEAR, FAR, jitter=1, frames=k, asynchronous=True)
+        g.sync()
+        for k, o in enumerate(outs):
+            full = oracle_frame(soup, c2w, ip, W, H, k)
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), full["hits"][:W * H]), k
+        check_members(g, soup, oracle_frame(soup, c2w, ip, W, H, 6), W, H, 6, 2)  # the latest frame's chains
+    finally:
+        g.close()
+
+
+def test_sponza_1080p_eight_members_copy_gather(sponza_scene):
+    """C2's scene at 1920x1080 dealt over 8 members (as on an 8-GPU node, here all on device 0): the gathered frame
+    equals the oracle's, and two members' bounce chains (the first and last rank) too."""
+    torch = _torch()
+    W, H, frames = 1920, 1080, 1
+    c2w, ip = tthip.unity_camera((-10, 2, 0), (1, 0, 0), (0, 1, 0), 60, W, H, 0.3, FAR)
+    g = tthip.Group(W, H, devices=[0] * 8, bounce=True, copy=True)
+    try:
+        g.upload(sponza_scene)
+        hits = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+        cam = dict(jitter=1, frames=frames, max_bounce=1)
+        g.trace_frame(hits, c2w, ip, 0.3, FAR, **cam)
+        full = O.generate(c2w, ip, W, H, 0.3, FAR, **cam)
+        assert O.trace(sponza_scene, full, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+        assert np.array_equal(hits.cpu().numpy().view(np.uint32), full["hits"][:W * H])
+        for m in (0, 7):
+            n, nb, ptr = g.frame_rays(m)
+            pix = tthip.group_tile_pixels(W, H, 8, m)
+            got = device_rays(ptr, W * H + n)
+            r = np.zeros(W * H + n, tthip.RAY_DTYPE)
+            r[:n] = full[pix.astype(np.int64)]
+            nb_ref = O.enqueue_bounce(sponza_scene, r, n, 0, FAR, W, H, frames=frames, max_bounce=1)
+            assert O.trace(sponza_scene, r, nb_ref, 1, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+            assert nb == nb_ref and nb > 0.9 * n
+            assert np.array_equal(got[:n].view(np.uint8), r[:n].view(np.uint8))
+            assert np.array_equal(got[W * H:W * H + nb].view(np.uint8), r[W * H:W * H + nb].view(np.uint8))
+    finally:
+        g.close()
+
+
+@pytest.fixture(scope="module")
+def sponza_scene():
+    am = tthip.AssetManager()
+    am.add_parent(tthip.Blas(tthip.Mesh.sponza()), None, np.zeros(7, tthip.MAT_DTYPE))
+    return am.build()
+
+
+def test_group_refusals(soup):
+    torch = _torch()
+    L = tthip._group_lib()
+    cfg = tthip.GroupConfig(width=64, height=64)
+    h = C.c_void_p()
+    devs = np.zeros(2, np.int32)
+    # RCCL takes one rank per device: two members on device 0 need the copy gather
+    assert L.tt_group_create(devs.ctypes.data, 2, C.byref(cfg), C.byref(h)) == tthip.TT_ERR_INVALID_ARG
+    bad = tthip.GroupConfig(width=64, height=64, tile=12)
+    assert L.tt_group_create(devs.ctypes.data, 1, C.byref(bad), C.byref(h)) == tthip.TT_ERR_INVALID_ARG
+    g = tthip.Group(64, 64, devices=[0, 0], copy=True)
+    try:
+        c2w, ip = soup_camera(64, 64)
+        hits = torch.zeros((64 * 64, 4), dtype=torch.int32, device="cuda:0")
+        with pytest.raises(tthip.TTError) as e:  # no scene yet
+            g.trace_frame(hits, c2w, ip, NEAR, FAR)
+        assert e.value.status == tthip.TT_ERR_NO_SCENE
+        g.upload(soup)
+        with pytest.raises(tthip.TTError) as e:  # hits_out in host memory
+            g.trace_frame(np.zeros((64 * 64, 4), np.uint32), c2w, ip, NEAR, FAR)
+        assert e.value.status == tthip.TT_ERR_INVALID_ARG
+        cam = tthip.Camera()
+        cam.width, cam.height, cam.far_plane = 32, 64, FAR  # not the group's screen
+        assert L.tt_group_trace_frame(g.h, C.byref(cam), hits.data_ptr(), 0) == tthip.TT_ERR_INVALID_ARG
+        g.trace_frame(hits, c2w, ip, NEAR, FAR)  # still usable after refusals
+    finally:
+        g.close()

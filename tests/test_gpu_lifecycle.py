@@ -25,14 +25,16 @@ def _run(cmd, tmp):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=90, cwd=tmp, env=env)
 
 
-@pytest.mark.parametrize("mode", ["contexts-destroyed", "keep-contexts"])
+@pytest.mark.parametrize("mode", ["contexts-destroyed", "keep-contexts", "worker-thread", "worker-shutdown"])
 def test_exit_with_live_dedicated_streams(tmp_path, mode):
     """A process that made 3 dedicated streams, traced on them, and exits without tt_stream_destroy ends
     with status 0 -- plainly and under rocprofv3 --kernel-trace, where the CU-mask queues alive at HIP
     teardown used to crash the exit (SIGSEGV in __cxa_finalize), and where a teardown from an atexit handler
     alone aborts in the tool's per-thread stream table (destroyed with the thread's thread_locals, before any
-    atexit handler runs; tt_api.hip arms the teardown from a main-thread thread_local for that reason)."""
-    args = [sys.executable, CHILD] + (["keep-contexts"] if mode == "keep-contexts" else [])
+    atexit handler runs; tt_api.hip arms the teardown from a main-thread thread_local for that reason, and the
+    atexit form runs it on a fresh thread). The worker modes trace only from a worker thread (Unity's render
+    thread shape): without tt_shutdown (the atexit path) and with it."""
+    args = [sys.executable, CHILD] + ([mode] if mode != "contexts-destroyed" else [])
     r = _run(args, str(tmp_path))
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     assert "live 3" in r.stdout and "ok" in r.stdout

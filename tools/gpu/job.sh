@@ -5,6 +5,8 @@
 # the first failing stage (no GPU step runs after a failure). Stages:
 #   tests      pytest -m gpu (the parity suite)
 #   bench      the driver's command: python bench.py --gpus 1 --steps 20 --warmup 5
+#   group      the multi-GPU group (tt_group_*), batched-frame oracle and lifecycle GPU tests
+#   groupbench the bench headline + aux_group_tiles (the library's group path) + interactive, no other aux legs
 #   smoke      __graft_entry__.smoke() (the driver runs it before the bench)
 #   blocks     the headline per persistent-grid size: BLOCKS="20 16 12" blocks per CU (TT_BLOCKS_PER_CU), REPS
 #   quick      bench without aux configs / CPU baseline (layout and headline only)
@@ -58,6 +60,10 @@ for stage in "$@"; do
                 run "blocks_${b}_$i" 300 env TT_BLOCKS_PER_CU=$b python -u bench.py --steps 20 --warmup 5 --aux "" \
                     --no-cpu-baseline --no-recur --no-shadow || exit $?
             done; done ;;
+    group) run group 900 env TT_TEST_ROCPROF=1 python -u -m pytest -x -v --timeout 400 --timeout-method thread \
+               tests/test_gpu_group.py tests/test_gpu_batch_oracle.py tests/test_gpu_lifecycle.py -m gpu || exit $? ;;
+    groupbench) run groupbench 400 python -u bench.py --steps 20 --warmup 5 --aux "" --no-cpu-baseline --no-recur \
+                    --no-shadow --no-single ${GB_ARGS:-} || exit $? ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     quick) run quick 300 python -u bench.py --steps 20 --warmup 5 --aux "" --cpu-seconds 2 || exit $? ;;

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -127,6 +128,7 @@ struct tt_ctx {
     uint32_t ring_n = 0, ring_base = 0;
     bool timing = true;  // tt_ctx_set_timing: asynchronous launches record their HIP-event pair
     uint32_t frame_pixels = 0;  // tt_ctx_set_frame_pixels: batched frames' bounce random numbers (0: off)
+    bool lib_stream = false;    // stream is one of tt_stream_create's (tt_shutdown / the exit teardown may end it)
     std::string err;
     // scene
     bool has_scene = false;
@@ -729,6 +731,11 @@ const char* tt_last_error(const tt_ctx* c) { return c ? c->err.c_str() : "null c
 namespace {
 std::mutex g_streams_mu;
 std::vector<std::pair<int, hipStream_t>> g_streams;
+// streams the teardown (tt_shutdown, the exit handlers) destroyed under a context still holding them: such a
+// context refuses launches and skips the stream sync in tt_ctx_destroy (a host's static destructors may
+// destroy contexts after the teardown ran)
+std::vector<hipStream_t> g_dead;
+std::atomic<uint32_t> g_dead_n{0};
 bool g_streams_handler = false;
 
 void release_live_streams() {
@@ -736,6 +743,8 @@ void release_live_streams() {
     {
         std::lock_guard<std::mutex> lk(g_streams_mu);
         live.swap(g_streams);
+        for (auto& ds : live) g_dead.push_back(ds.second);
+        g_dead_n.store((uint32_t)g_dead.size());
     }
     for (auto& ds : live) {
         if (hipSetDevice(ds.first) != hipSuccess) continue;
@@ -744,7 +753,37 @@ void release_live_streams() {
     }
     (void)hipGetLastError();
 }
+
+// The atexit form. exit() has already destroyed the exiting thread's thread_locals when atexit handlers
+// run, and a profiler that wraps the HIP API (rocprofv3) keeps per-thread state its stream calls need
+// ("'get_stream_stack()' Must be non nullptr", profiles/r05/lifecycle/atexit_only_abort_under_rocprofv3.txt):
+// so the teardown runs on a fresh thread, whose thread state is created on its first HIP call.
+void release_live_streams_at_exit() {
+    {
+        std::lock_guard<std::mutex> lk(g_streams_mu);
+        if (g_streams.empty()) return;
+    }
+    std::thread t(release_live_streams);
+    t.join();
+}
+
+bool stream_dead(hipStream_t s) {
+    if (g_dead_n.load(std::memory_order_relaxed) == 0) return false;
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    return std::find(g_dead.begin(), g_dead.end(), s) != g_dead.end();
+}
+bool is_lib_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    return std::any_of(g_streams.begin(), g_streams.end(), [s](const std::pair<int, hipStream_t>& ds) { return ds.second == s; });
+}
 }  // namespace
+
+// a context whose library stream the teardown destroyed refuses every launch
+#define TT_REFUSE_DEAD_STREAM(c)                                                                            \
+    do {                                                                                                    \
+        if ((c)->lib_stream && stream_dead((c)->stream))                                                    \
+            return fail((c), TT_ERR_INVALID_ARG, "the context's stream was destroyed by tt_shutdown / the exit teardown"); \
+    } while (0)
 
 extern "C" {
 
@@ -788,6 +827,11 @@ void note_stream_launch(hipStream_t s) {
 
 extern "C" {
 
+tt_status tt_shutdown(void) {
+    release_live_streams();
+    return TT_OK;
+}
+
 uint32_t tt_stream_live_count(void) {
     std::lock_guard<std::mutex> lk(g_streams_mu);
     return (uint32_t)g_streams.size();
@@ -822,7 +866,11 @@ tt_status tt_stream_create(int32_t device, void** stream) {
         *stream = s;
         std::lock_guard<std::mutex> lk(g_streams_mu);
         g_streams.emplace_back(device, s);
-        if (!g_streams_handler && stream_exit_handler_on()) g_streams_handler = std::atexit(release_live_streams) == 0;
+        // (a new stream may reuse a destroyed one's handle)
+        g_dead.erase(std::remove(g_dead.begin(), g_dead.end(), s), g_dead.end());
+        g_dead_n.store((uint32_t)g_dead.size());
+        if (!g_streams_handler && stream_exit_handler_on())
+            g_streams_handler = std::atexit(release_live_streams_at_exit) == 0;
     }
     return st;
 }
@@ -860,6 +908,7 @@ tt_status tt_ctx_create(const tt_config* cfg, tt_ctx** out) {
     }
     if (cfg->stream) {
         c->stream = static_cast<hipStream_t>(cfg->stream);
+        c->lib_stream = is_lib_stream(c->stream);
     } else {
         // blocking (default-flag) stream: ordered with the legacy NULL stream, so callers that
         // fill device buffers on it (torch's default stream) cannot race the engine
@@ -942,7 +991,7 @@ tt_status tt_ctx_destroy(tt_ctx* c) {
     if (!c) return TT_ERR_INVALID_ARG;
     if (c->borrowers > 0) return fail(c, TT_ERR_INVALID_ARG, "other contexts share this scene: destroy them first");
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream && !(c->lib_stream && stream_dead(c->stream))) (void)hipStreamSynchronize(c->stream);
     unlink_borrower(c);
     if (c->ev_scene) (void)hipEventDestroy(c->ev_scene);
     if (c->ev_blas) (void)hipEventDestroy(c->ev_blas);
@@ -1071,6 +1120,7 @@ tt_status tt_async_overflows(tt_ctx* c, uint64_t* count) {
 
 tt_status tt_sync(tt_ctx* c) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     TT_HIP(c, hipStreamSynchronize(c->stream));
     return TT_OK;
 }
@@ -1083,6 +1133,7 @@ tt_status tt_scene_upload(tt_ctx* c, const tt_cwbvh_node* nodes, uint32_t n_node
                           uint32_t n_tris, const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md,
                           uint32_t n_mesh, const tt_material* mats, uint32_t n_mat) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     TT_REFUSE_BORROWER(c);
     TT_REFUSE_LENDER(c);
     if (!nodes || !n_nodes || !tris || !n_tris || !tlas || !n_tlas || !md || !n_mesh || (n_mat && !mats))
@@ -1288,29 +1339,23 @@ tt_status tt_ctx_share_scene(tt_ctx* dst, tt_ctx* src) {
 // TraceArgs::tlas_base (the TLAS-level NodeOffset), so the BLAS nodes and triangles stay one shared copy.
 tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
     if (!dst || !src) return TT_ERR_INVALID_ARG;
-    if (src->has_scene && !src->lender && src->tlas_res == 0)
+    if (dst == src) return fail(dst, TT_ERR_INVALID_ARG, "a context cannot share its own scene");
+    if (!src->has_scene) return fail(dst, TT_ERR_NO_SCENE, "the source context has no scene");
+    if (src->lender) return fail(dst, TT_ERR_INVALID_ARG, "the source context shares another context's scene");
+    if (dst->borrowers > 0) return fail(dst, TT_ERR_INVALID_ARG, "other contexts share this context's scene");
+    if (dst->device != src->device) return fail(dst, TT_ERR_INVALID_ARG, "the contexts are on different devices");
+    if (src->tlas_res == 0)
         return fail(dst, TT_ERR_UNSUPPORTED, "the source scene has no overlay regions (TT_NODE_STRIDE != 80, or a node "
                                              "array near the 32-bit offset limit)");
-    if (src->has_scene && !src->lender && (n_tlas_nodes == 0 || n_tlas_nodes > src->tlas_res))
+    if (n_tlas_nodes == 0 || n_tlas_nodes > src->tlas_res)
         return fail(dst, TT_ERR_INVALID_ARG, "tt_ctx_share_blas: n_tlas_nodes %u outside (0, %u] (the TLAS region)",
                     n_tlas_nodes, src->tlas_res);
-    uint32_t slot = TT_TLAS_SLOTS;
-    if (src->has_scene && !src->lender) {
-        std::lock_guard<std::recursive_mutex> lk(src->mu);
-        for (uint32_t k = 0; k < TT_TLAS_SLOTS; k++)
-            if (!((src->ovl_used >> k) & 1u)) {
-                slot = k;
-                break;
-            }
-    }
-    const bool same_slot = dst->ovl && dst->lender == src;  // a re-share keeps its region
-    if (same_slot) slot = dst->ovl_slot;
-    if (slot == TT_TLAS_SLOTS && src->has_scene && !src->lender)
-        return fail(dst, TT_ERR_UNSUPPORTED, "all %u overlay regions of the source scene are in use", TT_TLAS_SLOTS);
-    const tt_status st = share_begin(dst, src);
-    if (st != TT_OK) return st;
-    // the TLAS-side state, as the device holds it now (a device TLAS refit leaves src's host copy stale)
-    SceneHost& h = dst->host;
+    // Everything that can fail on src's side -- the TLAS read-back and walk, the overlay buffers -- happens
+    // before dst is touched, so a refused call leaves dst as it was. The TLAS-side state is taken
+    // as the device holds it now (a device TLAS refit leaves src's host copy stale).
+    TT_HIP(dst, hipSetDevice(dst->device));
+    TT_HIP(dst, hipStreamSynchronize(src->stream));
+    SceneHost h;
     {
         std::lock_guard<std::recursive_mutex> lk(src->mu);
         copy_host_light(h, src->host);
@@ -1330,24 +1375,119 @@ tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
         for (uint32_t n : h.tlas_nodes) h.is_tlas_node[n] = 1u;
     }
     const uint32_t n_tlas = (uint32_t)h.tlas.size(), n_mesh = (uint32_t)h.mesh.size();
+    struct Fresh {  // dst's own TLAS-side buffers, adopted once nothing can fail any more
+        DevBuf<int32_t> tlas;
+        DevBuf<tt_mesh_data> mesh_raw;
+        DevBuf<MeshGpu> mesh;
+        DevBuf<LeafMesh> leaf;
+        ~Fresh() {
+            tlas.release();
+            mesh_raw.release();
+            mesh.release();
+            leaf.release();
+        }
+    } fr;
     hipError_t e;
-    if ((e = dst->tlas.alloc(n_tlas)) != hipSuccess || (e = dst->mesh_raw.alloc(n_mesh)) != hipSuccess ||
-        (e = dst->mesh.alloc(n_mesh)) != hipSuccess || (e = dst->leaf.alloc(src->leaf.n)) != hipSuccess)
+    if ((e = fr.tlas.alloc(n_tlas)) != hipSuccess || (e = fr.mesh_raw.alloc(n_mesh)) != hipSuccess ||
+        (e = fr.mesh.alloc(n_mesh)) != hipSuccess || (e = fr.leaf.alloc(src->leaf.n)) != hipSuccess)
         return hip_fail(dst, e, "overlay TLAS-side buffers");
+    // the overlay region: picked and reserved in one locked section (two frame slots made concurrently
+    // over one lender never get the same region); a re-share over the same lender keeps its region
+    uint32_t slot = TT_TLAS_SLOTS;
+    const bool same_slot = dst->ovl && dst->lender == src;
+    {
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
+        if (same_slot) {
+            slot = dst->ovl_slot;
+        } else {
+            for (uint32_t k = 0; k < TT_TLAS_SLOTS; k++)
+                if (!((src->ovl_used >> k) & 1u)) {
+                    slot = k;
+                    break;
+                }
+            if (slot == TT_TLAS_SLOTS)
+                return fail(dst, TT_ERR_UNSUPPORTED, "all %u overlay regions of the source scene are in use", TT_TLAS_SLOTS);
+            src->ovl_used |= 1u << slot;
+        }
+    }
+    auto release_slot = [&] {
+        if (same_slot) return;
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
+        src->ovl_used &= ~(1u << slot);
+    };
+    if (same_slot) {
+        // unlink_borrower (in share_begin) frees the region bit: keep it reserved across the re-share
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
+        dst->ovl = false;
+    }
+    const tt_status st = share_begin(dst, src);
+    if (st != TT_OK) {
+        if (same_slot) {
+            std::lock_guard<std::recursive_mutex> lk(src->mu);
+            if (dst->lender == src)
+                dst->ovl = true;  // failed before unlinking: dst keeps its frame slot as it was
+            else
+                src->ovl_used &= ~(1u << slot);  // unlinked, then failed: the region goes with it
+        } else {
+            release_slot();
+        }
+        return st;
+    }
+    auto adopt = [](auto& to, auto& from) {
+        to.release();
+        to.p = from.p;
+        to.n = from.n;
+        to.own = true;
+        from.p = nullptr;
+        from.n = 0;
+    };
+    adopt(dst->tlas, fr.tlas);
+    adopt(dst->mesh_raw, fr.mesh_raw);
+    adopt(dst->mesh, fr.mesh);
+    adopt(dst->leaf, fr.leaf);
+    dst->host = std::move(h);
     dst->ovl = true;
     dst->ovl_slot = slot;
     dst->n_tlas_own = n_tlas_nodes;
     dst->tlas_base = src->n_nodes_scene + slot * src->tlas_res;
-    TT_HIP(dst, hipMemcpyAsync(dst->nodes.p + dst->tlas_base, src->nodes.p, sizeof(tt_cwbvh_node) * n_tlas_nodes,
-                               hipMemcpyDeviceToDevice, dst->stream));
-    TT_HIP(dst, refresh_node_copy(dst, dst->tlas_base, n_tlas_nodes));
-    TT_HIP(dst, hipMemcpyAsync(dst->tlas.p, src->tlas.p, sizeof(int32_t) * n_tlas, hipMemcpyDeviceToDevice, dst->stream));
-    TT_HIP(dst, hipMemcpyAsync(dst->mesh_raw.p, src->mesh_raw.p, sizeof(tt_mesh_data) * n_mesh, hipMemcpyDeviceToDevice,
-                               dst->stream));
-    TT_HIP(dst, hipMemcpyAsync(dst->mesh.p, src->mesh.p, sizeof(MeshGpu) * n_mesh, hipMemcpyDeviceToDevice, dst->stream));
-    TT_HIP(dst, hipMemcpyAsync(dst->leaf.p, src->leaf.p, sizeof(LeafMesh) * src->leaf.n, hipMemcpyDeviceToDevice,
-                               dst->stream));
-    TT_HIP(dst, hipStreamSynchronize(dst->stream));
+    // device copies: a failure here leaves dst with no scene at all (never a half-linked one)
+    auto abort_share = [&](hipError_t err, const char* what) {
+        (void)hipStreamSynchronize(dst->stream);
+        dst->has_scene = false;
+        dst->ovl = false;
+        dst->tlas_base = 0;
+        dst->n_tlas_own = 0;
+        dst->root_known = false;
+        dst->host = SceneHost{};
+        dst->nodes.release();
+        dst->nodes_k.release();
+        dst->tris_raw.release();
+        dst->tris.release();
+        dst->mat_tag.release();
+        dst->mat_cut.release();
+        dst->mat_glass.release();
+        dst->tex.release();
+        dst->atlas.release();
+        dst->tlas.release();
+        dst->mesh_raw.release();
+        dst->mesh.release();
+        dst->leaf.release();
+        release_slot();
+        return hip_fail(dst, err, what);
+    };
+    if ((e = hipMemcpyAsync(dst->nodes.p + dst->tlas_base, src->nodes.p, sizeof(tt_cwbvh_node) * n_tlas_nodes,
+                            hipMemcpyDeviceToDevice, dst->stream)) != hipSuccess ||
+        (e = refresh_node_copy(dst, dst->tlas_base, n_tlas_nodes)) != hipSuccess ||
+        (e = hipMemcpyAsync(dst->tlas.p, src->tlas.p, sizeof(int32_t) * n_tlas, hipMemcpyDeviceToDevice, dst->stream)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(dst->mesh_raw.p, src->mesh_raw.p, sizeof(tt_mesh_data) * n_mesh, hipMemcpyDeviceToDevice,
+                            dst->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(dst->mesh.p, src->mesh.p, sizeof(MeshGpu) * n_mesh, hipMemcpyDeviceToDevice, dst->stream)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(dst->leaf.p, src->leaf.p, sizeof(LeafMesh) * src->leaf.n, hipMemcpyDeviceToDevice,
+                            dst->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(dst->stream)) != hipSuccess)
+        return abort_share(e, "tt_ctx_share_blas: overlay copies");
     dst->root_known = true;  // its host TLAS copy is what the device holds
     share_link(dst, src);
     return TT_OK;
@@ -1355,6 +1495,7 @@ tt_status tt_ctx_share_blas(tt_ctx* dst, tt_ctx* src, uint32_t n_tlas_nodes) {
 
 tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh, uint32_t flags) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     TT_REFUSE_BORROWER_TLAS(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     // (an overlay borrower's host.nodes are its own TLAS nodes: it refits those, in its overlay region)
@@ -1399,6 +1540,7 @@ tt_status tt_tlas_refit(tt_ctx* c, uint32_t n_tlas_nodes, const float* mesh_aabb
 tt_status tt_blas_refit(tt_ctx* c, const tt_blas_refit_params* p, const float* vertices, const int32_t* indices,
                         const int32_t* leaf_of_triangle) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     TT_REFUSE_BORROWER(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !vertices || !indices || !leaf_of_triangle || !p->n_tris || !p->n_vertices || p->vertex_stride < 6)
@@ -1575,6 +1717,7 @@ tt_status refresh_leaves(tt_ctx* c) {
 
 tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     TT_REFUSE_BORROWER_TLAS(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!nodes || (uint64_t)first + count > c->host.nodes.size())
@@ -1640,6 +1783,7 @@ tt_status tt_scene_update_nodes(tt_ctx* c, uint32_t first, uint32_t count, const
 
 tt_status tt_scene_update_meshdata(tt_ctx* c, uint32_t first, uint32_t count, const tt_mesh_data* md) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     TT_REFUSE_BORROWER_TLAS(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!md || (uint64_t)first + count > c->host.mesh.size())
@@ -1739,6 +1883,7 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
                                     uint32_t* info, const tt_col_data* colors, tt_stats* stats,
                                     uint32_t* hits_out = nullptr) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or rays");
     if (p->screen_width == 0 || p->screen_height == 0) return fail(c, TT_ERR_INVALID_ARG, "zero screen size");
@@ -2000,6 +2145,7 @@ static tt_status shadow_call(tt_ctx* c, const tt_shadow_params* p, tt_shadow_ray
                              tt_col_data* colors, float* nee_pos, tt_cache_data* cache, tt_stats* stats, bool full,
                              const uint32_t* n_dev = nullptr) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays) return fail(c, TT_ERR_INVALID_ARG, "null params or shadow rays");
     if (p->screen_width == 0 || p->screen_height == 0) return fail(c, TT_ERR_INVALID_ARG, "zero screen size");
@@ -2170,6 +2316,7 @@ tt_status tt_trace_shadow_ex_indirect(tt_ctx* c, const tt_shadow_params* p, cons
 
 tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_data* rays, float* normals6) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays || !normals6) return fail(c, TT_ERR_INVALID_ARG, "null argument");
     const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;
@@ -2199,6 +2346,7 @@ tt_status tt_resolve_normals(tt_ctx* c, const tt_trace_params* p, const tt_ray_d
 
 tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     if (!cam || !rays || !cam->width || !cam->height) return fail(c, TT_ERR_INVALID_ARG, "bad camera or rays");
     const uint64_t wh = (uint64_t)cam->width * cam->height;
     if (wh > 0x7fffffffull) return fail(c, TT_ERR_INVALID_ARG, "screen too large");
@@ -2232,6 +2380,7 @@ tt_status tt_generate_primary(tt_ctx* c, const tt_camera* cam, tt_ray_data* rays
 static tt_status enqueue_call(tt_ctx* c, const tt_trace_params* p, const uint32_t* n_dev, tt_ray_data* rays,
                               int32_t frames, int32_t max_bounce, uint32_t* n_next, uint32_t* n_next_dev) {
     if (!c) return TT_ERR_INVALID_ARG;
+    TT_REFUSE_DEAD_STREAM(c);
     if (!c->has_scene) return fail(c, TT_ERR_NO_SCENE, "no scene uploaded");
     if (!p || !rays || (!n_next && !n_next_dev)) return fail(c, TT_ERR_INVALID_ARG, "null argument");
     const uint64_t wh = (uint64_t)p->screen_width * p->screen_height;

@@ -84,12 +84,10 @@ __device__ __forceinline__ float3 mul_inv(const float* W, float3 x) {
 struct CamArgs {
     float c2w[16], ip[16];
 };
-__global__ __launch_bounds__(256) void tt_generate_kernel(const CamArgs cam,
-                                                          uint32_t width, uint32_t height, float near_plane,
-                                                          float far_plane, int32_t jitter, int32_t frames,
-                                                          int32_t max_bounce, tt_ray_data* __restrict__ rays) {
-    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (x >= width || y >= height) return;
+// one camera ray of pixel (x, y) into *o (RayData, hits = (0, 0, asuint(FarPlane), 0))
+__device__ __forceinline__ void generate_one(const CamArgs& cam, uint32_t x, uint32_t y, uint32_t width, uint32_t height,
+                                             float near_plane, float far_plane, int32_t jitter, int32_t frames,
+                                             int32_t max_bounce, uint4* o) {
     const uint32_t pixel_index = y * width + x;
     float jx = 0.0f, jy = 0.0f;
     if (jitter) {
@@ -108,11 +106,34 @@ __global__ __launch_bounds__(256) void tt_generate_kernel(const CamArgs cam,
                     fma_(C(1, 2), d.z, fma_(C(1, 1), d.y, C(1, 0) * d.x)),
                     fma_(C(2, 2), d.z, fma_(C(2, 1), d.y, C(2, 0) * d.x)));
     d = normalize3(d);
-    uint4* o = reinterpret_cast<uint4*>(rays + pixel_index);
     o[0] = make_uint4(__float_as_uint(origin.x + near_plane * d.x), __float_as_uint(origin.y + near_plane * d.y),
                       __float_as_uint(origin.z + near_plane * d.z), pixel_index);
     o[1] = make_uint4(__float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z), 0u);
     o[2] = make_uint4(0u, 0u, __float_as_uint(far_plane), 0u);
+}
+
+__global__ __launch_bounds__(256) void tt_generate_kernel(const CamArgs cam,
+                                                          uint32_t width, uint32_t height, float near_plane,
+                                                          float far_plane, int32_t jitter, int32_t frames,
+                                                          int32_t max_bounce, tt_ray_data* __restrict__ rays) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= width || y >= height) return;
+    generate_one(cam, x, y, width, height, near_plane, far_plane, jitter, frames, max_bounce,
+                 reinterpret_cast<uint4*>(rays + y * width + x));
+}
+
+// The rays of a pixel list (a multi-GPU group member's screen tiles, tt_group_trace_frame): ray i is
+// pixel pixels[i]'s camera ray, bit for bit the one tt_generate_kernel writes at GlobalRays[pixel].
+__global__ __launch_bounds__(256) void tt_generate_list_kernel(const CamArgs cam, const uint32_t* __restrict__ pixels,
+                                                               uint32_t n, uint32_t width, uint32_t height,
+                                                               float near_plane, float far_plane, int32_t jitter,
+                                                               int32_t frames, int32_t max_bounce,
+                                                               tt_ray_data* __restrict__ rays) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = pixels[i];
+    generate_one(cam, p % width, p / width, width, height, near_plane, far_plane, jitter, frames, max_bounce,
+                 reinterpret_cast<uint4*>(rays + i));
 }
 
 // sin/cos of the disc-sample angle phi in [-3pi/4, 3pi/4] (sample_disc's two branches give
@@ -348,6 +369,21 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
     }
     hipLaunchKernelGGL(tt_generate_kernel, dim3((w + 255u) / 256u, h), dim3(256), 0, st, cam, w, h, near_plane, far_plane,
                        jitter, frames, max_bounce, rays);
+    return hipGetLastError();
+}
+
+// pixels: DEVICE array of n pixel indices < w * h (the caller checked them)
+hipError_t tt_launch_generate_list(const float* c2w, const float* ip, const uint32_t* pixels, uint32_t n, uint32_t w,
+                                   uint32_t h, float near_plane, float far_plane, int32_t jitter, int32_t frames,
+                                   int32_t max_bounce, tt_ray_data* rays, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    CamArgs cam;
+    for (int i = 0; i < 16; i++) {
+        cam.c2w[i] = c2w[i];
+        cam.ip[i] = ip[i];
+    }
+    hipLaunchKernelGGL(tt_generate_list_kernel, dim3((n + 255u) / 256u), dim3(256), 0, st, cam, pixels, n, w, h,
+                       near_plane, far_plane, jitter, frames, max_bounce, rays);
     return hipGetLastError();
 }
 

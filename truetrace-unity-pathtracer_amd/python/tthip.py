@@ -331,6 +331,8 @@ def hip_lib():
                   "tt_scene_update_meshdata", "tt_scene_bytes", "tt_trace_closest", "tt_sync", "tt_resolve_normals",
                   "tt_generate_primary", "tt_enqueue_diffuse_bounce", "tt_timing_reset", "tt_timing_read"]:
             getattr(L, s).restype = i32
+        if hasattr(L, "tt_group_create"):  # (absent from older variant libraries)
+            _bind_group(L)
         _HIP = L
     return _HIP
 
@@ -1061,3 +1063,142 @@ def device_count() -> int:
         return hip_lib().tt_device_count()
     except (FileNotFoundError, OSError):
         return 0
+
+
+# ---------------------------------------------------------------- multi-GPU group (tt_group_*)
+TT_GROUP_COPY_GATHER = 1 << 0
+TT_GROUP_BOUNCE = 1 << 1
+GROUP_SYMBOLS = ["tt_group_create", "tt_group_unique_id", "tt_group_create_rank", "tt_group_destroy",
+                 "tt_group_last_error", "tt_group_local_members", "tt_group_member_ctx", "tt_group_scene_upload",
+                 "tt_group_trace_frame", "tt_group_sync", "tt_group_frame_rays", "tt_group_tile_pixels", "tt_shutdown"]
+
+
+class GroupConfig(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("tile", C.c_uint32), ("slots", C.c_uint32),
+                ("flags", C.c_uint32), ("pad", C.c_uint32)]
+
+
+def _group_lib():
+    L = hip_lib()
+    if not getattr(L, "_group_bound", False):
+        _bind_group(L)
+    return L
+
+
+def _bind_group(L):
+    if True:
+        vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int32
+        L.tt_group_create.argtypes = [vp, u32, C.POINTER(GroupConfig), C.POINTER(vp)]
+        L.tt_group_unique_id.argtypes = [vp]
+        L.tt_group_create_rank.argtypes = [vp, u32, u32, i32, C.POINTER(GroupConfig), C.POINTER(vp)]
+        L.tt_group_destroy.argtypes = [vp]
+        L.tt_group_last_error.argtypes = [vp]
+        L.tt_group_last_error.restype = C.c_char_p
+        L.tt_group_local_members.argtypes = [vp]
+        L.tt_group_local_members.restype = u32
+        L.tt_group_member_ctx.argtypes = [vp, u32]
+        L.tt_group_member_ctx.restype = vp
+        L.tt_group_scene_upload.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp, u32, vp, u32]
+        L.tt_group_trace_frame.argtypes = [vp, C.POINTER(Camera), vp, u32]
+        L.tt_group_sync.argtypes = [vp]
+        L.tt_group_frame_rays.argtypes = [vp, u32, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]
+        L.tt_group_tile_pixels.argtypes = [u32, u32, u32, u32, u32, vp, u32, C.POINTER(u32)]
+        for s in ["tt_group_create", "tt_group_unique_id", "tt_group_create_rank", "tt_group_destroy",
+                  "tt_group_scene_upload", "tt_group_trace_frame", "tt_group_sync", "tt_group_frame_rays",
+                  "tt_group_tile_pixels", "tt_shutdown"]:
+            getattr(L, s).restype = i32
+        L._group_bound = True
+
+
+def group_tile_pixels(width: int, height: int, world: int, rank: int, tile: int = 64) -> np.ndarray:
+    """tt_group_tile_pixels: the library's own shard of `rank` (host arithmetic, no GPU)."""
+    L = _group_lib()
+    n = C.c_uint32()
+    _check(L.tt_group_tile_pixels(width, height, tile, world, rank, None, 0, C.byref(n)), "tt_group_tile_pixels")
+    out = np.zeros(max(1, n.value), np.uint32)
+    _check(L.tt_group_tile_pixels(width, height, tile, world, rank, out.ctypes.data, n.value, C.byref(n)),
+           "tt_group_tile_pixels")
+    return out[: n.value]
+
+
+def group_unique_id() -> bytes:
+    """tt_group_unique_id: the 128-byte RCCL id rank 0 makes for tt_group_create_rank."""
+    buf = (C.c_uint8 * 128)()
+    _check(_group_lib().tt_group_unique_id(C.addressof(buf)), "tt_group_unique_id")
+    return bytes(buf)
+
+
+def shutdown():
+    """tt_shutdown: destroys every library stream still alive (hosts tracing from a non-main thread)."""
+    _check(hip_lib().tt_shutdown(), "tt_shutdown")
+
+
+class Group:
+    """A multi-GPU tile-sharded frame (tt_group_*): ``devices`` in one process (tt_group_create), or this
+    process as ``rank`` of ``world`` on ``device`` with the RCCL id ``uid`` (tt_group_create_rank)."""
+
+    def __init__(self, width: int, height: int, devices=None, tile: int = 64, slots: int = 2, bounce: bool = False,
+                 copy: bool = False, rank: int = None, world: int = None, uid: bytes = None, device: int = None):
+        L = _group_lib()
+        cfg = GroupConfig(width=width, height=height, tile=tile, slots=slots,
+                          flags=(TT_GROUP_BOUNCE if bounce else 0) | (TT_GROUP_COPY_GATHER if copy else 0))
+        h = C.c_void_p()
+        if devices is not None:
+            devs = np.ascontiguousarray(devices, np.int32)
+            st = L.tt_group_create(devs.ctypes.data, len(devs), C.byref(cfg), C.byref(h))
+            self.world = len(devs)
+        else:
+            idb = (C.c_uint8 * 128).from_buffer_copy(uid)
+            st = L.tt_group_create_rank(C.addressof(idb), world, rank, device, C.byref(cfg), C.byref(h))
+            self.world = world
+        if st != TT_OK:
+            raise TTError(st, "tt_group_create")
+        self.L, self.h = L, h.value
+        self.width, self.height, self.bounce = width, height, bounce
+
+    def _check(self, st, what):
+        if st != TT_OK:
+            raise TTError(st, f"{what}: {self.L.tt_group_last_error(self.h).decode()}")
+
+    def local_members(self) -> int:
+        return int(self.L.tt_group_local_members(self.h))
+
+    def member_ctx(self, m: int) -> int:
+        return self.L.tt_group_member_ctx(self.h, m)
+
+    def upload(self, s: Scene):
+        st = self.L.tt_group_scene_upload(self.h, _ptr(s.nodes), len(s.nodes), _ptr(s.tris), len(s.tris),
+                                          _ptr(s.tlas), len(s.tlas), _ptr(s.meshdata), len(s.meshdata),
+                                          _ptr(s.materials), len(s.materials))
+        self._check(st, "tt_group_scene_upload")
+
+    def trace_frame(self, hits_out, cam_to_world, cam_inv_proj, near, far, jitter=1, frames=0, max_bounce=1,
+                    asynchronous=False):
+        cam = Camera()
+        cam.cam_to_world[:] = unity_colmajor(cam_to_world)
+        cam.cam_inv_proj[:] = unity_colmajor(cam_inv_proj)
+        cam.near_plane, cam.far_plane, cam.width, cam.height = near, far, self.width, self.height
+        cam.jitter, cam.frames_accumulated, cam.max_bounce = jitter, frames, max_bounce
+        cam.flags = TT_TRACE_DEVICE_PTRS
+        self._check(self.L.tt_group_trace_frame(self.h, C.byref(cam), _ptr(hits_out),
+                                                TT_TRACE_ASYNC if asynchronous else 0), "tt_group_trace_frame")
+
+    def sync(self):
+        self._check(self.L.tt_group_sync(self.h), "tt_group_sync")
+
+    def frame_rays(self, m: int = 0):
+        """(n_primary, n_bounce, device pointer of the ray buffer) of member m's latest frame."""
+        a, b, p = C.c_uint32(), C.c_uint32(), C.c_void_p()
+        self._check(self.L.tt_group_frame_rays(self.h, m, C.byref(a), C.byref(b), C.byref(p)), "tt_group_frame_rays")
+        return a.value, b.value, p.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tt_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
