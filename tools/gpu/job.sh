@@ -27,6 +27,8 @@
 #   gloo4      the same with 4 ranks
 #   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
+#   l2loc      C2 per variant (AB_ORDER, AB_LIBS; default cur vs trint = non-temporal triangle loads): launch
+#              times, then TCC hit / miss / EA read requests and TCP / TD counters of the same launches
 #   order      tools/exp_order.py per TT_ORDER_HOT threshold (ORDER_HOT, ORDER_CFGS, ORDER_ARGS)
 #   sweep      randomized parity sweep (tools/parity_sweep.py): SWEEP_N plain + SWEEP_N variants/adaptive + SWEEP_N
 #              degenerate-direction cases + SWEEP_N frame-slot cases from seed SWEEP_SEED
@@ -105,6 +107,18 @@ for stage in "$@"; do
                    --output-format csv -- python tools/prof_config.py c4 --reps 2 || exit $?
                run "c4loc_fetch_$v" 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c4loc_fetch_$v" -o fetch \
                    --output-format csv -- python tools/prof_config.py c4 --reps 2 || exit $?
+               unset TT_HIP_LIB
+           done ;;
+    l2loc) export TMPDIR=/tmp  # C2 one launch at a time per variant (AB_ORDER), then per variant (AB_LIBS) the
+           # L2 side (TCC hit / miss / fabric read requests) and the L1 / TD side of the same launches
+           run l2loc_time 600 python -u tools/run_variants.py ${AB_ORDER:-cur trint cur trint cur trint} || exit $?
+           for v in ${AB_LIBS:-cur trint}; do
+               export TT_HIP_LIB=truetrace-unity-pathtracer_amd/lib/variants/libtruetrace_hip_$v.so
+               run "l2loc_tcc_$v" 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum \
+                   -d "$OUT/l2loc_tcc_$v" -o tcc --output-format csv -- python tools/prof_config.py c2 --reps 2 || exit $?
+               run "l2loc_tcp_$v" 300 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TD_TD_BUSY_sum \
+                   GRBM_GUI_ACTIVE -d "$OUT/l2loc_tcp_$v" -o tcp --output-format csv -- python tools/prof_config.py c2 \
+                   --reps 2 || exit $?
                unset TT_HIP_LIB
            done ;;
     order) for h in ${ORDER_HOT:-0 128}; do  # adaptive order, hoisting only chunks costing >= h node steps (0: full sort)

@@ -420,9 +420,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                         d_uniform += (same == all && lane == (uint32_t)__builtin_ctzll(all)) ? 1u : 0u;
                     }
                     const uint32_t no = node_offset(child);
-                    const uint4 n0 = buffer_load16(nodes, no), n1 = buffer_load16(nodes, no + 16u),
-                                n2 = buffer_load16(nodes, no + 32u), n3 = buffer_load16(nodes, no + 48u),
-                                n4 = buffer_load16(nodes, no + 64u);
+                    const uint4 n0 = buffer_load16<TT_NODE_CPOL>(nodes, no), n1 = buffer_load16<TT_NODE_CPOL>(nodes, no + 16u),
+                                n2 = buffer_load16<TT_NODE_CPOL>(nodes, no + 32u),
+                                n3 = buffer_load16<TT_NODE_CPOL>(nodes, no + 48u),
+                                n4 = buffer_load16<TT_NODE_CPOL>(nodes, no + 64u);
                     const uint32_t hitmask = node_intersect(n0, n1, n2, n3, n4, ray, oct, best.t);
                     cg.y = (hitmask & 0xff000000u) | (n0.w >> 24);
                     tg.y = hitmask & 0x00ffffffu;

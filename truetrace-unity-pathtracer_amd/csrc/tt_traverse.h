@@ -100,17 +100,29 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
+// CPOL: the load's cache-policy bits (gfx950: 2 = nt, non-temporal / streaming). A/B knobs only:
+// TT_TRI_CPOL for the triangle loads (does the 12.6 MB of C2's triangles evict its 2.5 MB node set from
+// each XCD's L2?), TT_NODE_CPOL for the node loads; both 0 (default policy) in the product.
+#ifndef TT_TRI_CPOL
+#define TT_TRI_CPOL 0
+#endif
+#ifndef TT_NODE_CPOL
+#define TT_NODE_CPOL 0
+#endif
+template <int CPOL = 0>
 __device__ __forceinline__ uint4 buffer_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CPOL);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int CPOL = 0>
 __device__ __forceinline__ uint2 buffer_load8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, CPOL);
     return make_uint2(v.x, v.y);
 }
+template <int CPOL = 0>
 __device__ __forceinline__ uint32_t buffer_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CPOL);
 }
 // i * 80 and i * 48 as shift-adds: written plainly, LLVM folds them back into v_mul_lo_u32, a
 // quarter-rate instruction on the traversal's critical path. TT_NODE_STRIDE 128: the kernels read a
@@ -287,12 +299,12 @@ template <bool MATCHECK>
 __device__ __forceinline__ TriData triangle_load(__amdgpu_buffer_rsrc_t tris, int32_t tri_id) {
     const uint32_t to = tri_offset((uint32_t)tri_id);
     TriData d;
-    d.a = buffer_load16(tris, to);
-    d.b = buffer_load16(tris, to + 16u);
+    d.a = buffer_load16<TT_TRI_CPOL>(tris, to);
+    d.b = buffer_load16<TT_TRI_CPOL>(tris, to + 16u);
     if (MATCHECK) {
-        d.c = buffer_load8(tris, to + 32u);
+        d.c = buffer_load8<TT_TRI_CPOL>(tris, to + 32u);
     } else {
-        d.c.x = buffer_load4(tris, to + 32u);
+        d.c.x = buffer_load4<TT_TRI_CPOL>(tris, to + 32u);
         d.c.y = 0u;
     }
     return d;
