@@ -170,7 +170,35 @@ int main(int argc, char** argv) {
            W, H, si.n_tris, si.n_nodes, (unsigned long long)s0.rays, (unsigned long long)s0.hits,
            s0.rays ? (double)s0.node_visits / (double)s0.rays : 0.0, n_next, (unsigned long long)s1.hits);
 
-    int rc = 0;
+    /* the same frame through the multi-GPU group of the ABI (tt_group_*): 2 members sharing device 0 (copy
+     * gather; on a node, devices {0, .., 7} and RCCL), the screen-order primary records into a host array */
+    uint32_t* ghits = (uint32_t*)malloc(sizeof(uint32_t) * 4 * (size_t)W * H);
+    if (!ghits) return 2;
+    tt_group_config gc;
+    memset(&gc, 0, sizeof(gc));
+    gc.width = W;
+    gc.height = H;
+    gc.flags = TT_GROUP_COPY_GATHER;
+    const int32_t gdev[2] = {0, 0};
+    tt_group* grp = NULL;
+    if (tt_group_create(gdev, 2, &gc, &grp) != TT_OK) {
+        fprintf(stderr, "tt_group_create failed\n");
+        return 1;
+    }
+    if (tt_group_scene_upload(grp, nodes, si.n_nodes, tris, si.n_tris, tlas, si.n_tlas_indices, md, si.n_mesh, mats, 1) !=
+            TT_OK ||
+        tt_group_trace_frame(grp, &cam, ghits, 0) != TT_OK) {
+        fprintf(stderr, "group frame failed: %s\n", tt_group_last_error(grp));
+        return 1;
+    }
+    size_t gdiff = 0;
+    for (size_t i = 0; i < (size_t)W * H; i++)
+        gdiff += memcmp(ghits + 4 * i, rays[i].hits, 16) != 0;
+    tt_group_destroy(grp);
+    free(ghits);
+    printf("tt_frame group: 2 members, %zu of %u primary records differ from the single-context frame\n", gdiff, W * H);
+
+    int rc = gdiff ? 4 : 0;
     if (dump) {
         FILE* f = fopen(dump, "wb");
         const uint32_t hdr[10] = {0x54544652u, W, H, si.n_nodes, si.n_tris, si.n_tlas_indices, si.n_mesh, 1u,

@@ -724,9 +724,10 @@ tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_
                                 const tt_material* materials, uint32_t n_mat);
 /* One frame: Generate (cam: width / height must be the group's; TT_TRACE_DEVICE_PTRS implied) on every
  * member for its tiles, the primary trace, the gather to rank 0 and, with TT_GROUP_BOUNCE, bounce 1 on
- * every member. hits_out: on the process holding rank 0, a 16-byte-aligned DEVICE buffer on rank 0's
- * device of width * height uint4 records (screen order); ignored (may be NULL) elsewhere.
- * flags: TT_TRACE_ASYNC (return without waiting). */
+ * every member. hits_out: on the process holding rank 0, a 16-byte-aligned buffer of width * height uint4
+ * records (screen order) -- device memory of rank 0's device, or host memory (then the frame must be
+ * synchronous: the records are staged on rank 0's device and copied back); ignored (may be NULL) elsewhere.
+ * flags: TT_TRACE_ASYNC (return without waiting; device hits_out only). */
 tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t flags);
 /* Waits for every frame issued so far (all members, all slots, the gathers). */
 tt_status tt_group_sync(tt_group* g);

@@ -60,6 +60,7 @@ def test_c_host_frame_matches_oracle(tmp_path):
     r = subprocess.run([BIN, str(W), str(H), dump], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "tt_frame" in r.stdout
+    assert "tt_frame group: 2 members, 0 of" in r.stdout  # the tt_group_* frame of the same camera
     sc, W2, H2, n1, rays, info = load_dump(dump)
     assert (W2, H2) == (W, H)
     assert int((rays["hits"][: W * H, 1] != 0xFFFFFFFF).sum()) > W * H // 2  # the room surrounds the view

@@ -229,9 +229,12 @@ def test_group_refusals(soup):
             g.trace_frame(hits, c2w, ip, NEAR, FAR)
         assert e.value.status == tthip.TT_ERR_NO_SCENE
         g.upload(soup)
-        with pytest.raises(tthip.TTError) as e:  # hits_out in host memory
-            g.trace_frame(np.zeros((64 * 64, 4), np.uint32), c2w, ip, NEAR, FAR)
+        host = np.zeros((64 * 64, 4), np.uint32)
+        with pytest.raises(tthip.TTError) as e:  # a host hits_out needs a synchronous frame
+            g.trace_frame(host, c2w, ip, NEAR, FAR, asynchronous=True)
         assert e.value.status == tthip.TT_ERR_INVALID_ARG
+        g.trace_frame(host, c2w, ip, NEAR, FAR, jitter=1, frames=2)  # staged on device 0, copied back
+        assert np.array_equal(host, oracle_frame(soup, c2w, ip, 64, 64, 2)["hits"][:64 * 64])
         cam = tthip.Camera()
         cam.width, cam.height, cam.far_plane = 32, 64, FAR  # not the group's screen
         assert L.tt_group_trace_frame(g.h, C.byref(cam), hits.data_ptr(), 0) == tthip.TT_ERR_INVALID_ARG

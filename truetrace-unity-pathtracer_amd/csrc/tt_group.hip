@@ -168,6 +168,7 @@ struct tt_group {
     bool root = false;
     Dev<uint4> recv[TT_GROUP_MAX_SLOTS];
     Dev<uint32_t> order;
+    Dev<uint4> stage;  // screen-order records for a host hits_out (copied back by a synchronous frame)
     uint64_t frame = 0;
     std::string err;
 };
@@ -299,6 +300,7 @@ void teardown(tt_group* g) {
     if (!g->m.empty()) (void)hipSetDevice(g->m[0].device);
     for (uint32_t s = 0; s < TT_GROUP_MAX_SLOTS; s++) g->recv[s].release();
     g->order.release();
+    g->stage.release();
     (void)hipGetLastError();
 }
 
@@ -311,13 +313,15 @@ int device_count() {
     return n;
 }
 
-bool on_device(const void* p, int device) {
+// 1: device memory of `device`; 0: host memory (pageable or pinned); -1: device memory of another device
+int where(const void* p, int device) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return 0;
     }
-    return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) && a.device == device;
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return a.device == device ? 1 : -1;
+    return 0;
 }
 
 }  // namespace
@@ -469,11 +473,20 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
     if (cam->width != g->W || cam->height != g->H)
         return gfail(g, TT_ERR_INVALID_ARG, "camera is %ux%u, the group's screen %ux%u", cam->width, cam->height, g->W, g->H);
     if (cam->far_plane != cam->far_plane) return gfail(g, TT_ERR_INVALID_ARG, "far_plane is NaN");
+    bool host_out = false;
     if (g->root) {
         if (!hits_out) return gfail(g, TT_ERR_INVALID_ARG, "rank 0 needs hits_out");
         if (reinterpret_cast<uintptr_t>(hits_out) % 16) return gfail(g, TT_ERR_INVALID_ARG, "hits_out must be 16-byte aligned");
-        if (!on_device(hits_out, g->m[0].device))
-            return gfail(g, TT_ERR_INVALID_ARG, "hits_out is not device memory of rank 0's device %d", g->m[0].device);
+        const int w = where(hits_out, g->m[0].device);
+        if (w < 0) return gfail(g, TT_ERR_INVALID_ARG, "hits_out is device memory of another device than rank 0's (%d)",
+                                g->m[0].device);
+        if (w == 0 && (flags & TT_TRACE_ASYNC))
+            return gfail(g, TT_ERR_INVALID_ARG, "a host hits_out needs a synchronous frame (no TT_TRACE_ASYNC)");
+        host_out = w == 0;
+        if (host_out && !g->stage.p) {
+            G_HIP(g, hipSetDevice(g->m[0].device));
+            G_HIP(g, g->stage.alloc((size_t)g->W * g->H));
+        }
     }
     const uint32_t s = (uint32_t)(g->frame % g->slots);
     const bool async = (flags & TT_TRACE_ASYNC) != 0;
@@ -543,8 +556,11 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         const uint32_t WH = g->W * g->H;
         hipLaunchKernelGGL(tt_group_scatter_kernel, dim3((WH + 255u) / 256u), dim3(256), 0,
                            static_cast<hipStream_t>(r0.comm_stream), g->recv[s].p, g->order.p, WH,
-                           reinterpret_cast<uint4*>(hits_out));
+                           host_out ? g->stage.p : reinterpret_cast<uint4*>(hits_out));
         G_HIP(g, hipGetLastError());
+        if (host_out)
+            G_HIP(g, hipMemcpyAsync(hits_out, g->stage.p, (size_t)WH * 16, hipMemcpyDeviceToHost,
+                                    static_cast<hipStream_t>(r0.comm_stream)));
     }
     // 3. bounce 1 on every member's own device (the gather reads only the send buffers, so it overlaps)
     if (g->bounce) {
