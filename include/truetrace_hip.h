@@ -227,8 +227,13 @@ tt_status tt_stream_create(int32_t device, void** stream);
  * destroyed by the library before the HIP runtime's own teardown (a CU-mask queue alive at that point
  * crashes the exit, SIGSEGV in __cxa_finalize): from the main thread's thread_local destructors (armed by
  * the first launch on such a stream, so they also run ahead of a profiler's per-thread state, e.g. under
- * rocprofv3) and, for launches made only from other threads, from an atexit handler. A host that exits
- * without tt_stream_destroy -- or a Unity domain reload that skips it -- ends cleanly. */
+ * rocprofv3) and, for launches made only from other threads, from an atexit handler (which runs the teardown on a
+ * fresh thread: the exiting thread's per-thread profiler state is gone by then). A host that exits without
+ * tt_stream_destroy -- or a Unity domain reload that skips it -- ends cleanly. A context whose stream the teardown
+ * (or tt_shutdown) destroyed refuses launches with TT_ERR_INVALID_ARG and tt_ctx_destroy skips its stream sync, so
+ * a host's static destructors may still destroy contexts after it. Note the main thread's teardown also runs when
+ * the main thread ends with pthread_exit while other threads go on: their launches on library streams are then
+ * refused -- such hosts destroy their streams themselves or call tt_shutdown. */
 tt_status tt_stream_destroy(void* stream);
 /* Streams made by tt_stream_create and not destroyed yet. */
 uint32_t tt_stream_live_count(void);
