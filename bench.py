@@ -798,76 +798,71 @@ def c5_tiles(torch, dist, tthip, eng, dev, red_dev, args, rank, world):
     return rec
 
 
-def group_tiles(torch, dist, tthip, scene, dev, gpu, args, rank, world, backend, red_dev, c2w, ip, far, W, H,
-                one_gpu_frame):
+def group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H):
     """aux_group_tiles: the LIBRARY's multi-GPU path (tt_group_*, csrc/tt_group.hip) -- what a C# host calls --
-    on this job's ranks: tt_group_unique_id on rank 0 (broadcast), tt_group_create_rank per process, the scene
-    replicated by tt_group_scene_upload, then K frames of tt_group_trace_frame: every rank generates and traces
-    its 64x64 tiles (round-robin) and their bounce-1 rays, and the primary hit records reach rank 0 in one RCCL
+    on this job's ranks: every rank starts tools/group_leg.py as a child process on its GPU; the children form
+    one group (tt_group_unique_id on rank 0, tt_group_create_rank everywhere), replicate the scene
+    (tt_group_scene_upload) and time K frames of tt_group_trace_frame: every rank generates and traces its
+    64x64 tiles (round-robin) and their bounce-1 rays, and the primary hit records reach rank 0 in one RCCL
     gather per frame (inside the library), scattered back to screen order. Frames are asynchronous over
     --group-slots slots. value = all ranks' rays (primary + bounce 1) / the slowest rank's time; strong scaling
-    (one 1080p frame per step whatever N). At N = 1 the group has one member (whole frame, RCCL self-gather)."""
+    (one 1080p frame per frame whatever N). At N = 1 the group has one member (whole frame, RCCL self-gather).
+    The child isolates the leg: its communicator and gathers can never stall the bench's own ranks -- a child
+    that fails or exceeds the time limit is killed and the leg reports the failure."""
+    import subprocess
+    import tempfile
+
     if backend != "nccl":
         return {"skipped": "needs RCCL: one process per GPU"}
-    uid = tthip.group_unique_id() if rank == 0 else None
+    d = tempfile.mkdtemp(prefix="tt_group_leg_") if rank == 0 else None
     if world > 1:
-        box = [uid]
+        box = [d]
         dist.broadcast_object_list(box, src=0)
-        uid = box[0]
+        d = box[0]
     S = max(1, args.group_slots)
-    R = max(1, args.cycle) if world > 1 else S  # samples cycled (each frame its own jitter)
-    g = tthip.Group(W, H, rank=rank, world=world, uid=uid, device=gpu, slots=S, bounce=True)
+    R = max(1, args.cycle) if world > 1 else S
+    cmd = [sys.executable, os.path.join(REPO, "tools", "group_leg.py"), "--rank", str(rank), "--world", str(world),
+           "--device", str(gpu), "--dir", d, "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--slots", str(S), "--cycle", str(R), "--width", str(W), "--height", str(H), "--tris", str(args.tris),
+           "--seed", hex(args.seed)]
+    res, err = None, None
     try:
-        g.upload(scene)
-        outs = [torch.zeros((W * H, 4), dtype=torch.int32, device=dev) for _ in range(S)] if rank == 0 else [None] * S
-        torch.cuda.synchronize(dev)
-        # one synchronous frame per sample: this rank's rays of each (the bounce count is device-resident)
-        mine = []
-        for k in range(R):
-            g.trace_frame(outs[0], c2w, ip, 0.3, far, jitter=1, frames=k, max_bounce=1)
-            n_p, n_b, _ = g.frame_rays(0)
-            mine.append(float(n_p + n_b))
-        per_sample = torch.tensor(mine, dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(per_sample, op=dist.ReduceOp.SUM)
-        per_sample = per_sample.cpu().numpy()
-        for k in range(args.warmup):
-            g.trace_frame(outs[k % S], c2w, ip, 0.3, far, jitter=1, frames=k % R, max_bounce=1, asynchronous=True)
-        g.sync()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            g.trace_frame(outs[k % S], c2w, ip, 0.3, far, jitter=1, frames=k % R, max_bounce=1, asynchronous=True)
-        g.sync()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        el = float(el.item())
-        rays = float(sum(per_sample[k % R] for k in range(args.steps)))
-        par = None
-        if rank == 0:  # the last frame's gathered records against one GPU tracing the whole frame
-            k = args.steps - 1
-            got = outs[k % S].cpu().numpy().view(np.uint32)
-            par = bool(np.array_equal(got, one_gpu_frame(k % R)))
-        out = {"value": round(rays / el / 1e6, 2), "unit": "Mrays/s", "scaling": "strong", "ranks": world,
-               "ms_per_frame": round(el * 1e3 / args.steps, 4), "frame_slots": S, "samples_cycled": R,
-               "rays_per_frame_all_ranks": int(round(rays / args.steps)),
-               "gather_identical_to_1gpu": par,
-               "api": "tt_group_unique_id + tt_group_create_rank + tt_group_scene_upload + tt_group_trace_frame "
-                      "(TT_TRACE_ASYNC) + tt_group_sync",
-               "layout": "one 1080p frame per step: 64x64 tiles round-robin over the ranks (world 1: the whole frame), "
-                         "each rank's Generate + primary trace + bounce-1 enqueue/trace on its own device, one RCCL "
-                         "gather of the primary hit records to rank 0 per frame inside the library"}
-        if world > 1 and getattr(args, "_solo_ms", None):
-            out["efficiency_vs_n1_frame"] = round(args._solo_ms / (world * el * 1e3 / args.steps), 4)
-        return out
-    finally:
-        g.close()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.group_timeout)
+        if r.returncode == 0 and r.stdout.strip():
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+        else:
+            err = f"rank {rank}: exit {r.returncode}: {r.stderr[-300:]}"
+    except subprocess.TimeoutExpired:
+        err = f"rank {rank}: the group leg exceeded {args.group_timeout} s (killed)"
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {type(e).__name__}: {e}"
+    ok = torch.tensor([0.0 if res is None else 1.0], dtype=torch.float64, device=red_dev)
+    el = torch.tensor([0.0 if res is None else res["elapsed_s"]], dtype=torch.float64, device=red_dev)
+    per = torch.tensor([0.0] * R if res is None else [float(x) for x in res["rays_per_sample"]], dtype=torch.float64,
+                       device=red_dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(per, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        shutil.rmtree(d, ignore_errors=True)
+    if float(ok.item()) < 1.0:
+        return {"error": err or "another rank's group leg failed"}
+    el = float(el.item())
+    per = per.cpu().numpy()
+    rays = float(sum(per[k % R] for k in range(args.steps)))
+    out = {"value": round(rays / el / 1e6, 2), "unit": "Mrays/s", "scaling": "strong", "ranks": world,
+           "ms_per_frame": round(el * 1e3 / args.steps, 4), "frame_slots": S, "samples_cycled": R,
+           "rays_per_frame_all_ranks": int(round(rays / args.steps)),
+           "gather_identical_to_1gpu": None if res is None else res.get("parity"),
+           "api": "tt_group_unique_id + tt_group_create_rank + tt_group_scene_upload + tt_group_trace_frame "
+                  "(TT_TRACE_ASYNC) + tt_group_sync, one child process per rank (tools/group_leg.py)",
+           "layout": "one 1080p frame per step: 64x64 tiles round-robin over the ranks (world 1: the whole frame), "
+                     "each rank's Generate + primary trace + bounce-1 enqueue/trace on its own device, one RCCL "
+                     "gather of the primary hit records to rank 0 per frame inside the library"}
+    if world > 1 and getattr(args, "_solo_ms", None):
+        out["efficiency_vs_n1_frame"] = round(args._solo_ms / (world * el * 1e3 / args.steps), 4)
+    return out
 
 
 def oracle_records_check(scene, layout, pre, post, colors, far, W, H):
@@ -1133,6 +1128,8 @@ def main():
     ap.add_argument("--group-slots", type=int, default=4,
                     help="frames in flight of the library's multi-GPU group leg (aux_group_tiles)")
     ap.add_argument("--no-group", action="store_true", help="skip aux_group_tiles (the tt_group_* library path)")
+    ap.add_argument("--group-timeout", type=float, default=240.0,
+                    help="seconds each rank's group-leg child may take before it is killed (aux_group_tiles)")
     ap.add_argument("--aux", default="c3,c4,dyn,refit,c5",
                     help="other BASELINE configs to measure after the metric at N=1 (comma list of c3,c4,dyn,refit,c5;"
                          " '' = none)")
@@ -1683,8 +1680,7 @@ def main():
         # every rank takes part (RCCL's init is collective); a failure is reported, never the metric lost
         args._solo_ms = solo_ms
         try:
-            group = group_tiles(torch, dist, tthip, scene, dev, gpu, args, rank, world, backend, red_dev, c2w, ip,
-                                far, W, H, one_gpu_frame)
+            group = group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H)
         except Exception as e:  # noqa: BLE001 — auxiliary
             group = {"error": f"{type(e).__name__}: {e}"}
         log(f"library group path (tt_group_*): {group}")
