@@ -1324,7 +1324,7 @@ def main():
     # times rocprofv3 reports for this command's trace kernels
     single = None
     frame_rays, frame_nb = (parts[0].rays, nb) if (P == 1 and world == 1 and layout.B == 1) else (None, None)
-    if world == 1 and (P > 1 or F > 1):
+    if world == 1 and (P > 1 or F > 1 or frame_rays is None):
         one = torch.zeros(2 * WH * 48, dtype=torch.uint8, device=dev)
         eng.generate(one, c2w, ip, W, H, 0.3, far, jitter=jitter, frames=frames, max_bounce=1, device=True)
         o_prim = eng.trace(one, WH, 0, far, W, H, info=info, device=True, stats=True)

@@ -32,6 +32,7 @@
 #   order      tools/exp_order.py per TT_ORDER_HOT threshold (ORDER_HOT, ORDER_CFGS, ORDER_ARGS)
 #   sweep      randomized parity sweep (tools/parity_sweep.py): SWEEP_N plain + SWEEP_N variants/adaptive + SWEEP_N
 #              degenerate-direction cases + SWEEP_N frame-slot cases from seed SWEEP_SEED
+#   sweepgroup the multi-GPU group sweep (random members / tiles / slots, copy gather on one GPU): SWEEP_N, SWEEP_SEED
 #   sweepslots the frame-slot sweep alone (SWEEP_MODES, default "slots": instanced cases also traced by a moved slot)
 #   ordercheck the shared-scene ordering tests on the no-ordering variant (expected to fail)
 #   variants   A/B of the library variants in lib/variants (tools/run_variants.py)
@@ -136,6 +137,8 @@ for stage in "$@"; do
            run sweep_var 900 python -u tools/parity_sweep.py $n $((s0 + 1000)) variants,adaptive || exit $?
            run sweep_axis 900 python -u tools/parity_sweep.py $n $((s0 + 2000)) axis,variants,adaptive || exit $?
            run sweep_slots 900 python -u tools/parity_sweep.py $n $((s0 + 3000)) slots,adaptive || exit $? ;;
+    sweepgroup) run sweep_group 900 python -u tools/parity_sweep.py ${SWEEP_N:-200} ${SWEEP_SEED:-60000} \
+                    ${SWEEP_MODES:-group,variants} || exit $? ;;
     sweepslots) run sweep_slots 900 python -u tools/parity_sweep.py ${SWEEP_N:-300} ${SWEEP_SEED:-43000} \
                ${SWEEP_MODES:-slots} || exit $? ;;
     ordercheck) # the shared-scene ordering tests against the variant whose sections order nothing (make variant

@@ -38,10 +38,26 @@ AXIS = "axis" in MODES
 # moved (its own _MeshData rewrite + TLAS refit): primary + info, bounce 1 and NEE rays against the oracle on
 # the scene as the slot holds it (its TLAS nodes read back, its _MeshData)
 SLOTS = "slots" in MODES
+# "group": every case is also traced through a multi-GPU group of the C ABI (tt_group_*): 1-5 members sharing
+# device 0 (copy gather), a random tile edge and slot count, bounce 1 on; the gathered screen-order records
+# against the oracle's jittered frame, and every member's bounce-1 rays and records against the oracle's
+# enqueue + trace over that member's own rays (tt_group_tile_pixels order)
+GROUP = "group" in MODES
 FLAG_SETS = (0, tthip.TT_TRACE_IGNORE_GLASS, tthip.TT_TRACE_IGNORE_BACKFACING,
              tthip.TT_TRACE_IGNORE_GLASS | tthip.TT_TRACE_IGNORE_BACKFACING)
 eng = tthip.Engine(0)
 bad_total, rays_total = 0, 0
+
+
+def device_rays(ptr, n):
+    """n RayData records copied back from a device pointer the group hands out (torch's HIP runtime)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.zeros(n, tthip.RAY_DTYPE)
+    assert hip.hipMemcpy(out.ctypes.data, ptr, 48 * n, 2) == 0  # hipMemcpyDeviceToHost
+    return out
 
 
 def compare(sc, rays, n, bounce, W, H, info=True, flags=0, e=None):
@@ -158,11 +174,43 @@ for k in range(N):
             n_rays += W * H + snb + len(ssr)
         finally:
             slot.close()
+    bgr = 0
+    if GROUP:
+        members = int(rng.integers(1, 6))
+        tile = int(rng.choice([8, 16, 32, 64]))
+        g = tthip.Group(W, H, devices=[0] * members, tile=tile, slots=int(rng.integers(1, 4)), bounce=True, copy=True)
+        try:
+            g.upload(sc)
+            hits = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+            g.trace_frame(hits, c2w, ip, 0.05, FAR, jitter=1, frames=k, max_bounce=2)
+            full = O.generate(c2w, ip, W, H, 0.05, FAR, jitter=1, frames=k, max_bounce=2)
+            assert O.trace(sc, full, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+            bgr += int((hits.cpu().numpy().view(np.uint32) != full["hits"][:W * H]).any(1).sum())
+            n_rays += W * H
+            for m in range(members):
+                n, nbm, ptr = g.frame_rays(m)
+                pix = tthip.group_tile_pixels(W, H, members, m, tile).astype(np.int64)
+                mr = np.zeros(W * H + n, tthip.RAY_DTYPE)
+                mr[:n] = full[pix]
+                nb_ref = O.enqueue_bounce(sc, mr, n, 0, FAR, W, H, frames=k, max_bounce=2)
+                if nb_ref:
+                    assert O.trace(sc, mr, nb_ref, 1, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+                got = device_rays(ptr, W * H + n)
+                if nbm != nb_ref:
+                    bgr += max(nbm, nb_ref)
+                else:
+                    same = (np.ascontiguousarray(got[W * H:W * H + nbm]).view(np.uint8).reshape(nbm, 48) ==
+                            np.ascontiguousarray(mr[W * H:W * H + nbm]).view(np.uint8).reshape(nbm, 48)).all(1)
+                    bgr += int((~same).sum())
+                n_rays += nbm
+        finally:
+            g.close()
     rays_total += n_rays
-    bad_total += b0 + b1 + bs + bsl
+    bad_total += b0 + b1 + bs + bsl + bgr
     print(f"case {k:3d} {kind:9s} seed {seed} flags {flags:#04x} tris {len(sc.tris):6d} {W}x{H}: primary+info mismatches {b0}, "
           f"bounce-1 ({nb} rays) {b1}, shadow ({len(sr)} rays) {bs}" + (f", frame slot {bsl}" if SLOTS and kind == "instanced"
-                                                                          else ""), flush=True)
+                                                                          else "")
+          + (f", group {bgr}" if GROUP else ""), flush=True)
 print(f"SUMMARY: {N} cases, {rays_total} rays traced on the GPU and the oracle, {bad_total} mismatching records, "
       f"{time.time() - t0:.0f} s", flush=True)
 sys.exit(1 if bad_total else 0)
