@@ -92,7 +92,7 @@ namespace TrueTrace.Hip
     }
 
     [Flags]
-    public enum TTGroupFlags : uint { None = 0, CopyGather = 1u << 0, Bounce = 1u << 1 }
+    public enum TTGroupFlags : uint { None = 0, CopyGather = 1u << 0, Bounce = 1u << 1, Info = 1u << 2 }
 
     /// tt_group_config: the screen a multi-GPU group traces, its tile edge, frames in flight and flags.
     [StructLayout(LayoutKind.Sequential)]
@@ -212,7 +212,7 @@ namespace TrueTrace.Hip
             void* nodes, uint nNodes, void* tris, uint nTris, int* tlasIndices, uint nTlas,
             void* meshData, uint nMesh, void* materials, uint nMat);
         [DllImport(Lib)] public static extern TTStatus tt_group_trace_frame(IntPtr group, ref TTCamera cam, IntPtr hitsOut,
-            uint flags);
+            IntPtr infoOut, uint flags);
         [DllImport(Lib)] public static extern TTStatus tt_group_sync(IntPtr group);
         [DllImport(Lib)] public static extern TTStatus tt_group_frame_rays(IntPtr group, uint member, out uint nPrimary,
             out uint nBounce, out IntPtr raysDev);
@@ -624,10 +624,11 @@ namespace TrueTrace.Hip
         }
 
         /// One frame: Generate + primary trace per device for its tiles, the gather of the primary hit records to
-        /// `hitsOut` (device 0, width*height uint4 in screen order), bounce 1 per device with TTGroupFlags.Bounce.
-        public void TraceFrame(ref TTCamera cam, IntPtr hitsOut, bool async = false)
+        /// `hitsOut` (device 0, width*height uint4 in screen order), bounce 1 per device with TTGroupFlags.Bounce;
+        /// with TTGroupFlags.Info the bounce-0 _PrimaryTriangleInfo texels go to `infoOut` the same way.
+        public void TraceFrame(ref TTCamera cam, IntPtr hitsOut, IntPtr infoOut = default, bool async = false)
         {
-            Check(Native.tt_group_trace_frame(m_g, ref cam, hitsOut, async ? (uint)TTTraceFlags.Async : 0u));
+            Check(Native.tt_group_trace_frame(m_g, ref cam, hitsOut, infoOut, async ? (uint)TTTraceFlags.Async : 0u));
         }
 
         public void Sync() { Check(Native.tt_group_sync(m_g)); }

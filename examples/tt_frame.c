@@ -187,7 +187,7 @@ int main(int argc, char** argv) {
     }
     if (tt_group_scene_upload(grp, nodes, si.n_nodes, tris, si.n_tris, tlas, si.n_tlas_indices, md, si.n_mesh, mats, 1) !=
             TT_OK ||
-        tt_group_trace_frame(grp, &cam, ghits, 0) != TT_OK) {
+        tt_group_trace_frame(grp, &cam, ghits, NULL, 0) != TT_OK) {
         fprintf(stderr, "group frame failed: %s\n", tt_group_last_error(grp));
         return 1;
     }

@@ -692,7 +692,8 @@ typedef struct tt_group tt_group;
 
 enum {
     TT_GROUP_COPY_GATHER = 1u << 0, /* gather with hipMemcpyAsync instead of RCCL (tt_group_create only)   */
-    TT_GROUP_BOUNCE = 1u << 1       /* each member traces bounce 1 of its primary hits (diffuse enqueue)  */
+    TT_GROUP_BOUNCE = 1u << 1,      /* each member traces bounce 1 of its primary hits (diffuse enqueue)  */
+    TT_GROUP_INFO = 1u << 2         /* gather the bounce-0 _PrimaryTriangleInfo texels too (info_out)      */
 };
 
 typedef struct tt_group_config {
@@ -732,8 +733,12 @@ tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_
  * every member. hits_out: on the process holding rank 0, a 16-byte-aligned buffer of width * height uint4
  * records (screen order) -- device memory of rank 0's device, or host memory (then the frame must be
  * synchronous: the records are staged on rank 0's device and copied back); ignored (may be NULL) elsewhere.
+ * info_out (TT_GROUP_INFO; else ignored): width * height uint4 _PrimaryTriangleInfo texels in screen order, the
+ * bounce-0 form tt_trace_closest writes (IntersectionKernels.compute:229-238), same kind of memory as hits_out;
+ * each member packs its texels behind its hit records, so they travel in the same RCCL group.
  * flags: TT_TRACE_ASYNC (return without waiting; device hits_out only). */
-tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t flags);
+tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t* info_out,
+                               uint32_t flags);
 /* Waits for every frame issued so far (all members, all slots, the gathers). */
 tt_status tt_group_sync(tt_group* g);
 /* Of the latest frame, member m: its primary ray count, its bounce-1 ray count (0 without

@@ -47,9 +47,10 @@ def test_every_header_function_is_bound_or_listed_host_only():
 
 
 def test_group_flags_match_header():
-    cs = dict(re.findall(r"(CopyGather|Bounce)\s*=\s*1u\s*<<\s*(\d+)", CS))
+    cs = dict(re.findall(r"(CopyGather|Bounce|Info)\s*=\s*1u\s*<<\s*(\d+)", CS))
     hdr = dict(re.findall(r"(TT_GROUP_\w+)\s*=\s*1u\s*<<\s*(\d+)", HDR))
     assert cs["CopyGather"] == hdr["TT_GROUP_COPY_GATHER"] and cs["Bounce"] == hdr["TT_GROUP_BOUNCE"]
+    assert cs["Info"] == hdr["TT_GROUP_INFO"]
 
 
 def test_flag_values_match_header():

@@ -57,10 +57,11 @@ def soup_camera(W, H):
     return tthip.unity_camera((0.3, 0.2, 2.6), (-0.1, -0.05, -1.0), (0, 1, 0), 60.0, W, H, NEAR, FAR)
 
 
-def oracle_frame(sc, c2w, ip, W, H, frames, max_bounce=1):
-    """The oracle's whole frame: Generate (jittered at `frames`) and the primary trace; returns the rays."""
+def oracle_frame(sc, c2w, ip, W, H, frames, max_bounce=1, info=None):
+    """The oracle's whole frame: Generate (jittered at `frames`) and the primary trace (with _PrimaryTriangleInfo
+    into `info` when given); returns the rays."""
     rays = O.generate(c2w, ip, W, H, NEAR, FAR, jitter=1, frames=frames, max_bounce=max_bounce)
-    assert O.trace(sc, rays, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+    assert O.trace(sc, rays, W * H, 0, FAR, W, H, info=info, nthreads=CPU_THREADS)[0] == 0
     return rays
 
 
@@ -89,20 +90,23 @@ def check_members(g, sc, full, W, H, frames, world):
 
 
 def test_copy_gather_three_members_equal_the_oracle_frame(soup):
-    """3 members on device 0 (copy gather), a screen that is no multiple of the tile: the gathered frame and
-    every member's bounce chain against the oracle."""
+    """3 members on device 0 (copy gather), a screen that is no multiple of the tile: the gathered frame (hit
+    records and _PrimaryTriangleInfo, TT_GROUP_INFO) and every member's bounce chain against the oracle."""
     torch = _torch()
     W, H, frames = 328, 200, 5
     c2w, ip = soup_camera(W, H)
-    g = tthip.Group(W, H, devices=[0, 0, 0], bounce=True, copy=True)
+    g = tthip.Group(W, H, devices=[0, 0, 0], bounce=True, copy=True, info=True)
     try:
         g.upload(soup)
         hits = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
-        g.trace_frame(hits, c2w, ip, NEAR, FAR, jitter=1, frames=frames, max_bounce=1)
-        full = oracle_frame(soup, c2w, ip, W, H, frames)
+        info = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+        g.trace_frame(hits, c2w, ip, NEAR, FAR, jitter=1, frames=frames, max_bounce=1, info_out=info)
+        info_ref = np.full((W * H, 4), 0xA5A5A5A5, np.uint32)
+        full = oracle_frame(soup, c2w, ip, W, H, frames, info=info_ref)
         got = hits.cpu().numpy().view(np.uint32)
         assert int((full["hits"][:W * H, 1] != 0xFFFFFFFF).sum()) > W * H // 4
         assert np.array_equal(got, full["hits"][:W * H]), "gathered screen-order records"
+        assert np.array_equal(info.cpu().numpy().view(np.uint32), info_ref), "gathered _PrimaryTriangleInfo"
         check_members(g, soup, full, W, H, frames, 3)
     finally:
         g.close()
@@ -180,15 +184,18 @@ def test_sponza_1080p_eight_members_copy_gather(sponza_scene):
     torch = _torch()
     W, H, frames = 1920, 1080, 1
     c2w, ip = tthip.unity_camera((-10, 2, 0), (1, 0, 0), (0, 1, 0), 60, W, H, 0.3, FAR)
-    g = tthip.Group(W, H, devices=[0] * 8, bounce=True, copy=True)
+    g = tthip.Group(W, H, devices=[0] * 8, bounce=True, copy=True, info=True)
     try:
         g.upload(sponza_scene)
         hits = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+        info = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
         cam = dict(jitter=1, frames=frames, max_bounce=1)
-        g.trace_frame(hits, c2w, ip, 0.3, FAR, **cam)
+        g.trace_frame(hits, c2w, ip, 0.3, FAR, info_out=info, **cam)
         full = O.generate(c2w, ip, W, H, 0.3, FAR, **cam)
-        assert O.trace(sponza_scene, full, W * H, 0, FAR, W, H, nthreads=CPU_THREADS)[0] == 0
+        info_ref = np.zeros((W * H, 4), np.uint32)
+        assert O.trace(sponza_scene, full, W * H, 0, FAR, W, H, info=info_ref, nthreads=CPU_THREADS)[0] == 0
         assert np.array_equal(hits.cpu().numpy().view(np.uint32), full["hits"][:W * H])
+        assert np.array_equal(info.cpu().numpy().view(np.uint32), info_ref)
         for m in (0, 7):
             n, nb, ptr = g.frame_rays(m)
             pix = tthip.group_tile_pixels(W, H, 8, m)
@@ -235,9 +242,25 @@ def test_group_refusals(soup):
         assert e.value.status == tthip.TT_ERR_INVALID_ARG
         g.trace_frame(host, c2w, ip, NEAR, FAR, jitter=1, frames=2)  # staged on device 0, copied back
         assert np.array_equal(host, oracle_frame(soup, c2w, ip, 64, 64, 2)["hits"][:64 * 64])
+    finally:
+        g.close()
+    # TT_GROUP_INFO into host arrays (staged) and its refusals: info_out missing, or not hits_out's kind of memory
+    g = tthip.Group(64, 64, devices=[0, 0], copy=True, info=True)
+    try:
+        g.upload(soup)
+        host, hinfo = np.zeros((64 * 64, 4), np.uint32), np.zeros((64 * 64, 4), np.uint32)
+        with pytest.raises(tthip.TTError):
+            g.trace_frame(host, c2w, ip, NEAR, FAR)
+        with pytest.raises(tthip.TTError):
+            g.trace_frame(host, c2w, ip, NEAR, FAR, info_out=torch.zeros((64 * 64, 4), dtype=torch.int32, device="cuda:0"))
+        g.trace_frame(host, c2w, ip, NEAR, FAR, jitter=1, frames=3, info_out=hinfo)
+        iref = np.zeros((64 * 64, 4), np.uint32)
+        assert np.array_equal(host, oracle_frame(soup, c2w, ip, 64, 64, 3, info=iref)["hits"][:64 * 64])
+        assert np.array_equal(hinfo, iref)
         cam = tthip.Camera()
         cam.width, cam.height, cam.far_plane = 32, 64, FAR  # not the group's screen
-        assert L.tt_group_trace_frame(g.h, C.byref(cam), hits.data_ptr(), 0) == tthip.TT_ERR_INVALID_ARG
-        g.trace_frame(hits, c2w, ip, NEAR, FAR)  # still usable after refusals
+        assert L.tt_group_trace_frame(g.h, C.byref(cam), hits.data_ptr(), None, 0) == tthip.TT_ERR_INVALID_ARG
+        dinfo = torch.zeros((64 * 64, 4), dtype=torch.int32, device="cuda:0")
+        g.trace_frame(hits, c2w, ip, NEAR, FAR, info_out=dinfo)  # still usable after refusals
     finally:
         g.close()

@@ -91,11 +91,23 @@ const Rccl& rccl() {
 // ------------------------------------------------------------------ kernels
 // hits_out[order[j]] = recv[j] for the j-th gathered record (rank-major blocks, each in its member's
 // trace order): the screen-order record array on rank 0.
+// With _PrimaryTriangleInfo gathered too (TT_GROUP_INFO), recv[n + j] is record j's info texel.
 __global__ __launch_bounds__(256) void tt_group_scatter_kernel(const uint4* __restrict__ recv,
                                                                const uint32_t* __restrict__ order, uint32_t n,
-                                                               uint4* __restrict__ out) {
+                                                               uint4* __restrict__ out, uint4* __restrict__ info_out) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) out[order[j]] = recv[j];
+    if (j >= n) return;
+    const uint32_t p = order[j];
+    out[p] = recv[j];
+    if (info_out) info_out[p] = recv[n + j];
+}
+// A member's _PrimaryTriangleInfo texels (written at their pixels by the primary trace) packed in its ray
+// order behind its hit records, so one message per rank carries both.
+__global__ __launch_bounds__(256) void tt_group_pack_info_kernel(const uint4* __restrict__ info_full,
+                                                                 const uint32_t* __restrict__ pixels, uint32_t n,
+                                                                 uint4* __restrict__ dst) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = info_full[pixels[i]];
 }
 
 // ------------------------------------------------------------------ shard arithmetic
@@ -149,7 +161,8 @@ struct Member {
     void* comm_stream = nullptr;
     ncclComm_t comm = nullptr;
     Dev<tt_ray_data> rays[TT_GROUP_MAX_SLOTS];
-    Dev<uint4> send[TT_GROUP_MAX_SLOTS];
+    Dev<uint4> send[TT_GROUP_MAX_SLOTS];       // hit records [0, n) (+ info texels [n, 2n) with TT_GROUP_INFO)
+    Dev<uint4> info_full[TT_GROUP_MAX_SLOTS];  // TT_GROUP_INFO: the primary trace's _PrimaryTriangleInfo, W*H
     Dev<uint32_t> count[TT_GROUP_MAX_SLOTS];  // bounce-1 survivors of the slot's last frame
     Dev<uint32_t> pixels;
     hipEvent_t ev_prim[TT_GROUP_MAX_SLOTS] = {};  // the slot's primary records are final
@@ -161,12 +174,12 @@ struct Member {
 
 struct tt_group {
     uint32_t W = 0, H = 0, tile = 64, slots = 2, flags = 0, world = 0;
-    bool bounce = false, copy = false;
+    bool bounce = false, copy = false, info = false;
     std::vector<Member> m;
     std::vector<uint64_t> shard_n, shard_off;  // per rank
     // rank 0's side (when this process holds it: member 0)
     bool root = false;
-    Dev<uint4> recv[TT_GROUP_MAX_SLOTS];
+    Dev<uint4> recv[TT_GROUP_MAX_SLOTS];  // W*H hit records in rank order (+ W*H info texels with TT_GROUP_INFO)
     Dev<uint32_t> order;
     Dev<uint4> stage;  // screen-order records for a host hits_out (copied back by a synchronous frame)
     uint64_t frame = 0;
@@ -211,7 +224,7 @@ bool check_config(const tt_group_config* cfg, std::string& why) {
     const uint32_t tile = cfg->tile ? cfg->tile : 64;
     if (tile % 8) return why = "tile must be a multiple of 8", false;
     if (cfg->slots > TT_GROUP_MAX_SLOTS) return why = "at most 8 slots", false;
-    if (cfg->flags & ~(uint32_t)(TT_GROUP_COPY_GATHER | TT_GROUP_BOUNCE)) return why = "unknown flags", false;
+    if (cfg->flags & ~(uint32_t)(TT_GROUP_COPY_GATHER | TT_GROUP_BOUNCE | TT_GROUP_INFO)) return why = "unknown flags", false;
     return true;
 }
 
@@ -224,6 +237,8 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
     g->flags = cfg->flags;
     g->bounce = (cfg->flags & TT_GROUP_BOUNCE) != 0;
     g->copy = (cfg->flags & TT_GROUP_COPY_GATHER) != 0;
+    g->info = (cfg->flags & TT_GROUP_INFO) != 0;
+    const size_t K = g->info ? 2 : 1;  // records per ray in the gather
     const uint64_t WH = (uint64_t)g->W * g->H;
     g->shard_n.resize(g->world);
     g->shard_off.resize(g->world);
@@ -250,7 +265,8 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
             (void)tt_ctx_set_timing(mb.ctx[s], 0);  // no per-launch event pair (a host turns it on per context)
             G_HIP(g, hipSetDevice(mb.device));
             G_HIP(g, mb.rays[s].alloc(WH + mb.n));
-            G_HIP(g, mb.send[s].alloc(mb.n));
+            G_HIP(g, mb.send[s].alloc(K * mb.n));
+            if (g->info) G_HIP(g, mb.info_full[s].alloc(WH));
             G_HIP(g, mb.count[s].alloc(1));
             G_HIP(g, hipMemset(mb.count[s].p, 0, 4));
             G_HIP(g, hipEventCreateWithFlags(&mb.ev_prim[s], hipEventDisableTiming));
@@ -268,7 +284,7 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
         }
         G_HIP(g, g->order.alloc(order.size()));
         G_HIP(g, hipMemcpy(g->order.p, order.data(), 4 * order.size(), hipMemcpyHostToDevice));
-        for (uint32_t s = 0; s < g->slots; s++) G_HIP(g, g->recv[s].alloc(WH));
+        for (uint32_t s = 0; s < g->slots; s++) G_HIP(g, g->recv[s].alloc(K * WH));
     }
     return TT_OK;
 }
@@ -289,6 +305,7 @@ void teardown(tt_group* g) {
         for (uint32_t s = 0; s < TT_GROUP_MAX_SLOTS; s++) {
             mb.rays[s].release();
             mb.send[s].release();
+            mb.info_full[s].release();
             mb.count[s].release();
             if (mb.ev_prim[s]) (void)hipEventDestroy(mb.ev_prim[s]);
             if (mb.ev_sent[s]) (void)hipEventDestroy(mb.ev_sent[s]);
@@ -467,7 +484,8 @@ tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_
     return TT_OK;
 }
 
-tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t flags) {
+tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t* info_out,
+                               uint32_t flags) {
     if (!g) return TT_ERR_INVALID_ARG;
     if (!cam) return gfail(g, TT_ERR_INVALID_ARG, "null camera");
     if (cam->width != g->W || cam->height != g->H)
@@ -483,9 +501,15 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         if (w == 0 && (flags & TT_TRACE_ASYNC))
             return gfail(g, TT_ERR_INVALID_ARG, "a host hits_out needs a synchronous frame (no TT_TRACE_ASYNC)");
         host_out = w == 0;
+        if (g->info) {  // the info texels' buffer: the same kind of memory as hits_out
+            if (!info_out) return gfail(g, TT_ERR_INVALID_ARG, "TT_GROUP_INFO: rank 0 needs info_out");
+            if (reinterpret_cast<uintptr_t>(info_out) % 16) return gfail(g, TT_ERR_INVALID_ARG, "info_out must be 16-byte aligned");
+            if (where(info_out, g->m[0].device) != w)
+                return gfail(g, TT_ERR_INVALID_ARG, "info_out must be the same kind of memory as hits_out");
+        }
         if (host_out && !g->stage.p) {
             G_HIP(g, hipSetDevice(g->m[0].device));
-            G_HIP(g, g->stage.alloc((size_t)g->W * g->H));
+            G_HIP(g, g->stage.alloc((g->info ? 2 : 1) * (size_t)g->W * g->H));
         }
     }
     const uint32_t s = (uint32_t)(g->frame % g->slots);
@@ -507,8 +531,14 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         p.screen_width = g->W;
         p.screen_height = g->H;
         p.flags = tflags;
-        if (mb.n) G_TT(g, mb.ctx[s], tt_trace_closest_hits(mb.ctx[s], &p, mb.rays[s].p, nullptr, nullptr,
-                                                           reinterpret_cast<uint32_t*>(mb.send[s].p)));
+        if (mb.n) G_TT(g, mb.ctx[s], tt_trace_closest_hits(mb.ctx[s], &p, mb.rays[s].p,
+                                                           g->info ? reinterpret_cast<uint32_t*>(mb.info_full[s].p) : nullptr,
+                                                           nullptr, reinterpret_cast<uint32_t*>(mb.send[s].p)));
+        if (g->info && mb.n) {
+            hipLaunchKernelGGL(tt_group_pack_info_kernel, dim3((mb.n + 255u) / 256u), dim3(256), 0, st, mb.info_full[s].p,
+                               mb.pixels.p, mb.n, mb.send[s].p + mb.n);
+            G_HIP(g, hipGetLastError());
+        }
         G_HIP(g, hipEventRecord(mb.ev_prim[s], st));
     }
     // 2. the gather: one fused RCCL group (or device copies) on the communication streams
@@ -522,11 +552,17 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         for (Member& mb : g->m) {
             hipStream_t cs = static_cast<hipStream_t>(mb.comm_stream);
             if (r == ncclSuccess && mb.n) r = rccl().Send(mb.send[s].p, (size_t)mb.n * 4, ncclUint32, 0, mb.comm, cs);
+            if (r == ncclSuccess && mb.n && g->info)
+                r = rccl().Send(mb.send[s].p + mb.n, (size_t)mb.n * 4, ncclUint32, 0, mb.comm, cs);
             if (mb.rank == 0)
                 for (uint32_t q = 0; q < g->world && r == ncclSuccess; q++)
-                    if (g->shard_n[q])
+                    if (g->shard_n[q]) {
                         r = rccl().Recv(g->recv[s].p + g->shard_off[q], (size_t)g->shard_n[q] * 4, ncclUint32, (int)q,
                                         mb.comm, cs);
+                        if (r == ncclSuccess && g->info)  // (messages between one pair match in call order)
+                            r = rccl().Recv(g->recv[s].p + (size_t)g->W * g->H + g->shard_off[q],
+                                            (size_t)g->shard_n[q] * 4, ncclUint32, (int)q, mb.comm, cs);
+                    }
         }
         const ncclResult_t re = rccl().GroupEnd();
         if (r != ncclSuccess || re != ncclSuccess)
@@ -545,6 +581,9 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
             if (mb.n)
                 G_HIP(g, hipMemcpyAsync(g->recv[s].p + g->shard_off[mb.rank], mb.send[s].p, (size_t)mb.n * 16,
                                         hipMemcpyDeviceToDevice, cs));
+            if (mb.n && g->info)
+                G_HIP(g, hipMemcpyAsync(g->recv[s].p + (size_t)g->W * g->H + g->shard_off[mb.rank], mb.send[s].p + mb.n,
+                                        (size_t)mb.n * 16, hipMemcpyDeviceToDevice, cs));
         }
         G_HIP(g, hipEventRecord(r0.ev_sent[s], cs));
         for (Member& mb : g->m) mb.sent_used[s] = true;
@@ -554,13 +593,18 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         Member& r0 = g->m[0];
         G_HIP(g, hipSetDevice(r0.device));
         const uint32_t WH = g->W * g->H;
+        uint4* oh = host_out ? g->stage.p : reinterpret_cast<uint4*>(hits_out);
+        uint4* oi = !g->info ? nullptr : host_out ? g->stage.p + WH : reinterpret_cast<uint4*>(info_out);
         hipLaunchKernelGGL(tt_group_scatter_kernel, dim3((WH + 255u) / 256u), dim3(256), 0,
-                           static_cast<hipStream_t>(r0.comm_stream), g->recv[s].p, g->order.p, WH,
-                           host_out ? g->stage.p : reinterpret_cast<uint4*>(hits_out));
+                           static_cast<hipStream_t>(r0.comm_stream), g->recv[s].p, g->order.p, WH, oh, oi);
         G_HIP(g, hipGetLastError());
-        if (host_out)
+        if (host_out) {
             G_HIP(g, hipMemcpyAsync(hits_out, g->stage.p, (size_t)WH * 16, hipMemcpyDeviceToHost,
                                     static_cast<hipStream_t>(r0.comm_stream)));
+            if (g->info)
+                G_HIP(g, hipMemcpyAsync(info_out, g->stage.p + WH, (size_t)WH * 16, hipMemcpyDeviceToHost,
+                                        static_cast<hipStream_t>(r0.comm_stream)));
+        }
     }
     // 3. bounce 1 on every member's own device (the gather reads only the send buffers, so it overlaps)
     if (g->bounce) {

@@ -1068,6 +1068,7 @@ def device_count() -> int:
 # ---------------------------------------------------------------- multi-GPU group (tt_group_*)
 TT_GROUP_COPY_GATHER = 1 << 0
 TT_GROUP_BOUNCE = 1 << 1
+TT_GROUP_INFO = 1 << 2
 GROUP_SYMBOLS = ["tt_group_create", "tt_group_unique_id", "tt_group_create_rank", "tt_group_destroy",
                  "tt_group_last_error", "tt_group_local_members", "tt_group_member_ctx", "tt_group_scene_upload",
                  "tt_group_trace_frame", "tt_group_sync", "tt_group_frame_rays", "tt_group_tile_pixels", "tt_shutdown"]
@@ -1099,7 +1100,7 @@ def _bind_group(L):
         L.tt_group_member_ctx.argtypes = [vp, u32]
         L.tt_group_member_ctx.restype = vp
         L.tt_group_scene_upload.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp, u32, vp, u32]
-        L.tt_group_trace_frame.argtypes = [vp, C.POINTER(Camera), vp, u32]
+        L.tt_group_trace_frame.argtypes = [vp, C.POINTER(Camera), vp, vp, u32]
         L.tt_group_sync.argtypes = [vp]
         L.tt_group_frame_rays.argtypes = [vp, u32, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]
         L.tt_group_tile_pixels.argtypes = [u32, u32, u32, u32, u32, vp, u32, C.POINTER(u32)]
@@ -1138,10 +1139,12 @@ class Group:
     process as ``rank`` of ``world`` on ``device`` with the RCCL id ``uid`` (tt_group_create_rank)."""
 
     def __init__(self, width: int, height: int, devices=None, tile: int = 64, slots: int = 2, bounce: bool = False,
-                 copy: bool = False, rank: int = None, world: int = None, uid: bytes = None, device: int = None):
+                 copy: bool = False, rank: int = None, world: int = None, uid: bytes = None, device: int = None,
+                 info: bool = False):
         L = _group_lib()
         cfg = GroupConfig(width=width, height=height, tile=tile, slots=slots,
-                          flags=(TT_GROUP_BOUNCE if bounce else 0) | (TT_GROUP_COPY_GATHER if copy else 0))
+                          flags=(TT_GROUP_BOUNCE if bounce else 0) | (TT_GROUP_COPY_GATHER if copy else 0)
+                          | (TT_GROUP_INFO if info else 0))
         h = C.c_void_p()
         if devices is not None:
             devs = np.ascontiguousarray(devices, np.int32)
@@ -1173,14 +1176,14 @@ class Group:
         self._check(st, "tt_group_scene_upload")
 
     def trace_frame(self, hits_out, cam_to_world, cam_inv_proj, near, far, jitter=1, frames=0, max_bounce=1,
-                    asynchronous=False):
+                    asynchronous=False, info_out=None):
         cam = Camera()
         cam.cam_to_world[:] = unity_colmajor(cam_to_world)
         cam.cam_inv_proj[:] = unity_colmajor(cam_inv_proj)
         cam.near_plane, cam.far_plane, cam.width, cam.height = near, far, self.width, self.height
         cam.jitter, cam.frames_accumulated, cam.max_bounce = jitter, frames, max_bounce
         cam.flags = TT_TRACE_DEVICE_PTRS
-        self._check(self.L.tt_group_trace_frame(self.h, C.byref(cam), _ptr(hits_out),
+        self._check(self.L.tt_group_trace_frame(self.h, C.byref(cam), _ptr(hits_out), _ptr(info_out),
                                                 TT_TRACE_ASYNC if asynchronous else 0), "tt_group_trace_frame")
 
     def sync(self):
