@@ -211,6 +211,10 @@ namespace TrueTrace.Hip
         [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_upload(IntPtr group,
             void* nodes, uint nNodes, void* tris, uint nTris, int* tlasIndices, uint nTlas,
             void* meshData, uint nMesh, void* materials, uint nMat);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_upload_alpha_atlas(IntPtr group, byte* texels,
+            uint width, uint height);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_upload_texture_atlas(IntPtr group,
+            ushort* rgbaHalf, uint width, uint height);
         [DllImport(Lib)] public static extern TTStatus tt_group_trace_frame(IntPtr group, ref TTCamera cam, IntPtr hitsOut,
             IntPtr infoOut, uint flags);
         [DllImport(Lib)] public static extern TTStatus tt_group_sync(IntPtr group);
@@ -621,6 +625,16 @@ namespace TrueTrace.Hip
             fixed (TMesh* m = meshData) fixed (TMat* mt = materials)
                 Check(Native.tt_group_scene_upload(m_g, n, (uint)nodes.Length, t, (uint)tris.Length, i, (uint)tlasIndices.Length,
                                                    m, (uint)meshData.Length, mt, (uint)materials.Length));
+        }
+
+        /// The _AlphaAtlas / decoded _TextureAtlas on every device (after SetMeshTraceBuffers).
+        public unsafe void SetAlphaAtlas(byte[] texels, int width, int height)
+        {
+            fixed (byte* t = texels) Check(Native.tt_group_scene_upload_alpha_atlas(m_g, t, (uint)width, (uint)height));
+        }
+        public unsafe void SetTextureAtlas(ushort[] rgbaHalf, int width, int height)
+        {
+            fixed (ushort* t = rgbaHalf) Check(Native.tt_group_scene_upload_texture_atlas(m_g, t, (uint)width, (uint)height));
         }
 
         /// One frame: Generate + primary trace per device for its tiles, the gather of the primary hit records to

@@ -728,6 +728,10 @@ tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_
                                 const int32_t* tlas_indices, uint32_t n_tlas_indices,
                                 const tt_mesh_data* meshdata, uint32_t n_mesh,
                                 const tt_material* materials, uint32_t n_mat);
+/* tt_scene_upload_alpha_atlas / tt_scene_upload_texture_atlas on every local member (after the scene upload:
+ * a scene with Cutout materials needs the alpha atlas before it is traced). */
+tt_status tt_group_scene_upload_alpha_atlas(tt_group* g, const uint8_t* texels, uint32_t width, uint32_t height);
+tt_status tt_group_scene_upload_texture_atlas(tt_group* g, const uint16_t* rgba_half, uint32_t width, uint32_t height);
 /* One frame: Generate (cam: width / height must be the group's; TT_TRACE_DEVICE_PTRS implied) on every
  * member for its tiles, the primary trace, the gather to rank 0 and, with TT_GROUP_BOUNCE, bounce 1 on
  * every member. hits_out: on the process holding rank 0, a 16-byte-aligned buffer of width * height uint4

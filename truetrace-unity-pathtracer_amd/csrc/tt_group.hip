@@ -459,19 +459,21 @@ tt_ctx* tt_group_member_ctx(tt_group* g, uint32_t m) {
     return (g && m < g->m.size()) ? g->m[m].ctx[0] : nullptr;
 }
 
-tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris,
-                                uint32_t n_tris, const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md,
-                                uint32_t n_mesh, const tt_material* mats, uint32_t n_mat) {
-    if (!g) return TT_ERR_INVALID_ARG;
-    // the borrowers let go first (a lender with borrowers refuses an upload), then re-share the new scene
+}  // extern "C"
+
+namespace {
+// An upload to every member's scene context (slot 0). The other slots borrow its scene, and a lender with
+// borrowers refuses uploads: they let go first and share the new scene after (up = the upload per member).
+template <class Up>
+tt_status reupload(tt_group* g, Up up) {
     for (Member& mb : g->m)
         for (uint32_t s = 1; s < g->slots; s++) {
-            (void)tt_ctx_destroy(mb.ctx[s]);
+            if (mb.ctx[s]) (void)tt_ctx_destroy(mb.ctx[s]);
             mb.ctx[s] = nullptr;
         }
     for (Member& mb : g->m) {
         tt_ctx* c0 = mb.ctx[0];
-        G_TT(g, c0, tt_scene_upload(c0, nodes, n_nodes, tris, n_tris, tlas, n_tlas, md, n_mesh, mats, n_mat));
+        G_TT(g, c0, up(c0));
         for (uint32_t s = 1; s < g->slots; s++) {
             tt_config c{};
             c.device = mb.device;
@@ -482,6 +484,28 @@ tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_
         }
     }
     return TT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_t n_nodes, const tt_cuda_triangle* tris,
+                                uint32_t n_tris, const int32_t* tlas, uint32_t n_tlas, const tt_mesh_data* md,
+                                uint32_t n_mesh, const tt_material* mats, uint32_t n_mat) {
+    if (!g) return TT_ERR_INVALID_ARG;
+    return reupload(g, [&](tt_ctx* c) {
+        return tt_scene_upload(c, nodes, n_nodes, tris, n_tris, tlas, n_tlas, md, n_mesh, mats, n_mat);
+    });
+}
+
+tt_status tt_group_scene_upload_alpha_atlas(tt_group* g, const uint8_t* texels, uint32_t width, uint32_t height) {
+    if (!g) return TT_ERR_INVALID_ARG;
+    return reupload(g, [&](tt_ctx* c) { return tt_scene_upload_alpha_atlas(c, texels, width, height); });
+}
+
+tt_status tt_group_scene_upload_texture_atlas(tt_group* g, const uint16_t* rgba_half, uint32_t width, uint32_t height) {
+    if (!g) return TT_ERR_INVALID_ARG;
+    return reupload(g, [&](tt_ctx* c) { return tt_scene_upload_texture_atlas(c, rgba_half, width, height); });
 }
 
 tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t* info_out,

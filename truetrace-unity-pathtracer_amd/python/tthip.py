@@ -1101,12 +1101,15 @@ def _bind_group(L):
         L.tt_group_member_ctx.restype = vp
         L.tt_group_scene_upload.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp, u32, vp, u32]
         L.tt_group_trace_frame.argtypes = [vp, C.POINTER(Camera), vp, vp, u32]
+        L.tt_group_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
+        L.tt_group_scene_upload_texture_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_group_sync.argtypes = [vp]
         L.tt_group_frame_rays.argtypes = [vp, u32, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]
         L.tt_group_tile_pixels.argtypes = [u32, u32, u32, u32, u32, vp, u32, C.POINTER(u32)]
         for s in ["tt_group_create", "tt_group_unique_id", "tt_group_create_rank", "tt_group_destroy",
                   "tt_group_scene_upload", "tt_group_trace_frame", "tt_group_sync", "tt_group_frame_rays",
-                  "tt_group_tile_pixels", "tt_shutdown"]:
+                  "tt_group_tile_pixels", "tt_shutdown", "tt_group_scene_upload_alpha_atlas",
+                  "tt_group_scene_upload_texture_atlas"]:
             getattr(L, s).restype = i32
         L._group_bound = True
 
@@ -1174,6 +1177,14 @@ class Group:
                                           _ptr(s.tlas), len(s.tlas), _ptr(s.meshdata), len(s.meshdata),
                                           _ptr(s.materials), len(s.materials))
         self._check(st, "tt_group_scene_upload")
+        if s.alpha_atlas is not None:
+            a = np.ascontiguousarray(s.alpha_atlas, np.uint8)
+            self._check(self.L.tt_group_scene_upload_alpha_atlas(self.h, a.ctypes.data, a.shape[1], a.shape[0]),
+                        "tt_group_scene_upload_alpha_atlas")
+        if s.texture_atlas is not None:
+            t = np.ascontiguousarray(s.texture_atlas, np.float16)
+            self._check(self.L.tt_group_scene_upload_texture_atlas(self.h, t.ctypes.data, t.shape[1], t.shape[0]),
+                        "tt_group_scene_upload_texture_atlas")
 
     def trace_frame(self, hits_out, cam_to_world, cam_inv_proj, near, far, jitter=1, frames=0, max_bounce=1,
                     asynchronous=False, info_out=None):
