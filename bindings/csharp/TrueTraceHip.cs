@@ -215,6 +215,12 @@ namespace TrueTrace.Hip
             uint width, uint height);
         [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_upload_texture_atlas(IntPtr group,
             ushort* rgbaHalf, uint width, uint height);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_update_meshdata(IntPtr group, uint first,
+            uint count, void* meshData);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_scene_update_nodes(IntPtr group, uint first,
+            uint count, void* nodes);
+        [DllImport(Lib)] public static extern unsafe TTStatus tt_group_tlas_refit(IntPtr group, uint nTlasNodes,
+            float* meshAabbs, uint nMesh, uint flags);
         [DllImport(Lib)] public static extern TTStatus tt_group_trace_frame(IntPtr group, ref TTCamera cam, IntPtr hitsOut,
             IntPtr infoOut, uint flags);
         [DllImport(Lib)] public static extern TTStatus tt_group_sync(IntPtr group);
@@ -625,6 +631,17 @@ namespace TrueTrace.Hip
             fixed (TMesh* m = meshData) fixed (TMat* mt = materials)
                 Check(Native.tt_group_scene_upload(m_g, n, (uint)nodes.Length, t, (uint)tris.Length, i, (uint)tlasIndices.Length,
                                                    m, (uint)meshData.Length, mt, (uint)materials.Length));
+        }
+
+        /// Per-frame MeshDataBuffer.SetData + RefitTLAS (AssetManager.cs:1767-1826) on every device, between frames.
+        public unsafe void SetMeshData<TMesh>(TMesh[] meshData) where TMesh : unmanaged
+        {
+            fixed (TMesh* m = meshData) Check(Native.tt_group_scene_update_meshdata(m_g, 0, (uint)meshData.Length, m));
+        }
+        public unsafe void RefitTLAS(float[] meshAabbs, int nTlasNodes)
+        {
+            fixed (float* b = meshAabbs)
+                Check(Native.tt_group_tlas_refit(m_g, (uint)nTlasNodes, b, (uint)(meshAabbs.Length / 6), 0));
         }
 
         /// The _AlphaAtlas / decoded _TextureAtlas on every device (after SetMeshTraceBuffers).

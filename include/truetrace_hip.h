@@ -732,6 +732,14 @@ tt_status tt_group_scene_upload(tt_group* g, const tt_cwbvh_node* nodes, uint32_
  * a scene with Cutout materials needs the alpha atlas before it is traced). */
 tt_status tt_group_scene_upload_alpha_atlas(tt_group* g, const uint8_t* texels, uint32_t width, uint32_t height);
 tt_status tt_group_scene_upload_texture_atlas(tt_group* g, const uint16_t* rgba_half, uint32_t width, uint32_t height);
+/* Per-frame scene updates on every local member, between frames (AssetManager.cs:1760-1825 on each device):
+ * tt_scene_update_meshdata / tt_scene_update_nodes / tt_tlas_refit of each member's scene context. The frame slots
+ * borrow that scene, and the library orders each update after the traces already issued and before later ones, so
+ * no synchronisation is needed. tt_group_tlas_refit takes host AABBs (flags: TT_TRACE_ASYNC). */
+tt_status tt_group_scene_update_meshdata(tt_group* g, uint32_t first, uint32_t count, const tt_mesh_data* meshdata);
+tt_status tt_group_scene_update_nodes(tt_group* g, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes);
+tt_status tt_group_tlas_refit(tt_group* g, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh,
+                              uint32_t flags);
 /* One frame: Generate (cam: width / height must be the group's; TT_TRACE_DEVICE_PTRS implied) on every
  * member for its tiles, the primary trace, the gather to rank 0 and, with TT_GROUP_BOUNCE, bounce 1 on
  * every member. hits_out: on the process holding rank 0, a 16-byte-aligned buffer of width * height uint4

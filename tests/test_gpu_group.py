@@ -264,3 +264,51 @@ def test_group_refusals(soup):
         g.trace_frame(hits, c2w, ip, NEAR, FAR, info_out=dinfo)  # still usable after refusals
     finally:
         g.close()
+
+
+def test_per_frame_scene_updates_reach_every_member():
+    """A dynamic two-level scene through the group: frame 0, then every instance moved (tt_group_scene_update_meshdata
+    + tt_group_tlas_refit, AssetManager.cs:1767-1826 on every device) and frame 1 issued with no synchronisation in
+    between (2 slots, 3 members, copy gather): each frame's gathered records equal the oracle's on the scene as it
+    was when the frame was issued (the refit TLAS read back from a member, the moved _MeshData)."""
+    torch = _torch()
+    from test_gpu_parity import instanced_scene
+
+    sc = instanced_scene(17, n_props=4, n_inst=40)
+    W, H = 160, 96
+    c2w, ip = tthip.unity_camera((0, 8, 45), (0, -0.2, -1), (0, 1, 0), 70, W, H, NEAR, FAR)
+    g = tthip.Group(W, H, devices=[0, 0, 0], slots=2, copy=True)
+    try:
+        g.upload(sc)
+        o0 = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+        o1 = torch.full((W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+        g.trace_frame(o0, c2w, ip, NEAR, FAR, jitter=1, frames=0, asynchronous=True)
+        rng = np.random.default_rng(17)
+        md = sc.meshdata.copy()
+        box = np.ascontiguousarray(sc.meta["mesh_aabbs"], np.float32).copy()
+        for i in range(1, len(md)):
+            d = rng.normal(0, 2.0, 3)
+            w2l = md["W2L"][i].astype(np.float64).reshape(4, 4).T
+            sh = np.eye(4)
+            sh[:3, 3] = -d
+            md["W2L"][i] = tthip.unity_colmajor(w2l @ sh)
+            box[i, 0:3] += d.astype(np.float32)
+            box[i, 3:6] += d.astype(np.float32)
+        g.update_meshdata(0, md)
+        g.tlas_refit(sc.tlas_nodes, box, asynchronous=True)
+        g.trace_frame(o1, c2w, ip, NEAR, FAR, jitter=1, frames=1, asynchronous=True)
+        g.sync()
+        L = tthip.hip_lib()
+        nodes = sc.nodes.copy()
+        tl = np.zeros(sc.tlas_nodes, tthip.NODE_DTYPE)
+        assert L.tt_scene_read_nodes(g.member_ctx(2), 0, sc.tlas_nodes, tl.ctypes.data) == tthip.TT_OK
+        nodes[: sc.tlas_nodes] = tl
+        moved = tthip.Scene(nodes, sc.tris, sc.tlas, md, sc.materials, tlas_nodes=sc.tlas_nodes)
+        f0 = oracle_frame(sc, c2w, ip, W, H, 0)
+        f1 = oracle_frame(moved, c2w, ip, W, H, 1)
+        assert np.array_equal(o0.cpu().numpy().view(np.uint32), f0["hits"][:W * H]), "frame 0: the scene before"
+        assert np.array_equal(o1.cpu().numpy().view(np.uint32), f1["hits"][:W * H]), "frame 1: the moved scene"
+        still = oracle_frame(sc, c2w, ip, W, H, 1)  # frame 1's rays on the scene before the move
+        assert not np.array_equal(still["hits"][:W * H], f1["hits"][:W * H])  # the move is visible
+    finally:
+        g.close()

@@ -508,6 +508,31 @@ tt_status tt_group_scene_upload_texture_atlas(tt_group* g, const uint16_t* rgba_
     return reupload(g, [&](tt_ctx* c) { return tt_scene_upload_texture_atlas(c, rgba_half, width, height); });
 }
 
+// Per-frame scene updates on every member's scene context (AssetManager.cs:1760-1825 per device): the slots
+// borrow that scene, and the library orders each update after their traces already issued and before the
+// ones issued after it (tt_ctx_share_scene), so a host calls these between frames with no synchronisation.
+tt_status tt_group_scene_update_meshdata(tt_group* g, uint32_t first, uint32_t count, const tt_mesh_data* md) {
+    if (!g) return TT_ERR_INVALID_ARG;
+    for (Member& mb : g->m) G_TT(g, mb.ctx[0], tt_scene_update_meshdata(mb.ctx[0], first, count, md));
+    return TT_OK;
+}
+
+tt_status tt_group_scene_update_nodes(tt_group* g, uint32_t first, uint32_t count, const tt_cwbvh_node* nodes) {
+    if (!g) return TT_ERR_INVALID_ARG;
+    for (Member& mb : g->m) G_TT(g, mb.ctx[0], tt_scene_update_nodes(mb.ctx[0], first, count, nodes));
+    return TT_OK;
+}
+
+tt_status tt_group_tlas_refit(tt_group* g, uint32_t n_tlas_nodes, const float* mesh_aabbs, uint32_t n_mesh,
+                              uint32_t flags) {
+    if (!g) return TT_ERR_INVALID_ARG;
+    if (flags & TT_TRACE_DEVICE_PTRS)  // (one device array cannot serve every member's device)
+        return gfail(g, TT_ERR_INVALID_ARG, "tt_group_tlas_refit takes host mesh AABBs");
+    for (Member& mb : g->m)
+        G_TT(g, mb.ctx[0], tt_tlas_refit(mb.ctx[0], n_tlas_nodes, mesh_aabbs, n_mesh, flags & TT_TRACE_ASYNC));
+    return TT_OK;
+}
+
 tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits_out, uint32_t* info_out,
                                uint32_t flags) {
     if (!g) return TT_ERR_INVALID_ARG;

@@ -1102,6 +1102,9 @@ def _bind_group(L):
         L.tt_group_scene_upload.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp, u32, vp, u32]
         L.tt_group_trace_frame.argtypes = [vp, C.POINTER(Camera), vp, vp, u32]
         L.tt_group_scene_upload_alpha_atlas.argtypes = [vp, vp, u32, u32]
+        L.tt_group_scene_update_meshdata.argtypes = [vp, u32, u32, vp]
+        L.tt_group_scene_update_nodes.argtypes = [vp, u32, u32, vp]
+        L.tt_group_tlas_refit.argtypes = [vp, u32, vp, u32, u32]
         L.tt_group_scene_upload_texture_atlas.argtypes = [vp, vp, u32, u32]
         L.tt_group_sync.argtypes = [vp]
         L.tt_group_frame_rays.argtypes = [vp, u32, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]
@@ -1109,7 +1112,8 @@ def _bind_group(L):
         for s in ["tt_group_create", "tt_group_unique_id", "tt_group_create_rank", "tt_group_destroy",
                   "tt_group_scene_upload", "tt_group_trace_frame", "tt_group_sync", "tt_group_frame_rays",
                   "tt_group_tile_pixels", "tt_shutdown", "tt_group_scene_upload_alpha_atlas",
-                  "tt_group_scene_upload_texture_atlas"]:
+                  "tt_group_scene_upload_texture_atlas", "tt_group_scene_update_meshdata",
+                  "tt_group_scene_update_nodes", "tt_group_tlas_refit"]:
             getattr(L, s).restype = i32
         L._group_bound = True
 
@@ -1199,6 +1203,19 @@ class Group:
 
     def sync(self):
         self._check(self.L.tt_group_sync(self.h), "tt_group_sync")
+
+    def update_meshdata(self, first: int, md: np.ndarray):
+        self._check(self.L.tt_group_scene_update_meshdata(self.h, first, len(md), _ptr(md)),
+                    "tt_group_scene_update_meshdata")
+
+    def update_nodes(self, first: int, nodes: np.ndarray):
+        self._check(self.L.tt_group_scene_update_nodes(self.h, first, len(nodes), _ptr(nodes)),
+                    "tt_group_scene_update_nodes")
+
+    def tlas_refit(self, n_tlas_nodes: int, mesh_aabbs: np.ndarray, asynchronous: bool = False):
+        a = np.ascontiguousarray(mesh_aabbs, np.float32)
+        self._check(self.L.tt_group_tlas_refit(self.h, n_tlas_nodes, a.ctypes.data, a.shape[0],
+                                               TT_TRACE_ASYNC if asynchronous else 0), "tt_group_tlas_refit")
 
     def frame_rays(self, m: int = 0):
         """(n_primary, n_bounce, device pointer of the ray buffer) of member m's latest frame."""
