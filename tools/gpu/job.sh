@@ -131,7 +131,7 @@ for stage in "$@"; do
            done ;;
     gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
-    rccl1) run rccl1 600 env TT_BENCH_RCCL_WORLD1=1 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline \
+    rccl1) run rccl1 600 env TT_BENCH_RCCL_WORLD1=1 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29611 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline \
                --no-shadow --steady-steps 0 --aux "" || exit $? ;;
     gloo4) run gloo4 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 4 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
