@@ -312,3 +312,28 @@ def test_per_frame_scene_updates_reach_every_member():
         assert not np.array_equal(still["hits"][:W * H], f1["hits"][:W * H])  # the move is visible
     finally:
         g.close()
+
+
+def test_group_create_destroy_releases_everything(soup):
+    """Groups made and destroyed repeatedly (copy and RCCL forms, several slot counts) leave no library stream
+    behind (each member's slot streams and its communication stream are tt_stream_create streams) and a group
+    made afterwards still traces correctly."""
+    torch = _torch()
+    L = tthip.hip_lib()
+    base = L.tt_stream_live_count()
+    for k in range(4):
+        g = tthip.Group(64, 64, devices=[0] * (1 + k % 3), slots=1 + k, copy=k % 2 == 0)
+        assert L.tt_stream_live_count() == base + (1 + k % 3) * (1 + k + 1)
+        if k == 3:
+            g.upload(soup)
+        g.close()
+        assert L.tt_stream_live_count() == base
+    c2w, ip = soup_camera(64, 64)
+    g = tthip.Group(64, 64, devices=[0, 0], copy=True)
+    try:
+        g.upload(soup)
+        out = torch.zeros((64 * 64, 4), dtype=torch.int32, device="cuda:0")
+        g.trace_frame(out, c2w, ip, NEAR, FAR, jitter=1, frames=4)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle_frame(soup, c2w, ip, 64, 64, 4)["hits"][:64 * 64])
+    finally:
+        g.close()
