@@ -321,9 +321,9 @@ def test_group_create_destroy_releases_everything(soup):
     torch = _torch()
     L = tthip.hip_lib()
     base = L.tt_stream_live_count()
-    for k in range(4):
-        g = tthip.Group(64, 64, devices=[0] * (1 + k % 3), slots=1 + k, copy=k % 2 == 0)
-        assert L.tt_stream_live_count() == base + (1 + k % 3) * (1 + k + 1)
+    for k, (members, slots, copy) in enumerate([(1, 1, False), (2, 2, True), (3, 3, True), (1, 4, False)]):
+        g = tthip.Group(64, 64, devices=[0] * members, slots=slots, copy=copy)
+        assert L.tt_stream_live_count() == base + members * (slots + 1)  # slot streams + the communication stream
         if k == 3:
             g.upload(soup)
         g.close()
