@@ -515,6 +515,8 @@ def lpt_deal(torch, tthip, ttdist, eng, dev, W, H, c2w, ip, near, far, world, ar
 def split_batched_gather(blocks, sizes, B):
     """A gather of B-frame launches (FrameLayout batch B): every rank's block holds its parts back to back, each
     part's records the B frames' back to back. Returns per frame b: (blocks, sizes) as assemble_parts takes them."""
+    # (the RCCL gather's blocks are device tensors: one copy to the host each, numpy from there on)
+    blocks = [g.cpu().numpy() if hasattr(g, "cpu") else np.asarray(g) for g in blocks]
     out = []
     for b in range(B):
         fb, sb = [], []

@@ -222,3 +222,43 @@ def test_lpt_deal_covers_every_tile_and_balances():
         sizes.append([len(p) for p in parts])
     assert np.all(seen == 1)
     assert np.array_equal(td.assemble_parts(blocks, sizes, W, H, world, P, owner=owner), frames)
+
+
+def test_split_batched_gather_takes_device_blocks_and_reassembles():
+    """bench.split_batched_gather: the RCCL gather hands rank 0 DEVICE tensors (one block per rank: its parts back to
+    back, each part's B frames back to back); the split must copy them to the host itself (np.concatenate on a
+    device tensor raises) and give per frame the blocks assemble_parts takes. Checked with tensors standing in for
+    the device blocks (anything with .cpu()) against the frames' own records."""
+    import importlib.util
+
+    import torch
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    W, H, world, P, B = 192, 128, 2, 2, 3
+
+    class Dev:  # a block that only converts through .cpu(), as a device tensor does
+        def __init__(self, t):
+            self.t = t
+
+        def cpu(self):
+            return self.t
+
+        def __getitem__(self, k):
+            return Dev(self.t[k])
+
+    frames = [np.arange(W * H * 4, dtype=np.uint32).reshape(-1, 4) + np.uint32(b * 10_000_000) for b in range(B)]
+    blocks, sizes = [], []
+    for r in range(world):
+        parts = ttdist.part_pixels(W, H, world, r, P)
+        rows = [frames[b][pix] for pix in parts for b in range(B)]
+        blocks.append(Dev(torch.from_numpy(np.concatenate(rows).view(np.int32))))
+        sizes.append([B * len(pix) for pix in parts])
+    out = bench.split_batched_gather(blocks, sizes, B)
+    assert len(out) == B
+    for b, (fb, sb) in enumerate(out):
+        assert all(isinstance(x, np.ndarray) for x in fb)
+        got = ttdist.assemble_parts(fb, sb, W, H, world, P)
+        assert np.array_equal(got, frames[b])
