@@ -27,7 +27,7 @@ def wait_for(path, seconds):
     while not os.path.exists(path):
         if time.time() - t0 > seconds:
             raise TimeoutError(f"{path} did not appear within {seconds} s")
-        time.sleep(0.002)
+        time.sleep(0.0002)
 
 
 def main():
