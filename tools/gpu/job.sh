@@ -25,6 +25,7 @@
 #   lifecycle  the GPU tests of stream teardown (rocprofv3 leg included), root-leaf bookkeeping and the timed kernels' jittered parity
 #   gloo2      the 2-rank bench rehearsal on this GPU (gloo collectives, C5 tiles included)
 #   gloo4      the same with 4 ranks
+#   groupscale the library group at world 1 on 1, 1/4, 1/8 of a 1080p frame x 2/4/8 slots (tools/group_scale.py)
 #   rccl1      one rank through the N > 1 tile path with a real RCCL communicator of size 1 (+ the group leg)
 #   longray    the C5 frame's degenerate ray: its chain alone and under load (tools/long_ray_chain.py)
 #   c4loc      C4 one-launch time, TCC hit / miss and FETCH_SIZE per variant (AB_LIBS, default "cur n128")
@@ -131,6 +132,7 @@ for stage in "$@"; do
            done ;;
     gloo2) run gloo2 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 4 --warmup 1 \
                --no-cpu-baseline --no-shadow --steady-steps 0 || exit $? ;;
+    groupscale) run groupscale 600 python -u tools/group_scale.py ${GS_FRAMES:-200} || exit $? ;;
     rccl1) run rccl1 600 env TT_BENCH_RCCL_WORLD1=1 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29611 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline \
                --no-shadow --steady-steps 0 --aux "" || exit $? ;;
     gloo4) run gloo4 600 env TT_BENCH_DIST_BACKEND=gloo python -u bench.py --gpus 4 --steps 4 --warmup 1 \
