@@ -823,9 +823,13 @@ def group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H):
         d = box[0]
     S = max(1, args.group_slots)
     R = max(1, args.cycle) if world > 1 else S
+    # frames per call: as the torch layouts (--batch at N > 1, --n1-batch at N = 1): each call traces B samples of
+    # the still view as one B-frames-tall screen (tt_group_config.batch)
+    Bg = max(1, args.batch if world > 1 else args.n1_batch)
     cmd = [sys.executable, os.path.join(REPO, "tools", "group_leg.py"), "--rank", str(rank), "--world", str(world),
            "--device", str(gpu), "--dir", d, "--steps", str(args.group_frames), "--warmup", str(max(args.warmup, 10)),
-           "--slots", str(S), "--cycle", str(R), "--width", str(W), "--height", str(H), "--tris", str(args.tris),
+           "--slots", str(S), "--cycle", str(R), "--batch", str(Bg), "--width", str(W), "--height", str(H),
+           "--tris", str(args.tris),
            "--seed", hex(args.seed)]
     res, err = None, None
     try:
@@ -852,11 +856,11 @@ def group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H):
         return {"error": err or "another rank's group leg failed"}
     el = float(el.item())
     per = per.cpu().numpy()
-    K = args.group_frames
+    K = args.group_frames  # calls, Bg frames each
     rays = float(sum(per[k % R] for k in range(K)))
     out = {"value": round(rays / el / 1e6, 2), "unit": "Mrays/s", "scaling": "strong", "ranks": world,
-           "ms_per_frame": round(el * 1e3 / K, 4), "frames": K, "frame_slots": S, "samples_cycled": R,
-           "rays_per_frame_all_ranks": int(round(rays / K)),
+           "ms_per_frame": round(el * 1e3 / (K * Bg), 4), "calls": K, "frames_per_call": Bg, "frame_slots": S,
+           "samples_cycled": R * Bg, "rays_per_frame_all_ranks": int(round(rays / (K * Bg))),
            "gather_identical_to_1gpu": None if res is None else res.get("parity"),
            "api": "tt_group_unique_id + tt_group_create_rank + tt_group_scene_upload + tt_group_trace_frame "
                   "(TT_TRACE_ASYNC) + tt_group_sync, one child process per rank (tools/group_leg.py)",
@@ -864,7 +868,7 @@ def group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H):
                      "each rank's Generate + primary trace + bounce-1 enqueue/trace on its own device, one RCCL "
                      "gather of the primary hit records to rank 0 per frame inside the library"}
     if world > 1 and getattr(args, "_solo_ms", None):
-        out["efficiency_vs_n1_frame"] = round(args._solo_ms / (world * el * 1e3 / K), 4)
+        out["efficiency_vs_n1_frame"] = round(args._solo_ms / (world * el * 1e3 / (K * Bg)), 4)
     return out
 
 
@@ -1131,8 +1135,9 @@ def main():
     ap.add_argument("--group-slots", type=int, default=4,
                     help="frames in flight of the library's multi-GPU group leg (aux_group_tiles)")
     ap.add_argument("--no-group", action="store_true", help="skip aux_group_tiles (the tt_group_* library path)")
-    ap.add_argument("--group-frames", type=int, default=200,
-                    help="timed frames of the group leg (aux_group_tiles): many, so the children's start skew "
+    ap.add_argument("--group-frames", type=int, default=100,
+                    help="timed calls of the group leg (aux_group_tiles; each --batch / --n1-batch frames): many, so "
+                         "the children's start skew "
                          "(a file barrier) stays small against the leg's time at N = 8")
     ap.add_argument("--group-timeout", type=float, default=240.0,
                     help="seconds each rank's group-leg child may take before it is killed (aux_group_tiles)")

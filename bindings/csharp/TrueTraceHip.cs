@@ -102,7 +102,7 @@ namespace TrueTrace.Hip
         public uint tile;      // 0: 64
         public uint slots;     // 0: 2
         public TTGroupFlags flags;
-        public uint pad;
+        public uint batch;     // frames per call (0: 1): frames_accumulated + b, b < batch, as one B-frames-tall screen
     }
 
     /// Column-major 4x4 (the memory order of UnityEngine.Matrix4x4: m00, m10, m20, m30, m01, ...).

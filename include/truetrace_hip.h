@@ -701,7 +701,11 @@ typedef struct tt_group_config {
     uint32_t tile;          /* tile edge in pixels, a multiple of 8 (0: 64)                               */
     uint32_t slots;         /* frames in flight per member (0: 2; at most 8)                              */
     uint32_t flags;         /* TT_GROUP_*                                                                 */
-    uint32_t pad;
+    uint32_t batch;         /* frames per call, B (0: 1; at most 16): a call traces frames_accumulated + b,
+                               b < B, of one camera as ONE screen B frames tall (frame b's PixelIndex + b W H,
+                               tt_ctx_set_frame_pixels): a launch's ramp-up and drain and every per-frame call
+                               are paid once per B frames -- for progressive accumulation of a still view (the
+                               next B samples' pose is known); B = 1 for a moving camera                  */
 } tt_group_config;
 
 /* One process, n devices (devices[i] is member i's HIP ordinal; member 0 is rank 0 and receives the
@@ -742,10 +746,11 @@ tt_status tt_group_tlas_refit(tt_group* g, uint32_t n_tlas_nodes, const float* m
                               uint32_t flags);
 /* One frame: Generate (cam: width / height must be the group's; TT_TRACE_DEVICE_PTRS implied) on every
  * member for its tiles, the primary trace, the gather to rank 0 and, with TT_GROUP_BOUNCE, bounce 1 on
- * every member. hits_out: on the process holding rank 0, a 16-byte-aligned buffer of width * height uint4
- * records (screen order) -- device memory of rank 0's device, or host memory (then the frame must be
+ * every member. hits_out: on the process holding rank 0, a 16-byte-aligned buffer of batch * width * height uint4
+ * records (frame b's screen-order records at [b W H, (b + 1) W H)) -- device memory of rank 0's device, or host
+ * memory (then the frame must be
  * synchronous: the records are staged on rank 0's device and copied back); ignored (may be NULL) elsewhere.
- * info_out (TT_GROUP_INFO; else ignored): width * height uint4 _PrimaryTriangleInfo texels in screen order, the
+ * info_out (TT_GROUP_INFO; else ignored): batch * width * height uint4 _PrimaryTriangleInfo texels, as hits_out, the
  * bounce-0 form tt_trace_closest writes (IntersectionKernels.compute:229-238), same kind of memory as hits_out;
  * each member packs its texels behind its hit records, so they travel in the same RCCL group.
  * flags: TT_TRACE_ASYNC (return without waiting; device hits_out only). */
@@ -753,10 +758,10 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
                                uint32_t flags);
 /* Waits for every frame issued so far (all members, all slots, the gathers). */
 tt_status tt_group_sync(tt_group* g);
-/* Of the latest frame, member m: its primary ray count, its bounce-1 ray count (0 without
- * TT_GROUP_BOUNCE) and the device pointer of its ray buffer (RayData[width * height + primary]:
- * primary rays at [0, primary), bounce-1 rays at [width * height, + bounce)). Synchronizes. Any
- * output may be NULL. */
+/* Of the latest call, member m: its primary ray count (batch x its pixels), its bounce-1 ray count (0 without
+ * TT_GROUP_BOUNCE) and the device pointer of its ray buffer (RayData[batch * width * height + primary]: primary
+ * rays at [0, primary) -- frame b's at [b n, (b + 1) n) --, bounce-1 rays at [batch * width * height, + bounce),
+ * each frame's survivors after the previous frame's). Synchronizes. Any output may be NULL. */
 tt_status tt_group_frame_rays(tt_group* g, uint32_t m, uint32_t* n_primary, uint32_t* n_bounce,
                               tt_ray_data** rays_dev);
 /* The shard arithmetic (host only, no GPU): the pixels rank `rank` of `world` traces, in trace order --

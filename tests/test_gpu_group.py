@@ -337,3 +337,48 @@ def test_group_create_destroy_releases_everything(soup):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle_frame(soup, c2w, ip, 64, 64, 4)["hits"][:64 * 64])
     finally:
         g.close()
+
+
+def test_batched_group_frames_equal_the_oracle_frames(soup):
+    """tt_group_config.batch = 3: each call traces frames f .. f + 2 of one camera as one 3-frames-tall screen (3
+    members, copy gather, bounce 1 and _PrimaryTriangleInfo). Frame b's gathered records and info texels (at
+    [b W H, (b + 1) W H)) equal the oracle's frame f + b traced alone; every member's primary rays are its pixels'
+    rays of each frame (PixelIndex + b W H) and its bounce-1 rays and records are the oracle's per-frame enqueue +
+    trace over its own rays at f + b, frame after frame (the enqueue keyed on the frame-local pixel)."""
+    torch = _torch()
+    W, H, B, f0, members = 200, 136, 3, 7, 3
+    WH = W * H
+    c2w, ip = soup_camera(W, H)
+    g = tthip.Group(W, H, devices=[0] * members, bounce=True, copy=True, info=True, batch=B, slots=2)
+    try:
+        g.upload(soup)
+        hits = torch.full((B * WH, 4), -1, dtype=torch.int32, device="cuda:0")
+        info = torch.full((B * WH, 4), -1, dtype=torch.int32, device="cuda:0")
+        g.trace_frame(hits, c2w, ip, NEAR, FAR, jitter=1, frames=f0, max_bounce=1, info_out=info)
+        got_h, got_i = hits.cpu().numpy().view(np.uint32), info.cpu().numpy().view(np.uint32)
+        fulls = []
+        for b in range(B):
+            iref = np.full((WH, 4), 0xA5A5A5A5, np.uint32)
+            full = oracle_frame(soup, c2w, ip, W, H, f0 + b, info=iref)
+            fulls.append(full)
+            assert np.array_equal(got_h[b * WH:(b + 1) * WH], full["hits"][:WH]), f"frame {b}: records"
+            assert np.array_equal(got_i[b * WH:(b + 1) * WH], iref), f"frame {b}: _PrimaryTriangleInfo"
+        for m in range(members):
+            n_all, nb, ptr = g.frame_rays(m)
+            pix = tthip.group_tile_pixels(W, H, members, m).astype(np.int64)
+            n = len(pix)
+            assert n_all == B * n
+            got = device_rays(ptr, B * WH + B * n)
+            off = B * WH
+            for b in range(B):
+                ref_p = fulls[b][pix].copy()
+                ref_p["PixelIndex"] += np.uint32(b * WH)
+                assert np.array_equal(got[b * n:(b + 1) * n].view(np.uint8), ref_p.view(np.uint8)), (m, b, "primary")
+                ref, nb_b = oracle_member(soup, fulls[b], pix, W, H, f0 + b)
+                ref_b = ref[WH:WH + nb_b].copy()
+                ref_b["PixelIndex"] += np.uint32(b * WH)
+                assert np.array_equal(got[off:off + nb_b].view(np.uint8), ref_b.view(np.uint8)), (m, b, "bounce 1")
+                off += nb_b
+            assert off == B * WH + nb
+    finally:
+        g.close()

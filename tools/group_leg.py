@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--cycle", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=1, help="frames per call (tt_group_config.batch)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--tris", type=int, default=262267)
@@ -67,37 +68,39 @@ def main():
     else:
         wait_for(uid_path, 60)
         uid = open(uid_path, "rb").read()
-    S, R = max(1, a.slots), max(1, a.cycle)
-    g = tthip.Group(W, H, rank=a.rank, world=a.world, uid=uid, device=a.device, slots=S, bounce=True)
+    S, R, B = max(1, a.slots), max(1, a.cycle), max(1, a.batch)
+    g = tthip.Group(W, H, rank=a.rank, world=a.world, uid=uid, device=a.device, slots=S, bounce=True, batch=B)
     try:
         g.upload(scene)
-        outs = [torch.zeros((W * H, 4), dtype=torch.int32, device=dev) for _ in range(S)] if a.rank == 0 else [None] * S
+        outs = [torch.zeros((B * W * H, 4), dtype=torch.int32, device=dev) for _ in range(S)] if a.rank == 0 else [None] * S
         torch.cuda.synchronize(dev)
         mine = []
+        # call k traces samples B (k mod R) .. B (k mod R) + B - 1
         for k in range(R):
-            g.trace_frame(outs[0], c2w, ip, near, far, jitter=1, frames=k, max_bounce=1)
+            g.trace_frame(outs[0], c2w, ip, near, far, jitter=1, frames=B * k, max_bounce=1)
             n_p, n_b, _ = g.frame_rays(0)
             mine.append(int(n_p + n_b))
         for k in range(a.warmup):
-            g.trace_frame(outs[k % S], c2w, ip, near, far, jitter=1, frames=k % R, max_bounce=1, asynchronous=True)
+            g.trace_frame(outs[k % S], c2w, ip, near, far, jitter=1, frames=B * (k % R), max_bounce=1, asynchronous=True)
         g.sync()
         open(os.path.join(a.dir, f"ready_{a.rank}"), "w").close()
         for r in range(a.world):
             wait_for(os.path.join(a.dir, f"ready_{r}"), 120)
         t0 = time.perf_counter()
         for k in range(a.steps):
-            g.trace_frame(outs[k % S], c2w, ip, near, far, jitter=1, frames=k % R, max_bounce=1, asynchronous=True)
+            g.trace_frame(outs[k % S], c2w, ip, near, far, jitter=1, frames=B * (k % R), max_bounce=1, asynchronous=True)
         g.sync()
         el = time.perf_counter() - t0
         parity = None
         if a.rank == 0:
-            k = a.steps - 1
-            got = outs[k % S].cpu().numpy().view(np.uint32)
+            k = a.steps - 1  # the last call's last frame: sample B (k mod R) + B - 1
+            got = outs[k % S][(B - 1) * W * H:].cpu().numpy().view(np.uint32)
             eng = tthip.Engine(a.device)
             try:
                 eng.upload(scene)
                 one = torch.zeros(W * H * 48, dtype=torch.uint8, device=dev)
-                eng.generate(one, c2w, ip, W, H, near, far, jitter=1, frames=k % R, max_bounce=1, device=True)
+                eng.generate(one, c2w, ip, W, H, near, far, jitter=1, frames=B * (k % R) + B - 1, max_bounce=1,
+                             device=True)
                 eng.trace(one, W * H, 0, far, W, H, device=True)
                 ref = one.view(W * H, 48)[:, 32:48].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
                 parity = bool(np.array_equal(got, ref))

@@ -30,9 +30,10 @@
 
 #include "../../include/truetrace_hip.h"
 
-hipError_t tt_launch_generate_list(const float* c2w, const float* ip, const uint32_t* pixels, uint32_t n, uint32_t w,
-                                   uint32_t h, float near_plane, float far_plane, int32_t jitter, int32_t frames,
-                                   int32_t max_bounce, tt_ray_data* rays, hipStream_t st);
+hipError_t tt_launch_generate_list(const float* c2w, const float* ip, const uint32_t* pixels, uint32_t n,
+                                   uint32_t batch, uint32_t w, uint32_t h, float near_plane, float far_plane,
+                                   int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays,
+                                   hipStream_t st);
 
 #define TT_GROUP_MAX_SLOTS 8u
 
@@ -89,25 +90,33 @@ const Rccl& rccl() {
 }
 
 // ------------------------------------------------------------------ kernels
-// hits_out[order[j]] = recv[j] for the j-th gathered record (rank-major blocks, each in its member's
-// trace order): the screen-order record array on rank 0.
-// With _PrimaryTriangleInfo gathered too (TT_GROUP_INFO), recv[n + j] is record j's info texel.
+// Back to screen order on rank 0. The gathered records are rank-major blocks, rank q's block its B frames'
+// records back to back, each frame in the member's trace order; record j of the rank-order concatenation of the
+// members' pixel lists (pixel order[j], of rank q, its l-th) sits for frame b at base[j] + b * stride[j]
+// (base = B * shard_off[q] + l, stride = shard_n[q]): frame b's record goes to out[b * WH + order[j]]. With
+// _PrimaryTriangleInfo gathered too (TT_GROUP_INFO) the info texels follow all records at recv + B * WH.
 __global__ __launch_bounds__(256) void tt_group_scatter_kernel(const uint4* __restrict__ recv,
-                                                               const uint32_t* __restrict__ order, uint32_t n,
-                                                               uint4* __restrict__ out, uint4* __restrict__ info_out) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t p = order[j];
-    out[p] = recv[j];
-    if (info_out) info_out[p] = recv[n + j];
+                                                               const uint32_t* __restrict__ order,
+                                                               const uint32_t* __restrict__ base,
+                                                               const uint32_t* __restrict__ stride, uint32_t wh,
+                                                               uint32_t batch, uint4* __restrict__ out,
+                                                               uint4* __restrict__ info_out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= wh * batch) return;
+    const uint32_t b = t / wh, j = t - b * wh;
+    const uint32_t src = base[j] + b * stride[j], dst = b * wh + order[j];
+    out[dst] = recv[src];
+    if (info_out) info_out[dst] = recv[(size_t)wh * batch + src];
 }
-// A member's _PrimaryTriangleInfo texels (written at their pixels by the primary trace) packed in its ray
-// order behind its hit records, so one message per rank carries both.
+// A member's _PrimaryTriangleInfo texels (written at their pixels of the B-frames-tall screen by the primary trace)
+// packed in its ray order behind its hit records, so they travel with them.
 __global__ __launch_bounds__(256) void tt_group_pack_info_kernel(const uint4* __restrict__ info_full,
                                                                  const uint32_t* __restrict__ pixels, uint32_t n,
-                                                                 uint4* __restrict__ dst) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = info_full[pixels[i]];
+                                                                 uint32_t batch, uint32_t wh, uint4* __restrict__ dst) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n * batch) return;
+    const uint32_t b = r / n;
+    dst[r] = info_full[pixels[r - b * n] + b * wh];
 }
 
 // ------------------------------------------------------------------ shard arithmetic
@@ -161,8 +170,8 @@ struct Member {
     void* comm_stream = nullptr;
     ncclComm_t comm = nullptr;
     Dev<tt_ray_data> rays[TT_GROUP_MAX_SLOTS];
-    Dev<uint4> send[TT_GROUP_MAX_SLOTS];       // hit records [0, n) (+ info texels [n, 2n) with TT_GROUP_INFO)
-    Dev<uint4> info_full[TT_GROUP_MAX_SLOTS];  // TT_GROUP_INFO: the primary trace's _PrimaryTriangleInfo, W*H
+    Dev<uint4> send[TT_GROUP_MAX_SLOTS];       // hit records [0, B n) (+ info texels [B n, 2 B n) with TT_GROUP_INFO)
+    Dev<uint4> info_full[TT_GROUP_MAX_SLOTS];  // TT_GROUP_INFO: the primary trace's _PrimaryTriangleInfo, B W H
     Dev<uint32_t> count[TT_GROUP_MAX_SLOTS];  // bounce-1 survivors of the slot's last frame
     Dev<uint32_t> pixels;
     hipEvent_t ev_prim[TT_GROUP_MAX_SLOTS] = {};  // the slot's primary records are final
@@ -174,13 +183,14 @@ struct Member {
 
 struct tt_group {
     uint32_t W = 0, H = 0, tile = 64, slots = 2, flags = 0, world = 0;
+    uint32_t B = 1;  // frames per call (tt_group_config.batch)
     bool bounce = false, copy = false, info = false;
     std::vector<Member> m;
     std::vector<uint64_t> shard_n, shard_off;  // per rank
     // rank 0's side (when this process holds it: member 0)
     bool root = false;
-    Dev<uint4> recv[TT_GROUP_MAX_SLOTS];  // W*H hit records in rank order (+ W*H info texels with TT_GROUP_INFO)
-    Dev<uint32_t> order;
+    Dev<uint4> recv[TT_GROUP_MAX_SLOTS];  // B W H hit records in rank order (+ B W H info texels, TT_GROUP_INFO)
+    Dev<uint32_t> order, base, stride;    // the scatter's tables (tt_group_scatter_kernel)
     Dev<uint4> stage;  // screen-order records for a host hits_out (copied back by a synchronous frame)
     uint64_t frame = 0;
     std::string err;
@@ -225,6 +235,10 @@ bool check_config(const tt_group_config* cfg, std::string& why) {
     if (tile % 8) return why = "tile must be a multiple of 8", false;
     if (cfg->slots > TT_GROUP_MAX_SLOTS) return why = "at most 8 slots", false;
     if (cfg->flags & ~(uint32_t)(TT_GROUP_COPY_GATHER | TT_GROUP_BOUNCE | TT_GROUP_INFO)) return why = "unknown flags", false;
+    const uint32_t B = cfg->batch ? cfg->batch : 1;
+    if (B > 16) return why = "at most 16 frames per call", false;
+    // (the batch is one screen B frames tall: its pixels and a member's B n rays per launch stay below 2^27)
+    if ((uint64_t)cfg->width * cfg->height * B > (1ull << 27)) return why = "batch x screen above 2^27 pixels", false;
     return true;
 }
 
@@ -238,8 +252,9 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
     g->bounce = (cfg->flags & TT_GROUP_BOUNCE) != 0;
     g->copy = (cfg->flags & TT_GROUP_COPY_GATHER) != 0;
     g->info = (cfg->flags & TT_GROUP_INFO) != 0;
+    g->B = cfg->batch ? cfg->batch : 1;
     const size_t K = g->info ? 2 : 1;  // records per ray in the gather
-    const uint64_t WH = (uint64_t)g->W * g->H;
+    const uint64_t WH = (uint64_t)g->W * g->H, B = g->B;
     g->shard_n.resize(g->world);
     g->shard_off.resize(g->world);
     uint64_t off = 0;
@@ -263,10 +278,12 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
             c.stream = mb.stream[s];
             if (tt_ctx_create(&c, &mb.ctx[s]) != TT_OK) return gfail(g, TT_ERR_HIP, "tt_ctx_create on device %d", mb.device);
             (void)tt_ctx_set_timing(mb.ctx[s], 0);  // no per-launch event pair (a host turns it on per context)
+            if (B > 1) (void)tt_ctx_set_frame_pixels(mb.ctx[s], (uint32_t)WH);
             G_HIP(g, hipSetDevice(mb.device));
-            G_HIP(g, mb.rays[s].alloc(WH + mb.n));
-            G_HIP(g, mb.send[s].alloc(K * mb.n));
-            if (g->info) G_HIP(g, mb.info_full[s].alloc(WH));
+            // GlobalRays of the B-frames-tall screen: the primary rays at [0, B n), bounce 1 at [B W H, + B n)
+            G_HIP(g, mb.rays[s].alloc(B * (WH + mb.n)));
+            G_HIP(g, mb.send[s].alloc(K * B * mb.n));
+            if (g->info) G_HIP(g, mb.info_full[s].alloc(B * WH));
             G_HIP(g, mb.count[s].alloc(1));
             G_HIP(g, hipMemset(mb.count[s].p, 0, 4));
             G_HIP(g, hipEventCreateWithFlags(&mb.ev_prim[s], hipEventDisableTiming));
@@ -276,15 +293,25 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
     if (g->root) {
         Member& r0 = g->m[0];
         G_HIP(g, hipSetDevice(r0.device));
-        std::vector<uint32_t> order;
+        std::vector<uint32_t> order, base, stride;
         order.reserve(WH);
+        base.reserve(WH);
+        stride.reserve(WH);
         for (uint32_t r = 0; r < g->world; r++) {
             tile_pixels(g->W, g->H, g->tile, g->world, r, pix);
             order.insert(order.end(), pix.begin(), pix.end());
+            for (uint32_t l = 0; l < (uint32_t)pix.size(); l++) {
+                base.push_back((uint32_t)(B * g->shard_off[r] + l));
+                stride.push_back((uint32_t)g->shard_n[r]);
+            }
         }
         G_HIP(g, g->order.alloc(order.size()));
         G_HIP(g, hipMemcpy(g->order.p, order.data(), 4 * order.size(), hipMemcpyHostToDevice));
-        for (uint32_t s = 0; s < g->slots; s++) G_HIP(g, g->recv[s].alloc(K * WH));
+        G_HIP(g, g->base.alloc(base.size()));
+        G_HIP(g, hipMemcpy(g->base.p, base.data(), 4 * base.size(), hipMemcpyHostToDevice));
+        G_HIP(g, g->stride.alloc(stride.size()));
+        G_HIP(g, hipMemcpy(g->stride.p, stride.data(), 4 * stride.size(), hipMemcpyHostToDevice));
+        for (uint32_t s = 0; s < g->slots; s++) G_HIP(g, g->recv[s].alloc(K * B * WH));
     }
     return TT_OK;
 }
@@ -317,6 +344,8 @@ void teardown(tt_group* g) {
     if (!g->m.empty()) (void)hipSetDevice(g->m[0].device);
     for (uint32_t s = 0; s < TT_GROUP_MAX_SLOTS; s++) g->recv[s].release();
     g->order.release();
+    g->base.release();
+    g->stride.release();
     g->stage.release();
     (void)hipGetLastError();
 }
@@ -480,6 +509,7 @@ tt_status reupload(tt_group* g, Up up) {
             c.stream = mb.stream[s];
             if (tt_ctx_create(&c, &mb.ctx[s]) != TT_OK) return gfail(g, TT_ERR_HIP, "tt_ctx_create on device %d", mb.device);
             (void)tt_ctx_set_timing(mb.ctx[s], 0);
+            if (g->B > 1) (void)tt_ctx_set_frame_pixels(mb.ctx[s], g->W * g->H);
             G_TT(g, mb.ctx[s], tt_ctx_share_scene(mb.ctx[s], c0));
         }
     }
@@ -558,39 +588,42 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         }
         if (host_out && !g->stage.p) {
             G_HIP(g, hipSetDevice(g->m[0].device));
-            G_HIP(g, g->stage.alloc((g->info ? 2 : 1) * (size_t)g->W * g->H));
+            G_HIP(g, g->stage.alloc((g->info ? 2 : 1) * (size_t)g->B * g->W * g->H));
         }
     }
     const uint32_t s = (uint32_t)(g->frame % g->slots);
     const bool async = (flags & TT_TRACE_ASYNC) != 0;
     const uint32_t tflags = TT_TRACE_DEVICE_PTRS | TT_TRACE_ASYNC;
-    // 1. every member: Generate its tiles, trace them (records into its send buffer)
+    const uint32_t B = g->B, WH = g->W * g->H, HB = g->H * B;  // the batch traces as one W x B H screen
+    // 1. every member: Generate its tiles of the B frames, trace them (records into its send buffer)
     for (Member& mb : g->m) {
         hipStream_t st = static_cast<hipStream_t>(mb.stream[s]);
         G_HIP(g, hipSetDevice(mb.device));
         // the send buffer is free again once the gather that last read it is done (rank 0's copies: its event)
         if (mb.sent_used[s]) G_HIP(g, hipStreamWaitEvent(st, g->copy ? g->m[0].ev_sent[s] : mb.ev_sent[s], 0));
-        G_HIP(g, tt_launch_generate_list(cam->cam_to_world, cam->cam_inv_proj, mb.pixels.p, mb.n, g->W, g->H,
+        G_HIP(g, tt_launch_generate_list(cam->cam_to_world, cam->cam_inv_proj, mb.pixels.p, mb.n, B, g->W, g->H,
                                          cam->near_plane, cam->far_plane, cam->jitter, cam->frames_accumulated,
                                          cam->max_bounce, mb.rays[s].p, st));
         tt_trace_params p{};
-        p.n_rays = mb.n;
+        p.n_rays = B * mb.n;
         p.bounce = 0;
         p.far_plane = cam->far_plane;
         p.screen_width = g->W;
-        p.screen_height = g->H;
+        p.screen_height = HB;
         p.flags = tflags;
         if (mb.n) G_TT(g, mb.ctx[s], tt_trace_closest_hits(mb.ctx[s], &p, mb.rays[s].p,
                                                            g->info ? reinterpret_cast<uint32_t*>(mb.info_full[s].p) : nullptr,
                                                            nullptr, reinterpret_cast<uint32_t*>(mb.send[s].p)));
         if (g->info && mb.n) {
-            hipLaunchKernelGGL(tt_group_pack_info_kernel, dim3((mb.n + 255u) / 256u), dim3(256), 0, st, mb.info_full[s].p,
-                               mb.pixels.p, mb.n, mb.send[s].p + mb.n);
+            hipLaunchKernelGGL(tt_group_pack_info_kernel, dim3((B * mb.n + 255u) / 256u), dim3(256), 0, st,
+                               mb.info_full[s].p, mb.pixels.p, mb.n, B, WH, mb.send[s].p + (size_t)B * mb.n);
             G_HIP(g, hipGetLastError());
         }
         G_HIP(g, hipEventRecord(mb.ev_prim[s], st));
     }
-    // 2. the gather: one fused RCCL group (or device copies) on the communication streams
+    // 2. the gather: one fused RCCL group (or device copies) on the communication streams; a rank's message is
+    // its B frames' records back to back (and as many info texels after them)
+    const size_t info_at = (size_t)B * WH;  // the info texels' region of rank 0's receive buffer
     if (!g->copy) {
         for (Member& mb : g->m) {
             G_HIP(g, hipSetDevice(mb.device));
@@ -600,17 +633,17 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         ncclResult_t r = ncclSuccess;
         for (Member& mb : g->m) {
             hipStream_t cs = static_cast<hipStream_t>(mb.comm_stream);
-            if (r == ncclSuccess && mb.n) r = rccl().Send(mb.send[s].p, (size_t)mb.n * 4, ncclUint32, 0, mb.comm, cs);
+            const size_t cnt = (size_t)B * mb.n * 4;  // uint32 words of the rank's records
+            if (r == ncclSuccess && mb.n) r = rccl().Send(mb.send[s].p, cnt, ncclUint32, 0, mb.comm, cs);
             if (r == ncclSuccess && mb.n && g->info)
-                r = rccl().Send(mb.send[s].p + mb.n, (size_t)mb.n * 4, ncclUint32, 0, mb.comm, cs);
+                r = rccl().Send(mb.send[s].p + (size_t)B * mb.n, cnt, ncclUint32, 0, mb.comm, cs);
             if (mb.rank == 0)
                 for (uint32_t q = 0; q < g->world && r == ncclSuccess; q++)
                     if (g->shard_n[q]) {
-                        r = rccl().Recv(g->recv[s].p + g->shard_off[q], (size_t)g->shard_n[q] * 4, ncclUint32, (int)q,
-                                        mb.comm, cs);
+                        const size_t at = (size_t)B * g->shard_off[q], qcnt = (size_t)B * g->shard_n[q] * 4;
+                        r = rccl().Recv(g->recv[s].p + at, qcnt, ncclUint32, (int)q, mb.comm, cs);
                         if (r == ncclSuccess && g->info)  // (messages between one pair match in call order)
-                            r = rccl().Recv(g->recv[s].p + (size_t)g->W * g->H + g->shard_off[q],
-                                            (size_t)g->shard_n[q] * 4, ncclUint32, (int)q, mb.comm, cs);
+                            r = rccl().Recv(g->recv[s].p + info_at + at, qcnt, ncclUint32, (int)q, mb.comm, cs);
                     }
         }
         const ncclResult_t re = rccl().GroupEnd();
@@ -627,12 +660,11 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         G_HIP(g, hipSetDevice(r0.device));
         for (Member& mb : g->m) {
             G_HIP(g, hipStreamWaitEvent(cs, mb.ev_prim[s], 0));
-            if (mb.n)
-                G_HIP(g, hipMemcpyAsync(g->recv[s].p + g->shard_off[mb.rank], mb.send[s].p, (size_t)mb.n * 16,
-                                        hipMemcpyDeviceToDevice, cs));
+            const size_t at = (size_t)B * g->shard_off[mb.rank], bytes = (size_t)B * mb.n * 16;
+            if (mb.n) G_HIP(g, hipMemcpyAsync(g->recv[s].p + at, mb.send[s].p, bytes, hipMemcpyDeviceToDevice, cs));
             if (mb.n && g->info)
-                G_HIP(g, hipMemcpyAsync(g->recv[s].p + (size_t)g->W * g->H + g->shard_off[mb.rank], mb.send[s].p + mb.n,
-                                        (size_t)mb.n * 16, hipMemcpyDeviceToDevice, cs));
+                G_HIP(g, hipMemcpyAsync(g->recv[s].p + info_at + at, mb.send[s].p + (size_t)B * mb.n, bytes,
+                                        hipMemcpyDeviceToDevice, cs));
         }
         G_HIP(g, hipEventRecord(r0.ev_sent[s], cs));
         for (Member& mb : g->m) mb.sent_used[s] = true;
@@ -641,30 +673,31 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
     if (g->root) {
         Member& r0 = g->m[0];
         G_HIP(g, hipSetDevice(r0.device));
-        const uint32_t WH = g->W * g->H;
         uint4* oh = host_out ? g->stage.p : reinterpret_cast<uint4*>(hits_out);
-        uint4* oi = !g->info ? nullptr : host_out ? g->stage.p + WH : reinterpret_cast<uint4*>(info_out);
-        hipLaunchKernelGGL(tt_group_scatter_kernel, dim3((WH + 255u) / 256u), dim3(256), 0,
-                           static_cast<hipStream_t>(r0.comm_stream), g->recv[s].p, g->order.p, WH, oh, oi);
+        uint4* oi = !g->info ? nullptr : host_out ? g->stage.p + info_at : reinterpret_cast<uint4*>(info_out);
+        hipLaunchKernelGGL(tt_group_scatter_kernel, dim3((B * WH + 255u) / 256u), dim3(256), 0,
+                           static_cast<hipStream_t>(r0.comm_stream), g->recv[s].p, g->order.p, g->base.p, g->stride.p,
+                           WH, B, oh, oi);
         G_HIP(g, hipGetLastError());
         if (host_out) {
-            G_HIP(g, hipMemcpyAsync(hits_out, g->stage.p, (size_t)WH * 16, hipMemcpyDeviceToHost,
+            G_HIP(g, hipMemcpyAsync(hits_out, g->stage.p, info_at * 16, hipMemcpyDeviceToHost,
                                     static_cast<hipStream_t>(r0.comm_stream)));
             if (g->info)
-                G_HIP(g, hipMemcpyAsync(info_out, g->stage.p + WH, (size_t)WH * 16, hipMemcpyDeviceToHost,
+                G_HIP(g, hipMemcpyAsync(info_out, g->stage.p + info_at, info_at * 16, hipMemcpyDeviceToHost,
                                         static_cast<hipStream_t>(r0.comm_stream)));
         }
     }
-    // 3. bounce 1 on every member's own device (the gather reads only the send buffers, so it overlaps)
+    // 3. bounce 1 on every member's own device (the gather reads only the send buffers, so it overlaps); with
+    // B > 1 the enqueue draws frame b's directions from its frame-local pixel at frames + b (frame_pixels = W H)
     if (g->bounce) {
         for (Member& mb : g->m) {
             if (!mb.n) continue;
             tt_trace_params p{};
-            p.n_rays = mb.n;
+            p.n_rays = B * mb.n;
             p.bounce = 0;
             p.far_plane = cam->far_plane;
             p.screen_width = g->W;
-            p.screen_height = g->H;
+            p.screen_height = HB;
             p.flags = tflags;
             G_TT(g, mb.ctx[s], tt_enqueue_diffuse_bounce_indirect(mb.ctx[s], &p, nullptr, mb.rays[s].p,
                                                                   cam->frames_accumulated, cam->max_bounce,
@@ -705,7 +738,7 @@ tt_status tt_group_frame_rays(tt_group* g, uint32_t m, uint32_t* n_primary, uint
     G_HIP(g, hipStreamSynchronize(static_cast<hipStream_t>(mb.stream[s])));
     uint32_t nb = 0;
     if (g->bounce) G_HIP(g, hipMemcpy(&nb, mb.count[s].p, 4, hipMemcpyDeviceToHost));
-    if (n_primary) *n_primary = mb.n;
+    if (n_primary) *n_primary = g->B * mb.n;
     if (n_bounce) *n_bounce = nb;
     if (rays_dev) *rays_dev = mb.rays[s].p;
     return TT_OK;

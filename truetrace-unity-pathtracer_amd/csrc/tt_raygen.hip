@@ -122,18 +122,22 @@ __global__ __launch_bounds__(256) void tt_generate_kernel(const CamArgs cam,
                  reinterpret_cast<uint4*>(rays + y * width + x));
 }
 
-// The rays of a pixel list (a multi-GPU group member's screen tiles, tt_group_trace_frame): ray i is
-// pixel pixels[i]'s camera ray, bit for bit the one tt_generate_kernel writes at GlobalRays[pixel].
+// The rays of a pixel list (a multi-GPU group member's screen tiles, tt_group_trace_frame) for `batch` frames:
+// ray b n + i is pixel pixels[i]'s camera ray of frame b (frames_accumulated = frames + b), bit for bit the one
+// tt_generate_kernel writes at GlobalRays[pixel] for that frame, with PixelIndex + b W H (frame b of a screen
+// `batch` frames tall, tt_ctx_set_frame_pixels).
 __global__ __launch_bounds__(256) void tt_generate_list_kernel(const CamArgs cam, const uint32_t* __restrict__ pixels,
-                                                               uint32_t n, uint32_t width, uint32_t height,
-                                                               float near_plane, float far_plane, int32_t jitter,
-                                                               int32_t frames, int32_t max_bounce,
+                                                               uint32_t n, uint32_t batch, uint32_t width,
+                                                               uint32_t height, float near_plane, float far_plane,
+                                                               int32_t jitter, int32_t frames, int32_t max_bounce,
                                                                tt_ray_data* __restrict__ rays) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t p = pixels[i];
-    generate_one(cam, p % width, p / width, width, height, near_plane, far_plane, jitter, frames, max_bounce,
-                 reinterpret_cast<uint4*>(rays + i));
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n * batch) return;
+    const uint32_t b = r / n, p = pixels[r - b * n];
+    uint4* o = reinterpret_cast<uint4*>(rays + r);
+    generate_one(cam, p % width, p / width, width, height, near_plane, far_plane, jitter, frames + (int32_t)b,
+                 max_bounce, o);
+    if (b) o[0].w = p + b * width * height;
 }
 
 // sin/cos of the disc-sample angle phi in [-3pi/4, 3pi/4] (sample_disc's two branches give
@@ -373,17 +377,18 @@ hipError_t tt_launch_generate(const float* c2w, const float* ip, uint32_t w, uin
 }
 
 // pixels: DEVICE array of n pixel indices < w * h (the caller checked them)
-hipError_t tt_launch_generate_list(const float* c2w, const float* ip, const uint32_t* pixels, uint32_t n, uint32_t w,
-                                   uint32_t h, float near_plane, float far_plane, int32_t jitter, int32_t frames,
-                                   int32_t max_bounce, tt_ray_data* rays, hipStream_t st) {
-    if (n == 0) return hipSuccess;
+hipError_t tt_launch_generate_list(const float* c2w, const float* ip, const uint32_t* pixels, uint32_t n,
+                                   uint32_t batch, uint32_t w, uint32_t h, float near_plane, float far_plane,
+                                   int32_t jitter, int32_t frames, int32_t max_bounce, tt_ray_data* rays,
+                                   hipStream_t st) {
+    if (n == 0 || batch == 0) return hipSuccess;
     CamArgs cam;
     for (int i = 0; i < 16; i++) {
         cam.c2w[i] = c2w[i];
         cam.ip[i] = ip[i];
     }
-    hipLaunchKernelGGL(tt_generate_list_kernel, dim3((n + 255u) / 256u), dim3(256), 0, st, cam, pixels, n, w, h,
-                       near_plane, far_plane, jitter, frames, max_bounce, rays);
+    hipLaunchKernelGGL(tt_generate_list_kernel, dim3((n * batch + 255u) / 256u), dim3(256), 0, st, cam, pixels, n,
+                       batch, w, h, near_plane, far_plane, jitter, frames, max_bounce, rays);
     return hipGetLastError();
 }
 

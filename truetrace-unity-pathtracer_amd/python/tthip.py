@@ -1076,7 +1076,7 @@ GROUP_SYMBOLS = ["tt_group_create", "tt_group_unique_id", "tt_group_create_rank"
 
 class GroupConfig(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("tile", C.c_uint32), ("slots", C.c_uint32),
-                ("flags", C.c_uint32), ("pad", C.c_uint32)]
+                ("flags", C.c_uint32), ("batch", C.c_uint32)]
 
 
 def _group_lib():
@@ -1147,9 +1147,9 @@ class Group:
 
     def __init__(self, width: int, height: int, devices=None, tile: int = 64, slots: int = 2, bounce: bool = False,
                  copy: bool = False, rank: int = None, world: int = None, uid: bytes = None, device: int = None,
-                 info: bool = False):
+                 info: bool = False, batch: int = 1):
         L = _group_lib()
-        cfg = GroupConfig(width=width, height=height, tile=tile, slots=slots,
+        cfg = GroupConfig(width=width, height=height, tile=tile, slots=slots, batch=batch,
                           flags=(TT_GROUP_BOUNCE if bounce else 0) | (TT_GROUP_COPY_GATHER if copy else 0)
                           | (TT_GROUP_INFO if info else 0))
         h = C.c_void_p()
@@ -1164,7 +1164,7 @@ class Group:
         if st != TT_OK:
             raise TTError(st, "tt_group_create")
         self.L, self.h = L, h.value
-        self.width, self.height, self.bounce = width, height, bounce
+        self.width, self.height, self.bounce, self.batch = width, height, bounce, max(1, batch)
 
     def _check(self, st, what):
         if st != TT_OK:
