@@ -10,7 +10,7 @@ frames. Each child: builds the bench scene (the same seeded Sponza-shaped C2 buf
 (tt_group_create_rank on --device), uploads, traces one synchronous frame per cycled sample to learn its ray
 counts (the bounce-1 count lives on the device), runs --warmup frames, waits at the barrier, times --steps
 asynchronous frames (frame k = sample k mod --cycle, --slots frames in flight), and prints ONE JSON line:
-{"elapsed_s", "rays_per_sample": this rank's primary + bounce-1 rays per sample, "parity": rank 0 only -- the
+{"elapsed_s", "host_s": the enqueue loop alone, "rays_per_sample": this rank's primary + bounce-1 rays per sample, "parity": rank 0 only -- the
 last frame's gathered screen-order records against one context tracing that whole frame}."""
 import argparse
 import json
@@ -89,6 +89,7 @@ def main():
         t0 = time.perf_counter()
         for k in range(a.steps):
             g.trace_frame(outs[k % S], c2w, ip, near, far, jitter=1, frames=B * (k % R), max_bounce=1, asynchronous=True)
+        host = time.perf_counter() - t0  # the host's enqueue time of all calls (the device may still be busy)
         g.sync()
         el = time.perf_counter() - t0
         parity = None
@@ -106,7 +107,7 @@ def main():
                 parity = bool(np.array_equal(got, ref))
             finally:
                 eng.close()
-        print(json.dumps({"elapsed_s": el, "rays_per_sample": mine, "parity": parity}), flush=True)
+        print(json.dumps({"elapsed_s": el, "host_s": host, "rays_per_sample": mine, "parity": parity}), flush=True)
     finally:
         g.close()
 

@@ -1999,7 +1999,13 @@ static tt_status trace_closest_call(tt_ctx* c, const tt_trace_params* p, const u
     // one dequeue chunk per wave: a launch smaller than the resident grid spreads over as many
     // waves as it has chunks (r02: sizing this for 256-ray chunks left a 260k-ray launch -- one
     // rank's shard at 8 GPUs -- on ~1 wave per SIMD, 4 chunks each)
-    const uint32_t waves_needed = (p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays();
+    static const uint32_t chunks_per_wave = [] {  // TT_CHUNKS_PER_WAVE: experiment knob (default 1)
+        const char* e = std::getenv("TT_CHUNKS_PER_WAVE");
+        const int v = e ? std::atoi(e) : 1;
+        return (uint32_t)std::max(1, std::min(v, 64));
+    }();
+    const uint32_t chunks_needed = (p->n_rays + tt_trace_chunk_rays() - 1u) / tt_trace_chunk_rays();
+    const uint32_t waves_needed = (chunks_needed + chunks_per_wave - 1u) / chunks_per_wave;
     const uint32_t wpb = std::max(1u, tt_trace_block_size() / 64u);  // waves per block
     const uint32_t blocks_needed = (waves_needed + wpb - 1u) / wpb;
     const uint32_t grid = std::max(
