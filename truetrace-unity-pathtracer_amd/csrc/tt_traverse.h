@@ -16,6 +16,10 @@
 #endif
 #ifndef TT_SEGS
 #define TT_SEGS 8         // ray-range segments, one per XCD group (blockIdx % 8), with stealing
+// (Within a dispatch each blockIdx % 8 class runs on one XCD, but the round-robin continues from where the
+// previous dispatch left it, so band s meets a different XCD launch after launch -- tools/xcc_map.hip.
+// Keying the start segment on the XCC_ID register instead measured neutral (profiles/r06/xcc/): a launch
+// finds no previous launch's lines in its XCD's L2 either way.)
 #endif
 #ifndef TT_CHUNK_BIG
 #define TT_CHUNK_BIG 64   // rays per dequeue (the surplus waits in the wave's pool)
