@@ -169,3 +169,42 @@ def test_frame_slot_guards():
             e.close()
     finally:
         lender.close()  # closes every slot first
+
+
+def test_refused_share_leaves_the_context_as_it_was():
+    """a tt_ctx_share_blas refused by the TLAS walk -- n_tlas_nodes inside the lender's TLAS
+    region but smaller than the TLAS the walk reaches -- must leave dst as it was: a frame slot keeps its own
+    moved TLAS and region, a context with its own scene keeps that scene; both still trace as before."""
+    a = refit_scene(43)
+    assert a.tlas_nodes > 1
+    rays = _rays()
+    lender, slot, own = tthip.Engine(0), tthip.Engine(0), tthip.Engine(0)
+    try:
+        lender.upload(a)
+        slot.share_blas(lender, a.tlas_nodes)
+        md_b, box_b = _pose(a, 7)
+        slot.update_meshdata(0, md_b)
+        slot.tlas_refit(a.tlas_nodes, box_b)
+        sc_slot = _scene_of(slot, a, md_b)
+        moved = _check(slot, sc_slot, rays)
+        b = refit_scene(44)
+        own.upload(b)
+        own_hits = _check(own, b, rays, bounce_too=False)
+        for dst in (slot, own):
+            with pytest.raises(tthip.TTError) as ex:
+                dst.share_blas(lender, 1)  # the TLAS walk leaves [0, 1)
+            assert ex.value.status == tthip.TT_ERR_INVALID_ARG
+        assert np.array_equal(_scene_of(slot, a, md_b).nodes, sc_slot.nodes)
+        assert np.array_equal(_check(slot, sc_slot, rays), moved)
+        assert np.array_equal(_check(own, b, rays, bounce_too=False), own_hits)
+        # the refused calls reserved no overlay region: the 7 regions besides the slot's are all still free
+        extra = [tthip.Engine(0) for _ in range(7)]
+        try:
+            for e in extra:
+                e.share_blas(lender, a.tlas_nodes)
+        finally:
+            for e in extra:
+                e.close()
+    finally:
+        own.close()
+        lender.close()
