@@ -133,9 +133,6 @@ __device__ __forceinline__ bool root_leaf_hit(const RootLeaf& R, const LaneRay& 
 }
 }  // namespace
 
-#if TT_BLAS_PREFETCH
-__shared__ uint32_t s_pf[2 * TT_BLOCK];  // the BLAS-root prefetches' LDS-DMA destination (never read)
-#endif
 
 // INFO: 0 = no _PrimaryTriangleInfo, 1 = bounce 0 form, 2 = bounce > 0 form (GlobalColors).
 // IND: the ray count is device-resident (tt_trace_closest_indirect): instantiated as its own kernel
@@ -191,10 +188,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     uint32_t c_nodes = 0, c_tris = 0, c_blas = 0, c_acc = 0, c_rays = 0, c_hits = 0, c_reps = 0, c_ovf = 0;
     uint32_t d_iter = 0, d_node_lanes = 0, d_node_iters = 0, d_tri_lanes = 0, d_tri_iters = 0, d_active_lanes = 0;
     uint32_t d_lead_same = 0, d_uniform = 0;  // node-step uniformity (lanes sharing the first lane's node)
-#if TT_BLAS_PREFETCH
-    uint32_t pf_no = 0;  // byte offset of the next pending instance's BLAS root (enter_blas)
-    bool pf = false;
-#endif
     // the world-space ray (ray2, IntersectionKernels.compute:151), kept in registers
     auto world_ray = [&]() -> LaneRay { return wray; };
 
@@ -210,18 +203,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             const float4 m0 = mp[0], m1 = mp[1], m2 = mp[2];
             const int4 mo4 = reinterpret_cast<const int4*>(mp)[3];
             const int4 mo5 = reinterpret_cast<const int4*>(mp)[4];
-#if TT_BLAS_PREFETCH
-            // TT_BLAS_PREFETCH (A/B variant): the next pending instance of this TLAS leaf group is
-            // entered when this BLAS is done; its root node's lines are requested now (LDS-DMA loads: no register
-            // destination, results never read) so that entry's first node step finds them in cache instead of
-            // starting a second dependent miss. Loads retire in order, so the next node step's wait covers them.
-            // (the loads themselves are issued in the loop body, outside this lambda: pf_no / pf)
-            if (tg.y != 0u) {
-                const uint32_t nmo = firstbithigh(tg.y);
-                pf_no = node_offset((uint32_t)reinterpret_cast<const int4*>(A.leaf + (tg.x + nmo))[3].w);
-                pf = true;
-            }
-#endif
             mesh_id = mo5.x;
             NodeOffset = mo4.y;
             TriOffset = mo4.x;
@@ -471,16 +452,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 d_tri_iters += tm ? 1u : 0u;
             }
         }
-#if TT_BLAS_PREFETCH
-        if (pf) {
-            typedef __attribute__((address_space(3))) void lds_void;
-            lds_void* l0 = (lds_void*)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                (int)(uint32_t)(uintptr_t)(lds_void*)s_pf);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(nodes, l0, 4, pf_no, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(nodes, (lds_void*)((char __attribute__((address_space(3)))*)l0 + 4 * TT_BLOCK), 4, pf_no + 64u, 0, 0, 0);
-            pf = false;
-        }
-#endif
         // --------------------------------------------------------- triangle phase
         if ((int32_t)tg.y > 0) {  // :220-226, highest bit first, one triangle per pass
             TT_DB(9);

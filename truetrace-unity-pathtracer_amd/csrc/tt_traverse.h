@@ -42,9 +42,6 @@
 #ifndef TT_UNIFORM_POOL
 #define TT_UNIFORM_POOL 1  // readfirstlane the scheduler's pool state after each refill (0: A/B; +1.2% bench, profiles/r04/ab)
 #endif
-#ifndef TT_BLAS_PREFETCH
-#define TT_BLAS_PREFETCH 0
-#endif
 #ifndef TT_LDS_STACK
 #define TT_LDS_STACK 12   // stack entries kept in LDS; deeper entries spill to a global area
 #endif
