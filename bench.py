@@ -864,9 +864,10 @@ def group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H):
            "gather_identical_to_1gpu": None if res is None else res.get("parity"),
            "api": "tt_group_unique_id + tt_group_create_rank + tt_group_scene_upload + tt_group_trace_frame "
                   "(TT_TRACE_ASYNC) + tt_group_sync, one child process per rank (tools/group_leg.py)",
-           "layout": "one 1080p frame per step: 64x64 tiles round-robin over the ranks (world 1: the whole frame), "
-                     "each rank's Generate + primary trace + bounce-1 enqueue/trace on its own device, one RCCL "
-                     "gather of the primary hit records to rank 0 per frame inside the library"}
+           "layout": "one 1080p frame per step: 64x64 tiles round-robin over the ranks, each rank's Generate + "
+                     "primary trace + bounce-1 enqueue/trace on its own device, one RCCL gather of the primary hit "
+                     "records to rank 0 per frame inside the library (world 1: the whole frame traced straight into "
+                     "the output, nothing to gather)"}
     if world > 1 and getattr(args, "_solo_ms", None):
         out["efficiency_vs_n1_frame"] = round(args._solo_ms / (world * el * 1e3 / (K * Bg)), 4)
     return out

@@ -112,10 +112,15 @@ def test_copy_gather_three_members_equal_the_oracle_frame(soup):
         g.close()
 
 
-def test_one_member_rccl_group_equals_the_single_launch(engine, soup):
-    """A one-device RCCL group (ncclCommInitAll over device 0; the gather is rank 0's send to itself): the frame
-    equals tt_generate_primary + tt_trace_closest on one context, and the member's bounce chain the engine's."""
+@pytest.mark.parametrize("gather", [False, True], ids=["direct", "forced_gather"])
+def test_one_member_rccl_group_equals_the_single_launch(engine, soup, gather, monkeypatch):
+    """A one-device RCCL group (ncclCommInitAll over device 0): the frame equals tt_generate_primary +
+    tt_trace_closest on one context, and the member's bounce chain the engine's -- traced straight into hits_out
+    (a one-rank group's path), and through the gather (rank 0's send to itself) + scatter with
+    TT_GROUP_FORCE_GATHER."""
     torch = _torch()
+    if gather:
+        monkeypatch.setenv("TT_GROUP_FORCE_GATHER", "1")
     W, H, frames = 320, 192, 2
     c2w, ip = soup_camera(W, H)
     g = tthip.Group(W, H, devices=[0], bounce=True)
@@ -140,9 +145,12 @@ def test_one_member_rccl_group_equals_the_single_launch(engine, soup):
         g.close()
 
 
-def test_rank_mode_world_one(soup):
+@pytest.mark.parametrize("gather", [False, True], ids=["direct", "forced_gather"])
+def test_rank_mode_world_one(soup, gather, monkeypatch):
     """tt_group_unique_id + tt_group_create_rank (the one-process-per-GPU shape bench.py uses) at world 1."""
     torch = _torch()
+    if gather:
+        monkeypatch.setenv("TT_GROUP_FORCE_GATHER", "1")
     W, H, frames = 256, 128, 0
     c2w, ip = soup_camera(W, H)
     g = tthip.Group(W, H, rank=0, world=1, uid=tthip.group_unique_id(), device=0)
@@ -382,3 +390,36 @@ def test_batched_group_frames_equal_the_oracle_frames(soup):
             assert off == B * WH + nb
     finally:
         g.close()
+
+
+def test_one_rank_direct_path_batched_info_host_outputs(soup, monkeypatch):
+    """A one-rank group traces straight into the caller's outputs: two frames per call with _PrimaryTriangleInfo,
+    into host arrays (the staging path) and into device tensors, equal to the same group forced through the
+    gather + scatter and to the oracle's frames."""
+    torch = _torch()
+    W, H, B, f0 = 200, 120, 2, 3
+    c2w, ip = soup_camera(W, H)
+    outs = {}
+    for mode in ("direct", "gather"):
+        if mode == "gather":
+            monkeypatch.setenv("TT_GROUP_FORCE_GATHER", "1")
+        g = tthip.Group(W, H, devices=[0], bounce=True, info=True, batch=B)
+        try:
+            g.upload(soup)
+            hh = np.full((B * W * H, 4), 0xA5A5A5A5, np.uint32)
+            hi = np.full((B * W * H, 4), 0xA5A5A5A5, np.uint32)
+            g.trace_frame(hh, c2w, ip, NEAR, FAR, jitter=1, frames=f0, max_bounce=1, info_out=hi)
+            dh = torch.full((B * W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+            di = torch.full((B * W * H, 4), -1, dtype=torch.int32, device="cuda:0")
+            g.trace_frame(dh, c2w, ip, NEAR, FAR, jitter=1, frames=f0, max_bounce=1, info_out=di)
+            assert np.array_equal(dh.cpu().numpy().view(np.uint32), hh)
+            assert np.array_equal(di.cpu().numpy().view(np.uint32), hi)
+            outs[mode] = (hh, hi)
+        finally:
+            g.close()
+    assert np.array_equal(outs["direct"][0], outs["gather"][0]) and np.array_equal(outs["direct"][1], outs["gather"][1])
+    for b in range(B):
+        info_ref = np.full((W * H, 4), 0xA5A5A5A5, np.uint32)
+        full = oracle_frame(soup, c2w, ip, W, H, f0 + b, info=info_ref)
+        assert np.array_equal(outs["direct"][0][b * W * H:(b + 1) * W * H], full["hits"][:W * H]), b
+        assert np.array_equal(outs["direct"][1][b * W * H:(b + 1) * W * H], info_ref), b

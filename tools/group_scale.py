@@ -16,10 +16,11 @@ configs = [tuple(int(x) for x in c.split("x")) for c in sys.argv[2].split(",")] 
     [(h, b, sl) for h in (1080, 272, 136) for b in (1, 4) for sl in (2, 4)]
 for height, batch, slots in configs:
     d = tempfile.mkdtemp(prefix="tt_group_scale_")
+    # TT_GROUP_FORCE_GATHER: keep the RCCL self-gather + scatter a one-rank group would skip, as an N-GPU rank has them
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "group_leg.py"), "--rank", "0", "--world", "1",
                         "--device", "0", "--dir", d, "--steps", str(frames), "--warmup", "10", "--slots", str(slots),
                         "--cycle", "4", "--batch", str(batch), "--height", str(height)], capture_output=True,
-                       text=True, timeout=300)
+                       text=True, timeout=300, env=dict(os.environ, TT_GROUP_FORCE_GATHER="1"))
     if r.returncode != 0:
         print(json.dumps({"height": height, "batch": batch, "slots": slots, "error": r.stderr[-400:]}), flush=True)
         sys.exit(r.returncode)

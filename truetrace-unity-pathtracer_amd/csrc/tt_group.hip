@@ -15,7 +15,8 @@
 // Per member and frame slot: one context (slot 0 lends its scene to the others, tt_ctx_share_scene) on a
 // dedicated hardware-queue stream (tt_stream_create), the slot's ray buffer, send buffer and device
 // bounce count. Per member: one communication stream for the gather. Frame k runs on slot k % slots, so a
-// member's frame k + 1 primary launch overlaps frame k's bounce drain and gather.
+// member's frame k + 1 primary launch overlaps frame k's bounce drain and gather. A group of one rank traces
+// the identity pixel order straight into the caller's hits_out / info_out (no gather, no scatter).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
@@ -23,6 +24,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -185,6 +187,7 @@ struct tt_group {
     uint32_t W = 0, H = 0, tile = 64, slots = 2, flags = 0, world = 0;
     uint32_t B = 1;  // frames per call (tt_group_config.batch)
     bool bounce = false, copy = false, info = false;
+    bool direct = false;  // one rank: traced straight into the caller's outputs (tt_group_trace_frame)
     std::vector<Member> m;
     std::vector<uint64_t> shard_n, shard_off;  // per rank
     // rank 0's side (when this process holds it: member 0)
@@ -253,6 +256,10 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
     g->copy = (cfg->flags & TT_GROUP_COPY_GATHER) != 0;
     g->info = (cfg->flags & TT_GROUP_INFO) != 0;
     g->B = cfg->batch ? cfg->batch : 1;
+    // TT_GROUP_FORCE_GATHER=1 keeps a one-rank group on the gather + scatter path (tools/group_scale.py: one GPU
+    // standing in for one rank of an N-GPU node)
+    const char* fg = std::getenv("TT_GROUP_FORCE_GATHER");
+    g->direct = g->world == 1 && !(fg && std::atoi(fg) != 0);
     const size_t K = g->info ? 2 : 1;  // records per ray in the gather
     const uint64_t WH = (uint64_t)g->W * g->H, B = g->B;
     g->shard_n.resize(g->world);
@@ -282,15 +289,17 @@ tt_status setup(tt_group* g, const tt_group_config* cfg) {
             G_HIP(g, hipSetDevice(mb.device));
             // GlobalRays of the B-frames-tall screen: the primary rays at [0, B n), bounce 1 at [B W H, + B n)
             G_HIP(g, mb.rays[s].alloc(B * (WH + mb.n)));
-            G_HIP(g, mb.send[s].alloc(K * B * mb.n));
-            if (g->info) G_HIP(g, mb.info_full[s].alloc(B * WH));
+            if (!g->direct) {  // (a one-rank group traces straight into the caller's buffers: tt_group_trace_frame)
+                G_HIP(g, mb.send[s].alloc(K * B * mb.n));
+                if (g->info) G_HIP(g, mb.info_full[s].alloc(B * WH));
+            }
             G_HIP(g, mb.count[s].alloc(1));
             G_HIP(g, hipMemset(mb.count[s].p, 0, 4));
             G_HIP(g, hipEventCreateWithFlags(&mb.ev_prim[s], hipEventDisableTiming));
             G_HIP(g, hipEventCreateWithFlags(&mb.ev_sent[s], hipEventDisableTiming));
         }
     }
-    if (g->root) {
+    if (g->root && !g->direct) {
         Member& r0 = g->m[0];
         G_HIP(g, hipSetDevice(r0.device));
         std::vector<uint32_t> order, base, stride;
@@ -595,12 +604,17 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
     const bool async = (flags & TT_TRACE_ASYNC) != 0;
     const uint32_t tflags = TT_TRACE_DEVICE_PTRS | TT_TRACE_ASYNC;
     const uint32_t B = g->B, WH = g->W * g->H, HB = g->H * B;  // the batch traces as one W x B H screen
+    // A group of one rank (world 1) traces the identity pixel order: ray b n + j is pixel j of frame b, so its
+    // records and info texels are already in hits_out / info_out order -- the trace writes them there directly
+    // and there is nothing to gather or scatter (host outputs: through the staging buffer).
+    const bool direct = g->direct;
     // 1. every member: Generate its tiles of the B frames, trace them (records into its send buffer)
     for (Member& mb : g->m) {
         hipStream_t st = static_cast<hipStream_t>(mb.stream[s]);
         G_HIP(g, hipSetDevice(mb.device));
         // the send buffer is free again once the gather that last read it is done (rank 0's copies: its event)
-        if (mb.sent_used[s]) G_HIP(g, hipStreamWaitEvent(st, g->copy ? g->m[0].ev_sent[s] : mb.ev_sent[s], 0));
+        if (mb.sent_used[s] && !direct)
+            G_HIP(g, hipStreamWaitEvent(st, g->copy ? g->m[0].ev_sent[s] : mb.ev_sent[s], 0));
         G_HIP(g, tt_launch_generate_list(cam->cam_to_world, cam->cam_inv_proj, mb.pixels.p, mb.n, B, g->W, g->H,
                                          cam->near_plane, cam->far_plane, cam->jitter, cam->frames_accumulated,
                                          cam->max_bounce, mb.rays[s].p, st));
@@ -611,6 +625,17 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         p.screen_width = g->W;
         p.screen_height = HB;
         p.flags = tflags;
+        if (direct) {
+            uint4* oh = host_out ? g->stage.p : reinterpret_cast<uint4*>(hits_out);
+            uint4* oi = !g->info ? nullptr : host_out ? g->stage.p + (size_t)B * WH : reinterpret_cast<uint4*>(info_out);
+            G_TT(g, mb.ctx[s], tt_trace_closest_hits(mb.ctx[s], &p, mb.rays[s].p, reinterpret_cast<uint32_t*>(oi), nullptr,
+                                                     reinterpret_cast<uint32_t*>(oh)));
+            if (host_out) {
+                G_HIP(g, hipMemcpyAsync(hits_out, oh, (size_t)B * WH * 16, hipMemcpyDeviceToHost, st));
+                if (g->info) G_HIP(g, hipMemcpyAsync(info_out, oi, (size_t)B * WH * 16, hipMemcpyDeviceToHost, st));
+            }
+            continue;
+        }
         if (mb.n) G_TT(g, mb.ctx[s], tt_trace_closest_hits(mb.ctx[s], &p, mb.rays[s].p,
                                                            g->info ? reinterpret_cast<uint32_t*>(mb.info_full[s].p) : nullptr,
                                                            nullptr, reinterpret_cast<uint32_t*>(mb.send[s].p)));
@@ -624,7 +649,9 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
     // 2. the gather: one fused RCCL group (or device copies) on the communication streams; a rank's message is
     // its B frames' records back to back (and as many info texels after them)
     const size_t info_at = (size_t)B * WH;  // the info texels' region of rank 0's receive buffer
-    if (!g->copy) {
+    if (direct) {
+        // (nothing crosses devices)
+    } else if (!g->copy) {
         for (Member& mb : g->m) {
             G_HIP(g, hipSetDevice(mb.device));
             G_HIP(g, hipStreamWaitEvent(static_cast<hipStream_t>(mb.comm_stream), mb.ev_prim[s], 0));
@@ -670,7 +697,7 @@ tt_status tt_group_trace_frame(tt_group* g, const tt_camera* cam, uint32_t* hits
         for (Member& mb : g->m) mb.sent_used[s] = true;
     }
     // rank 0: back to screen order (after its communication stream's receives)
-    if (g->root) {
+    if (g->root && !direct) {
         Member& r0 = g->m[0];
         G_HIP(g, hipSetDevice(r0.device));
         uint4* oh = host_out ? g->stage.p : reinterpret_cast<uint4*>(hits_out);
