@@ -44,7 +44,8 @@ def test_staged_build_equals_blas_build(mesh_fn):
 
 
 def test_presort_is_the_dotnet_sort_of_the_centroids():
-    L, v, aabbs, _ = _stages(tthip.Mesh.soup(5, 5_000))
+    mesh = tthip.Mesh.soup(5, 5_000)
+    L, v, aabbs, _ = _stages(mesh)
     n = len(aabbs)
     pre = np.zeros((3, n), np.int32)
     assert L.tt_bvh2_presort(aabbs.ctypes.data, n, pre.ctypes.data) == 0
@@ -57,7 +58,8 @@ def test_presort_is_the_dotnet_sort_of_the_centroids():
 
 
 def test_malformed_bvh2_is_rejected():
-    L, v, aabbs, bvh2 = _stages(tthip.Mesh.soup(9, 500))
+    mesh = tthip.Mesh.soup(9, 500)  # (v points into the mesh's arrays)
+    L, v, aabbs, bvh2 = _stages(mesh)
     fi, boxes, left, count = bvh2
     bad = [a.copy() for a in bvh2]
     bad[2][0] = 0  # root points at itself: a cycle

@@ -446,6 +446,7 @@ class Mesh:
     def view(self) -> MeshInput:
         v = MeshInput()
         self._check(scene_lib().tt_synth_mesh_view(self.h, C.byref(v)), "tt_synth_mesh_view")
+        v._owner = self  # the view points into this mesh's native arrays: it keeps the mesh alive
         return v
 
     def __del__(self):
