@@ -108,3 +108,21 @@ def test_prepared_handle_reassembles_the_host_blas(mesh_fn):
     h2 = tthip.C.c_void_p()
     assert L.tt_blas_build_from_cwbvh_prepared(prep2, nodes.ctypes.data, len(nodes), bad.ctypes.data,
                                                ref.info.bvh2_depth, tthip.C.byref(h2)) == tthip.TT_ERR_INVALID_ARG
+
+
+def test_a_mesh_view_keeps_its_mesh_alive():
+    """A tt_mesh_input view points into its mesh's native arrays: it must keep the mesh alive after the caller's
+    last reference to the mesh is gone (the intermittent use-after-free of round 6)."""
+    import gc
+
+    v = tthip.Mesh.soup(21, 2_000).view()  # the only reference to the mesh is the view's
+    gc.collect()
+    for _ in range(50):  # churn the allocator so freed arrays would be reused
+        tthip.Mesh.soup(22, 2_000)
+    n = v.n_indices // 3
+    a = np.zeros((n, 6), np.float32)
+    b = np.zeros((n, 6), np.float32)
+    L = tthip.scene_lib()
+    assert L.tt_blas_prepare_aabbs(v, a.ctypes.data) == 0
+    assert L.tt_blas_prepare_aabbs(tthip.Mesh.soup(21, 2_000).view(), b.ctypes.data) == 0
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
