@@ -808,7 +808,8 @@ def group_tiles(torch, dist, args, rank, world, backend, red_dev, gpu, W, H):
     64x64 tiles (round-robin) and their bounce-1 rays, and the primary hit records reach rank 0 in one RCCL
     gather per frame (inside the library), scattered back to screen order. Frames are asynchronous over
     --group-slots slots. value = all ranks' rays (primary + bounce 1) / the slowest rank's time; strong scaling
-    (one 1080p frame per frame whatever N). At N = 1 the group has one member (whole frame, RCCL self-gather).
+    (one 1080p frame per frame whatever N). At N = 1 the group has one member tracing the whole frame straight
+    into the output (a one-rank group has nothing to gather).
     The child isolates the leg: its communicator and gathers can never stall the bench's own ranks -- a child
     that fails or exceeds the time limit is killed and the leg reports the failure."""
     import subprocess
